@@ -1,0 +1,328 @@
+#!/usr/bin/env python3
+"""Golden-fixture generator: runs the *reference* ABIDES (read-only, /root/reference)
+in this build container and records what the product must reproduce.
+
+CONTAINER-ONLY TEST INFRASTRUCTURE.  Nothing under tests/, bench.py or the product
+imports this module; it is committed so the fixtures under tests/golden/ can be
+regenerated.  /root/reference does not exist on the GPU box.
+
+What is recorded per (config, seed):
+  * the kernel event trace: one int64 record per priority-queue pop
+      [t_ns_since_midnight, recipient, msg_type, kind, f0, f1, f2, f3, f4, f5]
+    (field meaning per kind: see KIND_* below and DESIGN.md §"Trace records")
+    The record is the parity unit of the whole project: the same record is produced
+    by the C oracle (oracle/) and by the HIP kernels (trace ring / rolling hash).
+  * a word-wise FNV-1a rolling hash over those records (checkpoint every 1000 pops),
+  * the final state: per-agent holdings + cash + open orders, the exchange book
+    (levels, FIFO order ids/qty), global order-id counter, message count, stdout
+    "Final holdings ..." and "Mean ending value" lines.
+
+Third-party modules the reference imports but this image lacks are replaced by
+logging-only stubs: `jsons.dump` (used only to log orders),
+pandas 2 API renames (`pandas.io.json.json_normalize`, `SparseDataFrame`), and the
+bz2 log writers are no-ops.  None of them touches the simulated arithmetic.
+
+Usage:  python tests/golden/gen_fixtures.py all          (writes tests/golden/*.npz/json)
+        python tests/golden/gen_fixtures.py run CFG SEED OUT [--full]
+"""
+import importlib
+import io
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import types
+import zlib
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+# ---- message kinds (shared with oracle/abides_oracle.h and csrc/mxa_trace.h) ----
+KIND = {
+    "WAKEUP": 0,
+    "WHEN_MKT_OPEN_REQ": 1, "WHEN_MKT_CLOSE_REQ": 2,
+    "WHEN_MKT_OPEN": 3, "WHEN_MKT_CLOSE": 4,
+    "QUERY_SPREAD_REQ": 5, "QUERY_SPREAD": 6,
+    "QUERY_LAST_TRADE_REQ": 7, "QUERY_LAST_TRADE": 8,
+    "QUERY_TRANSACTED_VOLUME_REQ": 9, "QUERY_TRANSACTED_VOLUME": 10,
+    "LIMIT_ORDER": 11, "CANCEL_ORDER": 12, "MODIFY_ORDER": 13,
+    "ORDER_ACCEPTED": 14, "ORDER_EXECUTED": 15, "ORDER_CANCELLED": 16,
+    "MKT_CLOSED": 17, "ORDER_MODIFIED": 18, "KERNEL_CANCEL_ORDER": 19,
+    "MARKET_DATA": 20,
+}
+
+FNV_OFF = 0xCBF29CE484222325
+FNV_PRIME = 0x100000001B3
+M64 = (1 << 64) - 1
+
+
+def fnv_words(h, words):
+    for w in words:
+        h = ((h ^ (int(w) & M64)) * FNV_PRIME) & M64
+    return h
+
+
+def _price(p):
+    """Integer cents (the simulated configs); marketreplay dollars -> 1e-4 units."""
+    if p is None:
+        return -1
+    if isinstance(p, (float, np.floating)):
+        return int(round(p * 10000))
+    return int(p)
+
+
+def _order_fields(o, with_qty=True):
+    return [int(o.order_id), int(o.agent_id), 1 if o.is_buy_order else 0,
+            int(o.quantity) if with_qty else 0, _price(o.limit_price)]
+
+
+def encode(t_rel, recipient, mtype, msg):
+    """Map one popped event to the fixed 10-word parity record."""
+    f = [0, 0, 0, 0, 0, 0]
+    if msg is None:
+        kind = KIND["WAKEUP"] if mtype == 2 else KIND["KERNEL_CANCEL_ORDER"]
+        return [t_rel, recipient, mtype, kind] + f
+    b = msg.body
+    m = b["msg"]
+    req = "sender" in b and m not in ("LIMIT_ORDER", "CANCEL_ORDER", "MODIFY_ORDER")
+    if m in ("WHEN_MKT_OPEN", "WHEN_MKT_CLOSE"):
+        if req:
+            kind = KIND[m + "_REQ"]
+            f[0] = b["sender"]
+        else:
+            kind = KIND[m]
+            f[0] = int(b["data"].value) - MIDNIGHT
+    elif m == "QUERY_SPREAD":
+        if req:
+            kind = KIND["QUERY_SPREAD_REQ"]
+            f[0], f[1] = b["sender"], int(b["depth"])
+        else:
+            kind = KIND["QUERY_SPREAD"]
+            bids, asks = b["bids"], b["asks"]
+            f[0] = _price(bids[0][0]) if bids else -1
+            f[1] = int(bids[0][1]) if bids else 0
+            f[2] = _price(asks[0][0]) if asks else -1
+            f[3] = int(asks[0][1]) if asks else 0
+            f[4] = _price(b["data"])
+            f[5] = (1 if b["mkt_closed"] else 0) + 2 * len(bids) + (1 << 20) * len(asks)
+    elif m == "QUERY_LAST_TRADE":
+        if req:
+            kind = KIND["QUERY_LAST_TRADE_REQ"]
+            f[0] = b["sender"]
+        else:
+            kind = KIND["QUERY_LAST_TRADE"]
+            f[0] = _price(b["data"])
+            f[5] = 1 if b["mkt_closed"] else 0
+    elif m == "QUERY_TRANSACTED_VOLUME":
+        if req:
+            kind = KIND["QUERY_TRANSACTED_VOLUME_REQ"]
+            import pandas as pd
+            f[0], f[1] = b["sender"], int(pd.to_timedelta(b["lookback_period"]).value)
+        else:
+            kind = KIND["QUERY_TRANSACTED_VOLUME"]
+            f[0] = int(b["transacted_volume"])
+            f[5] = 1 if b["mkt_closed"] else 0
+    elif m == "LIMIT_ORDER":
+        kind = KIND[m]
+        f[:5] = _order_fields(b["order"])
+    elif m == "CANCEL_ORDER":
+        kind = KIND[m]
+        # the agent's own order object travels by reference and may be partially
+        # executed before delivery; the exchange only uses id/side/price.
+        f[:5] = _order_fields(b["order"], with_qty=False)
+    elif m == "MODIFY_ORDER":
+        kind = KIND[m]
+        f[:5] = _order_fields(b["new_order"])
+    elif m in ("ORDER_ACCEPTED", "ORDER_CANCELLED"):
+        kind = KIND[m]
+        f[:5] = _order_fields(b["order"])
+    elif m == "ORDER_EXECUTED":
+        kind = KIND[m]
+        f[:5] = _order_fields(b["order"])
+        f[5] = _price(b["order"].fill_price)
+    elif m == "MKT_CLOSED":
+        kind = KIND[m]
+    elif m == "ORDER_MODIFIED":
+        kind = KIND[m]
+        f[:5] = _order_fields(b["new_order"])
+    elif m == "MARKET_DATA":
+        kind = KIND[m]
+    else:
+        raise RuntimeError("unknown message " + m)
+    return [t_rel, recipient, mtype, kind] + [int(x) for x in f]
+
+
+MIDNIGHT = 0
+TRACE = []
+
+
+def install_stubs():
+    jsons = types.ModuleType("jsons")
+    jsons.dump = lambda obj, **kw: dict(vars(obj))
+    sys.modules["jsons"] = jsons
+    import pandas
+    import pandas.io.json
+    pandas.io.json.json_normalize = pandas.json_normalize
+    pandas.SparseDataFrame = pandas.DataFrame
+    sys.path.insert(0, REF)
+
+
+def run_config(cfg, seed, out, full):
+    global MIDNIGHT
+    install_stubs()
+    import queue
+
+    import pandas as pd
+
+    class RecPQ(queue.PriorityQueue):
+        def get(self, *a, **k):
+            item = super().get(*a, **k)
+            t, (rcp, mtype, msg) = item
+            TRACE.append(encode(int(t.value) - MIDNIGHT, int(rcp), int(mtype.value), msg))
+            return item
+
+    import Kernel as K
+    orig_init = K.Kernel.__init__
+
+    def init(self, *a, **k):
+        orig_init(self, *a, **k)
+        self.messages = RecPQ()
+        CAPTURE["kernel"] = self
+
+    K.Kernel.__init__ = init
+    K.Kernel.writeLog = lambda *a, **k: None
+    K.Kernel.writeSummaryLog = lambda *a, **k: None
+    from agent.ExchangeAgent import ExchangeAgent
+    ExchangeAgent.logOrderBookSnapshots = lambda *a, **k: None
+    from agent.TradingAgent import TradingAgent
+    TradingAgent.getTransactedVolume = TradingAgent.get_transacted_volume  # SURVEY.md key finding 3
+
+    date = {"sparse_zi_100": "2019-06-28", "sparse_zi_1000": "2019-06-28", "rmsc03": "2019-06-28"}[cfg]
+    MIDNIGHT = int(pd.Timestamp(date).value)
+    argv = ["abides.py", "-c", cfg, "-s", str(seed)]
+    if cfg == "rmsc03":
+        argv += ["-t", "ABM", "-d", "20190628"]
+    sys.argv = argv
+    buf = io.StringIO()
+    real_stdout = sys.stdout
+    sys.stdout = buf
+    try:
+        importlib.import_module("config." + cfg)
+    finally:
+        sys.stdout = real_stdout
+    kern = CAPTURE["kernel"]
+    stdout = buf.getvalue().splitlines()
+
+    from util.order.Order import Order
+    agents = kern.agents
+    ex = agents[0]
+    sym = list(ex.order_books)[0]
+    ob = ex.order_books[sym]
+
+    def lvl(side):
+        return [[[int(o.order_id), int(o.agent_id), int(o.quantity), _price(o.limit_price)] for o in level] for level in side]
+
+    final = {
+        "config": cfg, "seed": seed, "events": len(TRACE),
+        "order_id_counter": int(Order.order_id),
+        "n_order_ids": len(Order._order_ids),
+        "bids": lvl(ob.bids), "asks": lvl(ob.asks),
+        "last_trade": _price(ob.last_trade),
+        "agents": [],
+        "final_holdings_lines": [s for s in stdout if s.startswith("Final holdings")],
+        "mean_lines": [],
+        "final_time": int(kern.currentTime.value) - MIDNIGHT,
+    }
+    take = False
+    for s in stdout:
+        if s.startswith("Mean ending value"):
+            take = True
+            continue
+        if take:
+            if s.startswith("Simulation ending"):
+                break
+            final["mean_lines"].append(s.strip())
+    for a in agents[1:]:
+        h = {k: int(v) for k, v in a.holdings.items()}
+        final["agents"].append({
+            "id": a.id, "cash": h.get("CASH"), "shares": h.get(sym, 0),
+            "open_orders": [[int(o.order_id), 1 if o.is_buy_order else 0, int(o.quantity), _price(o.limit_price)]
+                            for o in a.orders.values()],
+        })
+    tr = np.asarray(TRACE, dtype=np.int64)
+    hs, h = [], FNV_OFF
+    for i, rec in enumerate(TRACE):
+        h = fnv_words(h, rec)
+        if (i + 1) % 1000 == 0:
+            hs.append(h)
+    final["hash"] = "%016x" % h
+    final["hash_checkpoints"] = ["%016x" % x for x in hs]
+    with open(out + ".json", "w") as f:
+        json.dump(final, f, indent=0)
+    keep = tr if full else tr[:20000]
+    np.savez_compressed(out + ".npz", trace=keep)
+
+
+CAPTURE = {}
+
+
+def rng_kats(path):
+    """numpy legacy RandomState known answers (MT19937 + legacy distributions)."""
+    out = {}
+    for seed in (0, 1, 5489, 123456789, 2 ** 32 - 1):
+        rs = np.random.RandomState(seed)
+        d = {"u32": rs.randint(0, 2 ** 32, size=700, dtype=np.uint64).astype(np.int64).tolist()}
+        rs = np.random.RandomState(seed)
+        d["double"] = [float(rs.rand()) for _ in range(300)]
+        rs = np.random.RandomState(seed)
+        seq = []
+        for i in range(400):
+            k = i % 8
+            if k == 0:
+                seq.append(["randint", 0, 100, int(rs.randint(0, 100))])
+            elif k == 1:
+                seq.append(["normal", 1e5, 100.0, float(rs.normal(1e5, 100.0))])
+            elif k == 2:
+                seq.append(["exponential", 1e12, 0, float(rs.exponential(1e12))])
+            elif k == 3:
+                seq.append(["uniform", 21000.0, 100000.0, float(rs.uniform(21000, 100000))])
+            elif k == 4:
+                seq.append(["randint", 20, 50, int(rs.randint(20, 50))])
+            elif k == 5:
+                seq.append(["randint", 0, 2, int(rs.randint(0, 2))])
+            elif k == 6:
+                seq.append(["rand", 0, 0, float(rs.rand())])
+            else:
+                seq.append(["randint", 0, 1, int(rs.randint(0, 1))])
+        d["mixed"] = seq
+        out[str(seed)] = d
+    with open(path, "w") as f:
+        json.dump(out, f)
+
+
+def main():
+    if sys.argv[1] == "run":
+        run_config(sys.argv[2], int(sys.argv[3]), sys.argv[4], "--full" in sys.argv)
+        return
+    assert sys.argv[1] == "all"
+    rng_kats(os.path.join(HERE, "rng_kats.json"))
+    jobs = [("sparse_zi_100", 123456789, True), ("rmsc03", 123456789, False),
+            ("rmsc03", 1008, True), ("rmsc03", 7, False), ("sparse_zi_1000", 123456789, False)]
+    if len(sys.argv) > 2:
+        jobs = [j for j in jobs if j[0] == sys.argv[2]]
+    procs = []
+    for cfg, seed, full in jobs:
+        out = os.path.join(HERE, "%s_%d" % (cfg, seed))
+        cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out] + (["--full"] if full else [])
+        wd = tempfile.mkdtemp(prefix="gf_")
+        procs.append((cfg, seed, subprocess.Popen(cmd, cwd=wd, env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))))
+    for cfg, seed, p in procs:
+        rc = p.wait()
+        print(cfg, seed, "rc", rc)
+
+
+if __name__ == "__main__":
+    main()
