@@ -1,0 +1,1658 @@
+/* abides_oracle.c — CPU restatement (parity oracle) of the reference ABIDES hot path.
+ * TEST INFRASTRUCTURE ONLY — see abides_oracle.h for scope and the reference map.
+ *
+ * Structure intentionally mirrors the reference's Python objects (heap of events,
+ * per-side lists of price levels each holding a FIFO list of orders, per-agent
+ * ordered dict of open orders, history epochs) so that each function can be read
+ * side by side with the cited reference lines.  Transcendentals call the host libm
+ * (glibc), which is the libm the reference's numpy/math calls resolve to.
+ */
+#define _GNU_SOURCE
+#include "abides_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* ------------------------------------------------------------------------- */
+/* numpy legacy RandomState (numpy/random/src/mt19937, distributions/legacy)  */
+/* ------------------------------------------------------------------------- */
+#define MT_N 624
+#define MT_M 397
+struct ora_rs {
+    uint32_t key[MT_N];
+    int pos;
+    int has_gauss;
+    double gauss;
+};
+
+/* mt19937_seed == init_genrand (numpy _legacy_seeding with an int seed) */
+static void rs_seed(ora_rs* r, uint32_t s) {
+    for (int i = 0; i < MT_N; i++) {
+        r->key[i] = s;
+        s = (uint32_t)(1812433253u * (s ^ (s >> 30)) + (uint32_t)i + 1u);
+    }
+    r->pos = MT_N;
+    r->has_gauss = 0;
+    r->gauss = 0.0;
+}
+
+static void mt_gen(ora_rs* r) {
+    uint32_t y;
+    int i;
+    for (i = 0; i < MT_N - MT_M; i++) {
+        y = (r->key[i] & 0x80000000u) | (r->key[i + 1] & 0x7fffffffu);
+        r->key[i] = r->key[i + MT_M] ^ (y >> 1) ^ (-(y & 1u) & 0x9908b0dfu);
+    }
+    for (; i < MT_N - 1; i++) {
+        y = (r->key[i] & 0x80000000u) | (r->key[i + 1] & 0x7fffffffu);
+        r->key[i] = r->key[i + (MT_M - MT_N)] ^ (y >> 1) ^ (-(y & 1u) & 0x9908b0dfu);
+    }
+    y = (r->key[MT_N - 1] & 0x80000000u) | (r->key[0] & 0x7fffffffu);
+    r->key[MT_N - 1] = r->key[MT_M - 1] ^ (y >> 1) ^ (-(y & 1u) & 0x9908b0dfu);
+    r->pos = 0;
+}
+
+static uint32_t rs_u32(ora_rs* r) {
+    if (r->pos == MT_N) mt_gen(r);
+    uint32_t y = r->key[r->pos++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+/* mt19937_next_double: 53-bit (a>>5, b>>6) */
+static double rs_double(ora_rs* r) {
+    int32_t a = (int32_t)(rs_u32(r) >> 5), b = (int32_t)(rs_u32(r) >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+/* RandomState.randint(lo, hi) (legacy, masked rejection on 32-bit draws);
+ * rng == 0 consumes nothing (random_bounded_uint64_fill) */
+static int64_t rs_randint(ora_rs* r, int64_t lo, int64_t hi) {
+    uint64_t rng = (uint64_t)(hi - lo - 1);
+    if (rng == 0) return lo;
+    if (rng == 0xFFFFFFFFull) return lo + (int64_t)rs_u32(r);
+    uint32_t mask = (uint32_t)rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    while ((v = (rs_u32(r) & mask)) > (uint32_t)rng) {
+    }
+    return lo + (int64_t)v;
+}
+
+/* legacy_gauss: polar method with cached second value */
+static double rs_gauss(ora_rs* r) {
+    if (r->has_gauss) {
+        double t = r->gauss;
+        r->has_gauss = 0;
+        r->gauss = 0.0;
+        return t;
+    }
+    double f, x1, x2, r2;
+    do {
+        x1 = 2.0 * rs_double(r) - 1.0;
+        x2 = 2.0 * rs_double(r) - 1.0;
+        r2 = x1 * x1 + x2 * x2;
+    } while (r2 >= 1.0 || r2 == 0.0);
+    f = sqrt(-2.0 * log(r2) / r2);
+    r->gauss = f * x1;
+    r->has_gauss = 1;
+    return f * x2;
+}
+static double rs_normal(ora_rs* r, double loc, double scale) { return loc + scale * rs_gauss(r); }
+static double rs_exponential(ora_rs* r, double scale) { return scale * -log(1.0 - rs_double(r)); }
+static double rs_uniform(ora_rs* r, double lo, double hi) { return lo + (hi - lo) * rs_double(r); }
+
+ora_rs* ora_rs_new(uint32_t seed) {
+    ora_rs* r = (ora_rs*)malloc(sizeof(ora_rs));
+    rs_seed(r, seed);
+    return r;
+}
+void ora_rs_free(ora_rs* r) { free(r); }
+uint32_t ora_rs_u32(ora_rs* r) { return rs_u32(r); }
+double ora_rs_double(ora_rs* r) { return rs_double(r); }
+int64_t ora_rs_randint(ora_rs* r, int64_t lo, int64_t hi) { return rs_randint(r, lo, hi); }
+double ora_rs_normal(ora_rs* r, double loc, double scale) { return rs_normal(r, loc, scale); }
+double ora_rs_exponential(ora_rs* r, double scale) { return rs_exponential(r, scale); }
+double ora_rs_uniform(ora_rs* r, double lo, double hi) { return rs_uniform(r, lo, hi); }
+
+/* Python round(float) -> int : half-to-even (default FE_TONEAREST rint) */
+static int64_t py_round(double x) { return (int64_t)rint(x); }
+
+/* ------------------------------------------------------------------------- */
+/* message kinds / trace record (tests/golden/gen_fixtures.py KIND)           */
+/* ------------------------------------------------------------------------- */
+enum {
+    K_WAKEUP = 0, K_WHEN_OPEN_REQ = 1, K_WHEN_CLOSE_REQ = 2, K_WHEN_OPEN = 3, K_WHEN_CLOSE = 4,
+    K_SPREAD_REQ = 5, K_SPREAD = 6, K_LAST_REQ = 7, K_LAST = 8, K_TV_REQ = 9, K_TV = 10,
+    K_LIMIT = 11, K_CANCEL = 12, K_MODIFY = 13, K_ACCEPTED = 14, K_EXECUTED = 15, K_CANCELLED = 16,
+    K_MKT_CLOSED = 17, K_MODIFIED = 18, K_KCANCEL = 19, K_MARKET_DATA = 20
+};
+enum { T_MESSAGE = 1, T_WAKEUP = 2, T_CANCEL_ORDER = 3 };
+
+typedef struct {
+    int kind;
+    int32_t sender;
+    /* order payload */
+    int64_t oid;
+    int32_t oagent;
+    int is_buy;
+    int64_t qty, price, fill;
+    /* query payload */
+    int64_t data;
+    int data_float; /* reference returned a python float (daily open price) */
+    int has_data;
+    int depth, mkt_closed;
+    int nb, na;
+    int64_t bpx, bq, apx, aq;
+    int64_t lookback;
+} msg_t;
+
+typedef struct {
+    int64_t t;
+    int32_t rcp, type;
+    uint64_t seq;
+    int32_t mi;
+} ev_t;
+
+/* ------------------------------------------------------------------------- */
+/* order book (util/OrderBook.py)                                             */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    int64_t id;
+    int32_t agent;
+    int is_buy;
+    int64_t qty, price;
+} bord_t;
+typedef struct {
+    bord_t* o;
+    int n, cap;
+} level_t;
+typedef struct {
+    level_t* lv;
+    int n, cap;
+} side_t;
+typedef struct {
+    int64_t t, q;
+} txn_t;
+typedef struct {
+    int64_t oid;
+    txn_t* tx;
+    int ntx, captx;
+} hent_t;
+typedef struct {
+    hent_t* e;
+    int n, cap;
+} epoch_t;
+
+/* ------------------------------------------------------------------------- */
+/* agents                                                                     */
+/* ------------------------------------------------------------------------- */
+enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM };
+enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE };
+
+typedef struct {
+    int64_t id;
+    int is_buy;
+    int64_t qty, price;
+} aord_t;
+
+typedef struct {
+    int id, type;
+    char name[96], tname[96];
+    ora_rs rs;
+    int64_t cur_time;
+    /* TradingAgent */
+    int has_open, has_close, mkt_closed, first_wake, has_daily_close, trading;
+    int64_t mkt_open, mkt_close;
+    int64_t starting_cash, cash, shares;
+    aord_t* ord;
+    int nord, capord;
+    int has_last_trade, last_trade_float;
+    int64_t last_trade;
+    int has_known, nb, na;
+    int64_t bid, bidq, ask, askq;
+    int64_t tv;
+    int state;
+    /* ZI / Value */
+    double sigma_n, r_bar, kappa, sigma_s, lambda_a, eta;
+    int q_max;
+    int64_t R_min, R_max;
+    int64_t theta[20];
+    double r_t, sigma_t;
+    int has_prev_wake;
+    int64_t prev_wake;
+    int64_t size;
+    /* Noise */
+    int64_t wakeup_time;
+    /* POV market maker */
+    double pov;
+    int64_t min_size, window, num_ticks, wake_freq, order_size;
+    int aw_spread, aw_tv, has_last_mid;
+    int64_t last_mid;
+    /* Momentum */
+    int64_t* mids2;
+    int nmid, capmid, n20, n50;
+    double avg20, avg50;
+} agent_t;
+
+struct ora_env {
+    char config[32];
+    int n;
+    agent_t* ag;
+    /* exchange (agent 0) */
+    int64_t ex_open, ex_close, ex_pipeline, ex_comp;
+    int stream_history;
+    side_t book[2]; /* 0 bids, 1 asks */
+    int64_t last_trade;
+    int last_trade_float;
+    epoch_t hist[16];
+    int nhist;
+    /* SparseMeanRevertingOracle (one symbol) */
+    ora_rs O;
+    double o_rbar, o_kappa, o_fundvol, o_lambda, o_msmean, o_msvar;
+    int64_t o_open, o_close, o_pt, o_mst;
+    double o_pv, o_msv;
+    /* global / kernel / latency RNGs */
+    ora_rs G, K, L;
+    /* kernel */
+    int64_t start, stop, cur;
+    int have_cur;
+    int64_t* agent_time;
+    int64_t* comp_delay;
+    int64_t add_delay;
+    int lat_mode; /* 0 zero, 1 matrix + noise, 2 cubic model */
+    double* lat;  /* n*n */
+    int noise_len;
+    double jitter, clip, unit;
+    ev_t* heap;
+    int nheap, capheap;
+    msg_t* msgs;
+    int* freem;
+    int nfree, capmsg, nmsg;
+    uint64_t seq;
+    int64_t pops;
+    uint64_t hash;
+    int64_t* trace;
+    int64_t trace_cap, trace_len;
+    int done, err;
+    char errstr[160];
+    int64_t order_counter;
+    char* report;
+    int64_t report_len;
+};
+
+#define NS_SEC 1000000000LL
+#define NS_MIN (60LL * NS_SEC)
+#define NS_HOUR (3600LL * NS_SEC)
+#define FNV_OFF 0xCBF29CE484222325ull
+#define FNV_PRIME 0x100000001B3ull
+
+static void fail(ora_env* e, int code, const char* s) {
+    if (!e->err) {
+        e->err = code;
+        snprintf(e->errstr, sizeof e->errstr, "%s", s);
+    }
+    e->done = 1;
+}
+
+/* ---------------------------- event heap ---------------------------------- */
+static int ev_less(const ev_t* a, const ev_t* b) {
+    if (a->t != b->t) return a->t < b->t;
+    if (a->rcp != b->rcp) return a->rcp < b->rcp;
+    if (a->type != b->type) return a->type < b->type;
+    return a->seq < b->seq;
+}
+static void heap_push(ora_env* e, ev_t v) {
+    if (e->nheap == e->capheap) {
+        e->capheap = e->capheap ? 2 * e->capheap : 256;
+        e->heap = (ev_t*)realloc(e->heap, sizeof(ev_t) * e->capheap);
+    }
+    int i = e->nheap++;
+    while (i > 0) {
+        int p = (i - 1) >> 1;
+        if (!ev_less(&v, &e->heap[p])) break;
+        e->heap[i] = e->heap[p];
+        i = p;
+    }
+    e->heap[i] = v;
+}
+static ev_t heap_pop(ora_env* e) {
+    ev_t top = e->heap[0];
+    ev_t last = e->heap[--e->nheap];
+    int i = 0, n = e->nheap;
+    for (;;) {
+        int l = 2 * i + 1, r = l + 1, m = i;
+        const ev_t* best = &last;
+        if (l < n && ev_less(&e->heap[l], best)) { m = l; best = &e->heap[l]; }
+        if (r < n && ev_less(&e->heap[r], best)) { m = r; best = &e->heap[r]; }
+        if (m == i) break;
+        e->heap[i] = e->heap[m];
+        i = m;
+    }
+    if (n > 0) e->heap[i] = last;
+    return top;
+}
+static int msg_alloc(ora_env* e) {
+    if (e->nfree) return e->freem[--e->nfree];
+    if (e->nmsg == e->capmsg) {
+        e->capmsg = e->capmsg ? 2 * e->capmsg : 256;
+        e->msgs = (msg_t*)realloc(e->msgs, sizeof(msg_t) * e->capmsg);
+        e->freem = (int*)realloc(e->freem, sizeof(int) * e->capmsg);
+    }
+    return e->nmsg++;
+}
+static void msg_free(ora_env* e, int mi) { e->freem[e->nfree++] = mi; }
+
+/* ---------------------------- kernel services ----------------------------- */
+/* LatencyModel.get_latency, cubic (model/LatencyModel.py:119-140) */
+static double get_latency(ora_env* e, int s, int r) {
+    double x = rs_uniform(&e->L, e->clip, 1.0);
+    double m = e->lat[(size_t)s * e->n + r];
+    return m + ((e->jitter / pow(x, 3.0)) * (m / e->unit));
+}
+
+/* Kernel.sendMessage (Kernel.py:347-425) */
+static void k_send(ora_env* e, int sender, int recipient, const msg_t* m, int64_t delay) {
+    int64_t sent = e->cur + e->comp_delay[sender] + e->add_delay + delay;
+    int64_t deliver;
+    if (e->lat_mode == 2) {
+        double lat = get_latency(e, sender, recipient);
+        deliver = sent + (int64_t)lat; /* pd.Timedelta(float) truncates */
+    } else {
+        double lat = e->lat_mode == 1 ? e->lat[(size_t)sender * e->n + recipient] : 0.0;
+        int64_t noise = e->noise_len > 1 ? rs_randint(&e->K, 0, e->noise_len) : 0; /* choice(len,1,list) */
+        deliver = sent + (int64_t)(lat + (double)noise);
+    }
+    int mi = msg_alloc(e);
+    e->msgs[mi] = *m;
+    ev_t v = {deliver, recipient, T_MESSAGE, e->seq++, mi};
+    heap_push(e, v);
+}
+
+/* Kernel.setWakeup (Kernel.py:435-462) */
+static void k_wakeup(ora_env* e, int sender, int64_t t) {
+    if (e->have_cur && t < e->cur) {
+        fail(e, -3, "setWakeup() called with requested time not in future");
+        return;
+    }
+    ev_t v = {t, sender, T_WAKEUP, e->seq++, -1};
+    heap_push(e, v);
+}
+
+/* Order.generateOrderId (util/order/Order.py:27-42): ids are consecutive per process */
+static int64_t next_order_id(ora_env* e) { return e->order_counter++; }
+
+/* --------------------------- oracle (SMRO) -------------------------------- */
+/* compute_fundamental_at_timestamp (SMRO:88-125) */
+static double o_compute(ora_env* e, int64_t ts, double v_adj, int64_t pt, double pv) {
+    int64_t d = ts - pt;
+    double mu = e->o_rbar, gamma = e->o_kappa, theta = e->o_fundvol;
+    double loc = mu + (pv - mu) * exp(-gamma * (double)d);
+    double scale = (pow(theta, 2.0) / (2 * gamma)) * (1 - exp(-2 * gamma * (double)d));
+    double v = rs_normal(&e->O, loc, scale);
+    v += v_adj;
+    if (!(v > 0)) v = 0; /* max(0, v) */
+    int64_t vi = py_round(v);
+    e->o_pt = ts;
+    e->o_pv = (double)vi;
+    return (double)vi;
+}
+/* advance_fundamental_value_series (SMRO:131-181) */
+static double o_advance(ora_env* e, int64_t t) {
+    int64_t pt = e->o_pt;
+    double pv = e->o_pv;
+    if (t <= pt) return pv;
+    while (e->o_mst < t) {
+        double v = o_compute(e, e->o_mst, e->o_msv, pt, pv);
+        pt = e->o_mst;
+        pv = v;
+        e->o_mst = pt + (int64_t)rs_exponential(&e->G, 1.0 / e->o_lambda);
+        double msv = rs_normal(&e->O, e->o_msmean, sqrt(e->o_msvar));
+        e->o_msv = rs_randint(&e->O, 0, 2) == 0 ? msv : -msv;
+    }
+    return o_compute(e, t, 0, pt, pv);
+}
+/* observePrice (SMRO:210-227) with sigma_n > 0 */
+static int64_t o_observe(ora_env* e, int64_t t, double sigma_n, ora_rs* rs) {
+    double r_t = t >= e->o_close ? o_advance(e, e->o_close - 1) : o_advance(e, t);
+    if (sigma_n == 0) return (int64_t)r_t;
+    return py_round(rs_normal(rs, r_t, sqrt(sigma_n)));
+}
+
+/* ------------------------------ trace -------------------------------------- */
+static void encode(const ora_env* e, const ev_t* v, int64_t rec[10]) {
+    memset(rec, 0, sizeof(int64_t) * 10);
+    rec[0] = v->t;
+    rec[1] = v->rcp;
+    rec[2] = v->type;
+    if (v->mi < 0) {
+        rec[3] = v->type == T_WAKEUP ? K_WAKEUP : K_KCANCEL;
+        return;
+    }
+    const msg_t* m = &e->msgs[v->mi];
+    int64_t* f = rec + 4;
+    rec[3] = m->kind;
+    switch (m->kind) {
+    case K_WHEN_OPEN_REQ: case K_WHEN_CLOSE_REQ: case K_LAST_REQ:
+        f[0] = m->sender;
+        break;
+    case K_WHEN_OPEN: case K_WHEN_CLOSE:
+        f[0] = m->data;
+        break;
+    case K_SPREAD_REQ:
+        f[0] = m->sender;
+        f[1] = m->depth;
+        break;
+    case K_SPREAD:
+        f[0] = m->nb ? m->bpx : -1;
+        f[1] = m->nb ? m->bq : 0;
+        f[2] = m->na ? m->apx : -1;
+        f[3] = m->na ? m->aq : 0;
+        f[4] = !m->has_data ? -1 : (m->data_float ? m->data * 10000 : m->data);
+        f[5] = (m->mkt_closed ? 1 : 0) + 2 * (int64_t)m->nb + ((int64_t)1 << 20) * m->na;
+        break;
+    case K_LAST:
+        f[0] = !m->has_data ? -1 : (m->data_float ? m->data * 10000 : m->data);
+        f[5] = m->mkt_closed ? 1 : 0;
+        break;
+    case K_TV_REQ:
+        f[0] = m->sender;
+        f[1] = m->lookback;
+        break;
+    case K_TV:
+        f[0] = m->data;
+        f[5] = m->mkt_closed ? 1 : 0;
+        break;
+    case K_LIMIT: case K_ACCEPTED: case K_CANCELLED: case K_MODIFY: case K_MODIFIED:
+        f[0] = m->oid; f[1] = m->oagent; f[2] = m->is_buy; f[3] = m->qty; f[4] = m->price;
+        break;
+    case K_CANCEL:
+        f[0] = m->oid; f[1] = m->oagent; f[2] = m->is_buy; f[3] = 0; f[4] = m->price;
+        break;
+    case K_EXECUTED:
+        f[0] = m->oid; f[1] = m->oagent; f[2] = m->is_buy; f[3] = m->qty; f[4] = m->price; f[5] = m->fill;
+        break;
+    default:
+        break;
+    }
+}
+
+/* ------------------------------ order book --------------------------------- */
+static void level_remove(level_t* L, int i) {
+    memmove(L->o + i, L->o + i + 1, sizeof(bord_t) * (L->n - i - 1));
+    L->n--;
+}
+static void level_append(level_t* L, bord_t o) {
+    if (L->n == L->cap) {
+        L->cap = L->cap ? 2 * L->cap : 4;
+        L->o = (bord_t*)realloc(L->o, sizeof(bord_t) * L->cap);
+    }
+    L->o[L->n++] = o;
+}
+static void side_delete_level(side_t* S, int i) {
+    free(S->lv[i].o);
+    memmove(S->lv + i, S->lv + i + 1, sizeof(level_t) * (S->n - i - 1));
+    S->n--;
+}
+static void side_insert_level(side_t* S, int i, bord_t o) {
+    if (S->n == S->cap) {
+        S->cap = S->cap ? 2 * S->cap : 16;
+        S->lv = (level_t*)realloc(S->lv, sizeof(level_t) * S->cap);
+    }
+    memmove(S->lv + i + 1, S->lv + i, sizeof(level_t) * (S->n - i));
+    S->n++;
+    level_t L = {0, 0, 0};
+    level_append(&L, o);
+    S->lv[i] = L;
+}
+static int is_better(const bord_t* a, const bord_t* b) {
+    return a->is_buy ? (a->price > b->price) : (a->price < b->price);
+}
+
+/* history: epochs of {order_id -> transactions} (OrderBook.py:33, 51-60, 146-149) */
+static hent_t* hist_find(epoch_t* ep, int64_t oid) {
+    for (int i = 0; i < ep->n; i++)
+        if (ep->e[i].oid == oid) return &ep->e[i];
+    return NULL;
+}
+static void hist_add_order(ora_env* e, int64_t oid) {
+    epoch_t* ep = &e->hist[0];
+    hent_t* h = hist_find(ep, oid);
+    if (h) { /* dict re-assignment keeps position, resets value */
+        h->ntx = 0;
+        return;
+    }
+    if (ep->n == ep->cap) {
+        ep->cap = ep->cap ? 2 * ep->cap : 16;
+        ep->e = (hent_t*)realloc(ep->e, sizeof(hent_t) * ep->cap);
+    }
+    hent_t n0 = {oid, NULL, 0, 0};
+    ep->e[ep->n++] = n0;
+}
+static void hent_add_tx(hent_t* h, int64_t t, int64_t q) {
+    if (h->ntx == h->captx) {
+        h->captx = h->captx ? 2 * h->captx : 2;
+        h->tx = (txn_t*)realloc(h->tx, sizeof(txn_t) * h->captx);
+    }
+    txn_t x = {t, q};
+    h->tx[h->ntx++] = x;
+}
+static void epoch_free(epoch_t* ep) {
+    for (int i = 0; i < ep->n; i++) free(ep->e[i].tx);
+    free(ep->e);
+    ep->e = NULL;
+    ep->n = ep->cap = 0;
+}
+static void hist_shift(ora_env* e) {
+    /* history.insert(0, {}); history = history[:stream_history + 1] */
+    int keep = e->stream_history + 1;
+    if (e->nhist >= keep) {
+        for (int i = keep - 1; i < e->nhist; i++) epoch_free(&e->hist[i]);
+        e->nhist = keep - 1;
+    }
+    memmove(e->hist + 1, e->hist, sizeof(epoch_t) * e->nhist);
+    memset(&e->hist[0], 0, sizeof(epoch_t));
+    e->nhist++;
+}
+
+static void ex_send(ora_env* e, int recipient, msg_t* m) {
+    /* ExchangeAgent.sendMessage: order-book notifications carry the pipeline delay */
+    int64_t d = (m->kind == K_ACCEPTED || m->kind == K_CANCELLED || m->kind == K_EXECUTED) ? e->ex_pipeline : 0;
+    k_send(e, 0, recipient, m, d);
+}
+
+static void order_msg(msg_t* m, int kind, const bord_t* o) {
+    memset(m, 0, sizeof *m);
+    m->kind = kind;
+    m->oid = o->id;
+    m->oagent = o->agent;
+    m->is_buy = o->is_buy;
+    m->qty = o->qty;
+    m->price = o->price;
+    m->fill = -1;
+}
+
+/* executeOrder (OrderBook.py:172-240); returns 1 and fills *matched if a match happened */
+static int execute_order(ora_env* e, bord_t* order, bord_t* matched) {
+    side_t* book = &e->book[order->is_buy ? 1 : 0];
+    if (book->n == 0) return 0;
+    bord_t* head = &book->lv[0].o[0];
+    int match = order->is_buy ? (order->price >= head->price) : (order->price <= head->price);
+    if (!match) return 0;
+    if (order->qty >= head->qty) {
+        *matched = *head;
+        level_remove(&book->lv[0], 0);
+        if (book->lv[0].n == 0) side_delete_level(book, 0);
+    } else {
+        *matched = *head;
+        matched->qty = order->qty;
+        head->qty -= matched->qty;
+    }
+    /* history[0][order.order_id]['transactions'].append((t, order.quantity)) */
+    hent_t* h = hist_find(&e->hist[0], order->id);
+    if (h) hent_add_tx(h, e->cur, order->qty);
+    for (int i = 0; i < e->nhist; i++) {
+        hent_t* hm = hist_find(&e->hist[i], matched->id);
+        if (hm) hent_add_tx(hm, e->cur, matched->qty);
+    }
+    return 1;
+}
+
+/* enterOrder (OrderBook.py:256-282) */
+static void enter_order(ora_env* e, bord_t o) {
+    side_t* book = &e->book[o.is_buy ? 0 : 1];
+    if (book->n == 0) {
+        side_insert_level(book, 0, o);
+        return;
+    }
+    bord_t* last = &book->lv[book->n - 1].o[0];
+    if (!is_better(&o, last) && o.price != last->price) {
+        side_insert_level(book, book->n, o);
+        return;
+    }
+    for (int i = 0; i < book->n; i++) {
+        bord_t* h = &book->lv[i].o[0];
+        if (is_better(&o, h)) {
+            side_insert_level(book, i, o);
+            return;
+        }
+        if (o.price == h->price) {
+            level_append(&book->lv[i], o);
+            return;
+        }
+    }
+}
+
+/* handleLimitOrder (OrderBook.py:38-170) */
+static void handle_limit_order(ora_env* e, bord_t order) {
+    if (order.qty <= 0) return;
+    hist_add_order(e, order.id);
+    int64_t ex_q = 0, ex_pq = 0;
+    int executed = 0;
+    for (;;) {
+        bord_t matched;
+        if (execute_order(e, &order, &matched)) {
+            bord_t filled = order;
+            filled.qty = matched.qty;
+            order.qty -= filled.qty;
+            msg_t m;
+            order_msg(&m, K_EXECUTED, &filled);
+            m.fill = matched.price;
+            ex_send(e, order.agent, &m);
+            order_msg(&m, K_EXECUTED, &matched);
+            m.fill = matched.price;
+            ex_send(e, matched.agent, &m);
+            ex_q += filled.qty;
+            ex_pq += matched.price * filled.qty;
+            executed = 1;
+            if (order.qty <= 0) break;
+        } else {
+            enter_order(e, order);
+            msg_t m;
+            order_msg(&m, K_ACCEPTED, &order);
+            ex_send(e, order.agent, &m);
+            break;
+        }
+    }
+    if (executed) {
+        e->last_trade = py_round((double)ex_pq / (double)ex_q);
+        e->last_trade_float = 0;
+        hist_shift(e);
+    }
+}
+
+/* cancelOrder (OrderBook.py:284-339) */
+static void cancel_order(ora_env* e, const msg_t* req) {
+    side_t* book = &e->book[req->is_buy ? 0 : 1];
+    for (int i = 0; i < book->n; i++) {
+        level_t* L = &book->lv[i];
+        if (L->o[0].price != req->price) continue;
+        for (int j = 0; j < L->n; j++) {
+            if (L->o[j].id == req->oid) {
+                bord_t c = L->o[j];
+                level_remove(L, j);
+                if (L->n == 0) side_delete_level(book, i);
+                msg_t m;
+                order_msg(&m, K_CANCELLED, &c);
+                ex_send(e, req->oagent, &m);
+                return;
+            }
+        }
+    }
+}
+
+/* get_transacted_volume (OrderBook.py:400-436), restated: distinct (t, qty) pairs of
+ * all transaction records in the retained history with t >= now - lookback. */
+static int cmp_txn(const void* a, const void* b) {
+    const txn_t *x = (const txn_t*)a, *y = (const txn_t*)b;
+    if (x->t != y->t) return x->t < y->t ? -1 : 1;
+    if (x->q != y->q) return x->q < y->q ? -1 : 1;
+    return 0;
+}
+static int64_t transacted_volume(ora_env* e, int64_t lookback, int* err) {
+    int entries = 0, ntx = 0;
+    for (int i = 0; i < e->nhist; i++) {
+        entries += e->hist[i].n;
+        for (int j = 0; j < e->hist[i].n; j++) ntx += e->hist[i].e[j].ntx;
+    }
+    if (entries == 0) return 0;
+    if (ntx == 0) { /* pandas raises AttributeError here (no transaction records) */
+        *err = 1;
+        return 0;
+    }
+    txn_t* all = (txn_t*)malloc(sizeof(txn_t) * ntx);
+    int k = 0;
+    for (int i = 0; i < e->nhist; i++)
+        for (int j = 0; j < e->hist[i].n; j++)
+            for (int t = 0; t < e->hist[i].e[j].ntx; t++) all[k++] = e->hist[i].e[j].tx[t];
+    qsort(all, ntx, sizeof(txn_t), cmp_txn);
+    int64_t start = e->cur - lookback, vol = 0;
+    for (int i = 0; i < ntx; i++) {
+        if (i > 0 && cmp_txn(&all[i], &all[i - 1]) == 0) continue;
+        if (all[i].t >= start) vol += all[i].q;
+    }
+    free(all);
+    return vol;
+}
+
+/* ExchangeAgent.receiveMessage (ExchangeAgent.py:129-340) */
+static void ex_receive(ora_env* e, const msg_t* m) {
+    e->comp_delay[0] = e->ex_comp;
+    int closed = e->cur > e->ex_close;
+    msg_t r;
+    memset(&r, 0, sizeof r);
+    if (closed) {
+        if (m->kind == K_LIMIT || m->kind == K_CANCEL || m->kind == K_MODIFY) {
+            r.kind = K_MKT_CLOSED;
+            ex_send(e, m->sender, &r);
+            return;
+        } else if (m->kind == K_SPREAD_REQ || m->kind == K_LAST_REQ || m->kind == K_TV_REQ) {
+        } else {
+            r.kind = K_MKT_CLOSED;
+            ex_send(e, m->sender, &r);
+            return;
+        }
+    }
+    switch (m->kind) {
+    case K_WHEN_OPEN_REQ:
+    case K_WHEN_CLOSE_REQ:
+        e->comp_delay[0] = 0;
+        r.kind = m->kind == K_WHEN_OPEN_REQ ? K_WHEN_OPEN : K_WHEN_CLOSE;
+        r.data = m->kind == K_WHEN_OPEN_REQ ? e->ex_open : e->ex_close;
+        r.has_data = 1;
+        ex_send(e, m->sender, &r);
+        break;
+    case K_LAST_REQ:
+        r.kind = K_LAST;
+        r.data = e->last_trade;
+        r.data_float = e->last_trade_float;
+        r.has_data = 1;
+        r.mkt_closed = closed;
+        ex_send(e, m->sender, &r);
+        break;
+    case K_SPREAD_REQ: {
+        r.kind = K_SPREAD;
+        r.depth = m->depth;
+        side_t* b = &e->book[0];
+        side_t* a = &e->book[1];
+        r.nb = b->n < m->depth ? b->n : m->depth;
+        r.na = a->n < m->depth ? a->n : m->depth;
+        if (r.nb) {
+            r.bpx = b->lv[0].o[0].price;
+            for (int j = 0; j < b->lv[0].n; j++) r.bq += b->lv[0].o[j].qty;
+        }
+        if (r.na) {
+            r.apx = a->lv[0].o[0].price;
+            for (int j = 0; j < a->lv[0].n; j++) r.aq += a->lv[0].o[j].qty;
+        }
+        r.data = e->last_trade;
+        r.data_float = e->last_trade_float;
+        r.has_data = 1;
+        r.mkt_closed = closed;
+        ex_send(e, m->sender, &r);
+        break;
+    }
+    case K_TV_REQ: {
+        int perr = 0;
+        int64_t vol = transacted_volume(e, m->lookback, &perr);
+        if (perr) {
+            fail(e, -5, "get_transacted_volume: no transaction records (pandas AttributeError)");
+            return;
+        }
+        r.kind = K_TV;
+        r.data = vol;
+        r.has_data = 1;
+        r.mkt_closed = closed;
+        ex_send(e, m->sender, &r);
+        break;
+    }
+    case K_LIMIT: {
+        bord_t o = {m->oid, m->oagent, m->is_buy, m->qty, m->price};
+        handle_limit_order(e, o);
+        break;
+    }
+    case K_CANCEL:
+        cancel_order(e, m);
+        break;
+    default:
+        break;
+    }
+}
+
+/* --------------------------- TradingAgent --------------------------------- */
+static void ta_send_ex(ora_env* e, agent_t* a, msg_t* m) {
+    m->sender = a->id;
+    k_send(e, a->id, 0, m, 0);
+}
+static void get_spread(ora_env* e, agent_t* a, int depth) {
+    msg_t m;
+    memset(&m, 0, sizeof m);
+    m.kind = K_SPREAD_REQ;
+    m.depth = depth;
+    ta_send_ex(e, a, &m);
+}
+static void get_tv(ora_env* e, agent_t* a, int64_t lookback) {
+    msg_t m;
+    memset(&m, 0, sizeof m);
+    m.kind = K_TV_REQ;
+    m.lookback = lookback;
+    ta_send_ex(e, a, &m);
+}
+/* placeLimitOrder (TradingAgent.py:309-349) */
+static void place_limit(ora_env* e, agent_t* a, int64_t qty, int is_buy, int64_t price) {
+    int64_t oid = next_order_id(e);
+    if (qty > 0) {
+        if (a->nord == a->capord) {
+            a->capord = a->capord ? 2 * a->capord : 8;
+            a->ord = (aord_t*)realloc(a->ord, sizeof(aord_t) * a->capord);
+        }
+        aord_t o = {oid, is_buy, qty, price};
+        a->ord[a->nord++] = o;
+        msg_t m;
+        memset(&m, 0, sizeof m);
+        m.kind = K_LIMIT;
+        m.oid = oid;
+        m.oagent = a->id;
+        m.is_buy = is_buy;
+        m.qty = qty;
+        m.price = price;
+        m.fill = -1;
+        ta_send_ex(e, a, &m);
+    }
+}
+/* cancelOrder for every open order, dict insertion order */
+static void cancel_all(ora_env* e, agent_t* a) {
+    for (int i = 0; i < a->nord; i++) {
+        msg_t m;
+        memset(&m, 0, sizeof m);
+        m.kind = K_CANCEL;
+        m.oid = a->ord[i].id;
+        m.oagent = a->id;
+        m.is_buy = a->ord[i].is_buy;
+        m.qty = a->ord[i].qty;
+        m.price = a->ord[i].price;
+        m.fill = -1;
+        ta_send_ex(e, a, &m);
+    }
+}
+static int find_ord(agent_t* a, int64_t oid) {
+    for (int i = 0; i < a->nord; i++)
+        if (a->ord[i].id == oid) return i;
+    return -1;
+}
+static void del_ord(agent_t* a, int i) {
+    memmove(a->ord + i, a->ord + i + 1, sizeof(aord_t) * (a->nord - i - 1));
+    a->nord--;
+}
+
+/* TradingAgent.wakeup (TradingAgent.py:142-158); returns "ready to trade" */
+static int ta_wakeup(ora_env* e, agent_t* a) {
+    a->cur_time = e->cur;
+    if (a->first_wake) a->first_wake = 0;
+    if (!a->has_open) {
+        msg_t m;
+        memset(&m, 0, sizeof m);
+        m.kind = K_WHEN_OPEN_REQ;
+        ta_send_ex(e, a, &m);
+        m.kind = K_WHEN_CLOSE_REQ;
+        ta_send_ex(e, a, &m);
+    }
+    return (a->has_open && a->has_close) && !a->mkt_closed;
+}
+
+static int64_t wake_frequency(agent_t* a) {
+    switch (a->type) {
+    case AG_POVMM: return a->wake_freq;
+    case AG_MOMENTUM: return a->wake_freq;
+    default: return rs_randint(&a->rs, 0, 100);
+    }
+}
+
+static void query_last_trade(agent_t* a, const msg_t* m) {
+    a->has_last_trade = 1;
+    a->last_trade = m->data;
+    a->last_trade_float = m->data_float;
+    if (a->mkt_closed) a->has_daily_close = 1;
+}
+
+/* TradingAgent.receiveMessage (TradingAgent.py:181-268) */
+static void ta_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    a->cur_time = e->cur;
+    int had = a->has_open && a->has_close;
+    switch (m->kind) {
+    case K_WHEN_OPEN: a->mkt_open = m->data; a->has_open = 1; break;
+    case K_WHEN_CLOSE: a->mkt_close = m->data; a->has_close = 1; break;
+    case K_EXECUTED: { /* orderExecuted (TradingAgent.py:422-462) */
+        int64_t q = m->is_buy ? m->qty : -m->qty;
+        a->shares += q;
+        a->cash -= q * m->fill;
+        int i = find_ord(a, m->oid);
+        if (i >= 0) {
+            if (m->qty >= a->ord[i].qty) del_ord(a, i);
+            else a->ord[i].qty -= m->qty;
+        }
+        break;
+    }
+    case K_ACCEPTED: break;
+    case K_CANCELLED: {
+        int i = find_ord(a, m->oid);
+        if (i >= 0) del_ord(a, i);
+        break;
+    }
+    case K_MKT_CLOSED: a->mkt_closed = 1; break;
+    case K_LAST:
+        if (m->mkt_closed) a->mkt_closed = 1;
+        query_last_trade(a, m);
+        break;
+    case K_SPREAD:
+        if (m->mkt_closed) a->mkt_closed = 1;
+        query_last_trade(a, m);
+        a->has_known = 1;
+        a->nb = m->nb;
+        a->na = m->na;
+        a->bid = m->bpx;
+        a->bidq = m->bq;
+        a->ask = m->apx;
+        a->askq = m->aq;
+        break;
+    case K_TV:
+        if (m->mkt_closed) a->mkt_closed = 1;
+        a->tv = m->data;
+        break;
+    default: break;
+    }
+    int have = a->has_open && a->has_close;
+    if (have && !had) {
+        int64_t off = wake_frequency(a);
+        k_wakeup(e, a->id, a->mkt_open + off);
+    }
+}
+
+/* Bayesian fundamental estimate shared by ZI (ZI.py:215-263) and Value (ValueAgent.py:153-201) */
+static int64_t bayes_r_T(ora_env* e, agent_t* a, int64_t obs_t) {
+    if (!a->has_prev_wake) {
+        a->has_prev_wake = 1;
+        a->prev_wake = a->mkt_open;
+    }
+    double delta = (double)(e->cur - a->prev_wake);
+    double c = 1 - a->kappa;
+    double r_tprime = (1 - pow(c, delta)) * a->r_bar;
+    r_tprime += pow(c, delta) * a->r_t;
+    double sigma_tprime = pow(c, 2 * delta) * a->sigma_t;
+    sigma_tprime += ((1 - pow(c, 2 * delta)) / (1 - pow(c, 2.0))) * a->sigma_s;
+    a->r_t = (a->sigma_n / (a->sigma_n + sigma_tprime)) * r_tprime;
+    a->r_t += (sigma_tprime / (a->sigma_n + sigma_tprime)) * (double)obs_t;
+    a->sigma_t = (a->sigma_n * a->sigma_t) / (a->sigma_n + a->sigma_t);
+    double d2 = (double)(a->mkt_close - e->cur);
+    if (!(d2 > 0)) d2 = 0;
+    double r_T = (1 - pow(c, d2)) * a->r_bar;
+    r_T += pow(c, d2) * a->r_t;
+    a->prev_wake = e->cur;
+    return py_round(r_T);
+}
+
+/* --------------------------- ZeroIntelligenceAgent -------------------------- */
+static void zi_wakeup(ora_env* e, agent_t* a) {
+    ta_wakeup(e, a);
+    a->state = ST_INACTIVE;
+    if (!a->has_open || !a->has_close) return;
+    a->trading = 1;
+    if (a->mkt_closed && a->has_daily_close) return;
+    double dt = rs_exponential(&a->rs, 1.0 / a->lambda_a);
+    k_wakeup(e, a->id, e->cur + py_round(dt));
+    if (a->mkt_closed && !a->has_daily_close) {
+        get_spread(e, a, 1);
+        a->state = ST_AWAITING_SPREAD;
+        return;
+    }
+    cancel_all(e, a);
+    get_spread(e, a, 1);
+    a->state = ST_AWAITING_SPREAD;
+}
+static void zi_place(ora_env* e, agent_t* a) {
+    /* updateEstimates (ZI.py:189-275) */
+    int64_t obs = o_observe(e, e->cur, a->sigma_n, &a->rs);
+    int64_t q = (int64_t)((double)a->shares / 100); /* int(h / 100): truncation */
+    int buy;
+    if (q >= a->q_max) buy = 0;
+    else if (q <= -a->q_max) buy = 1;
+    else buy = (int)rs_randint(&a->rs, 0, 2);
+    int64_t r_T = bayes_r_T(e, a, obs);
+    q += a->q_max - 1;
+    int64_t idx = buy ? q + 1 : q;
+    if (idx < 0) idx += 20; /* python negative index */
+    if (idx < 0 || idx >= 20) {
+        fail(e, -6, "ZeroIntelligenceAgent theta index out of range (IndexError)");
+        return;
+    }
+    int64_t theta = a->theta[idx];
+    int64_t v = r_T + theta;
+    /* placeOrder (ZI.py:277-309) */
+    int64_t R = rs_randint(&a->rs, a->R_min, a->R_max + 1);
+    int64_t p = buy ? v - R : v + R;
+    int64_t bid = a->nb ? a->bid : 0, bid_vol = a->nb ? a->bidq : 0;
+    int64_t ask = a->na ? a->ask : 0, ask_vol = a->na ? a->askq : 0;
+    if (buy && ask_vol > 0) {
+        int64_t R_ask = v - ask;
+        if ((double)R_ask >= a->eta * (double)R) p = ask;
+    } else if (!buy && bid_vol > 0) {
+        int64_t R_bid = bid - v;
+        if ((double)R_bid >= a->eta * (double)R) p = bid;
+    }
+    place_limit(e, a, 100, buy, p);
+}
+static void zi_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    if (a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        if (a->mkt_closed) return;
+        zi_place(e, a);
+        a->state = ST_AWAITING_WAKEUP;
+    }
+}
+
+/* ------------------------------- ValueAgent -------------------------------- */
+static void value_wakeup(ora_env* e, agent_t* a) {
+    ta_wakeup(e, a);
+    a->state = ST_INACTIVE;
+    if (!a->has_open || !a->has_close) return;
+    a->trading = 1;
+    if (a->mkt_closed && a->has_daily_close) return;
+    double dt = rs_exponential(&a->rs, 1.0 / a->lambda_a);
+    k_wakeup(e, a->id, e->cur + py_round(dt));
+    if (a->mkt_closed && !a->has_daily_close) {
+        get_spread(e, a, 1);
+        a->state = ST_AWAITING_SPREAD;
+        return;
+    }
+    cancel_all(e, a);
+    get_spread(e, a, 1);
+    a->state = ST_AWAITING_SPREAD;
+}
+static void value_place(ora_env* e, agent_t* a) {
+    int64_t obs = o_observe(e, e->cur, a->sigma_n, &a->rs);
+    int64_t r_T = bayes_r_T(e, a, obs);
+    int have_bid = a->nb && a->bid != 0, have_ask = a->na && a->ask != 0;
+    int buy;
+    int64_t p;
+    if (have_bid && have_ask) {
+        int64_t mid = (int64_t)((double)(a->ask + a->bid) / 2);
+        int64_t spread = llabs(a->ask - a->bid);
+        int64_t adj;
+        if (rs_double(&e->G) < 0.1) adj = 0;
+        else adj = rs_randint(&e->G, 0, 2 * spread);
+        if (r_T < mid) {
+            buy = 0;
+            p = a->bid + adj;
+        } else {
+            buy = 1;
+            p = a->ask - adj;
+        }
+    } else {
+        buy = (int)rs_randint(&e->G, 0, 2);
+        p = r_T;
+    }
+    place_limit(e, a, a->size, buy, p);
+}
+static void value_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    if (a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        if (a->mkt_closed) return;
+        value_place(e, a);
+        a->state = ST_AWAITING_WAKEUP;
+    }
+}
+
+/* ------------------------------- NoiseAgent -------------------------------- */
+static void noise_wakeup(ora_env* e, agent_t* a) {
+    ta_wakeup(e, a);
+    a->state = ST_INACTIVE;
+    if (!a->has_open || !a->has_close) return;
+    a->trading = 1;
+    if (a->mkt_closed && a->has_daily_close) return;
+    if (a->wakeup_time > e->cur) k_wakeup(e, a->id, a->wakeup_time);
+    if (a->mkt_closed && !a->has_daily_close) {
+        get_spread(e, a, 1);
+        a->state = ST_AWAITING_SPREAD;
+        return;
+    }
+    get_spread(e, a, 1);
+    a->state = ST_AWAITING_SPREAD;
+}
+static void noise_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    if (a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        if (a->mkt_closed) return;
+        int buy = (int)rs_randint(&e->G, 0, 2);
+        int have_bid = a->nb && a->bid != 0, have_ask = a->na && a->ask != 0;
+        if (buy && have_ask) place_limit(e, a, a->size, 1, a->ask);
+        else if (!buy && have_bid) place_limit(e, a, a->size, 0, a->bid);
+        a->state = ST_AWAITING_WAKEUP;
+    }
+}
+
+/* --------------------------- POVMarketMakerAgent ---------------------------- */
+static void mm_wakeup(ora_env* e, agent_t* a) {
+    int can_trade = ta_wakeup(e, a);
+    if (can_trade) {
+        get_spread(e, a, 1);
+        get_tv(e, a, a->wake_freq);
+    }
+}
+static void mm_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    int64_t mid = a->last_mid;
+    if (m->kind == K_TV && a->aw_tv) {
+        int64_t qty = py_round(a->pov * (double)a->tv);
+        a->order_size = qty >= a->min_size ? qty : a->min_size;
+        a->aw_tv = 0;
+    }
+    if (m->kind == K_SPREAD && a->aw_spread) {
+        int have_bid = a->nb && a->bid != 0, have_ask = a->na && a->ask != 0;
+        if (have_bid && have_ask) {
+            mid = (int64_t)((double)(a->ask + a->bid) / 2);
+            a->last_mid = mid;
+            a->has_last_mid = 1;
+            a->aw_spread = 0;
+        }
+    }
+    if (!a->aw_spread && !a->aw_tv) {
+        cancel_all(e, a);
+        int64_t hb = mid - 1, la = mid + a->window;
+        int64_t lb = hb - a->num_ticks, ha = la + a->num_ticks;
+        for (int64_t p = lb; p <= hb; p++) place_limit(e, a, a->order_size, 1, p);
+        for (int64_t p = la; p <= ha; p++) place_limit(e, a, a->order_size, 0, p);
+        a->aw_spread = a->aw_tv = 1;
+        k_wakeup(e, a->id, e->cur + a->wake_freq);
+    }
+}
+
+/* ------------------------------- MomentumAgent ------------------------------ */
+static double mom_avg(agent_t* a, int n) {
+    /* MomentumAgent.ma(mid_list, n)[-1].round(2): exact half-integer sums */
+    int64_t s2 = 0;
+    for (int i = a->nmid - n; i < a->nmid; i++) s2 += a->mids2[i];
+    double x = ((double)s2 / 2.0) / (double)n;
+    return rint(x * 100.0) / 100.0;
+}
+static void mom_wakeup(ora_env* e, agent_t* a) {
+    int can_trade = ta_wakeup(e, a);
+    if (can_trade) {
+        get_spread(e, a, 1);
+        a->state = ST_AWAITING_SPREAD;
+    }
+}
+static void mom_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    if (a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        int have_bid = a->nb && a->bid != 0, have_ask = a->na && a->ask != 0;
+        if (have_bid && have_ask) {
+            if (a->nmid == a->capmid) {
+                a->capmid = a->capmid ? 2 * a->capmid : 64;
+                a->mids2 = (int64_t*)realloc(a->mids2, sizeof(int64_t) * a->capmid);
+            }
+            a->mids2[a->nmid++] = a->bid + a->ask;
+            if (a->nmid > 20) { a->avg20 = mom_avg(a, 20); a->n20++; }
+            if (a->nmid > 50) { a->avg50 = mom_avg(a, 50); a->n50++; }
+            if (a->n20 > 0 && a->n50 > 0) {
+                if (a->avg20 >= a->avg50) place_limit(e, a, a->size, 1, a->ask);
+                else place_limit(e, a, a->size, 0, a->bid);
+            }
+        }
+        k_wakeup(e, a->id, e->cur + a->wake_freq);
+        a->state = ST_AWAITING_WAKEUP;
+    }
+}
+
+/* ------------------------------- dispatch ---------------------------------- */
+static void dispatch_wakeup(ora_env* e, int id) {
+    agent_t* a = &e->ag[id];
+    switch (a->type) {
+    case AG_EXCHANGE: a->cur_time = e->cur; break; /* Agent.wakeup: no action */
+    case AG_ZI: zi_wakeup(e, a); break;
+    case AG_NOISE: noise_wakeup(e, a); break;
+    case AG_VALUE: value_wakeup(e, a); break;
+    case AG_POVMM: mm_wakeup(e, a); break;
+    case AG_MOMENTUM: mom_wakeup(e, a); break;
+    }
+}
+static void dispatch_message(ora_env* e, int id, const msg_t* m) {
+    agent_t* a = &e->ag[id];
+    switch (a->type) {
+    case AG_EXCHANGE: ex_receive(e, m); break;
+    case AG_ZI: zi_receive(e, a, m); break;
+    case AG_NOISE: noise_receive(e, a, m); break;
+    case AG_VALUE: value_receive(e, a, m); break;
+    case AG_POVMM: mm_receive(e, a, m); break;
+    case AG_MOMENTUM: mom_receive(e, a, m); break;
+    }
+}
+
+/* Kernel.runner event loop (Kernel.py:190-292) */
+int64_t ora_run(ora_env* e, int64_t max_pops) {
+    int64_t done = 0;
+    while (!e->done) {
+        if (max_pops >= 0 && done >= max_pops) break;
+        if (e->nheap == 0 || !(e->cur <= e->stop)) {
+            e->done = 1;
+            break;
+        }
+        ev_t v = heap_pop(e);
+        e->cur = v.t;
+        e->have_cur = 1;
+        int64_t rec[10];
+        encode(e, &v, rec);
+        for (int i = 0; i < 10; i++) e->hash = (e->hash ^ (uint64_t)rec[i]) * FNV_PRIME;
+        if (e->trace && e->trace_len < e->trace_cap) memcpy(e->trace + 10 * e->trace_len++, rec, sizeof rec);
+        e->pops++;
+        done++;
+        e->add_delay = 0;
+        int a = v.rcp;
+        if (e->agent_time[a] > e->cur) { /* agent in the future: requeue unchanged */
+            v.t = e->agent_time[a];
+            heap_push(e, v);
+            continue;
+        }
+        e->agent_time[a] = e->cur;
+        if (v.type == T_WAKEUP) {
+            dispatch_wakeup(e, a);
+        } else {
+            msg_t m = e->msgs[v.mi];
+            msg_free(e, v.mi);
+            dispatch_message(e, a, &m);
+        }
+        e->agent_time[a] += e->comp_delay[a] + e->add_delay;
+    }
+    return done;
+}
+
+/* ------------------------------- reporting --------------------------------- */
+static void rep_append(ora_env* e, const char* s) {
+    size_t l = strlen(s);
+    e->report = (char*)realloc(e->report, e->report_len + l + 2);
+    memcpy(e->report + e->report_len, s, l);
+    e->report_len += l;
+    e->report[e->report_len++] = '\n';
+    e->report[e->report_len] = 0;
+}
+
+/* TradingAgent.kernelStopping (TradingAgent.py:112-138) + Kernel mean print (Kernel.py:337-341) */
+int ora_finish(ora_env* e) {
+    char line[512];
+    const char* sym = strcmp(e->config, "rmsc03") == 0 ? "ABM" : "JPM";
+    char tnames[16][96];
+    long long gains[16];
+    int counts[16], nt = 0;
+    for (int i = 1; i < e->n; i++) {
+        agent_t* a = &e->ag[i];
+        char hold[128];
+        if (a->shares != 0) snprintf(hold, sizeof hold, "{ %s: %lld, CASH: %lld }", sym, (long long)a->shares, (long long)a->cash);
+        else snprintf(hold, sizeof hold, "{ CASH: %lld }", (long long)a->cash);
+        long long mtm = a->cash;
+        int mtm_float = 0;
+        if (a->shares != 0) {
+            mtm += (long long)a->last_trade * a->shares;
+            mtm_float = a->last_trade_float;
+        }
+        if (mtm_float) snprintf(line, sizeof line, "Final holdings for %s: %s.  Marked to market: %lld.0", a->name, hold, mtm);
+        else snprintf(line, sizeof line, "Final holdings for %s: %s.  Marked to market: %lld", a->name, hold, mtm);
+        rep_append(e, line);
+        int k;
+        for (k = 0; k < nt; k++)
+            if (strcmp(tnames[k], a->tname) == 0) break;
+        if (k == nt) {
+            snprintf(tnames[nt], 96, "%s", a->tname);
+            gains[nt] = 0;
+            counts[nt] = 0;
+            nt++;
+        }
+        gains[k] += mtm - a->starting_cash;
+        counts[k]++;
+    }
+    for (int k = 0; k < nt; k++) {
+        snprintf(line, sizeof line, "%s: %lld", tnames[k], (long long)rint((double)gains[k] / (double)counts[k]));
+        rep_append(e, line);
+    }
+    return 0;
+}
+
+/* ------------------------------- configs ----------------------------------- */
+static agent_t* add_agent(ora_env* e, int type) {
+    e->ag = (agent_t*)realloc(e->ag, sizeof(agent_t) * (e->n + 1));
+    agent_t* a = &e->ag[e->n];
+    memset(a, 0, sizeof *a);
+    a->id = e->n++;
+    a->type = type;
+    a->first_wake = 1;
+    a->state = ST_AWAITING_WAKEUP;
+    return a;
+}
+static uint32_t seed_u32(ora_rs* G) { return (uint32_t)rs_randint(G, 0, 4294967296LL); }
+
+static void oracle_init(ora_env* e, int64_t open, int64_t close, double r_bar, double kappa, double fund_vol,
+                        double lam, double ms_mean, double ms_var) {
+    e->o_open = open;
+    e->o_close = close;
+    e->o_rbar = r_bar;
+    e->o_kappa = kappa;
+    e->o_fundvol = fund_vol;
+    e->o_lambda = lam;
+    e->o_msmean = ms_mean;
+    e->o_msvar = ms_var;
+    e->o_pt = open;
+    e->o_pv = r_bar;
+    e->o_mst = open + (int64_t)rs_exponential(&e->G, 1.0 / lam);
+    double msv = rs_normal(&e->O, ms_mean, sqrt(ms_var));
+    e->o_msv = rs_randint(&e->O, 0, 2) == 0 ? msv : -msv;
+}
+
+static void trading_init(agent_t* a, int64_t cash) {
+    a->starting_cash = cash;
+    a->cash = cash;
+}
+
+static int cmp_desc(const void* x, const void* y) {
+    double a = *(const double*)x, b = *(const double*)y;
+    return a < b ? 1 : (a > b ? -1 : 0);
+}
+
+/* get_wake_time (util/util.py:35-58) with the global RNG */
+static int64_t get_wake_time(ora_env* e, int64_t open, int64_t close) {
+    double u = rs_double(&e->G);
+    double alpha = 12.0, beta = 0.5;
+    double n = (3 / alpha) * u - pow(beta - 0, 3.0);
+    double c = n < 0 ? -pow(-n, 1.0 / 3.0) : pow(n, 1.0 / 3.0);
+    double mult = c + beta;
+    return open + (int64_t)(mult * (double)(close - open));
+}
+
+static int build_sparse_zi(ora_env* e, uint32_t seed, int big) {
+    /* config/sparse_zi_100.py:73-334 (sparse_zi_1000.py for big) */
+    rs_seed(&e->G, seed);
+    rs_seed(&e->O, seed_u32(&e->G));
+    rs_seed(&e->K, seed_u32(&e->G));
+    if (!big) rs_seed(&e->L, seed_u32(&e->G));
+    e->start = 0;
+    e->stop = 17 * NS_HOUR;
+    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
+    oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+    agent_t* ex = add_agent(e, AG_EXCHANGE);
+    rs_seed(&ex->rs, seed_u32(&e->G));
+    snprintf(ex->name, 96, "Exchange Agent 0");
+    snprintf(ex->tname, 96, "ExchangeAgent");
+    e->ex_open = open;
+    e->ex_close = close;
+    e->ex_pipeline = 0;
+    e->ex_comp = 0;
+    e->stream_history = 10;
+    static const int n100[7] = {15, 15, 14, 14, 14, 14, 14};
+    static const int n1000[7] = {143, 143, 143, 143, 143, 143, 142};
+    static const int rmin[7] = {0, 0, 0, 0, 0, 250, 250};
+    static const int rmax[7] = {250, 500, 1000, 1000, 2000, 500, 500};
+    static const double eta[7] = {1, 1, 0.8, 1, 0.8, 0.8, 1};
+    static const char* etas[7] = {"1", "1", "0.8", "1", "0.8", "0.8", "1"};
+    for (int g = 0; g < 7; g++) {
+        int cnt = big ? n1000[g] : n100[g];
+        for (int k = 0; k < cnt; k++) {
+            agent_t* a = add_agent(e, AG_ZI);
+            rs_seed(&a->rs, seed_u32(&e->G));
+            snprintf(a->name, 96, "ZI Agent %d Type %d [%d <= R <= %d, eta=%s]", a->id, g + 1, rmin[g], rmax[g], etas[g]);
+            snprintf(a->tname, 96, "ZeroIntelligenceAgent Type %d [%d <= R <= %d, eta=%s]", g + 1, rmin[g], rmax[g], etas[g]);
+            trading_init(a, 10000000);
+            a->sigma_n = 1000000.0;
+            a->r_bar = 1e5;
+            a->kappa = 1.67e-15;
+            a->sigma_s = 1e-4;
+            a->q_max = 10;
+            a->R_min = rmin[g];
+            a->R_max = rmax[g];
+            a->eta = eta[g];
+            a->lambda_a = 1e-12;
+            a->r_t = 1e5;
+            a->sigma_t = 0;
+            double th[20];
+            for (int i = 0; i < 20; i++) th[i] = rint(rs_normal(&a->rs, 0, sqrt(5e6)));
+            qsort(th, 20, sizeof(double), cmp_desc);
+            for (int i = 0; i < 20; i++) a->theta[i] = (int64_t)th[i];
+        }
+    }
+    int n = e->n;
+    e->lat = (double*)malloc(sizeof(double) * (size_t)n * n);
+    if (!big) {
+        for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, 21000, 100000);
+        e->lat_mode = 2;
+        e->jitter = 0.3;
+        e->clip = 0.05;
+        e->unit = 5;
+        e->noise_len = 0;
+    } else {
+        for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, 21000, 13000000);
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                if (i > j) e->lat[(size_t)i * n + j] = e->lat[(size_t)j * n + i];
+                else if (i == j) e->lat[(size_t)i * n + j] = 20000;
+            }
+        e->lat_mode = 1;
+        e->noise_len = 6;
+    }
+    e->agent_time = (int64_t*)calloc(n, sizeof(int64_t));
+    e->comp_delay = (int64_t*)calloc(n, sizeof(int64_t));
+    for (int i = 0; i < n; i++) {
+        e->agent_time[i] = e->start;
+        e->comp_delay[i] = 1000000000;
+    }
+    return 0;
+}
+
+static int build_rmsc03(ora_env* e, uint32_t seed) {
+    /* config/rmsc03.py:55-235 */
+    rs_seed(&e->G, seed);
+    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 9 * NS_HOUR + 45 * NS_MIN;
+    rs_seed(&e->O, seed_u32(&e->G));
+    oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+    agent_t* ex = add_agent(e, AG_EXCHANGE);
+    rs_seed(&ex->rs, seed_u32(&e->G));
+    snprintf(ex->name, 96, "EXCHANGE_AGENT");
+    snprintf(ex->tname, 96, "ExchangeAgent");
+    e->ex_open = open;
+    e->ex_close = close;
+    e->ex_pipeline = 0;
+    e->ex_comp = 0;
+    e->stream_history = 10;
+    int64_t nopen = 9 * NS_HOUR, nclose = 16 * NS_HOUR;
+    for (int j = 0; j < 50; j++) {
+        int64_t wt = get_wake_time(e, nopen, nclose);
+        agent_t* a = add_agent(e, AG_NOISE);
+        a->wakeup_time = wt;
+        rs_seed(&a->rs, seed_u32(&e->G));
+        a->size = rs_randint(&e->G, 20, 50);
+        snprintf(a->name, 96, "NoiseAgent %d", a->id);
+        snprintf(a->tname, 96, "NoiseAgent");
+        trading_init(a, 10000000);
+    }
+    for (int j = 0; j < 10; j++) {
+        agent_t* a = add_agent(e, AG_VALUE);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        a->size = rs_randint(&e->G, 20, 50);
+        snprintf(a->name, 96, "Value Agent %d", a->id);
+        snprintf(a->tname, 96, "ValueAgent");
+        trading_init(a, 10000000);
+        a->sigma_n = 1e5 / 10;
+        a->r_bar = 1e5;
+        a->kappa = 1.67e-15;
+        a->sigma_s = 100000;
+        a->lambda_a = 7e-11;
+        a->r_t = 1e5;
+        a->sigma_t = 0;
+    }
+    {
+        agent_t* a = add_agent(e, AG_POVMM);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        snprintf(a->name, 96, "POV_MARKET_MAKER_AGENT_%d", a->id);
+        snprintf(a->tname, 96, "POVMarketMakerAgent");
+        trading_init(a, 10000000);
+        a->pov = 0.05;
+        a->min_size = 20;
+        a->window = 5;
+        a->num_ticks = 20;
+        a->wake_freq = NS_SEC;
+        a->order_size = 20;
+        a->aw_spread = a->aw_tv = 1;
+    }
+    for (int j = 0; j < 2; j++) {
+        agent_t* a = add_agent(e, AG_MOMENTUM);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        a->size = rs_randint(&a->rs, 1, 10);
+        snprintf(a->name, 96, "MOMENTUM_AGENT_%d", a->id);
+        snprintf(a->tname, 96, "MomentumAgent");
+        trading_init(a, 10000000);
+        a->wake_freq = 20 * NS_SEC;
+    }
+    rs_seed(&e->K, seed_u32(&e->G));
+    e->start = open;
+    e->stop = close + NS_MIN;
+    e->lat_mode = 0;
+    e->noise_len = 1;
+    int n = e->n;
+    e->agent_time = (int64_t*)calloc(n, sizeof(int64_t));
+    e->comp_delay = (int64_t*)calloc(n, sizeof(int64_t));
+    for (int i = 0; i < n; i++) e->agent_time[i] = e->start;
+    return 0;
+}
+
+int ora_create(const char* config, uint32_t seed, ora_env** out) {
+    ora_env* e = (ora_env*)calloc(1, sizeof(ora_env));
+    snprintf(e->config, sizeof e->config, "%s", config);
+    int rc;
+    if (!strcmp(config, "sparse_zi_100")) rc = build_sparse_zi(e, seed, 0);
+    else if (!strcmp(config, "sparse_zi_1000")) rc = build_sparse_zi(e, seed, 1);
+    else if (!strcmp(config, "rmsc03")) rc = build_rmsc03(e, seed);
+    else rc = -1;
+    if (rc) {
+        free(e);
+        return rc;
+    }
+    e->nhist = 1; /* history = [{}] */
+    e->hash = FNV_OFF;
+    /* kernelInitializing: exchange opening price = oracle.getDailyOpenPrice = r_bar (a float) */
+    e->last_trade = (int64_t)e->o_rbar;
+    e->last_trade_float = 1;
+    /* kernelStarting: every agent requests a wakeup at startTime, in id order */
+    for (int i = 0; i < e->n; i++) k_wakeup(e, i, e->start);
+    e->cur = e->start; /* Kernel.runner: currentTime = startTime before the loop */
+    *out = e;
+    return 0;
+}
+
+void ora_destroy(ora_env* e) {
+    if (!e) return;
+    for (int i = 0; i < e->n; i++) {
+        free(e->ag[i].ord);
+        free(e->ag[i].mids2);
+    }
+    free(e->ag);
+    for (int s = 0; s < 2; s++) {
+        for (int i = 0; i < e->book[s].n; i++) free(e->book[s].lv[i].o);
+        free(e->book[s].lv);
+    }
+    for (int i = 0; i < e->nhist; i++) epoch_free(&e->hist[i]);
+    free(e->lat);
+    free(e->agent_time);
+    free(e->comp_delay);
+    free(e->heap);
+    free(e->msgs);
+    free(e->freem);
+    free(e->report);
+    free(e);
+}
+
+int ora_done(const ora_env* e) { return e->done; }
+int ora_error(const ora_env* e) { return e->err; }
+const char* ora_error_str(const ora_env* e) { return e->errstr; }
+uint64_t ora_hash(const ora_env* e) { return e->hash; }
+int64_t ora_events(const ora_env* e) { return e->pops; }
+int64_t ora_current_time(const ora_env* e) { return e->cur; }
+void ora_set_trace(ora_env* e, int64_t* buf, int64_t cap) {
+    e->trace = buf;
+    e->trace_cap = cap;
+    e->trace_len = 0;
+}
+int64_t ora_trace_len(const ora_env* e) { return e->trace_len; }
+int ora_n_agents(const ora_env* e) { return e->n; }
+int ora_agent_state(const ora_env* e, int id, int64_t* cash, int64_t* shares, int64_t* n_open) {
+    if (id < 0 || id >= e->n) return -1;
+    *cash = e->ag[id].cash;
+    *shares = e->ag[id].shares;
+    *n_open = e->ag[id].nord;
+    return 0;
+}
+int64_t ora_book(const ora_env* e, int side, int64_t* buf, int64_t cap) {
+    const side_t* S = &e->book[side ? 1 : 0];
+    int64_t k = 0;
+#define PUT(x) do { if (k < cap) buf[k] = (x); k++; } while (0)
+    PUT(S->n);
+    for (int i = 0; i < S->n; i++) {
+        PUT(S->lv[i].n);
+        for (int j = 0; j < S->lv[i].n; j++) {
+            PUT(S->lv[i].o[j].id);
+            PUT(S->lv[i].o[j].agent);
+            PUT(S->lv[i].o[j].qty);
+            PUT(S->lv[i].o[j].price);
+        }
+    }
+#undef PUT
+    return k;
+}
+int64_t ora_order_counter(const ora_env* e) { return e->order_counter; }
+int64_t ora_last_trade(const ora_env* e) { return e->last_trade; }
+int64_t ora_report(const ora_env* e, char* buf, int64_t cap) {
+    if (!e->report) return 0;
+    if (buf && cap > 0) {
+        int64_t n = e->report_len < cap - 1 ? e->report_len : cap - 1;
+        memcpy(buf, e->report, n);
+        buf[n] = 0;
+    }
+    return e->report_len;
+}
+
+/* ------------------------------- batch runner ------------------------------- */
+typedef struct {
+    const char* config;
+    const uint32_t* seeds;
+    int n, next;
+    int64_t max_pops;
+    int64_t* ev;
+    uint64_t* h;
+    pthread_mutex_t mu;
+    int rc;
+} batch_t;
+
+static void* batch_worker(void* p) {
+    batch_t* b = (batch_t*)p;
+    for (;;) {
+        pthread_mutex_lock(&b->mu);
+        int i = b->next++;
+        pthread_mutex_unlock(&b->mu);
+        if (i >= b->n) break;
+        ora_env* e = NULL;
+        if (ora_create(b->config, b->seeds[i], &e)) {
+            b->rc = -1;
+            continue;
+        }
+        ora_run(e, b->max_pops);
+        b->ev[i] = e->pops;
+        b->h[i] = e->hash;
+        ora_destroy(e);
+    }
+    return NULL;
+}
+
+int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
+                  int64_t* events_out, uint64_t* hash_out, double* seconds_out) {
+    batch_t b;
+    memset(&b, 0, sizeof b);
+    b.config = config;
+    b.seeds = seeds;
+    b.n = n;
+    b.max_pops = max_pops;
+    b.ev = events_out;
+    b.h = hash_out;
+    pthread_mutex_init(&b.mu, NULL);
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, batch_worker, &b);
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (seconds_out) *seconds_out = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+    free(th);
+    pthread_mutex_destroy(&b.mu);
+    return b.rc;
+}

@@ -1,0 +1,81 @@
+/* abides_oracle.h — CPU restatement of the reference ABIDES hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only
+ * as the checker / reported CPU baseline.  The product path (libmxa, HIP) never
+ * links or calls it.
+ *
+ * Restates (file:line of /root/reference):
+ *   Kernel.runner loop ........................ Kernel.py:190-292
+ *   Kernel.sendMessage / setWakeup ............ Kernel.py:347-462
+ *   OrderBook (match/enter/cancel/history) .... util/OrderBook.py:38-436
+ *   ExchangeAgent.receiveMessage .............. agent/ExchangeAgent.py:129-340,471-485
+ *   TradingAgent protocol ..................... agent/TradingAgent.py:99-268,309-462,514-535,609-680
+ *   ZeroIntelligenceAgent ..................... agent/ZeroIntelligenceAgent.py:65-350
+ *   NoiseAgent / ValueAgent ................... agent/NoiseAgent.py, agent/ValueAgent.py
+ *   POVMarketMakerAgent / MomentumAgent ....... agent/market_makers/POVMarketMakerAgent.py,
+ *                                               agent/examples/MomentumAgent.py
+ *   SparseMeanRevertingOracle ................. util/oracle/SparseMeanRevertingOracle.py:36-227
+ *   LatencyModel (cubic) ...................... model/LatencyModel.py:109-140
+ *   configs sparse_zi_100 / sparse_zi_1000 / rmsc03 (global-RNG draw order)
+ *   numpy legacy RandomState (MT19937 + legacy_gauss/exponential/bounded ints), numpy 2.2.6
+ *   transcendental math: the host glibc libm (the same libm the reference ran on).
+ *
+ * Parity is pinned by tests/golden/* (traces produced by the reference itself) and by
+ * the reference's own known-answer file tests/sparse_zi_1000.txt.
+ */
+#ifndef ABIDES_ORACLE_H
+#define ABIDES_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ora_env ora_env;
+
+/* config: "sparse_zi_100" | "sparse_zi_1000" | "rmsc03" */
+int ora_create(const char* config, uint32_t seed, ora_env** out);
+void ora_destroy(ora_env* e);
+/* run up to max_pops kernel pops (<0: unlimited); returns pops performed by this call */
+int64_t ora_run(ora_env* e, int64_t max_pops);
+/* run the after-loop lifecycle (kernelStopping): fills the "Final holdings" lines */
+int ora_finish(ora_env* e);
+int ora_done(const ora_env* e);
+int ora_error(const ora_env* e);
+const char* ora_error_str(const ora_env* e);
+uint64_t ora_hash(const ora_env* e);
+int64_t ora_events(const ora_env* e);
+int64_t ora_current_time(const ora_env* e);
+/* optional trace capture: records of 10 int64 (see DESIGN.md "trace record") */
+void ora_set_trace(ora_env* e, int64_t* buf, int64_t cap_records);
+int64_t ora_trace_len(const ora_env* e);
+int ora_n_agents(const ora_env* e);
+/* per agent: cash, shares, number of open orders */
+int ora_agent_state(const ora_env* e, int id, int64_t* cash, int64_t* shares, int64_t* n_open);
+/* book side (0 bids, 1 asks) flattened: [n_levels, (n_orders, (id, agent, qty, price)*n)*] */
+int64_t ora_book(const ora_env* e, int side, int64_t* buf, int64_t cap);
+int64_t ora_order_counter(const ora_env* e);
+int64_t ora_last_trade(const ora_env* e);
+/* stdout restatement after ora_finish: "Final holdings ..." lines then "Mean..." lines */
+int64_t ora_report(const ora_env* e, char* buf, int64_t cap);
+
+/* CPU baseline: n independent envs (seeds[i]) over `threads` OS threads, one env per task.
+ * Each env runs at most max_pops pops (<0: to completion). Returns 0 on success. */
+int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
+                  int64_t* events_out, uint64_t* hash_out, double* seconds_out);
+
+/* numpy-legacy RNG known-answer helpers (tests) */
+typedef struct ora_rs ora_rs;
+ora_rs* ora_rs_new(uint32_t seed);
+void ora_rs_free(ora_rs* r);
+uint32_t ora_rs_u32(ora_rs* r);
+double ora_rs_double(ora_rs* r);
+int64_t ora_rs_randint(ora_rs* r, int64_t lo, int64_t hi);
+double ora_rs_normal(ora_rs* r, double loc, double scale);
+double ora_rs_exponential(ora_rs* r, double scale);
+double ora_rs_uniform(ora_rs* r, double lo, double hi);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,203 @@
+"""ctypes binding of the CPU parity oracle (oracle/abides_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg — never by the product package.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libabides_oracle.so")
+_lib = None
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P, I64, U64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
+        L.ora_create.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(P)]
+        L.ora_run.argtypes = [P, I64]
+        L.ora_run.restype = I64
+        L.ora_finish.argtypes = [P]
+        L.ora_done.argtypes = [P]
+        L.ora_error.argtypes = [P]
+        L.ora_error_str.argtypes = [P]
+        L.ora_error_str.restype = ctypes.c_char_p
+        L.ora_hash.argtypes = [P]
+        L.ora_hash.restype = U64
+        L.ora_events.argtypes = [P]
+        L.ora_events.restype = I64
+        L.ora_current_time.argtypes = [P]
+        L.ora_current_time.restype = I64
+        L.ora_set_trace.argtypes = [P, ctypes.c_void_p, I64]
+        L.ora_trace_len.argtypes = [P]
+        L.ora_trace_len.restype = I64
+        L.ora_n_agents.argtypes = [P]
+        L.ora_agent_state.argtypes = [P, I32, ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(I64)]
+        L.ora_book.argtypes = [P, I32, ctypes.c_void_p, I64]
+        L.ora_book.restype = I64
+        L.ora_order_counter.argtypes = [P]
+        L.ora_order_counter.restype = I64
+        L.ora_last_trade.argtypes = [P]
+        L.ora_last_trade.restype = I64
+        L.ora_report.argtypes = [P, ctypes.c_char_p, I64]
+        L.ora_report.restype = I64
+        L.ora_destroy.argtypes = [P]
+        L.ora_run_batch.argtypes = [ctypes.c_char_p, ctypes.c_void_p, I32, I32, I64, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        L.ora_rs_new.argtypes = [ctypes.c_uint32]
+        L.ora_rs_new.restype = P
+        L.ora_rs_free.argtypes = [P]
+        L.ora_rs_u32.argtypes = [P]
+        L.ora_rs_u32.restype = ctypes.c_uint32
+        L.ora_rs_double.argtypes = [P]
+        L.ora_rs_double.restype = ctypes.c_double
+        L.ora_rs_randint.argtypes = [P, I64, I64]
+        L.ora_rs_randint.restype = I64
+        L.ora_rs_normal.argtypes = [P, ctypes.c_double, ctypes.c_double]
+        L.ora_rs_normal.restype = ctypes.c_double
+        L.ora_rs_exponential.argtypes = [P, ctypes.c_double]
+        L.ora_rs_exponential.restype = ctypes.c_double
+        L.ora_rs_uniform.argtypes = [P, ctypes.c_double, ctypes.c_double]
+        L.ora_rs_uniform.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+class OracleEnv:
+    """One reference-semantics simulation (config + seed)."""
+
+    def __init__(self, config, seed, trace_cap=0):
+        L = lib()
+        self._h = ctypes.c_void_p()
+        rc = L.ora_create(config.encode(), seed & 0xFFFFFFFF, ctypes.byref(self._h))
+        if rc:
+            raise ValueError("oracle: bad config %r" % config)
+        self.trace_buf = None
+        if trace_cap:
+            self.trace_buf = np.zeros((trace_cap, 10), dtype=np.int64)
+            L.ora_set_trace(self._h, self.trace_buf.ctypes.data, trace_cap)
+
+    def run(self, max_pops=-1):
+        return lib().ora_run(self._h, max_pops)
+
+    def finish(self):
+        lib().ora_finish(self._h)
+
+    @property
+    def done(self):
+        return bool(lib().ora_done(self._h))
+
+    @property
+    def error(self):
+        L = lib()
+        return L.ora_error(self._h), L.ora_error_str(self._h).decode()
+
+    @property
+    def hash(self):
+        return lib().ora_hash(self._h)
+
+    @property
+    def events(self):
+        return lib().ora_events(self._h)
+
+    def trace(self):
+        n = lib().ora_trace_len(self._h)
+        return self.trace_buf[:n]
+
+    def agents(self):
+        L = lib()
+        out = []
+        for i in range(L.ora_n_agents(self._h)):
+            c, s, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            L.ora_agent_state(self._h, i, ctypes.byref(c), ctypes.byref(s), ctypes.byref(n))
+            out.append((c.value, s.value, n.value))
+        return out
+
+    def book(self, side):
+        L = lib()
+        n = L.ora_book(self._h, side, None, 0)
+        buf = np.zeros(n, dtype=np.int64)
+        L.ora_book(self._h, side, buf.ctypes.data, n)
+        levels, k = [], 1
+        for _ in range(buf[0]):
+            m = buf[k]
+            k += 1
+            levels.append([buf[k + 4 * j:k + 4 * j + 4].tolist() for j in range(m)])
+            k += 4 * m
+        return levels
+
+    @property
+    def order_counter(self):
+        return lib().ora_order_counter(self._h)
+
+    @property
+    def last_trade(self):
+        return lib().ora_last_trade(self._h)
+
+    def report(self):
+        L = lib()
+        n = L.ora_report(self._h, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        L.ora_report(self._h, buf, n + 1)
+        return buf.value.decode().splitlines()
+
+    def __del__(self):
+        try:
+            lib().ora_destroy(self._h)
+        except Exception:
+            pass
+
+
+def run_batch(config, seeds, threads, max_pops=-1):
+    L = lib()
+    seeds = np.asarray(seeds, dtype=np.uint32)
+    ev = np.zeros(len(seeds), dtype=np.int64)
+    hs = np.zeros(len(seeds), dtype=np.uint64)
+    sec = ctypes.c_double()
+    rc = L.ora_run_batch(config.encode(), seeds.ctypes.data, len(seeds), threads, max_pops, ev.ctypes.data,
+                         hs.ctypes.data, ctypes.byref(sec))
+    if rc:
+        raise RuntimeError("oracle batch failed")
+    return ev, hs, sec.value
+
+
+class RandomState:
+    """numpy-legacy RandomState restatement (for KAT tests)."""
+
+    def __init__(self, seed):
+        self._h = lib().ora_rs_new(seed)
+
+    def u32(self):
+        return lib().ora_rs_u32(self._h)
+
+    def rand(self):
+        return lib().ora_rs_double(self._h)
+
+    def randint(self, lo, hi):
+        return lib().ora_rs_randint(self._h, lo, hi)
+
+    def normal(self, loc, scale):
+        return lib().ora_rs_normal(self._h, loc, scale)
+
+    def exponential(self, scale):
+        return lib().ora_rs_exponential(self._h, scale)
+
+    def uniform(self, lo, hi):
+        return lib().ora_rs_uniform(self._h, lo, hi)
+
+    def __del__(self):
+        try:
+            lib().ora_rs_free(self._h)
+        except Exception:
+            pass
