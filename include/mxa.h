@@ -1,0 +1,90 @@
+/* mxa.h — C-ABI of libmxa, the MI355X-native vectorised ABIDES market step.
+ *
+ * One handle = n_envs independent markets (envs) of one configuration on one GPU,
+ * simulated by HIP kernels (one wavefront per env).  Plain pointers and sizes only; the
+ * caller owns every host array.  Every entry point returns 0 on success or a negative
+ * MXA_E* code; mxa_last_error() gives the message.  A handle is bound to one device and
+ * one HIP stream and is not thread-safe; multi-GPU runs use one process per GPU.
+ *
+ * Reference interfaces replaced (file:line in yutiansut/marl-optimal-execution):
+ *   mxa_create ......... config/{rmsc03,sparse_zi_100,sparse_zi_1000}.py module body
+ *                        (agent/oracle/kernel construction, global-RNG draw order) and
+ *                        Kernel.__init__ (Kernel.py:13-46)
+ *   mxa_reset .......... Kernel.runner kernelInitializing/kernelStarting (Kernel.py:143-177),
+ *                        ABIDESEnv.reset (ABIDESEnv.py:51-57)
+ *   mxa_run / mxa_launch Kernel.runner event loop (Kernel.py:190-292)
+ *   mxa_read_summary ... Kernel.runner's ttl_messages / currentTime (Kernel.py:211, 321-326)
+ *   mxa_read_agents .... TradingAgent.holdings / orders (TradingAgent.py:45-46, 112-138)
+ *   mxa_read_book ...... OrderBook.bids / asks (util/OrderBook.py:24-25, 377-398)
+ *   mxa_read_trace ..... (parity tooling; no reference equivalent)
+ */
+#ifndef MXA_H
+#define MXA_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mxa_handle mxa_handle;
+
+enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2 };
+enum {
+  MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
+};
+/* per-env status */
+enum { MXA_ENV_RUNNING = 0, MXA_ENV_DONE = 1, MXA_ENV_ERROR = 2 };
+
+typedef struct {
+  int32_t status;        /* MXA_ENV_* */
+  int32_t err;           /* capacity overflow / reference-crash code when status == ERROR */
+  int64_t events;        /* Kernel pops so far (ttl_messages, incl. busy requeues) */
+  uint64_t hash;         /* rolling FNV-1a-64 over the 10-word trace records */
+  int64_t current_time;  /* Kernel.currentTime, ns since midnight of the simulated date */
+  int64_t order_counter; /* next order id (Order.order_id + 1) */
+  int64_t last_trade;    /* OrderBook.last_trade (cents) */
+  int32_t max_queue, max_book; /* high-water marks of pending events / resting orders */
+} mxa_env_summary;
+
+typedef struct {
+  int64_t cash, shares, n_open;
+  int64_t last_trade;    /* the agent's last known trade price (TradingAgent.last_trade) */
+  int32_t type, flags;   /* agent class, TradingAgent state flags (mxa_layout.h FL_*) */
+} mxa_agent_state;
+
+/* configuration id + per-env seeds (the reference config's -s/--seed) */
+int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device,
+               int32_t trace_cap, mxa_handle** out);
+/* rebuild envs from their seeds (env_mask: NULL = all) — runs the config construction */
+int mxa_reset(mxa_handle* h, const uint8_t* env_mask);
+/* one asynchronous launch: every running env performs up to max_pops kernel pops */
+int mxa_launch(mxa_handle* h, int64_t max_pops);
+int mxa_sync(mxa_handle* h);
+/* launches of `chunk` pops until every env is done/errored (or max_launches reached) */
+int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launches_out);
+int mxa_read_summary(mxa_handle* h, mxa_env_summary* out /* [n_envs] */);
+int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t cap);
+/* book side 0 bids / 1 asks: levels best-first, FIFO within level; each order is
+ * (order_id, agent_id, quantity, price).  Returns the number of orders (<= cap). */
+int mxa_read_book(mxa_handle* h, int32_t env, int32_t side, int64_t* out4, int32_t cap);
+int mxa_read_trace(mxa_handle* h, int32_t env, int64_t* out /* [cap][10] */, int64_t cap, int64_t* n);
+int32_t mxa_n_agents(const mxa_handle* h);
+int32_t mxa_n_envs(const mxa_handle* h);
+/* device memory bytes per env block */
+int64_t mxa_env_bytes(const mxa_handle* h);
+/* replace the handle's HIP stream (hipStream_t as void*); NULL restores the own stream */
+int mxa_set_stream(mxa_handle* h, void* stream);
+/* HIP event timing of the last mxa_run / mxa_launch sequence, milliseconds */
+double mxa_last_kernel_ms(const mxa_handle* h);
+const char* mxa_last_error(const mxa_handle* h);
+void mxa_destroy(mxa_handle* h);
+
+/* parity probes: device numpy-legacy RNG (mode 0 u32, 1 double, 2 randint(a,b),
+ * 3 normal(a,b), 4 exponential(a), 5 uniform(a,b)) and device glibc math
+ * (mode 0 log, 1 exp, 2 pow) */
+int mxa_rng_probe(int32_t device, uint32_t seed, int32_t mode, double a, double b, int32_t n, double* out);
+int mxa_math_probe(int32_t device, int32_t mode, const double* x, const double* y, double* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,452 @@
+// mxa_api.hip — host side of libmxa: the C-ABI declared in include/mxa.h.
+//
+// Builds the per-configuration parameter block (the constants of the reference config
+// scripts), lays out one HBM block per env, and launches the kernels of
+// mxa_kernels.hip (included here so the templates are instantiated in one TU).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mxa.h"
+#include "mxa_kernels.hip"
+
+namespace {
+
+constexpr int64_t NS = 1000000000LL;
+constexpr int64_t MIN = 60 * NS;
+constexpr int64_t HOUR = 60 * MIN;
+
+typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, const MxaParams&, char*, const uint32_t*, const uint8_t*);
+typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, const MxaParams&, char*, int64_t);
+
+template <int SQ, int SO, bool PL>
+void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, const MxaParams& P, char* base, const uint32_t* seeds,
+                  const uint8_t* mask) {
+  hipLaunchKernelGGL((mxa_build_kernel<SQ, SO, PL>), g, b, lds, s, P, base, seeds, mask);
+}
+template <int SQ, int SO, bool PL>
+void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, const MxaParams& P, char* base, int64_t max_pops) {
+  hipLaunchKernelGGL((mxa_run_kernel<SQ, SO, PL>), g, b, lds, s, P, base, max_pops);
+}
+
+__global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int n, int* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && ((const EnvHdr*)(base + (size_t)i * stride))->status == ST_RUNNING) atomicAdd(out, 1);
+}
+
+}  // namespace
+
+struct mxa_handle {
+  MxaParams P;
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  char* d_env = nullptr;
+  uint32_t* d_seeds = nullptr;
+  uint8_t* d_mask = nullptr;
+  int* d_count = nullptr;
+  size_t lds = 0;
+  build_fn build = nullptr;
+  run_fn run = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_ms = 0;
+  std::string err;
+};
+
+static int hip_fail(mxa_handle* h, hipError_t e, const char* what) {
+  if (h) h->err = std::string(what) + ": " + hipGetErrorString(e);
+  return MXA_EHIP;
+}
+#define HIPCHK(h, x)                                 \
+  do {                                               \
+    hipError_t _e = (x);                             \
+    if (_e != hipSuccess) return hip_fail(h, _e, #x); \
+  } while (0)
+
+// ------------------------------------------------------------------ config restatements
+static void base_params(MxaParams& P) {
+  memset(&P, 0, sizeof P);
+  P.o_rbar = 1e5;
+  P.o_kappa = 1.67e-12;
+  P.o_fundvol = 1e-4;
+  P.o_lambda = 2.77778e-13;
+  P.o_msmean = 1e3;
+  P.o_msvar = 5e4;
+  P.starting_cash = 10000000;
+  P.ex_pipeline = 0;
+  P.ex_comp = 0;
+  P.stream_history = 10;
+  P.mkt_open = 9 * HOUR + 30 * MIN;
+}
+
+// config/rmsc03.py:55-235 (defaults of its argparse options)
+static void params_rmsc03(MxaParams& P, int& sq, int& so, bool& pl) {
+  base_params(P);
+  P.config = MXA_CFG_RMSC03;
+  P.mkt_close = 9 * HOUR + 45 * MIN;
+  P.start = P.mkt_open;
+  P.stop = P.mkt_close + MIN;
+  P.default_comp_delay = 0;
+  P.lat_mode = 0;
+  P.noise_len = 1;
+  P.first_noise = 1;
+  P.n_noise = 50;
+  P.first_value = 51;
+  P.n_value = 10;
+  P.first_mm = 61;
+  P.n_mm = 1;
+  P.first_mom = 62;
+  P.n_mom = 2;
+  P.n_agents = 64;
+  P.v_sigma_n = 1e5 / 10;
+  P.v_rbar = 1e5;
+  P.v_kappa = 1.67e-15;
+  P.v_sigma_s = 100000;
+  P.v_lambda = 7e-11;
+  P.v_percent_aggr = 0.1;
+  P.v_depth_spread = 2;
+  P.noise_open = 9 * HOUR;
+  P.noise_close = 16 * HOUR;
+  P.mm_pov = 0.05;
+  P.mm_min_size = 20;
+  P.mm_window = 5;
+  P.mm_ticks = 20;
+  P.mm_wake = NS;
+  P.mom_min = 1;
+  P.mom_max = 10;
+  P.mom_wake = 20 * NS;
+  P.L.open_cap = 128;
+  P.L.tx_cap = 256;
+  P.L.lat_len = 0;
+  sq = 4;
+  so = 2;
+  pl = true;
+}
+
+// config/sparse_zi_100.py:73-334 and sparse_zi_1000.py
+static void params_sparse_zi(MxaParams& P, bool big, int& sq, int& so, bool& pl) {
+  base_params(P);
+  P.config = big ? MXA_CFG_SPARSE_ZI_1000 : MXA_CFG_SPARSE_ZI_100;
+  P.mkt_close = 16 * HOUR;
+  P.start = 0;
+  P.stop = 17 * HOUR;
+  P.default_comp_delay = 1000000000;
+  static const int n100[7] = {15, 15, 14, 14, 14, 14, 14};
+  static const int n1000[7] = {143, 143, 143, 143, 143, 143, 142};
+  static const int rmin[7] = {0, 0, 0, 0, 0, 250, 250};
+  static const int rmax[7] = {250, 500, 1000, 1000, 2000, 500, 500};
+  static const double eta[7] = {1, 1, 0.8, 1, 0.8, 0.8, 1};
+  P.zi_ngroups = 7;
+  int n = 0;
+  for (int g = 0; g < 7; g++) {
+    P.zi_group_count[g] = big ? n1000[g] : n100[g];
+    P.zi_rmin[g] = rmin[g];
+    P.zi_rmax[g] = rmax[g];
+    P.zi_eta[g] = eta[g];
+    n += P.zi_group_count[g];
+  }
+  P.first_zi = 1;
+  P.n_zi = n;
+  P.n_agents = 1 + n;
+  P.zi_sigma_n = 1000000.0;
+  P.zi_rbar = 1e5;
+  P.zi_kappa = 1.67e-15;
+  P.zi_sigma_s = 1e-4;
+  P.zi_lambda = 1e-12;
+  P.zi_sigma_pv = 5e6;
+  P.zi_qmax = 10;
+  if (!big) {
+    P.lat_mode = 2;
+    P.jitter = 0.3;
+    P.clip = 0.05;
+    P.unit = 5;
+    P.lat_lo = 21000;
+    P.lat_hi = 100000;
+    P.L.lat_len = 2 * P.n_agents;
+    sq = 8;
+    so = 2;
+    pl = true;
+  } else {
+    P.lat_mode = 1;
+    P.noise_len = 6;
+    P.lat_lo = 21000;
+    P.lat_hi = 13000000;
+    P.L.lat_len = P.n_agents;
+    sq = 48;
+    so = 16;
+    pl = false;
+  }
+  P.L.open_cap = 8;
+  P.L.tx_cap = 256;
+}
+
+static uint32_t align_up(uint64_t x, uint64_t a) { return (uint32_t)((x + a - 1) / a * a); }
+
+static void layout(MxaParams& P, int sq, int so, bool pl, int trace_cap) {
+  Layout& L = P.L;
+  P.n_streams = 4 + P.n_agents;
+  L.n_agents = P.n_agents;
+  L.n_streams = P.n_streams;
+  L.qcap = sq * 64;
+  L.ocap = so * 64;
+  L.trace_cap = trace_cap;
+  uint64_t off = align_up(sizeof(EnvHdr), 256);
+  L.off_ag = (uint32_t)off;
+  off = align_up(off + (uint64_t)P.n_agents * 512, 256);
+  L.off_open = (uint32_t)off;
+  off = align_up(off + (uint64_t)P.n_agents * L.open_cap * sizeof(OpenOrder), 256);
+  L.off_rng = (uint32_t)off;
+  off = align_up(off + (uint64_t)P.n_streams * MXA_RNG_WORDS * 4, 256);
+  L.off_lat = (uint32_t)off;
+  off = align_up(off + (uint64_t)L.lat_len * 8, 256);
+  L.off_q = (uint32_t)off;
+  off = align_up(off + (uint64_t)L.qcap * sizeof(SavedEvent) + (pl ? 0 : (uint64_t)L.qcap * 24), 256);
+  L.off_book = (uint32_t)off;
+  off = align_up(off + (uint64_t)L.ocap * sizeof(SavedOrder), 256);
+  L.off_tx = (uint32_t)off;
+  off = align_up(off + 64 + (uint64_t)L.tx_cap * sizeof(TxRec), 256);
+  L.off_trace = (uint32_t)off;
+  off = align_up(off + (uint64_t)trace_cap * MXA_TRACE_WORDS * 8, 256);
+  L.env_stride = off;
+}
+
+template <int SQ, int SO, bool PL>
+static void bind(mxa_handle* h) {
+  h->build = launch_build<SQ, SO, PL>;
+  h->run = launch_run<SQ, SO, PL>;
+  h->lds = (size_t)SQ * 64 * (12 + (PL ? 24 : 0));
+}
+
+extern "C" {
+
+int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device, int32_t trace_cap,
+               mxa_handle** out) {
+  if (!out || n_envs <= 0 || !seeds || trace_cap < 0) return MXA_EINVAL;
+  mxa_handle* h = new mxa_handle();
+  int sq = 0, so = 0;
+  bool pl = true;
+  if (config == MXA_RMSC03) params_rmsc03(h->P, sq, so, pl);
+  else if (config == MXA_SPARSE_ZI_100) params_sparse_zi(h->P, false, sq, so, pl);
+  else if (config == MXA_SPARSE_ZI_1000) params_sparse_zi(h->P, true, sq, so, pl);
+  else {
+    delete h;
+    return MXA_EINVAL;
+  }
+  h->P.n_envs = n_envs;
+  layout(h->P, sq, so, pl, trace_cap);
+  if (sq == 4 && so == 2 && pl) bind<4, 2, true>(h);
+  else if (sq == 8 && so == 2 && pl) bind<8, 2, true>(h);
+  else bind<48, 16, false>(h);
+  h->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    *out = h;
+    return hip_fail(h, e, "hipSetDevice");
+  }
+  *out = h;
+  HIPCHK(h, hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking));
+  h->stream = h->own;
+  HIPCHK(h, hipEventCreate(&h->ev0));
+  HIPCHK(h, hipEventCreate(&h->ev1));
+  size_t bytes = (size_t)h->P.L.env_stride * n_envs;
+  HIPCHK(h, hipMalloc(&h->d_env, bytes));
+  HIPCHK(h, hipMalloc(&h->d_seeds, sizeof(uint32_t) * n_envs));
+  HIPCHK(h, hipMalloc(&h->d_mask, n_envs));
+  HIPCHK(h, hipMalloc(&h->d_count, sizeof(int)));
+  HIPCHK(h, hipMemsetAsync(h->d_env, 0, bytes, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->d_seeds, seeds, sizeof(uint32_t) * n_envs, hipMemcpyHostToDevice, h->stream));
+  return mxa_reset(h, nullptr);
+}
+
+int mxa_reset(mxa_handle* h, const uint8_t* mask) {
+  if (!h) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  const uint8_t* dm = nullptr;
+  if (mask) {
+    HIPCHK(h, hipMemcpyAsync(h->d_mask, mask, h->P.n_envs, hipMemcpyHostToDevice, h->stream));
+    dm = h->d_mask;
+  }
+  h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->P, h->d_env, h->d_seeds, dm);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_launch(mxa_handle* h, int64_t max_pops) {
+  if (!h) return MXA_EINVAL;
+  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->P, h->d_env, max_pops);
+  HIPCHK(h, hipGetLastError());
+  return MXA_OK;
+}
+
+int mxa_sync(mxa_handle* h) {
+  if (!h) return MXA_EINVAL;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launches_out) {
+  if (!h || chunk <= 0) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  int launches = 0;
+  float total = 0;
+  for (;;) {
+    if (max_launches > 0 && launches >= max_launches) break;
+    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->P, h->d_env, chunk);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    launches++;
+    HIPCHK(h, hipMemsetAsync(h->d_count, 0, sizeof(int), h->stream));
+    int n = h->P.n_envs;
+    hipLaunchKernelGGL(mxa_count_running_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env,
+                       h->P.L.env_stride, n, h->d_count);
+    int running = 0;
+    HIPCHK(h, hipMemcpyAsync(&running, h->d_count, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    float ms = 0;
+    HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    total += ms;
+    if (running == 0) break;
+  }
+  h->last_ms = total;
+  if (launches_out) *launches_out = launches;
+  return MXA_OK;
+}
+
+int mxa_read_summary(mxa_handle* h, mxa_env_summary* out) {
+  if (!h || !out) return MXA_EINVAL;
+  int n = h->P.n_envs;
+  std::vector<EnvHdr> hd(n);
+  HIPCHK(h, hipMemcpy2DAsync(hd.data(), sizeof(EnvHdr), h->d_env, h->P.L.env_stride, sizeof(EnvHdr), n,
+                             hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (int i = 0; i < n; i++) {
+    out[i].status = hd[i].status;
+    out[i].err = hd[i].err;
+    out[i].events = hd[i].pops;
+    out[i].hash = hd[i].hash;
+    out[i].current_time = hd[i].cur;
+    out[i].order_counter = hd[i].order_counter;
+    out[i].last_trade = hd[i].last_trade;
+    out[i].max_queue = hd[i].max_q;
+    out[i].max_book = hd[i].max_book;
+  }
+  return MXA_OK;
+}
+
+int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t cap) {
+  if (!h || env < 0 || env >= h->P.n_envs) return MXA_ERANGE;
+  int n = std::min(cap, h->P.n_agents);
+  std::vector<uint32_t> rec((size_t)h->P.n_agents * 128);
+  HIPCHK(h, hipMemcpy(rec.data(), h->d_env + (size_t)env * h->P.L.env_stride + h->P.L.off_ag, rec.size() * 4,
+                      hipMemcpyDeviceToHost));
+  for (int a = 0; a < n; a++) {
+    const uint32_t* r = &rec[(size_t)a * 128];
+    auto g64 = [&](int f) { return (int64_t)(((uint64_t)r[f + 1] << 32) | r[f]); };
+    out[a].cash = g64(AF_CASH);
+    out[a].shares = g64(AF_SHARES);
+    out[a].n_open = (int32_t)r[AF_NORD];
+    out[a].last_trade = g64(AF_LAST_TRADE);
+    out[a].type = (int32_t)r[AF_TYPE];
+    out[a].flags = (int32_t)r[AF_FLAGS];
+  }
+  return n;
+}
+
+int mxa_read_book(mxa_handle* h, int32_t env, int32_t side, int64_t* out4, int32_t cap) {
+  if (!h || env < 0 || env >= h->P.n_envs) return MXA_ERANGE;
+  int oc = h->P.L.ocap;
+  std::vector<SavedOrder> so(oc);
+  HIPCHK(h, hipMemcpy(so.data(), h->d_env + (size_t)env * h->P.L.env_stride + h->P.L.off_book,
+                      sizeof(SavedOrder) * oc, hipMemcpyDeviceToHost));
+  std::vector<SavedOrder> v;
+  int buy = side == 0 ? 1 : 0;
+  for (auto& o : so)
+    if (o.meta >= 0 && (o.meta & 1) == buy) v.push_back(o);
+  std::sort(v.begin(), v.end(), [&](const SavedOrder& a, const SavedOrder& b) {
+    if (a.price != b.price) return buy ? a.price > b.price : a.price < b.price;
+    return a.arrival < b.arrival;
+  });
+  int n = 0;
+  for (auto& o : v) {
+    if (n >= cap) break;
+    out4[4 * n + 0] = o.oid;
+    out4[4 * n + 1] = o.meta >> 1;
+    out4[4 * n + 2] = o.qty;
+    out4[4 * n + 3] = o.price;
+    n++;
+  }
+  return (int)v.size() <= cap ? (int)v.size() : n;
+}
+
+int mxa_read_trace(mxa_handle* h, int32_t env, int64_t* out, int64_t cap, int64_t* nout) {
+  if (!h || env < 0 || env >= h->P.n_envs) return MXA_ERANGE;
+  EnvHdr hd;
+  char* e = h->d_env + (size_t)env * h->P.L.env_stride;
+  HIPCHK(h, hipMemcpy(&hd, e, sizeof hd, hipMemcpyDeviceToHost));
+  int64_t n = std::min<int64_t>(std::min<int64_t>(hd.trace_len, h->P.L.trace_cap), cap);
+  if (n > 0) HIPCHK(h, hipMemcpy(out, e + h->P.L.off_trace, (size_t)n * 80, hipMemcpyDeviceToHost));
+  if (nout) *nout = n;
+  return MXA_OK;
+}
+
+int32_t mxa_n_agents(const mxa_handle* h) { return h ? h->P.n_agents : 0; }
+int32_t mxa_n_envs(const mxa_handle* h) { return h ? h->P.n_envs : 0; }
+int64_t mxa_env_bytes(const mxa_handle* h) { return h ? (int64_t)h->P.L.env_stride : 0; }
+int mxa_set_stream(mxa_handle* h, void* s) {
+  if (!h) return MXA_EINVAL;
+  h->stream = s ? (hipStream_t)s : h->own;
+  return MXA_OK;
+}
+double mxa_last_kernel_ms(const mxa_handle* h) { return h ? h->last_ms : 0; }
+const char* mxa_last_error(const mxa_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+void mxa_destroy(mxa_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->device);
+  if (h->d_env) hipFree(h->d_env);
+  if (h->d_seeds) hipFree(h->d_seeds);
+  if (h->d_mask) hipFree(h->d_mask);
+  if (h->d_count) hipFree(h->d_count);
+  if (h->ev0) hipEventDestroy(h->ev0);
+  if (h->ev1) hipEventDestroy(h->ev1);
+  if (h->own) hipStreamDestroy(h->own);
+  delete h;
+}
+
+int mxa_rng_probe(int32_t device, uint32_t seed, int32_t mode, double a, double b, int32_t n, double* out) {
+  if (n <= 0 || !out) return MXA_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return MXA_EHIP;
+  double* d_out = nullptr;
+  uint32_t* d_s = nullptr;
+  if (hipMalloc(&d_out, sizeof(double) * n) != hipSuccess) return MXA_ENOMEM;
+  if (hipMalloc(&d_s, MXA_RNG_WORDS * 4) != hipSuccess) return MXA_ENOMEM;
+  hipLaunchKernelGGL(mxa_rng_probe_kernel, dim3(1), dim3(64), 0, 0, seed, mode, a, b, n, d_out, d_s);
+  hipError_t e = hipMemcpy(out, d_out, sizeof(double) * n, hipMemcpyDeviceToHost);
+  hipFree(d_out);
+  hipFree(d_s);
+  return e == hipSuccess ? MXA_OK : MXA_EHIP;
+}
+
+int mxa_math_probe(int32_t device, int32_t mode, const double* x, const double* y, double* out, int64_t n) {
+  if (n <= 0 || !x || !out) return MXA_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return MXA_EHIP;
+  double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  size_t bytes = sizeof(double) * n;
+  if (hipMalloc(&dx, bytes) != hipSuccess || hipMalloc(&dy, bytes) != hipSuccess || hipMalloc(&dout, bytes) != hipSuccess)
+    return MXA_ENOMEM;
+  hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice);
+  hipMemcpy(dy, y ? y : x, bytes, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(mxa_math_probe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, mode, dx, dy, dout, n);
+  hipError_t e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+  hipFree(dx);
+  hipFree(dy);
+  hipFree(dout);
+  return e == hipSuccess ? MXA_OK : MXA_EHIP;
+}
+
+}  // extern "C"

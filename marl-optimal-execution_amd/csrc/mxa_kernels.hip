@@ -1,0 +1,1706 @@
+// mxa_kernels.hip — MI355X (gfx950) kernels of the vectorised ABIDES market step.
+//
+// Execution model: ONE wavefront (64 lanes) simulates ONE independent market (env)
+// end to end — the reference's Kernel.runner loop (Kernel.py:190-292) with its
+// agents.  Control flow is wave-uniform (every branch of every agent handler is taken
+// by the whole wave, so there is no divergence between envs); the 64 lanes are used as
+// a SIMD engine for the data-parallel parts of each event:
+//   * event queue (heapq of Kernel.messages): QCAP slots in LDS; every lane owns
+//     SQ slots and caches their minimum (t, recipient, type, seq) key in VGPRs, so a
+//     pop is one 64-lane lexicographic min-reduction + one rescan by the winning lane;
+//   * limit order book (util/OrderBook.py): a pool of OCAP resting orders held in VGPRs
+//     (SO slots per lane); best price, level volume and FIFO head (price-time priority)
+//     are wave min/max/sum reductions, so insert/cancel/match never walk a list;
+//   * MT19937 twist (numpy legacy RandomState): cooperative over the 64 lanes;
+//   * agent state: the recipient's 512-byte record is loaded with ONE coalesced
+//     64-lane load per event and its fields read with v_readlane.
+// Everything that is not in LDS/VGPRs is one contiguous per-env HBM block (mxa_layout.h).
+//
+// Arithmetic follows the reference bit for bit: numpy-legacy MT19937 and distributions,
+// glibc log/exp/pow (glibc_math.h), Python round-half-even / truncation, pandas ns
+// truncation.  Compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include "glibc_math.h"
+#include "mxa_layout.h"
+
+typedef uint64_t u64;
+typedef int64_t i64;
+typedef uint32_t u32;
+typedef int32_t i32;
+
+#define DEV __device__ __forceinline__
+#define FNV_OFF 0xCBF29CE484222325ull
+#define FNV_PRIME 0x100000001B3ull
+#define KEY_EMPTY 0xFFFFFFFFFFFFFFFFull
+#define NS_SEC 1000000000LL
+
+namespace mxa {
+
+DEV int laneid() { return (int)__lane_id(); }
+DEV u32 rdl(u32 v, int l) { return (u32)__builtin_amdgcn_readlane((int)v, l); }
+DEV i32 rdli(i32 v, int l) { return __builtin_amdgcn_readlane(v, l); }
+DEV u64 rdl64(u64 v, int l) {
+  return ((u64)rdl((u32)(v >> 32), l) << 32) | rdl((u32)v, l);
+}
+DEV u64 bal(bool p) { return __ballot(p); }
+DEV int ffs64(u64 b) { return __ffsll((unsigned long long)b) - 1; }
+DEV int ffs32(u32 b) { return __ffs(b) - 1; }
+DEV u32 sxor(u32 v, int m) { return (u32)__shfl_xor((int)v, m, 64); }
+DEV i32 wmax_i32(i32 v) {
+  for (int o = 1; o < 64; o <<= 1) { i32 t = (i32)sxor((u32)v, o); v = t > v ? t : v; }
+  return v;
+}
+DEV i32 wmin_i32(i32 v) {
+  for (int o = 1; o < 64; o <<= 1) { i32 t = (i32)sxor((u32)v, o); v = t < v ? t : v; }
+  return v;
+}
+DEV u32 wmin_u32(u32 v) {
+  for (int o = 1; o < 64; o <<= 1) { u32 t = sxor(v, o); v = t < v ? t : v; }
+  return v;
+}
+DEV i64 wsum_i64(i64 v) {
+  for (int o = 1; o < 64; o <<= 1) {
+    u64 u = (u64)v;
+    u64 t = ((u64)sxor((u32)(u >> 32), o) << 32) | sxor((u32)u, o);
+    v += (i64)t;
+  }
+  return v;
+}
+DEV void wfence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+DEV i64 py_round(double x) { return (i64)__builtin_rint(x); }
+DEV double as_d(u64 x) { return __builtin_bit_cast(double, x); }
+DEV u64 as_u(double x) { return __builtin_bit_cast(u64, x); }
+
+// ------------------------------------------------------------------------------------
+// numpy legacy RandomState (numpy/random/src/mt19937, distributions/legacy)
+// ------------------------------------------------------------------------------------
+struct RS {
+  u32* key;
+  i32 pos, hasg;
+  double gauss;
+};
+
+// cooperative MT19937 generation step (mt19937_gen) over the wave, in four dependency
+// phases: [0,227) reads only old words; [227,454) reads phase-1 words at i-227;
+// [454,623) reads [227,396); 623 reads key[0] and key[396].
+DEV void mt_twist(u32* key) {
+  const int lane = laneid();
+  for (int b = 0; b < 227; b += 64) {
+    int i = b + lane;
+    if (i < 227) {
+      u32 y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
+      key[i] = key[i + 397] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
+  }
+  wfence();
+  for (int b = 227; b < 454; b += 64) {
+    int i = b + lane;
+    if (i < 454) {
+      u32 y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
+      key[i] = key[i - 227] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
+  }
+  wfence();
+  for (int b = 454; b < 623; b += 64) {
+    int i = b + lane;
+    if (i < 623) {
+      u32 y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
+      key[i] = key[i - 227] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
+  }
+  wfence();
+  if (lane == 0) {
+    u32 y = (key[623] & 0x80000000u) | (key[0] & 0x7fffffffu);
+    key[623] = key[396] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+  }
+  wfence();
+}
+
+// init_genrand (numpy _legacy_seeding with an int): every lane runs the recurrence,
+// lane (i % 64) stores word i.
+DEV void mt_seed(u32* key, u32 s) {
+  const int lane = laneid();
+  for (int i = 0; i < MXA_MT_N; i++) {
+    if ((i & 63) == lane) key[i] = s;
+    s = 1812433253u * (s ^ (s >> 30)) + (u32)i + 1u;
+  }
+  wfence();
+}
+
+DEV u32 rs_u32(RS& r) {
+  if (r.pos >= MXA_MT_N) {
+    mt_twist(r.key);
+    r.pos = 0;
+  }
+  u32 y = r.key[r.pos];
+  r.pos++;
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+DEV double rs_double(RS& r) {
+  i32 a = (i32)(rs_u32(r) >> 5);
+  i32 b = (i32)(rs_u32(r) >> 6);
+  return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+DEV i64 rs_randint(RS& r, i64 lo, i64 hi) {
+  u64 rng = (u64)(hi - lo - 1);
+  if (rng == 0) return lo;
+  if (rng == 0xFFFFFFFFull) return lo + (i64)rs_u32(r);
+  u32 mask = (u32)rng;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+  u32 v;
+  do {
+    v = rs_u32(r) & mask;
+  } while (v > (u32)rng);
+  return lo + (i64)v;
+}
+DEV double rs_gauss(RS& r) {
+  if (r.hasg) {
+    double t = r.gauss;
+    r.hasg = 0;
+    r.gauss = 0.0;
+    return t;
+  }
+  double f, x1, x2, r2;
+  do {
+    x1 = 2.0 * rs_double(r) - 1.0;
+    x2 = 2.0 * rs_double(r) - 1.0;
+    r2 = x1 * x1 + x2 * x2;
+  } while (r2 >= 1.0 || r2 == 0.0);
+  f = __builtin_sqrt(-2.0 * gm_log(r2) / r2);
+  r.gauss = f * x1;
+  r.hasg = 1;
+  return f * x2;
+}
+DEV double rs_normal(RS& r, double loc, double scale) { return loc + scale * rs_gauss(r); }
+DEV double rs_exponential(RS& r, double scale) { return scale * -gm_log(1.0 - rs_double(r)); }
+DEV double rs_uniform(RS& r, double lo, double hi) { return lo + (hi - lo) * rs_double(r); }
+// advance a stream by k 32-bit outputs without tempering them (whole blocks = one twist)
+DEV void rs_skip_words(RS& r, i64 k) {
+  while (k > 0) {
+    if (r.pos >= MXA_MT_N) {
+      mt_twist(r.key);
+      r.pos = 0;
+    }
+    i64 step = MXA_MT_N - r.pos;
+    if (step > k) step = k;
+    r.pos += (i32)step;
+    k -= step;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// message payload (24 B)
+// ------------------------------------------------------------------------------------
+struct Msg {
+  u32 w[6];
+};
+DEV u32 m_kind(const Msg& m) { return m.w[0] & 63u; }
+DEV int m_buy(const Msg& m) { return (m.w[0] >> 6) & 1; }
+DEV int m_closed(const Msg& m) { return (m.w[0] >> 7) & 1; }
+DEV int m_dfloat(const Msg& m) { return (m.w[0] >> 8) & 1; }
+DEV int m_nb(const Msg& m) { return (m.w[0] >> 9) & 1; }
+DEV int m_na(const Msg& m) { return (m.w[0] >> 10) & 1; }
+DEV int m_hasdata(const Msg& m) { return (m.w[0] >> 11) & 1; }
+DEV i32 m_agent(const Msg& m) { return (i32)(m.w[0] >> 16); }
+DEV i64 m_i64(const Msg& m, int i) { return (i64)(((u64)m.w[i + 1] << 32) | m.w[i]); }
+DEV u32 msel(const Msg& m, int i) {
+  u32 v = m.w[0];
+  v = i == 1 ? m.w[1] : v;
+  v = i == 2 ? m.w[2] : v;
+  v = i == 3 ? m.w[3] : v;
+  v = i == 4 ? m.w[4] : v;
+  v = i == 5 ? m.w[5] : v;
+  return v;
+}
+DEV Msg msg_make(u32 kind, i32 agent) {
+  Msg m;
+  m.w[0] = kind | ((u32)agent << 16);
+  m.w[1] = m.w[2] = m.w[3] = m.w[4] = m.w[5] = 0;
+  return m;
+}
+DEV Msg msg_order(u32 kind, i32 oid, i32 agent, int is_buy, i32 qty, i32 price, i32 fill) {
+  Msg m = msg_make(kind, agent);
+  m.w[0] |= (u32)is_buy << 6;
+  m.w[1] = (u32)oid;
+  m.w[2] = (u32)qty;
+  m.w[3] = (u32)price;
+  m.w[4] = (u32)fill;
+  return m;
+}
+
+// the 10-word parity record (tests/golden/gen_fixtures.py encode())
+DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
+  for (int i = 0; i < 10; i++) rec[i] = 0;
+  rec[0] = (i64)(key >> 13);
+  rec[1] = (i64)((key >> 2) & 0x7FF);
+  i32 type = (i32)(key & 3);
+  rec[2] = type;
+  u32 k = m_kind(m);
+  if (type != MT_MESSAGE) {
+    rec[3] = type == MT_WAKEUP ? MK_WAKEUP : MK_KCANCEL;
+    return;
+  }
+  rec[3] = k;
+  i64* f = rec + 4;
+  switch (k) {
+  case MK_WHEN_OPEN_REQ: case MK_WHEN_CLOSE_REQ: case MK_LAST_REQ:
+    f[0] = m_agent(m);
+    break;
+  case MK_WHEN_OPEN: case MK_WHEN_CLOSE:
+    f[0] = m_i64(m, 1);
+    break;
+  case MK_SPREAD_REQ:
+    f[0] = m_agent(m);
+    f[1] = (i32)m.w[1];
+    break;
+  case MK_SPREAD: {
+    int nb = m_nb(m), na = m_na(m);
+    i64 d = (i32)m.w[5];
+    f[0] = nb ? (i64)(i32)m.w[1] : -1;
+    f[1] = nb ? (i64)(i32)m.w[2] : 0;
+    f[2] = na ? (i64)(i32)m.w[3] : -1;
+    f[3] = na ? (i64)(i32)m.w[4] : 0;
+    f[4] = !m_hasdata(m) ? -1 : (m_dfloat(m) ? d * 10000 : d);
+    f[5] = (i64)m_closed(m) + 2 * (i64)nb + ((i64)1 << 20) * na;
+    break;
+  }
+  case MK_LAST: {
+    i64 d = (i32)m.w[5];
+    f[0] = !m_hasdata(m) ? -1 : (m_dfloat(m) ? d * 10000 : d);
+    f[5] = m_closed(m);
+    break;
+  }
+  case MK_TV_REQ:
+    f[0] = m_agent(m);
+    f[1] = m_i64(m, 1);
+    break;
+  case MK_TV:
+    f[0] = m_i64(m, 1);
+    f[5] = m_closed(m);
+    break;
+  case MK_LIMIT: case MK_ACCEPTED: case MK_CANCELLED: case MK_MODIFY: case MK_MODIFIED:
+  case MK_CANCEL: case MK_EXECUTED:
+    f[0] = (i32)m.w[1];
+    f[1] = m_agent(m);
+    f[2] = m_buy(m);
+    f[3] = k == MK_CANCEL ? 0 : (i64)(i32)m.w[2];
+    f[4] = (i32)m.w[3];
+    if (k == MK_EXECUTED) f[5] = (i32)m.w[4];
+    break;
+  default:
+    break;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// the engine: one instance per wave (= per env), lives in registers / LDS
+// ------------------------------------------------------------------------------------
+template <int SQ, int SO, bool PL_LDS>
+struct Eng {
+  static constexpr int QCAP = SQ * 64;
+  const MxaParams& P;
+  char* env;
+  int lane;
+  EnvHdr h;
+  // event queue: keys in LDS, payload in LDS (PL_LDS) or HBM; per-lane min cache
+  u64* qk;
+  u32* qs;
+  u32* qpl;
+  u64 mk;
+  u32 ms;
+  i32 mj;
+  u64 qfree;
+  // order book pool in VGPRs: slot (j, lane)
+  i32 bp[SO], bq[SO], bo[SO], bm[SO], bh[SO];
+  u32 ba[SO];
+  // current agent record (lane l holds dwords 2l, 2l+1)
+  u32 rlo, rhi;
+  i32 cur_agent;
+  i64 add_delay;
+  i64* trace;
+
+  DEV Eng(const MxaParams& p, char* e, char* lds) : P(p), env(e) {
+    lane = laneid();
+    qk = (u64*)lds;
+    qs = (u32*)(lds + 8 * QCAP);
+    if (PL_LDS) qpl = (u32*)(lds + 12 * QCAP);
+    else qpl = (u32*)(env + P.L.off_q + sizeof(SavedEvent) * QCAP);
+    trace = P.L.trace_cap ? (i64*)(env + P.L.off_trace) : nullptr;
+  }
+
+  // ---------------- env block accessors
+  DEV EnvHdr* hdr() { return (EnvHdr*)env; }
+  DEV u64* agent_ptr(int a) { return (u64*)(env + P.L.off_ag + (size_t)a * 512); }
+  DEV OpenOrder* open_ptr(int a) { return (OpenOrder*)(env + P.L.off_open + (size_t)a * P.L.open_cap * sizeof(OpenOrder)); }
+  DEV u32* rng_key(int s) { return (u32*)(env + P.L.off_rng + (size_t)s * MXA_RNG_WORDS * 4); }
+  DEV double* lat() { return (double*)(env + P.L.off_lat); }
+  DEV i32* ep_entries() { return (i32*)(env + P.L.off_tx); }               // 16 x i32
+  DEV TxRec* txr() { return (TxRec*)(env + P.L.off_tx + 64); }
+
+  DEV void fail(int code) {
+    if (h.status != ST_ERROR) {
+      h.status = ST_ERROR;
+      h.err = code;
+    }
+  }
+
+  // ---------------- agent record
+  DEV void rec_load(int a) {
+    u64 v = agent_ptr(a)[lane];
+    rlo = (u32)v;
+    rhi = (u32)(v >> 32);
+    cur_agent = a;
+  }
+  DEV void rec_store() { agent_ptr(cur_agent)[lane] = ((u64)rhi << 32) | rlo; }
+  DEV u32 rg(int f) { return (f & 1) ? rdl(rhi, f >> 1) : rdl(rlo, f >> 1); }
+  DEV i32 rgi(int f) { return (i32)rg(f); }
+  DEV i64 rg64(int f) { return (i64)(((u64)rdl(rhi, f >> 1) << 32) | rdl(rlo, f >> 1)); }
+  DEV double rgd(int f) { return as_d((u64)rg64(f)); }
+  DEV void rs(int f, u32 v) {
+    if (lane == (f >> 1)) {
+      if (f & 1) rhi = v;
+      else rlo = v;
+    }
+  }
+  DEV void rs64(int f, i64 v) {
+    if (lane == (f >> 1)) {
+      rlo = (u32)(u64)v;
+      rhi = (u32)((u64)v >> 32);
+    }
+  }
+  DEV void rsd(int f, double v) { rs64(f, (i64)as_u(v)); }
+  DEV u32 flags() { return rg(AF_FLAGS); }
+  DEV bool fl(u32 bit) { return (flags() & bit) != 0; }
+  DEV void fl_set(u32 bit, bool on) {
+    u32 f = flags();
+    rs(AF_FLAGS, on ? (f | bit) : (f & ~bit));
+  }
+
+  // agent RNG stream (Agent.random_state): key words in HBM, pos/gauss cache in the record
+  DEV RS agent_rs() {
+    RS r;
+    r.key = rng_key(4 + cur_agent);
+    r.pos = rgi(AF_RS_POS);
+    r.hasg = rgi(AF_RS_HASG);
+    r.gauss = rgd(AF_RS_GAUSS);
+    return r;
+  }
+  DEV void agent_rs_put(const RS& r) {
+    rs(AF_RS_POS, (u32)r.pos);
+    rs(AF_RS_HASG, (u32)r.hasg);
+    rsd(AF_RS_GAUSS, r.gauss);
+  }
+  // global streams: 0 = G (np.random), 1 = O (oracle symbol), 2 = K (kernel), 3 = L (latency)
+  DEV RS grs(int s) {
+    RS r;
+    r.key = rng_key(s);
+    r.pos = h.rs_pos[s];
+    r.hasg = h.rs_has_gauss[s];
+    r.gauss = h.rs_gauss[s];
+    return r;
+  }
+  DEV void grs_put(int s, const RS& r) {
+    h.rs_pos[s] = r.pos;
+    h.rs_has_gauss[s] = r.hasg;
+    h.rs_gauss[s] = r.gauss;
+  }
+
+  // ---------------- event queue
+  DEV void q_rescan() {  // lane-local: recompute this lane's min over its slots
+    u64 bk = KEY_EMPTY;
+    u32 bs = 0xFFFFFFFFu;
+    i32 bj = -1;
+    for (int j = 0; j < SQ; j++) {
+      int slot = j * 64 + lane;
+      u64 k = qk[slot];
+      u32 s = qs[slot];
+      if (k < bk || (k == bk && s < bs)) {
+        bk = k;
+        bs = s;
+        bj = j;
+      }
+    }
+    mk = bk;
+    ms = bs;
+    mj = bj;
+  }
+  DEV void pl_write(int slot, const Msg& m) {
+    for (int i = 0; i < 6; i++) qpl[slot * 6 + i] = m.w[i];
+  }
+  DEV Msg pl_read(int slot) {
+    Msg m;
+    for (int i = 0; i < 6; i++) m.w[i] = qpl[slot * 6 + i];
+    return m;
+  }
+  DEV void q_push(u64 key, u32 seq, const Msg& m) {
+    u64 b = bal(qfree != 0);
+    if (b == 0) {
+      fail(ERR_QUEUE_FULL);
+      return;
+    }
+    int r = (int)(seq & 63u);
+    u64 rot = r ? ((b >> r) | (b << (64 - r))) : b;
+    int L = (ffs64(rot) + r) & 63;
+    u64 fm = rdl64(qfree, L);
+    int j = ffs64(fm);
+    int slot = j * 64 + L;
+    if (lane == L) {
+      qk[slot] = key;
+      qs[slot] = seq;
+      qfree &= ~(1ull << j);
+      if (key < mk || (key == mk && seq < ms)) {
+        mk = key;
+        ms = seq;
+        mj = j;
+      }
+      if (PL_LDS) pl_write(slot, m);
+    }
+    if (!PL_LDS) {
+      if (lane < 6) qpl[slot * 6 + lane] = msel(m, lane);
+    }
+    h.q_count++;
+    if (h.q_count > h.max_q) h.max_q = h.q_count;
+  }
+  // lexicographic wave-min of the per-lane cached (key, seq); returns winning slot or -1
+  DEV int q_peek(u64& key, u32& seq) {
+    u64 k = mk;
+    u32 s = ms;
+    for (int o = 1; o < 64; o <<= 1) {
+      u64 k2 = ((u64)sxor((u32)(k >> 32), o) << 32) | sxor((u32)k, o);
+      u32 s2 = sxor(s, o);
+      bool lt = k2 < k || (k2 == k && s2 < s);
+      k = lt ? k2 : k;
+      s = lt ? s2 : s;
+    }
+    key = k;
+    seq = s;
+    if (k == KEY_EMPTY) return -1;
+    u64 b = bal(mk == k && ms == s);
+    int L = ffs64(b);
+    int j = rdli(mj, L);
+    return j * 64 + L;
+  }
+  DEV void q_remove(int slot) {
+    if (lane == (slot & 63)) {
+      qk[slot] = KEY_EMPTY;
+      qs[slot] = 0xFFFFFFFFu;
+      qfree |= 1ull << (slot >> 6);
+      q_rescan();
+    }
+    h.q_count--;
+  }
+  DEV void q_rekey(int slot, u64 key) {
+    if (lane == (slot & 63)) {
+      qk[slot] = key;
+      q_rescan();
+    }
+  }
+
+  // ---------------- kernel services
+  // Kernel.sendMessage (Kernel.py:347-425)
+  DEV void send(int recipient, const Msg& m, i64 delay) {
+    i64 sent = h.cur + rg64(AF_COMP) + add_delay + delay;
+    i64 deliver;
+    if (P.lat_mode == 2) {
+      RS L = grs(3);
+      double x = rs_uniform(L, P.clip, 1.0);
+      grs_put(3, L);
+      double mn = cur_agent == 0 ? lat()[recipient] : lat()[P.n_agents + cur_agent];
+      double l = mn + ((P.jitter / gm_pow(x, 3.0)) * (mn / P.unit));
+      deliver = sent + (i64)l;
+    } else {
+      double l = 0.0;
+      if (P.lat_mode == 1) l = lat()[cur_agent == 0 ? recipient : cur_agent];
+      i64 noise = 0;
+      if (P.noise_len > 1) {
+        RS K = grs(2);
+        noise = rs_randint(K, 0, P.noise_len);
+        grs_put(2, K);
+      }
+      deliver = sent + (i64)(l + (double)noise);
+    }
+    u64 key = ((u64)deliver << 13) | ((u64)recipient << 2) | MT_MESSAGE;
+    q_push(key, h.seq++, m);
+  }
+  // Kernel.setWakeup (Kernel.py:435-462)
+  DEV void wakeup_at(int agent, i64 t) {
+    if (t < h.cur) {
+      fail(ERR_WAKEUP_PAST);
+      return;
+    }
+    Msg m = msg_make(MK_WAKEUP, 0);
+    u64 key = ((u64)t << 13) | ((u64)agent << 2) | MT_WAKEUP;
+    q_push(key, h.seq++, m);
+  }
+  DEV i64 next_order_id() { return h.order_counter++; }
+
+  // ---------------- SparseMeanRevertingOracle (SMRO:88-227)
+  DEV double o_compute(i64 ts, double v_adj, i64 pt, double pv) {
+    i64 d = ts - pt;
+    double mu = P.o_rbar, gamma = P.o_kappa, theta = P.o_fundvol;
+    double loc = mu + (pv - mu) * gm_exp(-gamma * (double)d);
+    double scale = (gm_pow(theta, 2.0) / (2 * gamma)) * (1 - gm_exp(-2 * gamma * (double)d));
+    RS O = grs(1);
+    double v = rs_normal(O, loc, scale);
+    grs_put(1, O);
+    v += v_adj;
+    if (!(v > 0)) v = 0;
+    i64 vi = py_round(v);
+    h.o_pt = ts;
+    h.o_pv = (double)vi;
+    return (double)vi;
+  }
+  DEV double o_advance(i64 t) {
+    i64 pt = h.o_pt;
+    double pv = h.o_pv;
+    if (t <= pt) return pv;
+    while (h.o_mst < t) {
+      double v = o_compute(h.o_mst, h.o_msv, pt, pv);
+      pt = h.o_mst;
+      pv = v;
+      RS G = grs(0);
+      h.o_mst = pt + (i64)rs_exponential(G, 1.0 / P.o_lambda);
+      grs_put(0, G);
+      RS O = grs(1);
+      double msv = rs_normal(O, P.o_msmean, __builtin_sqrt(P.o_msvar));
+      h.o_msv = rs_randint(O, 0, 2) == 0 ? msv : -msv;
+      grs_put(1, O);
+    }
+    return o_compute(t, 0, pt, pv);
+  }
+  DEV i64 o_observe(i64 t, double sigma_n) {
+    double r_t = t >= P.mkt_close ? o_advance(P.mkt_close - 1) : o_advance(t);
+    if (sigma_n == 0) return (i64)r_t;
+    RS A = agent_rs();
+    i64 obs = py_round(rs_normal(A, r_t, __builtin_sqrt(sigma_n)));
+    agent_rs_put(A);
+    return obs;
+  }
+
+  // ---------------- order book pool (VGPR resident)
+  DEV i32 b_best(int buy_side) {  // best bid (max) or best ask (min); INT_MIN/INT_MAX if empty
+    i32 v = buy_side ? INT32_MIN : INT32_MAX;
+    for (int j = 0; j < SO; j++) {
+      bool m = bm[j] >= 0 && (bm[j] & 1) == buy_side;
+      if (m) v = buy_side ? (bp[j] > v ? bp[j] : v) : (bp[j] < v ? bp[j] : v);
+    }
+    return buy_side ? wmax_i32(v) : wmin_i32(v);
+  }
+  DEV i64 b_level_qty(int buy_side, i32 price) {
+    i64 s = 0;
+    for (int j = 0; j < SO; j++)
+      if (bm[j] >= 0 && (bm[j] & 1) == buy_side && bp[j] == price) s += bq[j];
+    return wsum_i64(s);
+  }
+  // FIFO head of a price level: min arrival; returns slot j*64+L
+  DEV int b_head(int buy_side, i32 price) {
+    u32 a = 0xFFFFFFFFu;
+    for (int j = 0; j < SO; j++)
+      if (bm[j] >= 0 && (bm[j] & 1) == buy_side && bp[j] == price && ba[j] < a) a = ba[j];
+    u32 amin = wmin_u32(a);
+    for (int j = 0; j < SO; j++) {
+      u64 b = bal(bm[j] >= 0 && (bm[j] & 1) == buy_side && bp[j] == price && ba[j] == amin);
+      if (b) return j * 64 + ffs64(b);
+    }
+    return -1;
+  }
+  DEV int b_find(int buy_side, i32 price, i32 oid) {
+    for (int j = 0; j < SO; j++) {
+      u64 b = bal(bm[j] >= 0 && (bm[j] & 1) == buy_side && bp[j] == price && bo[j] == oid);
+      if (b) return j * 64 + ffs64(b);
+    }
+    return -1;
+  }
+  DEV i32 b_get(const i32* arr, int slot) {
+    i32 v = 0;
+    for (int j = 0; j < SO; j++)
+      if (j == (slot >> 6)) v = rdli(arr[j], slot & 63);
+    return v;
+  }
+  DEV void b_set(i32* arr, int slot, i32 v) {
+    for (int j = 0; j < SO; j++)
+      if (j == (slot >> 6) && lane == (slot & 63)) arr[j] = v;
+  }
+  DEV int b_free_slot() {
+    for (int j = 0; j < SO; j++) {
+      u64 b = bal(bm[j] < 0);
+      if (b) return j * 64 + ffs64(b);
+    }
+    return -1;
+  }
+  DEV void b_enter(i32 oid, i32 agent, int is_buy, i32 qty, i32 price, i32 hep) {
+    int s = b_free_slot();
+    if (s < 0) {
+      fail(ERR_BOOK_FULL);
+      return;
+    }
+    u32 arr = h.arrival++;
+    for (int j = 0; j < SO; j++)
+      if (j == (s >> 6) && lane == (s & 63)) {
+        bp[j] = price;
+        bq[j] = qty;
+        bo[j] = oid;
+        bm[j] = (agent << 1) | is_buy;
+        ba[j] = arr;
+        bh[j] = hep;
+      }
+    h.b_count++;
+    if (h.b_count > h.max_book) h.max_book = h.b_count;
+  }
+  DEV void b_free(int s) {
+    b_set(bm, s, -1);
+    h.b_count--;
+  }
+
+  // ---------------- OrderBook.history transaction ring (OrderBook.py:146-149, 227-237, 400-436)
+  DEV void tx_add(i64 t, i32 q, i32 ep) {
+    TxRec* R = txr();
+    int cap = P.L.tx_cap;
+    int pos = h.tx_head % cap;
+    if (h.tx_head >= cap) {  // overwriting the oldest record: it must be dead
+      TxRec old = R[pos];
+      if (old.epoch >= h.epoch - P.stream_history) {
+        fail(ERR_TX_FULL);
+        return;
+      }
+    }
+    if (lane == 0) {
+      TxRec r;
+      r.t = t;
+      r.q = q;
+      r.epoch = ep;
+      R[pos] = r;
+    }
+    h.tx_head++;
+  }
+  DEV i64 transacted_volume(i64 lookback, int* perr) {
+    int lo_ep = h.epoch - P.stream_history;
+    i32 entries = 0;
+    i32* EP = ep_entries();
+    for (int e = lo_ep < 0 ? 0 : lo_ep; e <= h.epoch; e++) entries += EP[e & 15];
+    if (entries == 0) return 0;
+    TxRec* R = txr();
+    int cap = P.L.tx_cap;
+    int n = h.tx_head < cap ? h.tx_head : cap;
+    int first = h.tx_head - n;
+    i64 start = h.cur - lookback;
+    i64 vol = 0;
+    int live_total = 0;
+    for (int b = 0; b < n; b += 64) {
+      int k = b + lane;  // k-th record in chronological order
+      bool live = false, dup = false, inwin = false;
+      i64 t = 0;
+      i32 q = 0;
+      if (k < n) {
+        TxRec r = R[(first + k) % cap];
+        t = r.t;
+        q = r.q;
+        live = r.epoch >= lo_ep;
+        inwin = t >= start;
+        // records are chronological: equal (t, q) pairs sit in one contiguous t-block
+        for (int j = k - 1; live && j >= 0; j--) {
+          TxRec o = R[(first + j) % cap];
+          if (o.t != t) break;
+          if (o.epoch >= lo_ep && o.q == q) {
+            dup = true;
+            break;
+          }
+        }
+      }
+      live_total += __popcll(bal(live));
+      vol += wsum_i64((live && !dup && inwin) ? (i64)q : 0);
+    }
+    if (live_total == 0) *perr = 1;  // pandas raises when no transaction records exist
+    return vol;
+  }
+
+  // ---------------- OrderBook.handleLimitOrder / executeOrder / cancelOrder
+  DEV void ex_notify(int recipient, const Msg& m) {
+    // ExchangeAgent.sendMessage: ORDER_* notifications carry the pipeline delay
+    u32 k = m_kind(m);
+    i64 d = (k == MK_ACCEPTED || k == MK_CANCELLED || k == MK_EXECUTED) ? P.ex_pipeline : 0;
+    send(recipient, m, d);
+  }
+  DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
+    if (qty <= 0) return;
+    i32 hep = h.epoch;
+    i32* EP = ep_entries();
+    i32 ne = EP[h.epoch & 15] + 1;
+    if (lane == 0) EP[h.epoch & 15] = ne;
+    i64 ex_q = 0, ex_pq = 0;
+    bool executed = false;
+    for (;;) {
+      int opp = is_buy ? 0 : 1;  // resting side: asks for a buy (is_buy == 0)
+      i32 best = b_best(opp);
+      bool any = opp ? best != INT32_MIN : best != INT32_MAX;
+      bool match = any && (is_buy ? price >= best : price <= best);
+      if (match) {
+        int s = b_head(opp, best);
+        i32 hq = b_get(bq, s), ho = b_get(bo, s), hm = b_get(bm, s), hh = b_get(bh, s);
+        i32 mq;
+        if (qty >= hq) {
+          mq = hq;
+          b_free(s);
+        } else {
+          mq = qty;
+          b_set(bq, s, hq - qty);
+        }
+        // history: taker logs its pre-match remaining qty; maker its matched qty if retained
+        tx_add(h.cur, qty, h.epoch);
+        if (hh >= h.epoch - P.stream_history) tx_add(h.cur, mq, hh);
+        qty -= mq;
+        Msg mt = msg_order(MK_EXECUTED, oid, agent, is_buy, mq, price, best);
+        ex_notify(agent, mt);
+        Msg mm = msg_order(MK_EXECUTED, ho, hm >> 1, hm & 1, mq, best, best);
+        ex_notify(hm >> 1, mm);
+        ex_q += mq;
+        ex_pq += (i64)best * mq;
+        executed = true;
+        if (qty <= 0) break;
+      } else {
+        b_enter(oid, agent, is_buy, qty, price, hep);
+        Msg ma = msg_order(MK_ACCEPTED, oid, agent, is_buy, qty, price, 0);
+        ex_notify(agent, ma);
+        break;
+      }
+      if (h.status == ST_ERROR) return;
+    }
+    if (executed) {
+      h.last_trade = py_round((double)ex_pq / (double)ex_q);
+      h.last_trade_float = 0;
+      h.epoch++;
+      if (lane == 0) EP[h.epoch & 15] = 0;
+    }
+  }
+  DEV void cancel_order(const Msg& m) {
+    int buy = m_buy(m);
+    int s = b_find(buy, (i32)m.w[3], (i32)m.w[1]);
+    if (s < 0) return;
+    i32 q = b_get(bq, s), o = b_get(bo, s), mm = b_get(bm, s), p = b_get(bp, s);
+    b_free(s);
+    Msg r = msg_order(MK_CANCELLED, o, mm >> 1, mm & 1, q, p, 0);
+    ex_notify(m_agent(m), r);
+  }
+
+  // ExchangeAgent.receiveMessage (ExchangeAgent.py:129-340)
+  DEV void ex_receive(const Msg& m) {
+    rs64(AF_COMP, P.ex_comp);
+    u32 k = m_kind(m);
+    i32 sender = m_agent(m);
+    bool closed = h.cur > P.mkt_close;
+    if (closed) {
+      if (k == MK_LIMIT || k == MK_CANCEL || k == MK_MODIFY) {
+        ex_notify(sender, msg_make(MK_MKT_CLOSED, 0));
+        return;
+      } else if (k == MK_SPREAD_REQ || k == MK_LAST_REQ || k == MK_TV_REQ) {
+      } else {
+        ex_notify(sender, msg_make(MK_MKT_CLOSED, 0));
+        return;
+      }
+    }
+    switch (k) {
+    case MK_WHEN_OPEN_REQ:
+    case MK_WHEN_CLOSE_REQ: {
+      rs64(AF_COMP, 0);
+      Msg r = msg_make(k == MK_WHEN_OPEN_REQ ? MK_WHEN_OPEN : MK_WHEN_CLOSE, 0);
+      i64 d = k == MK_WHEN_OPEN_REQ ? P.mkt_open : P.mkt_close;
+      r.w[0] |= 1u << 11;
+      r.w[1] = (u32)(u64)d;
+      r.w[2] = (u32)((u64)d >> 32);
+      ex_notify(sender, r);
+      break;
+    }
+    case MK_LAST_REQ: {
+      Msg r = msg_make(MK_LAST, 0);
+      r.w[0] |= (1u << 11) | ((u32)h.last_trade_float << 8) | ((u32)closed << 7);
+      r.w[5] = (u32)h.last_trade;
+      ex_notify(sender, r);
+      break;
+    }
+    case MK_SPREAD_REQ: {
+      i32 depth = (i32)m.w[1];
+      Msg r = msg_make(MK_SPREAD, 0);
+      i32 bb = b_best(1), aa = b_best(0);
+      bool hb = bb != INT32_MIN && depth > 0, ha = aa != INT32_MAX && depth > 0;
+      if (hb) {
+        r.w[1] = (u32)bb;
+        r.w[2] = (u32)b_level_qty(1, bb);
+      }
+      if (ha) {
+        r.w[3] = (u32)aa;
+        r.w[4] = (u32)b_level_qty(0, aa);
+      }
+      r.w[5] = (u32)h.last_trade;
+      r.w[0] |= ((u32)hb << 9) | ((u32)ha << 10) | (1u << 11) | ((u32)h.last_trade_float << 8) | ((u32)closed << 7);
+      ex_notify(sender, r);
+      break;
+    }
+    case MK_TV_REQ: {
+      int perr = 0;
+      i64 vol = transacted_volume(m_i64(m, 1), &perr);
+      if (perr) {
+        fail(ERR_PANDAS_NO_TX);
+        return;
+      }
+      Msg r = msg_make(MK_TV, 0);
+      r.w[0] |= (1u << 11) | ((u32)closed << 7);
+      r.w[1] = (u32)(u64)vol;
+      r.w[2] = (u32)((u64)vol >> 32);
+      ex_notify(sender, r);
+      break;
+    }
+    case MK_LIMIT:
+      handle_limit((i32)m.w[1], sender, m_buy(m), (i32)m.w[2], (i32)m.w[3]);
+      break;
+    case MK_CANCEL:
+      cancel_order(m);
+      break;
+    default:
+      break;
+    }
+  }
+
+  // ---------------- TradingAgent (TradingAgent.py)
+  DEV void send_ex(Msg m) {
+    m.w[0] = (m.w[0] & 0xFFFFu) | ((u32)cur_agent << 16);
+    send(0, m, 0);
+  }
+  DEV void get_spread(int depth) {
+    Msg m = msg_make(MK_SPREAD_REQ, cur_agent);
+    m.w[1] = (u32)depth;
+    send_ex(m);
+  }
+  DEV void get_tv(i64 lookback) {
+    Msg m = msg_make(MK_TV_REQ, cur_agent);
+    m.w[1] = (u32)(u64)lookback;
+    m.w[2] = (u32)((u64)lookback >> 32);
+    send_ex(m);
+  }
+  // placeLimitOrder (TradingAgent.py:309-349)
+  DEV void place_limit(i64 qty, int is_buy, i64 price) {
+    i64 oid = next_order_id();
+    if (qty > 0) {
+      i32 n = rgi(AF_NORD);
+      if (n >= P.L.open_cap) {
+        fail(ERR_OPEN_FULL);
+        return;
+      }
+      OpenOrder* oo = open_ptr(cur_agent);
+      if (lane == 0) {
+        OpenOrder o;
+        o.oid = (i32)oid;
+        o.is_buy = is_buy;
+        o.qty = (i32)qty;
+        o.price = (i32)price;
+        oo[n] = o;
+      }
+      rs(AF_NORD, (u32)(n + 1));
+      send_ex(msg_order(MK_LIMIT, (i32)oid, cur_agent, is_buy, (i32)qty, (i32)price, 0));
+    }
+  }
+  // cancelOrder for every open order in dict (= ascending order id) order
+  DEV void cancel_all() {
+    i32 n = rgi(AF_NORD);
+    OpenOrder* oo = open_ptr(cur_agent);
+    for (int b = 0; b < n; b += 64) {
+      OpenOrder my;
+      int k = b + lane;
+      if (k < n) my = oo[k];
+      int cnt = n - b < 64 ? n - b : 64;
+      for (int i = 0; i < cnt; i++) {
+        i32 oid = rdli(my.oid, i), ib = rdli(my.is_buy, i), q = rdli(my.qty, i), p = rdli(my.price, i);
+        send_ex(msg_order(MK_CANCEL, oid, cur_agent, ib, q, p, 0));
+      }
+    }
+  }
+  DEV int find_open(i32 oid, OpenOrder& out) {
+    i32 n = rgi(AF_NORD);
+    OpenOrder* oo = open_ptr(cur_agent);
+    for (int b = 0; b < n; b += 64) {
+      int k = b + lane;
+      OpenOrder my;
+      my.oid = -1;
+      if (k < n) my = oo[k];
+      u64 hit = bal(k < n && my.oid == oid);
+      if (hit) {
+        int L = ffs64(hit);
+        out.oid = oid;
+        out.is_buy = rdli(my.is_buy, L);
+        out.qty = rdli(my.qty, L);
+        out.price = rdli(my.price, L);
+        return b + L;
+      }
+    }
+    return -1;
+  }
+  DEV void del_open(int idx) {
+    i32 n = rgi(AF_NORD);
+    OpenOrder* oo = open_ptr(cur_agent);
+    for (int b = idx; b < n - 1; b += 64) {
+      int k = b + lane;
+      OpenOrder nx;
+      if (k < n - 1) nx = oo[k + 1];
+      if (k < n - 1) oo[k] = nx;
+    }
+    rs(AF_NORD, (u32)(n - 1));
+  }
+
+  // TradingAgent.wakeup (TradingAgent.py:142-158)
+  DEV bool ta_wakeup() {
+    u32 f = flags();
+    if (f & FL_FIRST_WAKE) rs(AF_FLAGS, f & ~FL_FIRST_WAKE);
+    if (!(f & FL_HAS_OPEN)) {
+      send_ex(msg_make(MK_WHEN_OPEN_REQ, cur_agent));
+      send_ex(msg_make(MK_WHEN_CLOSE_REQ, cur_agent));
+    }
+    f = flags();
+    return (f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE) && !(f & FL_MKT_CLOSED);
+  }
+  DEV i64 wake_frequency(int type) {
+    if (type == AG_POVMM) return P.mm_wake;
+    if (type == AG_MOMENTUM) return P.mom_wake;
+    RS A = agent_rs();
+    i64 v = rs_randint(A, 0, 100);
+    agent_rs_put(A);
+    return v;
+  }
+  DEV void query_last_trade(const Msg& m) {
+    u32 f = flags() | FL_HAS_LAST;
+    f = m_dfloat(m) ? (f | FL_LAST_FLOAT) : (f & ~FL_LAST_FLOAT);
+    if (f & FL_MKT_CLOSED) f |= FL_DAILY_CLOSE;
+    rs(AF_FLAGS, f);
+    rs64(AF_LAST_TRADE, (i64)(i32)m.w[5]);
+  }
+  // TradingAgent.receiveMessage (TradingAgent.py:181-268)
+  DEV void ta_receive(const Msg& m, int type) {
+    u32 f0 = flags();
+    bool had = (f0 & FL_HAS_OPEN) && (f0 & FL_HAS_CLOSE);
+    switch (m_kind(m)) {
+    case MK_WHEN_OPEN:
+      rs64(AF_MKT_OPEN, m_i64(m, 1));
+      fl_set(FL_HAS_OPEN, true);
+      break;
+    case MK_WHEN_CLOSE:
+      rs64(AF_MKT_CLOSE, m_i64(m, 1));
+      fl_set(FL_HAS_CLOSE, true);
+      break;
+    case MK_EXECUTED: {  // orderExecuted (TradingAgent.py:422-462)
+      i64 q = m_buy(m) ? (i64)(i32)m.w[2] : -(i64)(i32)m.w[2];
+      rs64(AF_SHARES, rg64(AF_SHARES) + q);
+      rs64(AF_CASH, rg64(AF_CASH) - q * (i64)(i32)m.w[4]);
+      OpenOrder o;
+      int idx = find_open((i32)m.w[1], o);
+      if (idx >= 0) {
+        if ((i32)m.w[2] >= o.qty) del_open(idx);
+        else if (lane == 0) open_ptr(cur_agent)[idx].qty = o.qty - (i32)m.w[2];
+      }
+      break;
+    }
+    case MK_CANCELLED: {
+      OpenOrder o;
+      int idx = find_open((i32)m.w[1], o);
+      if (idx >= 0) del_open(idx);
+      break;
+    }
+    case MK_MKT_CLOSED:
+      fl_set(FL_MKT_CLOSED, true);
+      break;
+    case MK_LAST:
+      if (m_closed(m)) fl_set(FL_MKT_CLOSED, true);
+      query_last_trade(m);
+      break;
+    case MK_SPREAD: {
+      if (m_closed(m)) fl_set(FL_MKT_CLOSED, true);
+      query_last_trade(m);
+      u32 f = flags() | FL_HAS_KNOWN;
+      f = m_nb(m) ? (f | FL_NB) : (f & ~FL_NB);
+      f = m_na(m) ? (f | FL_NA) : (f & ~FL_NA);
+      rs(AF_FLAGS, f);
+      rs(AF_BID, m.w[1]);
+      rs(AF_BIDQ, m.w[2]);
+      rs(AF_ASK, m.w[3]);
+      rs(AF_ASKQ, m.w[4]);
+      break;
+    }
+    case MK_TV:
+      if (m_closed(m)) fl_set(FL_MKT_CLOSED, true);
+      rs64(AF_TV, m_i64(m, 1));
+      break;
+    default:
+      break;
+    }
+    u32 f1 = flags();
+    bool have = (f1 & FL_HAS_OPEN) && (f1 & FL_HAS_CLOSE);
+    if (have && !had) {
+      i64 off = wake_frequency(type);
+      wakeup_at(cur_agent, rg64(AF_MKT_OPEN) + off);
+    }
+  }
+  DEV bool known_bid(i32& bid) {
+    bid = rgi(AF_BID);
+    return fl(FL_NB) && bid != 0;
+  }
+  DEV bool known_ask(i32& ask) {
+    ask = rgi(AF_ASK);
+    return fl(FL_NA) && ask != 0;
+  }
+
+  // Bayesian estimate shared by ZI (ZI.py:215-263) and Value (ValueAgent.py:153-201)
+  DEV i64 bayes_r_T(i64 obs, double kappa, double r_bar, double sigma_n, double sigma_s) {
+    if (!fl(FL_PREV_WAKE)) {
+      fl_set(FL_PREV_WAKE, true);
+      rs64(AF_PREV_WAKE, rg64(AF_MKT_OPEN));
+    }
+    double delta = (double)(h.cur - rg64(AF_PREV_WAKE));
+    double c = 1 - kappa;
+    double r_t = rgd(AF_R_T), sigma_t = rgd(AF_SIGMA_T);
+    double r_tprime = (1 - gm_pow(c, delta)) * r_bar;
+    r_tprime += gm_pow(c, delta) * r_t;
+    double sigma_tprime = gm_pow(c, 2 * delta) * sigma_t;
+    sigma_tprime += ((1 - gm_pow(c, 2 * delta)) / (1 - gm_pow(c, 2.0))) * sigma_s;
+    r_t = (sigma_n / (sigma_n + sigma_tprime)) * r_tprime;
+    r_t += (sigma_tprime / (sigma_n + sigma_tprime)) * (double)obs;
+    sigma_t = (sigma_n * sigma_t) / (sigma_n + sigma_t);
+    double d2 = (double)(rg64(AF_MKT_CLOSE) - h.cur);
+    if (!(d2 > 0)) d2 = 0;
+    double r_T = (1 - gm_pow(c, d2)) * r_bar;
+    r_T += gm_pow(c, d2) * r_t;
+    rsd(AF_R_T, r_t);
+    rsd(AF_SIGMA_T, sigma_t);
+    rs64(AF_PREV_WAKE, h.cur);
+    return py_round(r_T);
+  }
+
+  // ---------------- ZeroIntelligenceAgent (ZI.py:125-309)
+  DEV void zi_wakeup() {
+    ta_wakeup();
+    rs(AF_STATE, AS_INACTIVE);
+    if (!fl(FL_HAS_OPEN) || !fl(FL_HAS_CLOSE)) return;
+    fl_set(FL_TRADING, true);
+    if (fl(FL_MKT_CLOSED) && fl(FL_DAILY_CLOSE)) return;
+    RS A = agent_rs();
+    double dt = rs_exponential(A, 1.0 / P.zi_lambda);
+    agent_rs_put(A);
+    wakeup_at(cur_agent, h.cur + py_round(dt));
+    if (fl(FL_MKT_CLOSED) && !fl(FL_DAILY_CLOSE)) {
+      get_spread(1);
+      rs(AF_STATE, AS_AWAITING_SPREAD);
+      return;
+    }
+    cancel_all();
+    get_spread(1);
+    rs(AF_STATE, AS_AWAITING_SPREAD);
+  }
+  DEV void zi_place() {
+    i64 obs = o_observe(h.cur, P.zi_sigma_n);
+    i64 q = (i64)((double)rg64(AF_SHARES) / 100);
+    int buy;
+    if (q >= P.zi_qmax) buy = 0;
+    else if (q <= -P.zi_qmax) buy = 1;
+    else {
+      RS A = agent_rs();
+      buy = (int)rs_randint(A, 0, 2);
+      agent_rs_put(A);
+    }
+    i64 r_T = bayes_r_T(obs, P.zi_kappa, P.zi_rbar, P.zi_sigma_n, P.zi_sigma_s);
+    q += P.zi_qmax - 1;
+    i64 idx = buy ? q + 1 : q;
+    if (idx < 0) idx += 2 * P.zi_qmax;
+    if (idx < 0 || idx >= 2 * P.zi_qmax) {
+      fail(ERR_THETA_INDEX);
+      return;
+    }
+    i64 v = r_T + (i64)rgi(AF_THETA + (int)idx);
+    int g = rgi(AF_GROUP);
+    RS A = agent_rs();
+    i64 R = rs_randint(A, P.zi_rmin[g], (i64)P.zi_rmax[g] + 1);
+    agent_rs_put(A);
+    i64 p = buy ? v - R : v + R;
+    i32 bid = 0, ask = 0;
+    i64 bid_vol = fl(FL_NB) ? (i64)rgi(AF_BIDQ) : 0, ask_vol = fl(FL_NA) ? (i64)rgi(AF_ASKQ) : 0;
+    bid = rgi(AF_BID);
+    ask = rgi(AF_ASK);
+    if (buy && ask_vol > 0) {
+      i64 R_ask = v - ask;
+      if ((double)R_ask >= P.zi_eta[g] * (double)R) p = ask;
+    } else if (!buy && bid_vol > 0) {
+      i64 R_bid = bid - v;
+      if ((double)R_bid >= P.zi_eta[g] * (double)R) p = bid;
+    }
+    place_limit(100, buy, p);
+  }
+  DEV void zi_receive(const Msg& m) {
+    ta_receive(m, AG_ZI);
+    if (rgi(AF_STATE) == AS_AWAITING_SPREAD && m_kind(m) == MK_SPREAD) {
+      if (fl(FL_MKT_CLOSED)) return;
+      zi_place();
+      rs(AF_STATE, AS_AWAITING_WAKEUP);
+    }
+  }
+
+  // ---------------- ValueAgent (ValueAgent.py:100-268)
+  DEV void value_wakeup() {
+    ta_wakeup();
+    rs(AF_STATE, AS_INACTIVE);
+    if (!fl(FL_HAS_OPEN) || !fl(FL_HAS_CLOSE)) return;
+    fl_set(FL_TRADING, true);
+    if (fl(FL_MKT_CLOSED) && fl(FL_DAILY_CLOSE)) return;
+    RS A = agent_rs();
+    double dt = rs_exponential(A, 1.0 / P.v_lambda);
+    agent_rs_put(A);
+    wakeup_at(cur_agent, h.cur + py_round(dt));
+    if (fl(FL_MKT_CLOSED) && !fl(FL_DAILY_CLOSE)) {
+      get_spread(1);
+      rs(AF_STATE, AS_AWAITING_SPREAD);
+      return;
+    }
+    cancel_all();
+    get_spread(1);
+    rs(AF_STATE, AS_AWAITING_SPREAD);
+  }
+  DEV void value_place() {
+    i64 obs = o_observe(h.cur, P.v_sigma_n);
+    i64 r_T = bayes_r_T(obs, P.v_kappa, P.v_rbar, P.v_sigma_n, P.v_sigma_s);
+    i32 bid, ask;
+    bool hb = known_bid(bid), ha = known_ask(ask);
+    int buy;
+    i64 p;
+    RS G = grs(0);
+    if (hb && ha) {
+      i64 mid = (i64)((double)((i64)ask + bid) / 2);
+      i64 spread = (i64)ask - bid;
+      if (spread < 0) spread = -spread;
+      i64 adj;
+      if (rs_double(G) < P.v_percent_aggr) adj = 0;
+      else adj = rs_randint(G, 0, P.v_depth_spread * spread);
+      if (r_T < mid) {
+        buy = 0;
+        p = bid + adj;
+      } else {
+        buy = 1;
+        p = ask - adj;
+      }
+    } else {
+      buy = (int)rs_randint(G, 0, 2);
+      p = r_T;
+    }
+    grs_put(0, G);
+    place_limit(rgi(AF_SIZE), buy, p);
+  }
+  DEV void value_receive(const Msg& m) {
+    ta_receive(m, AG_VALUE);
+    if (rgi(AF_STATE) == AS_AWAITING_SPREAD && m_kind(m) == MK_SPREAD) {
+      if (fl(FL_MKT_CLOSED)) return;
+      value_place();
+      rs(AF_STATE, AS_AWAITING_WAKEUP);
+    }
+  }
+
+  // ---------------- NoiseAgent (NoiseAgent.py:82-154)
+  DEV void noise_wakeup() {
+    ta_wakeup();
+    rs(AF_STATE, AS_INACTIVE);
+    if (!fl(FL_HAS_OPEN) || !fl(FL_HAS_CLOSE)) return;
+    fl_set(FL_TRADING, true);
+    if (fl(FL_MKT_CLOSED) && fl(FL_DAILY_CLOSE)) return;
+    i64 wt = rg64(AF_WAKEUP_TIME);
+    if (wt > h.cur) wakeup_at(cur_agent, wt);
+    get_spread(1);
+    rs(AF_STATE, AS_AWAITING_SPREAD);
+  }
+  DEV void noise_receive(const Msg& m) {
+    ta_receive(m, AG_NOISE);
+    if (rgi(AF_STATE) == AS_AWAITING_SPREAD && m_kind(m) == MK_SPREAD) {
+      if (fl(FL_MKT_CLOSED)) return;
+      RS G = grs(0);
+      int buy = (int)rs_randint(G, 0, 2);
+      grs_put(0, G);
+      i32 bid, ask;
+      bool hb = known_bid(bid), ha = known_ask(ask);
+      if (buy && ha) place_limit(rgi(AF_SIZE), 1, ask);
+      else if (!buy && hb) place_limit(rgi(AF_SIZE), 0, bid);
+      rs(AF_STATE, AS_AWAITING_WAKEUP);
+    }
+  }
+
+  // ---------------- POVMarketMakerAgent (POVMarketMakerAgent.py:83-206)
+  DEV void mm_wakeup() {
+    if (ta_wakeup()) {
+      get_spread(1);
+      get_tv(P.mm_wake);
+    }
+  }
+  DEV void mm_receive(const Msg& m) {
+    ta_receive(m, AG_POVMM);
+    i64 mid = rg64(AF_LAST_MID);
+    u32 k = m_kind(m);
+    if (k == MK_TV && fl(FL_AW_TV)) {
+      i64 qty = py_round(P.mm_pov * (double)rg64(AF_TV));
+      rs(AF_ORDER_SIZE, (u32)(qty >= P.mm_min_size ? qty : P.mm_min_size));
+      fl_set(FL_AW_TV, false);
+    }
+    if (k == MK_SPREAD && fl(FL_AW_SPREAD)) {
+      i32 bid, ask;
+      bool hb = known_bid(bid), ha = known_ask(ask);
+      if (hb && ha) {
+        mid = (i64)((double)((i64)ask + bid) / 2);
+        rs64(AF_LAST_MID, mid);
+        fl_set(FL_LAST_MID, true);
+        fl_set(FL_AW_SPREAD, false);
+      }
+    }
+    if (!fl(FL_AW_SPREAD) && !fl(FL_AW_TV)) {
+      cancel_all();
+      i64 hb = mid - 1, la = mid + P.mm_window;
+      i64 lb = hb - P.mm_ticks, ha = la + P.mm_ticks;
+      i64 sz = rgi(AF_ORDER_SIZE);
+      for (i64 p = lb; p <= hb; p++) place_limit(sz, 1, p);
+      for (i64 p = la; p <= ha; p++) place_limit(sz, 0, p);
+      fl_set(FL_AW_SPREAD, true);
+      fl_set(FL_AW_TV, true);
+      wakeup_at(cur_agent, h.cur + P.mm_wake);
+    }
+  }
+
+  // ---------------- MomentumAgent (MomentumAgent.py:53-99)
+  DEV double mom_avg(int n) {
+    i32 nm = rgi(AF_NMID);
+    i64 s2 = 0;
+    for (int i = nm - n; i < nm; i++) s2 += rgi(AF_MIDS + (i % 50));
+    double x = ((double)s2 / 2.0) / (double)n;
+    return __builtin_rint(x * 100.0) / 100.0;
+  }
+  DEV void mom_wakeup() {
+    if (ta_wakeup()) {
+      get_spread(1);
+      rs(AF_STATE, AS_AWAITING_SPREAD);
+    }
+  }
+  DEV void mom_receive(const Msg& m) {
+    ta_receive(m, AG_MOMENTUM);
+    if (rgi(AF_STATE) == AS_AWAITING_SPREAD && m_kind(m) == MK_SPREAD) {
+      i32 bid, ask;
+      bool hb = known_bid(bid), ha = known_ask(ask);
+      if (hb && ha) {
+        i32 nm = rgi(AF_NMID);
+        rs(AF_MIDS + (nm % 50), (u32)(bid + ask));
+        nm++;
+        rs(AF_NMID, (u32)nm);
+        if (nm > 20) {
+          rsd(AF_AVG20, mom_avg(20));
+          rs(AF_N20, rg(AF_N20) + 1);
+        }
+        if (nm > 50) {
+          rsd(AF_AVG50, mom_avg(50));
+          rs(AF_N50, rg(AF_N50) + 1);
+        }
+        if (rgi(AF_N20) > 0 && rgi(AF_N50) > 0) {
+          if (rgd(AF_AVG20) >= rgd(AF_AVG50)) place_limit(rgi(AF_SIZE), 1, ask);
+          else place_limit(rgi(AF_SIZE), 0, bid);
+        }
+      }
+      wakeup_at(cur_agent, h.cur + P.mom_wake);
+      rs(AF_STATE, AS_AWAITING_WAKEUP);
+    }
+  }
+
+  // ---------------- dispatch
+  DEV void dispatch(int type, bool wake, const Msg& m) {
+    if (wake) {
+      switch (type) {
+      case AG_ZI: zi_wakeup(); break;
+      case AG_NOISE: noise_wakeup(); break;
+      case AG_VALUE: value_wakeup(); break;
+      case AG_POVMM: mm_wakeup(); break;
+      case AG_MOMENTUM: mom_wakeup(); break;
+      default: break;  // ExchangeAgent: Agent.wakeup does nothing
+      }
+    } else {
+      switch (type) {
+      case AG_EXCHANGE: ex_receive(m); break;
+      case AG_ZI: zi_receive(m); break;
+      case AG_NOISE: noise_receive(m); break;
+      case AG_VALUE: value_receive(m); break;
+      case AG_POVMM: mm_receive(m); break;
+      case AG_MOMENTUM: mom_receive(m); break;
+      default: break;
+      }
+    }
+  }
+
+  // ---------------- state save/restore around a launch
+  DEV void load() {
+    h = *hdr();
+    SavedEvent* sq = (SavedEvent*)(env + P.L.off_q);
+    qfree = 0;
+    for (int j = 0; j < SQ; j++) {
+      int slot = j * 64 + lane;
+      SavedEvent e = sq[slot];
+      qk[slot] = e.key;
+      qs[slot] = e.seq;
+      if (PL_LDS)
+        for (int i = 0; i < 6; i++) qpl[slot * 6 + i] = e.pl[i];
+      if (e.key == KEY_EMPTY) qfree |= 1ull << j;
+    }
+    q_rescan();
+    SavedOrder* so = (SavedOrder*)(env + P.L.off_book);
+    for (int j = 0; j < SO; j++) {
+      SavedOrder o = so[j * 64 + lane];
+      bp[j] = o.price;
+      bq[j] = o.qty;
+      bo[j] = o.oid;
+      bm[j] = o.meta;
+      ba[j] = o.arrival;
+      bh[j] = o.hepoch;
+    }
+  }
+  DEV void save() {
+    SavedEvent* sq = (SavedEvent*)(env + P.L.off_q);
+    for (int j = 0; j < SQ; j++) {
+      int slot = j * 64 + lane;
+      SavedEvent e;
+      e.key = qk[slot];
+      e.seq = qs[slot];
+      e.pad = 0;
+      for (int i = 0; i < 6; i++) e.pl[i] = PL_LDS ? qpl[slot * 6 + i] : 0u;
+      sq[slot] = e;
+    }
+    SavedOrder* so = (SavedOrder*)(env + P.L.off_book);
+    for (int j = 0; j < SO; j++) {
+      SavedOrder o;
+      o.price = bp[j];
+      o.qty = bq[j];
+      o.oid = bo[j];
+      o.meta = bm[j];
+      o.arrival = ba[j];
+      o.hepoch = bh[j];
+      o.pad[0] = o.pad[1] = 0;
+      so[j * 64 + lane] = o;
+    }
+    if (lane == 0) *hdr() = h;
+  }
+
+  // ---------------- Kernel.runner event loop (Kernel.py:190-292)
+  DEV void run(i64 max_pops) {
+    for (i64 n = 0; n < max_pops && h.status == ST_RUNNING; n++) {
+      u64 key;
+      u32 seq;
+      int slot = q_peek(key, seq);
+      if (slot < 0 || !(h.cur <= P.stop)) {
+        h.status = ST_DONE;
+        break;
+      }
+      Msg m = pl_read(slot);
+      i64 t = (i64)(key >> 13);
+      int rcp = (int)((key >> 2) & 0x7FF);
+      int type = (int)(key & 3);
+      h.cur = t;
+      i64 rec[10];
+      encode(key, m, rec);
+      u64 hs = h.hash;
+      for (int i = 0; i < 10; i++) hs = (hs ^ (u64)rec[i]) * FNV_PRIME;
+      h.hash = hs;
+      if (trace && h.trace_len < P.L.trace_cap) {
+        if (lane < 10) {
+          i64 v = 0;
+          for (int i = 0; i < 10; i++)
+            if (i == lane) v = rec[i];
+          trace[h.trace_len * 10 + lane] = v;
+        }
+        h.trace_len++;
+      }
+      h.pops++;
+      add_delay = 0;
+      rec_load(rcp);
+      i64 at = rg64(AF_ATIME);
+      if (at > t) {  // agent in the future: requeue unchanged (same uniq)
+        q_rekey(slot, ((u64)at << 13) | (key & 0x1FFF));
+        continue;
+      }
+      q_remove(slot);
+      rs64(AF_ATIME, t);
+      dispatch(rgi(AF_TYPE), type == MT_WAKEUP, m);
+      rs64(AF_ATIME, t + rg64(AF_COMP) + add_delay);
+      rec_store();
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// env construction (config scripts' global-RNG draw order)
+// ------------------------------------------------------------------------------------
+template <int SQ, int SO, bool PL_LDS>
+struct Builder : Eng<SQ, SO, PL_LDS> {
+  typedef Eng<SQ, SO, PL_LDS> E;
+  DEV Builder(const MxaParams& p, char* e, char* lds) : E(p, e, lds) {}
+
+  DEV u32 g_seed(RS& G) { return (u32)rs_randint(G, 0, 4294967296LL); }
+  DEV void set_seed(int stream, u32 s) {
+    if (this->lane == 0) this->rng_key(stream)[0] = s;
+  }
+  DEV void rec_init(int a, int type) {
+    this->rlo = this->rhi = 0;
+    this->cur_agent = a;
+    this->rs(AF_TYPE, (u32)type);
+    this->rs(AF_FLAGS, FL_FIRST_WAKE | FL_AW_SPREAD | FL_AW_TV);
+    this->rs(AF_RS_POS, MXA_MT_N);
+    this->rs64(AF_START_CASH, this->P.starting_cash);
+    this->rs64(AF_CASH, this->P.starting_cash);
+    this->rs64(AF_ATIME, this->P.start);
+    this->rs64(AF_COMP, this->P.default_comp_delay);
+  }
+  DEV i64 get_wake_time(RS& G, i64 open, i64 close) {  // util/util.py:35-58
+    double u = rs_double(G);
+    double alpha = 12.0, beta = 0.5;
+    double n = (3 / alpha) * u - gm_pow(beta - 0, 3.0);
+    double c = n < 0 ? -gm_pow(-n, 1.0 / 3.0) : gm_pow(n, 1.0 / 3.0);
+    double mult = c + beta;
+    return open + (i64)(mult * (double)(close - open));
+  }
+  // expand every stream's init_genrand in parallel (lane = stream)
+  DEV void seed_streams(int first) {
+    const MxaParams& P = this->P;
+    wfence();
+    for (int b = first; b < P.n_streams; b += 64) {
+      int s = b + this->lane;
+      if (s < P.n_streams) {
+        u32* key = this->rng_key(s);
+        u32 x = key[0];
+        for (int i = 1; i < MXA_MT_N; i++) {
+          x = 1812433253u * (x ^ (x >> 30)) + (u32)i;
+          key[i] = x;
+        }
+      }
+    }
+    wfence();
+  }
+
+  DEV void build(u32 seed) {
+    const MxaParams& P = this->P;
+    EnvHdr& h = this->h;
+    h = EnvHdr();
+    h.hash = FNV_OFF;
+    h.status = ST_RUNNING;
+    h.cur = P.start;
+    for (int s = 0; s < 4; s++) h.rs_pos[s] = MXA_MT_N;
+    this->mk = KEY_EMPTY;
+    this->ms = 0xFFFFFFFFu;
+    this->mj = -1;
+    this->qfree = SQ >= 64 ? ~0ull : ((1ull << SQ) - 1ull);
+    for (int j = 0; j < SQ; j++) {
+      this->qk[j * 64 + this->lane] = KEY_EMPTY;
+      this->qs[j * 64 + this->lane] = 0xFFFFFFFFu;
+    }
+    for (int j = 0; j < SO; j++) this->bm[j] = -1;
+    mt_seed(this->rng_key(0), seed);
+    RS G = this->grs(0);
+    int n = P.n_agents;
+    u32 tmp;
+    if (P.config == MXA_CFG_RMSC03) {
+      set_seed(1, g_seed(G));  // O
+      h.o_pt = P.mkt_open;
+      h.o_pv = P.o_rbar;
+      h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
+      tmp = g_seed(G);  // exchange
+      set_seed(4 + 0, tmp);
+      for (int a = P.first_noise; a < P.first_noise + P.n_noise; a++) {
+        i64 wt = get_wake_time(G, P.noise_open, P.noise_close);
+        set_seed(4 + a, g_seed(G));
+        i64 size = rs_randint(G, 20, 50);
+        rec_init(a, AG_NOISE);
+        this->rs64(AF_WAKEUP_TIME, wt);
+        this->rs(AF_SIZE, (u32)size);
+        this->rec_store();
+      }
+      for (int a = P.first_value; a < P.first_value + P.n_value; a++) {
+        set_seed(4 + a, g_seed(G));
+        i64 size = rs_randint(G, 20, 50);
+        rec_init(a, AG_VALUE);
+        this->rs(AF_SIZE, (u32)size);
+        this->rsd(AF_R_T, P.v_rbar);
+        this->rec_store();
+      }
+      for (int a = P.first_mm; a < P.first_mm + P.n_mm; a++) {
+        set_seed(4 + a, g_seed(G));
+        rec_init(a, AG_POVMM);
+        this->rs(AF_ORDER_SIZE, (u32)P.mm_min_size);
+        this->rec_store();
+      }
+      for (int a = P.first_mom; a < P.first_mom + P.n_mom; a++) {
+        set_seed(4 + a, g_seed(G));
+        rec_init(a, AG_MOMENTUM);
+        this->rec_store();
+      }
+      set_seed(2, g_seed(G));  // K
+    } else {
+      set_seed(1, g_seed(G));  // O
+      set_seed(2, g_seed(G));  // K
+      if (P.config == MXA_CFG_SPARSE_ZI_100) set_seed(3, g_seed(G));  // L
+      h.o_pt = P.mkt_open;
+      h.o_pv = P.o_rbar;
+      h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
+      set_seed(4 + 0, g_seed(G));  // exchange
+      int a = P.first_zi;
+      for (int g = 0; g < P.zi_ngroups; g++)
+        for (int k = 0; k < P.zi_group_count[g]; k++, a++) {
+          set_seed(4 + a, g_seed(G));
+          rec_init(a, AG_ZI);
+          this->rs(AF_GROUP, (u32)g);
+          this->rsd(AF_R_T, P.zi_rbar);
+          this->rec_store();
+        }
+      // latency matrix G.uniform(lo, hi, (n, n)) in C order: only min_latency[0][*] and
+      // (sparse_zi_100) min_latency[*][0] are ever read; the other draws only advance G.
+      double* lat = this->lat();
+      i64 total = (i64)n * n, prev = -1;
+      bool col = P.config == MXA_CFG_SPARSE_ZI_100;
+      i64 nneed = col ? 2 * (i64)n - 1 : (i64)n;
+      for (i64 k = 0; k < nneed; k++) {
+        i64 d = k < n ? k : (k - n + 1) * (i64)n;  // row 0, then column 0 (d = r*n)
+        rs_skip_words(G, 2 * (d - prev - 1));
+        double v = rs_uniform(G, P.lat_lo, P.lat_hi);
+        if (this->lane == 0) {
+          if (d < n) lat[d] = v;
+          if (col && d % n == 0) lat[n + d / n] = v;
+        }
+        prev = d;
+      }
+      rs_skip_words(G, 2 * (total - prev - 1));
+      if (P.config == MXA_CFG_SPARSE_ZI_1000) {
+        if (this->lane == 0) lat[0] = 20000.0;  // diagonal (never used)
+      }
+      wfence();
+    }
+    this->grs_put(0, G);
+    // expand all other streams, then the per-stream config-time draws
+    seed_streams(1);
+    h.rs_pos[1] = h.rs_pos[2] = h.rs_pos[3] = MXA_MT_N;
+    {  // oracle first megashock (SMRO:71-72)
+      RS O = this->grs(1);
+      double msv = rs_normal(O, P.o_msmean, __builtin_sqrt(P.o_msvar));
+      h.o_msv = rs_randint(O, 0, 2) == 0 ? msv : -msv;
+      this->grs_put(1, O);
+    }
+    // exchange record
+    rec_init(0, AG_EXCHANGE);
+    this->rs64(AF_COMP, P.default_comp_delay);
+    this->rec_store();
+    // momentum size = A.randint(min, max); ZI theta = sorted(round(A.normal(0, sqrt(sigma_pv), 2 qmax)))
+    for (int a = P.first_mom; a < P.first_mom + P.n_mom; a++) {
+      this->rec_load(a);
+      RS A = this->agent_rs();
+      this->rs(AF_SIZE, (u32)rs_randint(A, P.mom_min, P.mom_max));
+      this->agent_rs_put(A);
+      this->rec_store();
+    }
+    for (int a = P.first_zi; a < P.first_zi + P.n_zi; a++) {
+      this->rec_load(a);
+      RS A = this->agent_rs();
+      double th[20];
+      int nq = 2 * P.zi_qmax;
+      for (int i = 0; i < 20; i++) th[i] = 0;
+      for (int i = 0; i < nq; i++) th[i] = __builtin_rint(rs_normal(A, 0, __builtin_sqrt(P.zi_sigma_pv)));
+      // stable descending insertion sort (wave-uniform, 20 elements)
+      for (int i = 1; i < nq; i++) {
+        double x = th[i];
+        int j = i - 1;
+        while (j >= 0 && th[j] < x) {
+          th[j + 1] = th[j];
+          j--;
+        }
+        th[j + 1] = x;
+      }
+      for (int i = 0; i < nq; i++) this->rs(AF_THETA + i, (u32)(i32)th[i]);
+      this->agent_rs_put(A);
+      this->rec_store();
+    }
+    // Kernel.runner: kernelInitializing (exchange opening price = r_bar, a python float),
+    // kernelStarting (every agent wakes at startTime, in id order)
+    h.last_trade = (i64)P.o_rbar;
+    h.last_trade_float = 1;
+    h.cur = P.start;
+    for (int a = 0; a < n; a++) this->wakeup_at(a, P.start);
+    h.cur = P.start;
+    this->save();
+    // zero the history-epoch entry counts and the transaction ring
+    if (this->lane < 16) this->ep_entries()[this->lane] = 0;
+    TxRec* R = this->txr();
+    for (int i = this->lane; i < P.L.tx_cap; i += 64) {
+      TxRec z;
+      z.t = 0;
+      z.q = 0;
+      z.epoch = -1000000;
+      R[i] = z;
+    }
+  }
+};
+
+}  // namespace mxa
+
+// ------------------------------------------------------------------------------------
+// kernels (one wavefront per env; grid = n_envs)
+// ------------------------------------------------------------------------------------
+template <int SQ, int SO, bool PL_LDS>
+__global__ __launch_bounds__(64) void mxa_build_kernel(MxaParams P, char* base, const uint32_t* seeds, const uint8_t* mask) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int env = blockIdx.x;
+  if (env >= P.n_envs) return;
+  if (mask && !mask[env]) return;
+  mxa::Builder<SQ, SO, PL_LDS> b(P, base + (size_t)env * P.L.env_stride, lds);
+  b.build(seeds[env]);
+}
+
+template <int SQ, int SO, bool PL_LDS>
+__global__ __launch_bounds__(64) void mxa_run_kernel(MxaParams P, char* base, int64_t max_pops) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int env = blockIdx.x;
+  if (env >= P.n_envs) return;
+  char* e = base + (size_t)env * P.L.env_stride;
+  if (((EnvHdr*)e)->status != ST_RUNNING) return;
+  mxa::Eng<SQ, SO, PL_LDS> g(P, e, lds);
+  g.load();
+  g.run(max_pops);
+  g.save();
+}
+
+// parity helpers: numpy-legacy RNG draws and glibc math on the device (tests only call
+// these through the C-ABI; they exercise exactly the device functions the engine uses)
+__global__ __launch_bounds__(64) void mxa_rng_probe_kernel(uint32_t seed, int mode, double a, double b, int n, double* out, uint32_t* scratch) {
+  mxa::mt_seed(scratch, seed);
+  mxa::RS r;
+  r.key = scratch;
+  r.pos = MXA_MT_N;
+  r.hasg = 0;
+  r.gauss = 0;
+  for (int i = 0; i < n; i++) {
+    double v;
+    switch (mode) {
+    case 0: v = (double)mxa::rs_u32(r); break;
+    case 1: v = mxa::rs_double(r); break;
+    case 2: v = (double)mxa::rs_randint(r, (int64_t)a, (int64_t)b); break;
+    case 3: v = mxa::rs_normal(r, a, b); break;
+    case 4: v = mxa::rs_exponential(r, a); break;
+    default: v = mxa::rs_uniform(r, a, b); break;
+    }
+    if (__lane_id() == 0) out[i] = v;
+  }
+}
+
+__global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y, double* out, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = mode == 0 ? gm_log(x[i]) : mode == 1 ? gm_exp(x[i]) : gm_pow(x[i], y[i]);
+}
+
+// explicit instantiations per supported configuration
+#define MXA_INST(SQ, SO, PL)                                                                              \
+  template __global__ void mxa_build_kernel<SQ, SO, PL>(MxaParams, char*, const uint32_t*, const uint8_t*); \
+  template __global__ void mxa_run_kernel<SQ, SO, PL>(MxaParams, char*, int64_t);
+MXA_INST(4, 2, true)     // rmsc03
+MXA_INST(8, 2, true)     // sparse_zi_100
+MXA_INST(48, 16, false)  // sparse_zi_1000

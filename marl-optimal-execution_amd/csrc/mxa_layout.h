@@ -1,0 +1,151 @@
+// mxa_layout.h — plain-old-data shared by the host C-ABI (mxa_api.cpp) and the HIP
+// kernels (mxa_kernels.hip): configuration parameters, the per-environment HBM block
+// layout, the 24-byte message payload and the 10-word trace record.
+//
+// One environment (= one independent market = one reference Kernel run) is simulated by
+// ONE wavefront.  Its state lives in one contiguous HBM block ("env block", stride
+// Layout::env_stride) so that every per-env array is read/written by the wave as
+// coalesced 64-lane accesses; while a kernel runs, the event queue lives in LDS and the
+// limit order book in VGPRs (see DESIGN.md §Data layout).
+#pragma once
+#include <stdint.h>
+
+#define MXA_MAX_AGENTS 2047  // 11-bit recipient field in the event key
+#define MXA_MT_N 624
+#define MXA_MT_M 397
+#define MXA_RNG_WORDS 640     // 624 key words + pos/has_gauss/gauss/pad (2560 B per stream)
+
+enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2 };
+
+// message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
+enum {
+  MK_WAKEUP = 0, MK_WHEN_OPEN_REQ = 1, MK_WHEN_CLOSE_REQ = 2, MK_WHEN_OPEN = 3, MK_WHEN_CLOSE = 4,
+  MK_SPREAD_REQ = 5, MK_SPREAD = 6, MK_LAST_REQ = 7, MK_LAST = 8, MK_TV_REQ = 9, MK_TV = 10,
+  MK_LIMIT = 11, MK_CANCEL = 12, MK_MODIFY = 13, MK_ACCEPTED = 14, MK_EXECUTED = 15, MK_CANCELLED = 16,
+  MK_MKT_CLOSED = 17, MK_MODIFIED = 18, MK_KCANCEL = 19, MK_MARKET_DATA = 20
+};
+// kernel message types (message/Message.py:5-8)
+enum { MT_MESSAGE = 1, MT_WAKEUP = 2, MT_CANCEL_ORDER = 3 };
+
+// agent classes
+enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_MOMENTUM = 5 };
+
+// env status flags (EnvHdr::status)
+enum { ST_RUNNING = 0, ST_DONE = 1, ST_ERROR = 2 };
+enum {
+  ERR_NONE = 0, ERR_QUEUE_FULL = 1, ERR_BOOK_FULL = 2, ERR_OPEN_FULL = 3, ERR_TX_FULL = 4,
+  ERR_PANDAS_NO_TX = 5, ERR_WAKEUP_PAST = 6, ERR_THETA_INDEX = 7, ERR_BAD_CONFIG = 8
+};
+
+// per-env scalar header (first bytes of the env block)
+typedef struct {
+  int64_t cur;          // Kernel.currentTime (ns since midnight of the simulated date)
+  int64_t pops;         // ttl_messages
+  uint64_t hash;        // rolling FNV over trace records
+  int64_t order_counter;
+  int32_t status, err;
+  uint32_t seq;         // Message.uniq analogue (per env)
+  uint32_t arrival;     // book FIFO arrival counter
+  int32_t epoch;        // OrderBook.history shift counter
+  int32_t tx_head;      // transaction ring write position (monotonic)
+  int64_t last_trade;
+  int32_t last_trade_float, pad0;
+  int32_t pad_ep[16];
+  // oracle (SparseMeanRevertingOracle)
+  int64_t o_pt, o_mst;
+  double o_pv, o_msv;
+  // global RNG streams G, O, K, L: pos / gauss cache
+  int32_t rs_pos[4], rs_has_gauss[4];
+  double rs_gauss[4];
+  int32_t q_count, b_count;      // saved queue / book occupancy
+  int64_t trace_len;
+  int64_t ex_comp_delay;         // exchange's current computation delay
+  int32_t max_q, max_book;       // capacity high-water marks (diagnostics)
+  int64_t pad1[3];
+} EnvHdr;
+
+// one event slot as saved between launches (and payload as pushed)
+typedef struct {
+  uint64_t key;   // t << 13 | recipient << 2 | type
+  uint32_t seq;
+  uint32_t pad;
+  uint32_t pl[6]; // payload
+} SavedEvent;   // 32 B
+
+// book slot as saved between launches
+typedef struct {
+  int32_t price, qty, oid, meta;  // meta = agent << 1 | is_buy, -1 = free
+  uint32_t arrival;
+  int32_t hepoch;
+  int32_t pad[2];
+} SavedOrder;   // 32 B
+
+typedef struct {  // transaction record of OrderBook.history (util/OrderBook.py:227,235)
+  int64_t t;
+  int32_t q, epoch;
+} TxRec;
+
+typedef struct {  // TradingAgent.orders entry (agent's copy of an open order)
+  int32_t oid, is_buy, qty, price;
+} OpenOrder;
+
+typedef struct {
+  uint64_t env_stride;
+  uint32_t off_ag, off_open, off_rng, off_lat, off_q, off_book, off_tx, off_trace;
+  int32_t n_agents, n_streams, qcap, ocap, open_cap, tx_cap, trace_cap, lat_len;
+} Layout;
+
+// agent record: 128 dwords (512 B); lane i of the owning wave holds dwords 2i, 2i+1
+enum {
+  AF_TYPE = 0, AF_FLAGS = 1, AF_STATE = 2, AF_NORD = 3,
+  AF_MKT_OPEN = 4, AF_MKT_CLOSE = 6, AF_CASH = 8, AF_SHARES = 10, AF_LAST_TRADE = 12,
+  AF_BID = 14, AF_BIDQ = 15, AF_ASK = 16, AF_ASKQ = 17, AF_TV = 18, AF_PREV_WAKE = 20,
+  AF_R_T = 22, AF_SIGMA_T = 24, AF_START_CASH = 26, AF_SIZE = 28, AF_GROUP = 29,
+  AF_WAKEUP_TIME = 30, AF_RS_POS = 32, AF_RS_HASG = 33, AF_RS_GAUSS = 34, AF_LAST_MID = 36,
+  AF_ORDER_SIZE = 38, AF_NMID = 39, AF_N20 = 40, AF_N50 = 41, AF_AVG20 = 42, AF_AVG50 = 44,
+  AF_THETA = 46,      // 20 x int32
+  AF_MIDS = 66,       // 50 x int32 (2*mid ring), momentum
+  AF_ATIME = 120,     // Kernel.agentCurrentTimes[a]
+  AF_COMP = 122,      // Kernel.agentComputationDelays[a]
+  AF_END = 128
+};
+// AF_FLAGS bits
+enum {
+  FL_HAS_OPEN = 1, FL_HAS_CLOSE = 2, FL_MKT_CLOSED = 4, FL_FIRST_WAKE = 8, FL_DAILY_CLOSE = 16,
+  FL_TRADING = 32, FL_HAS_KNOWN = 64, FL_NB = 128, FL_NA = 256, FL_HAS_LAST = 512,
+  FL_LAST_FLOAT = 1024, FL_PREV_WAKE = 2048, FL_AW_SPREAD = 4096, FL_AW_TV = 8192, FL_LAST_MID = 16384
+};
+enum { AS_AWAITING_WAKEUP = 0, AS_INACTIVE = 1, AS_AWAITING_SPREAD = 2, AS_ACTIVE = 3 };
+
+typedef struct {
+  int32_t config, n_envs, n_agents, n_streams;
+  int64_t start, stop, mkt_open, mkt_close, default_comp_delay;
+  int32_t lat_mode, noise_len;   // 0 zero, 1 matrix (+uniform noise index), 2 cubic model
+  double jitter, clip, unit;
+  int64_t ex_pipeline, ex_comp;
+  int32_t stream_history, pad0;
+  double o_rbar, o_kappa, o_fundvol, o_lambda, o_msmean, o_msvar;
+  int64_t starting_cash;
+  int32_t first_zi, n_zi, first_noise, n_noise, first_value, n_value, first_mm, n_mm, first_mom, n_mom;
+  // ZeroIntelligenceAgent
+  double zi_sigma_n, zi_rbar, zi_kappa, zi_sigma_s, zi_lambda, zi_sigma_pv;
+  int32_t zi_qmax, zi_ngroups;
+  int32_t zi_group_count[8], zi_rmin[8], zi_rmax[8];
+  double zi_eta[8];
+  // ValueAgent
+  double v_sigma_n, v_rbar, v_kappa, v_sigma_s, v_lambda, v_percent_aggr;
+  int32_t v_depth_spread, pad1;
+  // NoiseAgent wake window
+  int64_t noise_open, noise_close;
+  // POVMarketMakerAgent
+  double mm_pov;
+  int32_t mm_min_size, mm_window, mm_ticks, pad2;
+  int64_t mm_wake;
+  // MomentumAgent
+  int32_t mom_min, mom_max;
+  int64_t mom_wake;
+  double lat_lo, lat_hi;   // G.uniform bounds of the latency matrix
+  Layout L;
+} MxaParams;
+
+#define MXA_TRACE_WORDS 10

@@ -1,0 +1,73 @@
+"""ctypes binding of libmxa (include/mxa.h).
+
+The product path is the HIP library only: if lib/libmxa.so is missing or cannot be
+loaded this module raises — there is deliberately no CPU fallback.
+"""
+import ctypes
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libmxa.so")
+
+MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000 = 0, 1, 2
+CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000}
+ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
+ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",
+             4: "transaction history capacity", 5: "get_transacted_volume without transactions (pandas error)",
+             6: "setWakeup in the past", 7: "ZI theta index (IndexError)", 8: "bad config"}
+
+
+class EnvSummary(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("err", ctypes.c_int32), ("events", ctypes.c_int64),
+                ("hash", ctypes.c_uint64), ("current_time", ctypes.c_int64), ("order_counter", ctypes.c_int64),
+                ("last_trade", ctypes.c_int64), ("max_queue", ctypes.c_int32), ("max_book", ctypes.c_int32)]
+
+
+class AgentState(ctypes.Structure):
+    _fields_ = [("cash", ctypes.c_int64), ("shares", ctypes.c_int64), ("n_open", ctypes.c_int64),
+                ("last_trade", ctypes.c_int64), ("type", ctypes.c_int32), ("flags", ctypes.c_int32)]
+
+
+EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_read_summary", "mxa_read_agents",
+           "mxa_read_book", "mxa_read_trace", "mxa_n_agents", "mxa_n_envs", "mxa_env_bytes", "mxa_set_stream",
+           "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe"]
+
+_lib = None
+
+
+class MxaError(RuntimeError):
+    pass
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MxaError("libmxa.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, U32, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_double
+    L.mxa_create.argtypes = [I32, I32, P, I32, I32, ctypes.POINTER(P)]
+    L.mxa_reset.argtypes = [P, P]
+    L.mxa_launch.argtypes = [P, I64]
+    L.mxa_sync.argtypes = [P]
+    L.mxa_run.argtypes = [P, I64, I32, ctypes.POINTER(I32)]
+    L.mxa_read_summary.argtypes = [P, P]
+    L.mxa_read_agents.argtypes = [P, I32, P, I32]
+    L.mxa_read_book.argtypes = [P, I32, I32, P, I32]
+    L.mxa_read_trace.argtypes = [P, I32, P, I64, ctypes.POINTER(I64)]
+    L.mxa_n_agents.argtypes = [P]
+    L.mxa_n_envs.argtypes = [P]
+    L.mxa_env_bytes.argtypes = [P]
+    L.mxa_env_bytes.restype = I64
+    L.mxa_set_stream.argtypes = [P, P]
+    L.mxa_last_kernel_ms.argtypes = [P]
+    L.mxa_last_kernel_ms.restype = D
+    L.mxa_last_error.argtypes = [P]
+    L.mxa_last_error.restype = ctypes.c_char_p
+    L.mxa_destroy.argtypes = [P]
+    L.mxa_destroy.restype = None
+    L.mxa_rng_probe.argtypes = [I32, U32, I32, D, D, I32, P]
+    L.mxa_math_probe.argtypes = [I32, I32, P, P, P, I64]
+    _lib = L
+    return L

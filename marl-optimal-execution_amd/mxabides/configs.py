@@ -1,0 +1,35 @@
+"""Agent naming of the reference configs (used for the reference-format stdout report).
+
+config/rmsc03.py:95-197, config/sparse_zi_100.py:177-256, config/sparse_zi_1000.py.
+"""
+ZI_GROUPS = [(0, 250, "1"), (0, 500, "1"), (0, 1000, "0.8"), (0, 1000, "1"), (0, 2000, "0.8"), (250, 500, "0.8"),
+             (250, 500, "1")]
+ZI_COUNTS = {"sparse_zi_100": [15, 15, 14, 14, 14, 14, 14], "sparse_zi_1000": [143] * 6 + [142]}
+
+
+def symbol_of(config):
+    return "ABM" if config == "rmsc03" else "JPM"
+
+
+def agent_names(config):
+    if config == "rmsc03":
+        return (["EXCHANGE_AGENT"] + ["NoiseAgent %d" % j for j in range(1, 51)] +
+                ["Value Agent %d" % j for j in range(51, 61)] + ["POV_MARKET_MAKER_AGENT_61"] +
+                ["MOMENTUM_AGENT_%d" % j for j in (62, 63)])
+    names, a = ["Exchange Agent 0"], 1
+    for g, cnt in enumerate(ZI_COUNTS[config]):
+        lo, hi, eta = ZI_GROUPS[g]
+        for _ in range(cnt):
+            names.append("ZI Agent %d Type %d [%d <= R <= %d, eta=%s]" % (a, g + 1, lo, hi, eta))
+            a += 1
+    return names
+
+
+def agent_type_names(config):
+    if config == "rmsc03":
+        return ["ExchangeAgent"] + ["NoiseAgent"] * 50 + ["ValueAgent"] * 10 + ["POVMarketMakerAgent"] + ["MomentumAgent"] * 2
+    out = ["ExchangeAgent"]
+    for g, cnt in enumerate(ZI_COUNTS[config]):
+        lo, hi, eta = ZI_GROUPS[g]
+        out += ["ZeroIntelligenceAgent Type %d [%d <= R <= %d, eta=%s]" % (g + 1, lo, hi, eta)] * cnt
+    return out

@@ -1,0 +1,135 @@
+"""VecMarket: N independent ABIDES markets of one configuration on one MI355X.
+
+Host mirror of the reference's batch entry point (`python abides.py -c <config> -s <seed>`,
+abides.py:19-29 -> config/<config>.py -> Kernel.runner, Kernel.py:50-345): every env is
+one reference simulation with its own seed, all simulated by libmxa's HIP kernels.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .configs import agent_names, agent_type_names, symbol_of
+
+CHUNK_DEFAULT = 1 << 20
+
+
+class VecMarket:
+    def __init__(self, config, seeds, device=0, trace_cap=0):
+        if config not in _lib.CONFIG_IDS:
+            raise ValueError("unknown config %r (supported: %s)" % (config, sorted(_lib.CONFIG_IDS)))
+        self.L = _lib.load()
+        self.config = config
+        self.seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
+        self.n_envs = len(self.seeds)
+        self.device = device
+        self.trace_cap = trace_cap
+        self._h = ctypes.c_void_p()
+        rc = self.L.mxa_create(_lib.CONFIG_IDS[config], self.n_envs, self.seeds.ctypes.data, device, trace_cap,
+                               ctypes.byref(self._h))
+        self._check(rc, "mxa_create")
+        self.n_agents = self.L.mxa_n_agents(self._h)
+
+    def _check(self, rc, what):
+        if rc < 0:
+            msg = self.L.mxa_last_error(self._h).decode() if self._h else ""
+            raise _lib.MxaError("%s failed (%d): %s" % (what, rc, msg))
+        return rc
+
+    # ---- lifecycle
+    def reset(self, mask=None):
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(mask, dtype=np.uint8)
+        self._check(self.L.mxa_reset(self._h, m.ctypes.data if m is not None else None), "mxa_reset")
+
+    def launch(self, max_pops):
+        self._check(self.L.mxa_launch(self._h, max_pops), "mxa_launch")
+
+    def sync(self):
+        self._check(self.L.mxa_sync(self._h), "mxa_sync")
+
+    def run(self, chunk=CHUNK_DEFAULT, max_launches=0):
+        n = ctypes.c_int32()
+        self._check(self.L.mxa_run(self._h, chunk, max_launches, ctypes.byref(n)), "mxa_run")
+        return n.value
+
+    @property
+    def last_kernel_ms(self):
+        return self.L.mxa_last_kernel_ms(self._h)
+
+    @property
+    def env_bytes(self):
+        return self.L.mxa_env_bytes(self._h)
+
+    # ---- inspection
+    def summary(self):
+        arr = (_lib.EnvSummary * self.n_envs)()
+        self._check(self.L.mxa_read_summary(self._h, arr), "mxa_read_summary")
+        names = [f[0] for f in _lib.EnvSummary._fields_]
+        out = {k: np.array([getattr(a, k) for a in arr]) for k in names}
+        out["hash"] = out["hash"].astype(np.uint64)
+        return out
+
+    def agents(self, env):
+        arr = (_lib.AgentState * self.n_agents)()
+        self._check(self.L.mxa_read_agents(self._h, env, arr, self.n_agents), "mxa_read_agents")
+        return [dict(cash=a.cash, shares=a.shares, n_open=a.n_open, last_trade=a.last_trade, type=a.type,
+                     flags=a.flags) for a in arr]
+
+    def book(self, env, side):
+        """OrderBook.bids (side 0) / asks (side 1): list of levels, each a FIFO list of
+        [order_id, agent_id, quantity, price]."""
+        cap = 4096
+        buf = np.zeros((cap, 4), dtype=np.int64)
+        n = self._check(self.L.mxa_read_book(self._h, env, side, buf.ctypes.data, cap), "mxa_read_book")
+        levels = []
+        for o in buf[:n].tolist():
+            if levels and levels[-1][0][3] == o[3]:
+                levels[-1].append(o)
+            else:
+                levels.append([o])
+        return levels
+
+    def trace(self, env):
+        if not self.trace_cap:
+            raise ValueError("created with trace_cap=0")
+        buf = np.zeros((self.trace_cap, 10), dtype=np.int64)
+        n = ctypes.c_int64()
+        self._check(self.L.mxa_read_trace(self._h, env, buf.ctypes.data, self.trace_cap, ctypes.byref(n)),
+                    "mxa_read_trace")
+        return buf[:n.value]
+
+    def report(self, env):
+        """The reference's end-of-run stdout: TradingAgent.kernelStopping "Final holdings"
+        lines (TradingAgent.py:121-126) and Kernel's mean ending value per agent type
+        (Kernel.py:337-341)."""
+        FL_LAST_FLOAT = 1024
+        names, tnames, sym = agent_names(self.config), agent_type_names(self.config), symbol_of(self.config)
+        lines, gains, counts, order = [], {}, {}, []
+        for a, st in enumerate(self.agents(env)):
+            if a == 0:
+                continue
+            hold = "{ %s: %d, CASH: %d }" % (sym, st["shares"], st["cash"]) if st["shares"] else "{ CASH: %d }" % st["cash"]
+            mtm = st["cash"] + (st["last_trade"] * st["shares"] if st["shares"] else 0)
+            flt = bool(st["shares"]) and bool(st["flags"] & FL_LAST_FLOAT)
+            lines.append("Final holdings for %s: %s.  Marked to market: %s" % (names[a], hold, ("%d.0" % mtm) if flt else str(mtm)))
+            t = tnames[a]
+            if t not in gains:
+                gains[t], counts[t] = 0, 0
+                order.append(t)
+            gains[t] += mtm - 10000000
+            counts[t] += 1
+        means = ["%s: %d" % (t, int(round(gains[t] / counts[t]))) for t in order]
+        return lines, means
+
+    def close(self):
+        if self._h:
+            self.L.mxa_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

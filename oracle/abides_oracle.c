@@ -284,6 +284,7 @@ struct ora_env {
     int done, err;
     char errstr[160];
     int64_t order_counter;
+    int64_t st_max_heap, st_max_resting, st_max_open, st_resting, st_max_hist_tx;
     char* report;
     int64_t report_len;
 };
@@ -322,6 +323,7 @@ static void heap_push(ora_env* e, ev_t v) {
         i = p;
     }
     e->heap[i] = v;
+    if (e->nheap > e->st_max_heap) e->st_max_heap = e->nheap;
 }
 static ev_t heap_pop(ora_env* e) {
     ev_t top = e->heap[0];
@@ -588,6 +590,7 @@ static int execute_order(ora_env* e, bord_t* order, bord_t* matched) {
     if (!match) return 0;
     if (order->qty >= head->qty) {
         *matched = *head;
+        e->st_resting--;
         level_remove(&book->lv[0], 0);
         if (book->lv[0].n == 0) side_delete_level(book, 0);
     } else {
@@ -607,6 +610,7 @@ static int execute_order(ora_env* e, bord_t* order, bord_t* matched) {
 
 /* enterOrder (OrderBook.py:256-282) */
 static void enter_order(ora_env* e, bord_t o) {
+    if (++e->st_resting > e->st_max_resting) e->st_max_resting = e->st_resting;
     side_t* book = &e->book[o.is_buy ? 0 : 1];
     if (book->n == 0) {
         side_insert_level(book, 0, o);
@@ -677,6 +681,7 @@ static void cancel_order(ora_env* e, const msg_t* req) {
         for (int j = 0; j < L->n; j++) {
             if (L->o[j].id == req->oid) {
                 bord_t c = L->o[j];
+                e->st_resting--;
                 level_remove(L, j);
                 if (L->n == 0) side_delete_level(book, i);
                 msg_t m;
@@ -713,6 +718,7 @@ static int64_t transacted_volume(ora_env* e, int64_t lookback, int* err) {
         for (int j = 0; j < e->hist[i].n; j++)
             for (int t = 0; t < e->hist[i].e[j].ntx; t++) all[k++] = e->hist[i].e[j].tx[t];
     qsort(all, ntx, sizeof(txn_t), cmp_txn);
+    if (ntx > e->st_max_hist_tx) e->st_max_hist_tx = ntx;
     int64_t start = e->cur - lookback, vol = 0;
     for (int i = 0; i < ntx; i++) {
         if (i > 0 && cmp_txn(&all[i], &all[i - 1]) == 0) continue;
@@ -835,6 +841,7 @@ static void place_limit(ora_env* e, agent_t* a, int64_t qty, int is_buy, int64_t
         }
         aord_t o = {oid, is_buy, qty, price};
         a->ord[a->nord++] = o;
+        if (a->nord > e->st_max_open) e->st_max_open = a->nord;
         msg_t m;
         memset(&m, 0, sizeof m);
         m.kind = K_LIMIT;
@@ -1590,6 +1597,14 @@ int64_t ora_book(const ora_env* e, int side, int64_t* buf, int64_t cap) {
     return k;
 }
 int64_t ora_order_counter(const ora_env* e) { return e->order_counter; }
+/* capacity statistics: max pending events, max resting orders, max open orders of one agent,
+ * max live transaction records */
+void ora_stats(const ora_env* e, int64_t* out) {
+    out[0] = e->st_max_heap;
+    out[1] = e->st_max_resting;
+    out[2] = e->st_max_open;
+    out[3] = e->st_max_hist_tx;
+}
 int64_t ora_last_trade(const ora_env* e) { return e->last_trade; }
 int64_t ora_report(const ora_env* e, char* buf, int64_t cap) {
     if (!e->report) return 0;

@@ -33,7 +33,7 @@ extern "C" {
 
 typedef struct ora_env ora_env;
 
-/* config: "sparse_zi_100" | "sparse_zi_1000" | "rmsc03" */
+/* config: sparse_zi_100, sparse_zi_1000 or rmsc03 */
 int ora_create(const char* config, uint32_t seed, ora_env** out);
 void ora_destroy(ora_env* e);
 /* run up to max_pops kernel pops (<0: unlimited); returns pops performed by this call */
@@ -56,6 +56,7 @@ int ora_agent_state(const ora_env* e, int id, int64_t* cash, int64_t* shares, in
 int64_t ora_book(const ora_env* e, int side, int64_t* buf, int64_t cap);
 int64_t ora_order_counter(const ora_env* e);
 int64_t ora_last_trade(const ora_env* e);
+void ora_stats(const ora_env* e, int64_t* out);
 /* stdout restatement after ora_finish: "Final holdings ..." lines then "Mean..." lines */
 int64_t ora_report(const ora_env* e, char* buf, int64_t cap);
 

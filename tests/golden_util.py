@@ -1,0 +1,37 @@
+"""Helpers to read the committed reference fixtures (tests/golden/)."""
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = [("sparse_zi_100", 123456789), ("rmsc03", 123456789), ("rmsc03", 1008), ("rmsc03", 7),
+            ("sparse_zi_1000", 123456789)]
+
+
+def load(cfg, seed):
+    with open(os.path.join(GOLDEN, "%s_%d.json" % (cfg, seed))) as f:
+        d = json.load(f)
+    tr = np.load(os.path.join(GOLDEN, "%s_%d.npz" % (cfg, seed)))["trace"]
+    return d, tr
+
+
+def first_mismatch(a, b):
+    n = min(len(a), len(b))
+    bad = np.nonzero((a[:n] != b[:n]).any(1))[0]
+    return int(bad[0]) if len(bad) else (-1 if len(a) == len(b) else n)
+
+
+def kat_lines():
+    lines = open(os.path.join(GOLDEN, "sparse_zi_1000_kat.txt")).read().splitlines()
+    holdings = [l.strip() for l in lines if l.startswith("Final holdings")]
+    means, take = [], False
+    for l in lines:
+        if l.startswith("Mean ending value"):
+            take = True
+            continue
+        if take:
+            if not l.startswith("\t"):
+                break
+            means.append(l.strip())
+    return holdings, means

@@ -1,0 +1,74 @@
+"""The CPU parity oracle is pinned against the reference's own outputs:
+golden traces captured from the reference (tests/golden/gen_fixtures.py) and the
+reference's known-answer file tests/sparse_zi_1000.txt."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from golden_util import FIXTURES, first_mismatch, kat_lines, load
+
+
+@pytest.mark.parametrize("cfg,seed", FIXTURES)
+def test_oracle_matches_reference_fixture(cfg, seed):
+    d, ref = load(cfg, seed)
+    e = pyoracle.OracleEnv(cfg, seed, trace_cap=len(ref))
+    e.run()
+    assert e.error[0] == 0
+    tr = e.trace()
+    assert first_mismatch(tr, ref) == -1 or len(tr) == len(ref) and first_mismatch(tr, ref) == -1
+    assert e.events == d["events"]
+    assert "%016x" % e.hash == d["hash"]
+    e.finish()
+    rep = e.report()
+    assert [l for l in rep if l.startswith("Final holdings")] == d["final_holdings_lines"]
+    assert [l for l in rep if not l.startswith("Final holdings")] == d["mean_lines"]
+    assert e.book(0) == d["bids"] and e.book(1) == d["asks"]
+    assert e.order_counter - 1 == d["order_id_counter"]
+    assert e.last_trade == d["last_trade"]
+
+
+def test_oracle_sparse_zi_1000_known_answer():
+    """tests/sparse_zi_1000.txt of the reference: 1000 holdings lines, 7 means, 185200 msgs."""
+    holdings, means = kat_lines()
+    e = pyoracle.OracleEnv("sparse_zi_1000", 123456789)
+    e.run()
+    assert e.events == 185200
+    e.finish()
+    rep = e.report()
+    assert sorted(l for l in rep if l.startswith("Final holdings")) == sorted(holdings)
+    assert [l for l in rep if not l.startswith("Final holdings")] == means
+
+
+def test_oracle_rng_known_answers(golden):
+    kats = json.load(open(os.path.join(golden, "rng_kats.json")))
+    for seed, d in kats.items():
+        r = pyoracle.RandomState(int(seed))
+        assert [r.u32() for _ in range(len(d["u32"]))] == d["u32"]
+        r = pyoracle.RandomState(int(seed))
+        assert [r.rand() for _ in range(len(d["double"]))] == d["double"]
+        r = pyoracle.RandomState(int(seed))
+        for name, a, b, v in d["mixed"]:
+            if name == "randint":
+                assert r.randint(a, b) == v
+            elif name == "normal":
+                assert r.normal(a, b) == v
+            elif name == "exponential":
+                assert r.exponential(a) == v
+            elif name == "uniform":
+                assert r.uniform(a, b) == v
+            else:
+                assert r.rand() == v
+
+
+def test_oracle_batch_runner_deterministic():
+    seeds = np.arange(1, 9, dtype=np.uint32)
+    ev1, h1, _ = pyoracle.run_batch("rmsc03", seeds, threads=4)
+    ev2, h2, _ = pyoracle.run_batch("rmsc03", seeds[::-1].copy(), threads=2)
+    assert (ev1 == ev2[::-1]).all() and (h1 == h2[::-1]).all()
+    for i, s in enumerate(seeds[:2]):
+        e = pyoracle.OracleEnv("rmsc03", int(s))
+        e.run()
+        assert e.events == ev1[i] and e.hash == h1[i]
