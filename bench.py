@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/sec of the rmsc03 market step on MI355X (BASELINE.json metric).
+
+One env-step = one Kernel event pop in one env (the reference's ttl_messages,
+Kernel.py:211, 321-326).  One bench "step" = one full rmsc03 episode (config build from
+seeds + the whole 15-minute session + stop-time tail) of every env on every GPU; the
+per-env episode records are all-gathered over RCCL (the only collective: envs are
+independent, so the batch shards with no data-path exchange — weak scaling, 4096 envs
+per GPU).  Rank 0 prints one JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--config rmsc03]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "marl-optimal-execution_amd"), os.path.join(ROOT, "oracle")]
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+import mxabides
+
+METRIC = "env-steps/sec (whole node), rmsc03 100-agent market ×4096 envs, 1/2/4/8 GPUs"
+SEED0 = 123456789
+ALGO_BYTES_PER_EVENT = 256  # nominal algorithmic HBM bytes per event
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--config", default="rmsc03")
+    ap.add_argument("--chunk", type=int, default=1 << 22, help="max pops per env per kernel launch")
+    ap.add_argument("--cpu-envs", type=int, default=2048, help="CPU-baseline sample size (envs)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n = args.envs
+
+    def seeds_for(step):
+        first = SEED0 + (step * world + rank) * n
+        return (np.arange(first, first + n, dtype=np.int64)) & 0xFFFFFFFF
+
+    m = mxabides.VecMarket(args.config, seeds_for(0), device=local)
+    stream = torch.cuda.current_stream()
+    m.set_stream(stream.cuda_stream)
+    res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    gathered = torch.zeros((world * n, 4), dtype=torch.int64, device="cuda") if world > 1 else res
+
+    kernel_ms, launches = [0.0], [0]
+
+    def step(k):
+        m.set_seeds(seeds_for(k))
+        m.reset()
+        launches[0] += m.run(chunk=args.chunk)
+        kernel_ms[0] += m.last_kernel_ms
+        m.write_results(res.data_ptr())
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, res)  # episode records over RCCL/xGMI
+        return res[:, 0].sum()
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    kernel_ms[0], launches[0] = 0.0, 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev = torch.zeros((), dtype=torch.int64, device="cuda")
+    for k in range(args.warmup, args.warmup + args.steps):
+        ev += step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+    elapsed = float(elapsed.item())
+    events = int(ev.item())
+    summ = m.summary()
+    n_err = int((summ["status"] == 2).sum())
+
+    if rank == 0:
+        ms_step = 1000.0 * elapsed / args.steps
+        my_events_per_launch = events / world / max(1, launches[0])
+        avg_launch_ms = kernel_ms[0] / max(1, launches[0])
+        achieved = ALGO_BYTES_PER_EVENT * my_events_per_launch / (avg_launch_ms * 1e-3) / 1e9
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", "hbm_traffic_r01.json")
+        if os.path.exists(prof):
+            with open(prof) as f:
+                p = json.load(f)
+            if p.get("config") == args.config and p.get("envs") == n:
+                traffic = p.get("bytes_per_launch")
+        out = {
+            "metric": METRIC, "value": events / elapsed, "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "%s x%d envs per GPU, full episode per step (config build from seeds + "
+                                   "09:30-09:45 session + 1 min tail), seeds %d+global_env" % (args.config, n, SEED0),
+                       "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": m.n_agents,
+                       "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
+                       "env_errors": n_err},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "mxa_run_kernel<4,2,true>", "avg_launch_ms": avg_launch_ms,
+                         "launches": launches[0], "algo_bytes_per_event": ALGO_BYTES_PER_EVENT},
+        }
+        if not args.no_cpu:
+            import pyoracle
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            cseeds = (SEED0 + np.arange(args.cpu_envs, dtype=np.int64)) & 0xFFFFFFFF
+            cev, _, csec = pyoracle.run_batch(args.config, cseeds.astype(np.uint32), threads)
+            out["cpu_baseline"] = {"value": float(cev.sum()) / csec, "unit": "env-steps/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": "%d %s envs (seeds %d..), full episodes, C oracle, %d threads, %.1f s wall"
+                                             % (args.cpu_envs, args.config, SEED0, threads, csec)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -67,6 +67,15 @@ int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t ca
  * (order_id, agent_id, quantity, price).  Returns the number of orders (<= cap). */
 int mxa_read_book(mxa_handle* h, int32_t env, int32_t side, int64_t* out4, int32_t cap);
 int mxa_read_trace(mxa_handle* h, int32_t env, int64_t* out /* [cap][10] */, int64_t cap, int64_t* n);
+/* replace the per-env seeds used by the next mxa_reset (n_envs values) */
+int mxa_set_seeds(mxa_handle* h, const uint32_t* seeds);
+/* write the per-env episode record [n_envs][4] int64 = (events, hash, status, current_time)
+ * into DEVICE memory on the handle's stream (e.g. a torch tensor to all-gather over RCCL) */
+int mxa_write_results(mxa_handle* h, void* device_out);
+/* diagnostics: copy `bytes` raw bytes of env `env`'s HBM block starting at `offset`; and
+ * the block's section offsets (Layout: ag, open, rng, lat, q, book, tx, trace) */
+int mxa_read_raw(mxa_handle* h, int32_t env, int64_t offset, int64_t bytes, void* out);
+int mxa_layout(const mxa_handle* h, int64_t* offsets8);
 int32_t mxa_n_agents(const mxa_handle* h);
 int32_t mxa_n_envs(const mxa_handle* h);
 /* device memory bytes per env block */

@@ -18,9 +18,15 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define GM_FN __host__ __device__ __forceinline__ static
+#ifdef MXA_NOINLINE_MATH
+#define GM_BIG __host__ __device__ __attribute__((noinline)) static
+#else
+#define GM_BIG __host__ __device__ __forceinline__ static
+#endif
 #define GM_TABLE_QUAL static __device__ __constant__ const
 #else
 #define GM_FN static inline
+#define GM_BIG static inline
 #define GM_TABLE_QUAL static const
 #endif
 
@@ -30,7 +36,7 @@ GM_FN uint64_t gm_asu64(double x) { return __builtin_bit_cast(uint64_t, x); }
 GM_FN double gm_asf64(uint64_t x) { return __builtin_bit_cast(double, x); }
 
 // ---------------------------------------------------------------- log (__log_fma)
-GM_FN double gm_log(double x) {
+GM_BIG double gm_log(double x) {
   uint64_t ix = gm_asu64(x);
   uint32_t top = (uint32_t)(ix >> 48);
   const uint64_t LO = 0x3fee000000000000ull, HI = 0x3ff1090000000000ull;
@@ -109,7 +115,7 @@ GM_FN double gm_exp_special(double tmp, uint64_t sbits, uint64_t ki) {
   return y * 0x1p-1022;
 }
 
-GM_FN double gm_exp(double x) {
+GM_BIG double gm_exp(double x) {
   uint64_t ix = gm_asu64(x);
   uint32_t abstop = (uint32_t)(ix >> 52) & 0x7ffu;
   if (abstop - 0x3c9u > 0x3eu) {
@@ -175,7 +181,7 @@ GM_FN double gm_pow_special(double tmp, uint64_t sbits, uint64_t ki) {
   return y * 0x1p-1022;
 }
 
-GM_FN double gm_pow(double x, double y) {
+GM_BIG double gm_pow(double x, double y) {
   uint32_t sign_bias = 0;
   uint64_t ix = gm_asu64(x), iy = gm_asu64(y);
   uint32_t topx = (uint32_t)(ix >> 52), topy = (uint32_t)(iy >> 52);

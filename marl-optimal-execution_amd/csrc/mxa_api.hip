@@ -20,17 +20,17 @@ constexpr int64_t NS = 1000000000LL;
 constexpr int64_t MIN = 60 * NS;
 constexpr int64_t HOUR = 60 * MIN;
 
-typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, const MxaParams&, char*, const uint32_t*, const uint8_t*);
-typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, const MxaParams&, char*, int64_t);
+typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, const MxaParams*, char*, const uint32_t*, const uint8_t*);
+typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, const MxaParams*, char*, int64_t);
 
 template <int SQ, int SO, bool PL>
-void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, const MxaParams& P, char* base, const uint32_t* seeds,
+void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, const MxaParams* P, char* base, const uint32_t* seeds,
                   const uint8_t* mask) {
   hipLaunchKernelGGL((mxa_build_kernel<SQ, SO, PL>), g, b, lds, s, P, base, seeds, mask);
 }
-template <int SQ, int SO, bool PL>
-void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, const MxaParams& P, char* base, int64_t max_pops) {
-  hipLaunchKernelGGL((mxa_run_kernel<SQ, SO, PL>), g, b, lds, s, P, base, max_pops);
+template <int SQ, int SO, bool PL, int W>
+void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, const MxaParams* P, char* base, int64_t max_pops) {
+  hipLaunchKernelGGL((mxa_run_kernel<SQ, SO, PL, W>), g, b, lds, s, P, base, max_pops);
 }
 
 __global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int n, int* out) {
@@ -38,10 +38,21 @@ __global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int 
   if (i < n && ((const EnvHdr*)(base + (size_t)i * stride))->status == ST_RUNNING) atomicAdd(out, 1);
 }
 
+__global__ void mxa_results_kernel(const char* base, uint64_t stride, int n, int64_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const EnvHdr* h = (const EnvHdr*)(base + (size_t)i * stride);
+  out[4 * i + 0] = h->pops;
+  out[4 * i + 1] = (int64_t)h->hash;
+  out[4 * i + 2] = h->status;
+  out[4 * i + 3] = h->cur;
+}
+
 }  // namespace
 
 struct mxa_handle {
   MxaParams P;
+  MxaParams* d_P = nullptr;  // device copy read by the kernels (s_load)
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
   char* d_env = nullptr;
@@ -213,11 +224,11 @@ static void layout(MxaParams& P, int sq, int so, bool pl, int trace_cap) {
   L.env_stride = off;
 }
 
-template <int SQ, int SO, bool PL>
+template <int SQ, int SO, bool PL, int W>
 static void bind(mxa_handle* h) {
   h->build = launch_build<SQ, SO, PL>;
-  h->run = launch_run<SQ, SO, PL>;
-  h->lds = (size_t)SQ * 64 * (12 + (PL ? 24 : 0));
+  h->run = launch_run<SQ, SO, PL, W>;
+  h->lds = (size_t)SQ * 64 * (12 + (PL ? 24 : 0)) + 512;  // queue + EnvHdr
 }
 
 extern "C" {
@@ -237,9 +248,11 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   }
   h->P.n_envs = n_envs;
   layout(h->P, sq, so, pl, trace_cap);
-  if (sq == 4 && so == 2 && pl) bind<4, 2, true>(h);
-  else if (sq == 8 && so == 2 && pl) bind<8, 2, true>(h);
-  else bind<48, 16, false>(h);
+  if (sq == 4 && so == 2 && pl) bind<4, 2, true, MXA_MIN_WAVES>(h);
+#ifndef MXA_ONLY_RMSC03
+  else if (sq == 8 && so == 2 && pl) bind<8, 2, true, 2>(h);
+  else bind<48, 16, false, 1>(h);
+#endif
   h->device = device;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
@@ -256,6 +269,8 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   HIPCHK(h, hipMalloc(&h->d_seeds, sizeof(uint32_t) * n_envs));
   HIPCHK(h, hipMalloc(&h->d_mask, n_envs));
   HIPCHK(h, hipMalloc(&h->d_count, sizeof(int)));
+  HIPCHK(h, hipMalloc(&h->d_P, sizeof(MxaParams)));
+  HIPCHK(h, hipMemcpyAsync(h->d_P, &h->P, sizeof(MxaParams), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(h->d_env, 0, bytes, h->stream));
   HIPCHK(h, hipMemcpyAsync(h->d_seeds, seeds, sizeof(uint32_t) * n_envs, hipMemcpyHostToDevice, h->stream));
   return mxa_reset(h, nullptr);
@@ -269,7 +284,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
     HIPCHK(h, hipMemcpyAsync(h->d_mask, mask, h->P.n_envs, hipMemcpyHostToDevice, h->stream));
     dm = h->d_mask;
   }
-  h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->P, h->d_env, h->d_seeds, dm);
+  h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_P, h->d_env, h->d_seeds, dm);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;
@@ -277,7 +292,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
 
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
   if (!h) return MXA_EINVAL;
-  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->P, h->d_env, max_pops);
+  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_P, h->d_env, max_pops);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
 }
@@ -296,7 +311,7 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   for (;;) {
     if (max_launches > 0 && launches >= max_launches) break;
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->P, h->d_env, chunk);
+    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_P, h->d_env, chunk);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     launches++;
@@ -394,6 +409,38 @@ int mxa_read_trace(mxa_handle* h, int32_t env, int64_t* out, int64_t cap, int64_
   return MXA_OK;
 }
 
+int mxa_set_seeds(mxa_handle* h, const uint32_t* seeds) {
+  if (!h || !seeds) return MXA_EINVAL;
+  HIPCHK(h, hipMemcpyAsync(h->d_seeds, seeds, sizeof(uint32_t) * h->P.n_envs, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_write_results(mxa_handle* h, void* device_out) {
+  if (!h || !device_out) return MXA_EINVAL;
+  int n = h->P.n_envs;
+  hipLaunchKernelGGL(mxa_results_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env, h->P.L.env_stride,
+                     n, (int64_t*)device_out);
+  HIPCHK(h, hipGetLastError());
+  return MXA_OK;
+}
+
+int mxa_read_raw(mxa_handle* h, int32_t env, int64_t offset, int64_t bytes, void* out) {
+  if (!h || env < 0 || env >= h->P.n_envs || offset < 0 || bytes < 0 || offset + bytes > (int64_t)h->P.L.env_stride)
+    return MXA_ERANGE;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpy(out, h->d_env + (size_t)env * h->P.L.env_stride + offset, bytes, hipMemcpyDeviceToHost));
+  return MXA_OK;
+}
+
+int mxa_layout(const mxa_handle* h, int64_t* o) {
+  if (!h || !o) return MXA_EINVAL;
+  const Layout& L = h->P.L;
+  o[0] = L.off_ag; o[1] = L.off_open; o[2] = L.off_rng; o[3] = L.off_lat;
+  o[4] = L.off_q; o[5] = L.off_book; o[6] = L.off_tx; o[7] = L.off_trace;
+  return MXA_OK;
+}
+
 int32_t mxa_n_agents(const mxa_handle* h) { return h ? h->P.n_agents : 0; }
 int32_t mxa_n_envs(const mxa_handle* h) { return h ? h->P.n_envs : 0; }
 int64_t mxa_env_bytes(const mxa_handle* h) { return h ? (int64_t)h->P.L.env_stride : 0; }
@@ -412,6 +459,7 @@ void mxa_destroy(mxa_handle* h) {
   if (h->d_seeds) hipFree(h->d_seeds);
   if (h->d_mask) hipFree(h->d_mask);
   if (h->d_count) hipFree(h->d_count);
+  if (h->d_P) hipFree(h->d_P);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
   if (h->own) hipStreamDestroy(h->own);

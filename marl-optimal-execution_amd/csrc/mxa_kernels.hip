@@ -24,6 +24,10 @@
 #include "glibc_math.h"
 #include "mxa_layout.h"
 
+#ifndef MXA_MIN_WAVES
+#define MXA_MIN_WAVES 4  // waves per SIMD the run kernel is register-budgeted for
+#endif
+
 typedef uint64_t u64;
 typedef int64_t i64;
 typedef uint32_t u32;
@@ -47,25 +51,68 @@ DEV u64 bal(bool p) { return __ballot(p); }
 DEV int ffs64(u64 b) { return __ffsll((unsigned long long)b) - 1; }
 DEV int ffs32(u32 b) { return __ffs(b) - 1; }
 DEV u32 sxor(u32 v, int m) { return (u32)__shfl_xor((int)v, m, 64); }
-DEV i32 wmax_i32(i32 v) {
-  for (int o = 1; o < 64; o <<= 1) { i32 t = (i32)sxor((u32)v, o); v = t > v ? t : v; }
-  return v;
+// ---- wave reductions on DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast15/31
+// across rows): lane 63 ends with the result, read back with v_readlane.  Every step is a
+// VALU op with a DPP source operand — no LDS round trip (ds_swizzle/bpermute).
+template <int CTRL, int ROWMASK>
+DEV u32 dpp(u32 identity, u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp((int)identity, (int)v, CTRL, ROWMASK, 0xf, false);
 }
-DEV i32 wmin_i32(i32 v) {
-  for (int o = 1; o < 64; o <<= 1) { i32 t = (i32)sxor((u32)v, o); v = t < v ? t : v; }
-  return v;
+#define MXA_DPP_STEPS(OP, ID, V)                        \
+  V = OP(V, dpp<0x111, 0xf>(ID, V));                    \
+  V = OP(V, dpp<0x112, 0xf>(ID, V));                    \
+  V = OP(V, dpp<0x114, 0xf>(ID, V));                    \
+  V = OP(V, dpp<0x118, 0xf>(ID, V));                    \
+  V = OP(V, dpp<0x142, 0xa>(ID, V));                    \
+  V = OP(V, dpp<0x143, 0xc>(ID, V));
+DEV u32 op_minu(u32 a, u32 b) { return a < b ? a : b; }
+DEV u32 op_add(u32 a, u32 b) { return a + b; }
+DEV u32 op_maxi(u32 a, u32 b) { return (i32)a > (i32)b ? a : b; }
+DEV u32 op_mini(u32 a, u32 b) { return (i32)a < (i32)b ? a : b; }
+DEV i32 wmax_i32(i32 x) {
+  u32 v = (u32)x;
+  MXA_DPP_STEPS(op_maxi, 0x80000000u, v)
+  return (i32)rdl(v, 63);
+}
+DEV i32 wmin_i32(i32 x) {
+  u32 v = (u32)x;
+  MXA_DPP_STEPS(op_mini, 0x7fffffffu, v)
+  return (i32)rdl(v, 63);
 }
 DEV u32 wmin_u32(u32 v) {
-  for (int o = 1; o < 64; o <<= 1) { u32 t = sxor(v, o); v = t < v ? t : v; }
-  return v;
+  MXA_DPP_STEPS(op_minu, 0xffffffffu, v)
+  return rdl(v, 63);
 }
-DEV i64 wsum_i64(i64 v) {
-  for (int o = 1; o < 64; o <<= 1) {
-    u64 u = (u64)v;
-    u64 t = ((u64)sxor((u32)(u >> 32), o) << 32) | sxor((u32)u, o);
-    v += (i64)t;
+// 64-bit sum: reduce the two 32-bit halves separately (each fits: |parts| < 2^32 * 64)
+DEV i64 wsum_i64(i64 x) {
+  // values summed here are non-negative quantities < 2^31; sum the low and high 32 bits as
+  // 64-bit-safe u32 pairs would need carries, so use two 32-bit sums of 16-bit splits
+  u32 lo = (u32)((u64)x & 0xFFFFu), hi = (u32)((u64)x >> 16);
+  MXA_DPP_STEPS(op_add, 0u, lo)
+  MXA_DPP_STEPS(op_add, 0u, hi)
+  return (i64)(((u64)rdl(hi, 63) << 16) + rdl(lo, 63));
+}
+// lexicographic (key64, seq32) min over the wave; returns in k/s (uniform)
+DEV void wmin_key(u64& k, u32& s) {
+  u32 kh = (u32)(k >> 32), kl = (u32)k;
+#define MXA_KSTEP(CTRL, RM)                                                   \
+  {                                                                           \
+    u32 th = dpp<CTRL, RM>(0xffffffffu, kh), tl = dpp<CTRL, RM>(0xffffffffu, kl); \
+    u32 ts = dpp<CTRL, RM>(0xffffffffu, s);                                    \
+    bool lt = th < kh || (th == kh && (tl < kl || (tl == kl && ts < s)));      \
+    kh = lt ? th : kh;                                                        \
+    kl = lt ? tl : kl;                                                        \
+    s = lt ? ts : s;                                                          \
   }
-  return v;
+  MXA_KSTEP(0x111, 0xf)
+  MXA_KSTEP(0x112, 0xf)
+  MXA_KSTEP(0x114, 0xf)
+  MXA_KSTEP(0x118, 0xf)
+  MXA_KSTEP(0x142, 0xa)
+  MXA_KSTEP(0x143, 0xc)
+#undef MXA_KSTEP
+  k = ((u64)rdl(kh, 63) << 32) | rdl(kl, 63);
+  s = rdl(s, 63);
 }
 DEV void wfence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 DEV i64 py_round(double x) { return (i64)__builtin_rint(x); }
@@ -303,10 +350,15 @@ DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
 template <int SQ, int SO, bool PL_LDS>
 struct Eng {
   static constexpr int QCAP = SQ * 64;
-  const MxaParams& P;
+  const MxaParams* PP;  // kernarg; re-laundered every event so LICM cannot pin its fields in SGPRs
   char* env;
   int lane;
-  EnvHdr h;
+  EnvHdr& h;  // cold header fields live in LDS for the duration of a launch
+  // hot header fields in SGPRs
+  i64 cur, pops, ocnt;
+  u64 hash;
+  u32 seq;
+  i32 status, err, qcount;
   // event queue: keys in LDS, payload in LDS (PL_LDS) or HBM; per-lane min cache
   u64* qk;
   u32* qs;
@@ -324,28 +376,29 @@ struct Eng {
   i64 add_delay;
   i64* trace;
 
-  DEV Eng(const MxaParams& p, char* e, char* lds) : P(p), env(e) {
+  static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 24 : 0));
+  DEV Eng(const MxaParams& p, char* e, char* lds) : PP(&p), env(e), h(*(EnvHdr*)(lds + LDS_Q)) {
     lane = laneid();
     qk = (u64*)lds;
     qs = (u32*)(lds + 8 * QCAP);
     if (PL_LDS) qpl = (u32*)(lds + 12 * QCAP);
-    else qpl = (u32*)(env + P.L.off_q + sizeof(SavedEvent) * QCAP);
-    trace = P.L.trace_cap ? (i64*)(env + P.L.off_trace) : nullptr;
+    else qpl = (u32*)(env + PP->L.off_q + sizeof(SavedEvent) * QCAP);
+    trace = PP->L.trace_cap ? (i64*)(env + PP->L.off_trace) : nullptr;
   }
 
   // ---------------- env block accessors
   DEV EnvHdr* hdr() { return (EnvHdr*)env; }
-  DEV u64* agent_ptr(int a) { return (u64*)(env + P.L.off_ag + (size_t)a * 512); }
-  DEV OpenOrder* open_ptr(int a) { return (OpenOrder*)(env + P.L.off_open + (size_t)a * P.L.open_cap * sizeof(OpenOrder)); }
-  DEV u32* rng_key(int s) { return (u32*)(env + P.L.off_rng + (size_t)s * MXA_RNG_WORDS * 4); }
-  DEV double* lat() { return (double*)(env + P.L.off_lat); }
-  DEV i32* ep_entries() { return (i32*)(env + P.L.off_tx); }               // 16 x i32
-  DEV TxRec* txr() { return (TxRec*)(env + P.L.off_tx + 64); }
+  DEV u64* agent_ptr(int a) { return (u64*)(env + PP->L.off_ag + (size_t)a * 512); }
+  DEV OpenOrder* open_ptr(int a) { return (OpenOrder*)(env + PP->L.off_open + (size_t)a * PP->L.open_cap * sizeof(OpenOrder)); }
+  DEV u32* rng_key(int s) { return (u32*)(env + PP->L.off_rng + (size_t)s * MXA_RNG_WORDS * 4); }
+  DEV double* lat() { return (double*)(env + PP->L.off_lat); }
+  DEV i32* ep_entries() { return (i32*)(env + PP->L.off_tx); }               // 16 x i32
+  DEV TxRec* txr() { return (TxRec*)(env + PP->L.off_tx + 64); }
 
   DEV void fail(int code) {
-    if (h.status != ST_ERROR) {
-      h.status = ST_ERROR;
-      h.err = code;
+    if (status != ST_ERROR) {
+      status = ST_ERROR;
+      err = code;
     }
   }
 
@@ -463,20 +516,14 @@ struct Eng {
     if (!PL_LDS) {
       if (lane < 6) qpl[slot * 6 + lane] = msel(m, lane);
     }
-    h.q_count++;
-    if (h.q_count > h.max_q) h.max_q = h.q_count;
+    qcount++;
+    if (qcount > h.max_q) h.max_q = qcount;
   }
   // lexicographic wave-min of the per-lane cached (key, seq); returns winning slot or -1
   DEV int q_peek(u64& key, u32& seq) {
     u64 k = mk;
     u32 s = ms;
-    for (int o = 1; o < 64; o <<= 1) {
-      u64 k2 = ((u64)sxor((u32)(k >> 32), o) << 32) | sxor((u32)k, o);
-      u32 s2 = sxor(s, o);
-      bool lt = k2 < k || (k2 == k && s2 < s);
-      k = lt ? k2 : k;
-      s = lt ? s2 : s;
-    }
+    wmin_key(k, s);
     key = k;
     seq = s;
     if (k == KEY_EMPTY) return -1;
@@ -492,7 +539,7 @@ struct Eng {
       qfree |= 1ull << (slot >> 6);
       q_rescan();
     }
-    h.q_count--;
+    qcount--;
   }
   DEV void q_rekey(int slot, u64 key) {
     if (lane == (slot & 63)) {
@@ -504,45 +551,45 @@ struct Eng {
   // ---------------- kernel services
   // Kernel.sendMessage (Kernel.py:347-425)
   DEV void send(int recipient, const Msg& m, i64 delay) {
-    i64 sent = h.cur + rg64(AF_COMP) + add_delay + delay;
+    i64 sent = cur + rg64(AF_COMP) + add_delay + delay;
     i64 deliver;
-    if (P.lat_mode == 2) {
+    if (PP->lat_mode == 2) {
       RS L = grs(3);
-      double x = rs_uniform(L, P.clip, 1.0);
+      double x = rs_uniform(L, PP->clip, 1.0);
       grs_put(3, L);
-      double mn = cur_agent == 0 ? lat()[recipient] : lat()[P.n_agents + cur_agent];
-      double l = mn + ((P.jitter / gm_pow(x, 3.0)) * (mn / P.unit));
+      double mn = cur_agent == 0 ? lat()[recipient] : lat()[PP->n_agents + cur_agent];
+      double l = mn + ((PP->jitter / gm_pow(x, 3.0)) * (mn / PP->unit));
       deliver = sent + (i64)l;
     } else {
       double l = 0.0;
-      if (P.lat_mode == 1) l = lat()[cur_agent == 0 ? recipient : cur_agent];
+      if (PP->lat_mode == 1) l = lat()[cur_agent == 0 ? recipient : cur_agent];
       i64 noise = 0;
-      if (P.noise_len > 1) {
+      if (PP->noise_len > 1) {
         RS K = grs(2);
-        noise = rs_randint(K, 0, P.noise_len);
+        noise = rs_randint(K, 0, PP->noise_len);
         grs_put(2, K);
       }
       deliver = sent + (i64)(l + (double)noise);
     }
     u64 key = ((u64)deliver << 13) | ((u64)recipient << 2) | MT_MESSAGE;
-    q_push(key, h.seq++, m);
+    q_push(key, seq++, m);
   }
   // Kernel.setWakeup (Kernel.py:435-462)
   DEV void wakeup_at(int agent, i64 t) {
-    if (t < h.cur) {
+    if (t < cur) {
       fail(ERR_WAKEUP_PAST);
       return;
     }
     Msg m = msg_make(MK_WAKEUP, 0);
     u64 key = ((u64)t << 13) | ((u64)agent << 2) | MT_WAKEUP;
-    q_push(key, h.seq++, m);
+    q_push(key, seq++, m);
   }
-  DEV i64 next_order_id() { return h.order_counter++; }
+  DEV i64 next_order_id() { return ocnt++; }
 
   // ---------------- SparseMeanRevertingOracle (SMRO:88-227)
   DEV double o_compute(i64 ts, double v_adj, i64 pt, double pv) {
     i64 d = ts - pt;
-    double mu = P.o_rbar, gamma = P.o_kappa, theta = P.o_fundvol;
+    double mu = PP->o_rbar, gamma = PP->o_kappa, theta = PP->o_fundvol;
     double loc = mu + (pv - mu) * gm_exp(-gamma * (double)d);
     double scale = (gm_pow(theta, 2.0) / (2 * gamma)) * (1 - gm_exp(-2 * gamma * (double)d));
     RS O = grs(1);
@@ -564,17 +611,17 @@ struct Eng {
       pt = h.o_mst;
       pv = v;
       RS G = grs(0);
-      h.o_mst = pt + (i64)rs_exponential(G, 1.0 / P.o_lambda);
+      h.o_mst = pt + (i64)rs_exponential(G, 1.0 / PP->o_lambda);
       grs_put(0, G);
       RS O = grs(1);
-      double msv = rs_normal(O, P.o_msmean, __builtin_sqrt(P.o_msvar));
+      double msv = rs_normal(O, PP->o_msmean, __builtin_sqrt(PP->o_msvar));
       h.o_msv = rs_randint(O, 0, 2) == 0 ? msv : -msv;
       grs_put(1, O);
     }
     return o_compute(t, 0, pt, pv);
   }
   DEV i64 o_observe(i64 t, double sigma_n) {
-    double r_t = t >= P.mkt_close ? o_advance(P.mkt_close - 1) : o_advance(t);
+    double r_t = t >= PP->mkt_close ? o_advance(PP->mkt_close - 1) : o_advance(t);
     if (sigma_n == 0) return (i64)r_t;
     RS A = agent_rs();
     i64 obs = py_round(rs_normal(A, r_t, __builtin_sqrt(sigma_n)));
@@ -660,11 +707,11 @@ struct Eng {
   // ---------------- OrderBook.history transaction ring (OrderBook.py:146-149, 227-237, 400-436)
   DEV void tx_add(i64 t, i32 q, i32 ep) {
     TxRec* R = txr();
-    int cap = P.L.tx_cap;
+    int cap = PP->L.tx_cap;
     int pos = h.tx_head % cap;
     if (h.tx_head >= cap) {  // overwriting the oldest record: it must be dead
       TxRec old = R[pos];
-      if (old.epoch >= h.epoch - P.stream_history) {
+      if (old.epoch >= h.epoch - PP->stream_history) {
         fail(ERR_TX_FULL);
         return;
       }
@@ -679,16 +726,16 @@ struct Eng {
     h.tx_head++;
   }
   DEV i64 transacted_volume(i64 lookback, int* perr) {
-    int lo_ep = h.epoch - P.stream_history;
+    int lo_ep = h.epoch - PP->stream_history;
     i32 entries = 0;
     i32* EP = ep_entries();
     for (int e = lo_ep < 0 ? 0 : lo_ep; e <= h.epoch; e++) entries += EP[e & 15];
     if (entries == 0) return 0;
     TxRec* R = txr();
-    int cap = P.L.tx_cap;
+    int cap = PP->L.tx_cap;
     int n = h.tx_head < cap ? h.tx_head : cap;
     int first = h.tx_head - n;
-    i64 start = h.cur - lookback;
+    i64 start = cur - lookback;
     i64 vol = 0;
     int live_total = 0;
     for (int b = 0; b < n; b += 64) {
@@ -723,7 +770,7 @@ struct Eng {
   DEV void ex_notify(int recipient, const Msg& m) {
     // ExchangeAgent.sendMessage: ORDER_* notifications carry the pipeline delay
     u32 k = m_kind(m);
-    i64 d = (k == MK_ACCEPTED || k == MK_CANCELLED || k == MK_EXECUTED) ? P.ex_pipeline : 0;
+    i64 d = (k == MK_ACCEPTED || k == MK_CANCELLED || k == MK_EXECUTED) ? PP->ex_pipeline : 0;
     send(recipient, m, d);
   }
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
@@ -751,8 +798,8 @@ struct Eng {
           b_set(bq, s, hq - qty);
         }
         // history: taker logs its pre-match remaining qty; maker its matched qty if retained
-        tx_add(h.cur, qty, h.epoch);
-        if (hh >= h.epoch - P.stream_history) tx_add(h.cur, mq, hh);
+        tx_add(cur, qty, h.epoch);
+        if (hh >= h.epoch - PP->stream_history) tx_add(cur, mq, hh);
         qty -= mq;
         Msg mt = msg_order(MK_EXECUTED, oid, agent, is_buy, mq, price, best);
         ex_notify(agent, mt);
@@ -768,7 +815,7 @@ struct Eng {
         ex_notify(agent, ma);
         break;
       }
-      if (h.status == ST_ERROR) return;
+      if (status == ST_ERROR) return;
     }
     if (executed) {
       h.last_trade = py_round((double)ex_pq / (double)ex_q);
@@ -789,10 +836,10 @@ struct Eng {
 
   // ExchangeAgent.receiveMessage (ExchangeAgent.py:129-340)
   DEV void ex_receive(const Msg& m) {
-    rs64(AF_COMP, P.ex_comp);
+    rs64(AF_COMP, PP->ex_comp);
     u32 k = m_kind(m);
     i32 sender = m_agent(m);
-    bool closed = h.cur > P.mkt_close;
+    bool closed = cur > PP->mkt_close;
     if (closed) {
       if (k == MK_LIMIT || k == MK_CANCEL || k == MK_MODIFY) {
         ex_notify(sender, msg_make(MK_MKT_CLOSED, 0));
@@ -808,7 +855,7 @@ struct Eng {
     case MK_WHEN_CLOSE_REQ: {
       rs64(AF_COMP, 0);
       Msg r = msg_make(k == MK_WHEN_OPEN_REQ ? MK_WHEN_OPEN : MK_WHEN_CLOSE, 0);
-      i64 d = k == MK_WHEN_OPEN_REQ ? P.mkt_open : P.mkt_close;
+      i64 d = k == MK_WHEN_OPEN_REQ ? PP->mkt_open : PP->mkt_close;
       r.w[0] |= 1u << 11;
       r.w[1] = (u32)(u64)d;
       r.w[2] = (u32)((u64)d >> 32);
@@ -886,7 +933,7 @@ struct Eng {
     i64 oid = next_order_id();
     if (qty > 0) {
       i32 n = rgi(AF_NORD);
-      if (n >= P.L.open_cap) {
+      if (n >= PP->L.open_cap) {
         fail(ERR_OPEN_FULL);
         return;
       }
@@ -962,8 +1009,8 @@ struct Eng {
     return (f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE) && !(f & FL_MKT_CLOSED);
   }
   DEV i64 wake_frequency(int type) {
-    if (type == AG_POVMM) return P.mm_wake;
-    if (type == AG_MOMENTUM) return P.mom_wake;
+    if (type == AG_POVMM) return PP->mm_wake;
+    if (type == AG_MOMENTUM) return PP->mom_wake;
     RS A = agent_rs();
     i64 v = rs_randint(A, 0, 100);
     agent_rs_put(A);
@@ -1056,7 +1103,7 @@ struct Eng {
       fl_set(FL_PREV_WAKE, true);
       rs64(AF_PREV_WAKE, rg64(AF_MKT_OPEN));
     }
-    double delta = (double)(h.cur - rg64(AF_PREV_WAKE));
+    double delta = (double)(cur - rg64(AF_PREV_WAKE));
     double c = 1 - kappa;
     double r_t = rgd(AF_R_T), sigma_t = rgd(AF_SIGMA_T);
     double r_tprime = (1 - gm_pow(c, delta)) * r_bar;
@@ -1066,13 +1113,13 @@ struct Eng {
     r_t = (sigma_n / (sigma_n + sigma_tprime)) * r_tprime;
     r_t += (sigma_tprime / (sigma_n + sigma_tprime)) * (double)obs;
     sigma_t = (sigma_n * sigma_t) / (sigma_n + sigma_t);
-    double d2 = (double)(rg64(AF_MKT_CLOSE) - h.cur);
+    double d2 = (double)(rg64(AF_MKT_CLOSE) - cur);
     if (!(d2 > 0)) d2 = 0;
     double r_T = (1 - gm_pow(c, d2)) * r_bar;
     r_T += gm_pow(c, d2) * r_t;
     rsd(AF_R_T, r_t);
     rsd(AF_SIGMA_T, sigma_t);
-    rs64(AF_PREV_WAKE, h.cur);
+    rs64(AF_PREV_WAKE, cur);
     return py_round(r_T);
   }
 
@@ -1084,9 +1131,9 @@ struct Eng {
     fl_set(FL_TRADING, true);
     if (fl(FL_MKT_CLOSED) && fl(FL_DAILY_CLOSE)) return;
     RS A = agent_rs();
-    double dt = rs_exponential(A, 1.0 / P.zi_lambda);
+    double dt = rs_exponential(A, 1.0 / PP->zi_lambda);
     agent_rs_put(A);
-    wakeup_at(cur_agent, h.cur + py_round(dt));
+    wakeup_at(cur_agent, cur + py_round(dt));
     if (fl(FL_MKT_CLOSED) && !fl(FL_DAILY_CLOSE)) {
       get_spread(1);
       rs(AF_STATE, AS_AWAITING_SPREAD);
@@ -1097,28 +1144,28 @@ struct Eng {
     rs(AF_STATE, AS_AWAITING_SPREAD);
   }
   DEV void zi_place() {
-    i64 obs = o_observe(h.cur, P.zi_sigma_n);
+    i64 obs = o_observe(cur, PP->zi_sigma_n);
     i64 q = (i64)((double)rg64(AF_SHARES) / 100);
     int buy;
-    if (q >= P.zi_qmax) buy = 0;
-    else if (q <= -P.zi_qmax) buy = 1;
+    if (q >= PP->zi_qmax) buy = 0;
+    else if (q <= -PP->zi_qmax) buy = 1;
     else {
       RS A = agent_rs();
       buy = (int)rs_randint(A, 0, 2);
       agent_rs_put(A);
     }
-    i64 r_T = bayes_r_T(obs, P.zi_kappa, P.zi_rbar, P.zi_sigma_n, P.zi_sigma_s);
-    q += P.zi_qmax - 1;
+    i64 r_T = bayes_r_T(obs, PP->zi_kappa, PP->zi_rbar, PP->zi_sigma_n, PP->zi_sigma_s);
+    q += PP->zi_qmax - 1;
     i64 idx = buy ? q + 1 : q;
-    if (idx < 0) idx += 2 * P.zi_qmax;
-    if (idx < 0 || idx >= 2 * P.zi_qmax) {
+    if (idx < 0) idx += 2 * PP->zi_qmax;
+    if (idx < 0 || idx >= 2 * PP->zi_qmax) {
       fail(ERR_THETA_INDEX);
       return;
     }
     i64 v = r_T + (i64)rgi(AF_THETA + (int)idx);
     int g = rgi(AF_GROUP);
     RS A = agent_rs();
-    i64 R = rs_randint(A, P.zi_rmin[g], (i64)P.zi_rmax[g] + 1);
+    i64 R = rs_randint(A, PP->zi_rmin[g], (i64)PP->zi_rmax[g] + 1);
     agent_rs_put(A);
     i64 p = buy ? v - R : v + R;
     i32 bid = 0, ask = 0;
@@ -1127,10 +1174,10 @@ struct Eng {
     ask = rgi(AF_ASK);
     if (buy && ask_vol > 0) {
       i64 R_ask = v - ask;
-      if ((double)R_ask >= P.zi_eta[g] * (double)R) p = ask;
+      if ((double)R_ask >= PP->zi_eta[g] * (double)R) p = ask;
     } else if (!buy && bid_vol > 0) {
       i64 R_bid = bid - v;
-      if ((double)R_bid >= P.zi_eta[g] * (double)R) p = bid;
+      if ((double)R_bid >= PP->zi_eta[g] * (double)R) p = bid;
     }
     place_limit(100, buy, p);
   }
@@ -1151,9 +1198,9 @@ struct Eng {
     fl_set(FL_TRADING, true);
     if (fl(FL_MKT_CLOSED) && fl(FL_DAILY_CLOSE)) return;
     RS A = agent_rs();
-    double dt = rs_exponential(A, 1.0 / P.v_lambda);
+    double dt = rs_exponential(A, 1.0 / PP->v_lambda);
     agent_rs_put(A);
-    wakeup_at(cur_agent, h.cur + py_round(dt));
+    wakeup_at(cur_agent, cur + py_round(dt));
     if (fl(FL_MKT_CLOSED) && !fl(FL_DAILY_CLOSE)) {
       get_spread(1);
       rs(AF_STATE, AS_AWAITING_SPREAD);
@@ -1164,8 +1211,8 @@ struct Eng {
     rs(AF_STATE, AS_AWAITING_SPREAD);
   }
   DEV void value_place() {
-    i64 obs = o_observe(h.cur, P.v_sigma_n);
-    i64 r_T = bayes_r_T(obs, P.v_kappa, P.v_rbar, P.v_sigma_n, P.v_sigma_s);
+    i64 obs = o_observe(cur, PP->v_sigma_n);
+    i64 r_T = bayes_r_T(obs, PP->v_kappa, PP->v_rbar, PP->v_sigma_n, PP->v_sigma_s);
     i32 bid, ask;
     bool hb = known_bid(bid), ha = known_ask(ask);
     int buy;
@@ -1176,8 +1223,8 @@ struct Eng {
       i64 spread = (i64)ask - bid;
       if (spread < 0) spread = -spread;
       i64 adj;
-      if (rs_double(G) < P.v_percent_aggr) adj = 0;
-      else adj = rs_randint(G, 0, P.v_depth_spread * spread);
+      if (rs_double(G) < PP->v_percent_aggr) adj = 0;
+      else adj = rs_randint(G, 0, PP->v_depth_spread * spread);
       if (r_T < mid) {
         buy = 0;
         p = bid + adj;
@@ -1209,7 +1256,7 @@ struct Eng {
     fl_set(FL_TRADING, true);
     if (fl(FL_MKT_CLOSED) && fl(FL_DAILY_CLOSE)) return;
     i64 wt = rg64(AF_WAKEUP_TIME);
-    if (wt > h.cur) wakeup_at(cur_agent, wt);
+    if (wt > cur) wakeup_at(cur_agent, wt);
     get_spread(1);
     rs(AF_STATE, AS_AWAITING_SPREAD);
   }
@@ -1232,7 +1279,7 @@ struct Eng {
   DEV void mm_wakeup() {
     if (ta_wakeup()) {
       get_spread(1);
-      get_tv(P.mm_wake);
+      get_tv(PP->mm_wake);
     }
   }
   DEV void mm_receive(const Msg& m) {
@@ -1240,8 +1287,8 @@ struct Eng {
     i64 mid = rg64(AF_LAST_MID);
     u32 k = m_kind(m);
     if (k == MK_TV && fl(FL_AW_TV)) {
-      i64 qty = py_round(P.mm_pov * (double)rg64(AF_TV));
-      rs(AF_ORDER_SIZE, (u32)(qty >= P.mm_min_size ? qty : P.mm_min_size));
+      i64 qty = py_round(PP->mm_pov * (double)rg64(AF_TV));
+      rs(AF_ORDER_SIZE, (u32)(qty >= PP->mm_min_size ? qty : PP->mm_min_size));
       fl_set(FL_AW_TV, false);
     }
     if (k == MK_SPREAD && fl(FL_AW_SPREAD)) {
@@ -1256,14 +1303,14 @@ struct Eng {
     }
     if (!fl(FL_AW_SPREAD) && !fl(FL_AW_TV)) {
       cancel_all();
-      i64 hb = mid - 1, la = mid + P.mm_window;
-      i64 lb = hb - P.mm_ticks, ha = la + P.mm_ticks;
+      i64 hb = mid - 1, la = mid + PP->mm_window;
+      i64 lb = hb - PP->mm_ticks, ha = la + PP->mm_ticks;
       i64 sz = rgi(AF_ORDER_SIZE);
       for (i64 p = lb; p <= hb; p++) place_limit(sz, 1, p);
       for (i64 p = la; p <= ha; p++) place_limit(sz, 0, p);
       fl_set(FL_AW_SPREAD, true);
       fl_set(FL_AW_TV, true);
-      wakeup_at(cur_agent, h.cur + P.mm_wake);
+      wakeup_at(cur_agent, cur + PP->mm_wake);
     }
   }
 
@@ -1304,7 +1351,7 @@ struct Eng {
           else place_limit(rgi(AF_SIZE), 0, bid);
         }
       }
-      wakeup_at(cur_agent, h.cur + P.mom_wake);
+      wakeup_at(cur_agent, cur + PP->mom_wake);
       rs(AF_STATE, AS_AWAITING_WAKEUP);
     }
   }
@@ -1334,9 +1381,39 @@ struct Eng {
   }
 
   // ---------------- state save/restore around a launch
+  DEV void hdr_from_global() {
+    const u64* src = (const u64*)hdr();
+    u64* dst = (u64*)&h;
+    if (lane < (int)(sizeof(EnvHdr) / 8)) dst[lane] = src[lane];
+    wfence();
+    cur = h.cur;
+    pops = h.pops;
+    ocnt = h.order_counter;
+    hash = h.hash;
+    seq = h.seq;
+    status = h.status;
+    err = h.err;
+    qcount = h.q_count;
+  }
+  DEV void hdr_to_global() {
+    if (lane == 0) {
+      h.cur = cur;
+      h.pops = pops;
+      h.order_counter = ocnt;
+      h.hash = hash;
+      h.seq = seq;
+      h.status = status;
+      h.err = err;
+      h.q_count = qcount;
+    }
+    wfence();
+    const u64* src = (const u64*)&h;
+    u64* dst = (u64*)hdr();
+    if (lane < (int)(sizeof(EnvHdr) / 8)) dst[lane] = src[lane];
+  }
   DEV void load() {
-    h = *hdr();
-    SavedEvent* sq = (SavedEvent*)(env + P.L.off_q);
+    hdr_from_global();
+    SavedEvent* sq = (SavedEvent*)(env + PP->L.off_q);
     qfree = 0;
     for (int j = 0; j < SQ; j++) {
       int slot = j * 64 + lane;
@@ -1348,7 +1425,7 @@ struct Eng {
       if (e.key == KEY_EMPTY) qfree |= 1ull << j;
     }
     q_rescan();
-    SavedOrder* so = (SavedOrder*)(env + P.L.off_book);
+    SavedOrder* so = (SavedOrder*)(env + PP->L.off_book);
     for (int j = 0; j < SO; j++) {
       SavedOrder o = so[j * 64 + lane];
       bp[j] = o.price;
@@ -1360,7 +1437,7 @@ struct Eng {
     }
   }
   DEV void save() {
-    SavedEvent* sq = (SavedEvent*)(env + P.L.off_q);
+    SavedEvent* sq = (SavedEvent*)(env + PP->L.off_q);
     for (int j = 0; j < SQ; j++) {
       int slot = j * 64 + lane;
       SavedEvent e;
@@ -1370,7 +1447,7 @@ struct Eng {
       for (int i = 0; i < 6; i++) e.pl[i] = PL_LDS ? qpl[slot * 6 + i] : 0u;
       sq[slot] = e;
     }
-    SavedOrder* so = (SavedOrder*)(env + P.L.off_book);
+    SavedOrder* so = (SavedOrder*)(env + PP->L.off_book);
     for (int j = 0; j < SO; j++) {
       SavedOrder o;
       o.price = bp[j];
@@ -1382,30 +1459,39 @@ struct Eng {
       o.pad[0] = o.pad[1] = 0;
       so[j * 64 + lane] = o;
     }
-    if (lane == 0) *hdr() = h;
+    hdr_to_global();
   }
 
   // ---------------- Kernel.runner event loop (Kernel.py:190-292)
   DEV void run(i64 max_pops) {
-    for (i64 n = 0; n < max_pops && h.status == ST_RUNNING; n++) {
+    for (i64 n = 0; n < max_pops && status == ST_RUNNING; n++) {
+      {  // opaque per event: params are re-read (s_load) instead of pinned in SGPRs by LICM
+        u64 pv = (u64)PP;
+        u32 plo = (u32)__builtin_amdgcn_readfirstlane((int)(u32)pv);
+        u32 phi = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(pv >> 32));
+#ifndef MXA_NO_LAUNDER
+        asm volatile("" : "+s"(plo), "+s"(phi));
+#endif
+        PP = (const MxaParams*)(((u64)phi << 32) | plo);
+      }
       u64 key;
-      u32 seq;
-      int slot = q_peek(key, seq);
-      if (slot < 0 || !(h.cur <= P.stop)) {
-        h.status = ST_DONE;
+      u32 eseq;
+      int slot = q_peek(key, eseq);
+      if (slot < 0 || !(cur <= PP->stop)) {
+        status = ST_DONE;
         break;
       }
       Msg m = pl_read(slot);
       i64 t = (i64)(key >> 13);
       int rcp = (int)((key >> 2) & 0x7FF);
       int type = (int)(key & 3);
-      h.cur = t;
+      cur = t;
       i64 rec[10];
       encode(key, m, rec);
-      u64 hs = h.hash;
+      u64 hs = hash;
       for (int i = 0; i < 10; i++) hs = (hs ^ (u64)rec[i]) * FNV_PRIME;
-      h.hash = hs;
-      if (trace && h.trace_len < P.L.trace_cap) {
+      hash = hs;
+      if (trace && h.trace_len < PP->L.trace_cap) {
         if (lane < 10) {
           i64 v = 0;
           for (int i = 0; i < 10; i++)
@@ -1414,7 +1500,7 @@ struct Eng {
         }
         h.trace_len++;
       }
-      h.pops++;
+      pops++;
       add_delay = 0;
       rec_load(rcp);
       i64 at = rg64(AF_ATIME);
@@ -1449,10 +1535,10 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
     this->rs(AF_TYPE, (u32)type);
     this->rs(AF_FLAGS, FL_FIRST_WAKE | FL_AW_SPREAD | FL_AW_TV);
     this->rs(AF_RS_POS, MXA_MT_N);
-    this->rs64(AF_START_CASH, this->P.starting_cash);
-    this->rs64(AF_CASH, this->P.starting_cash);
-    this->rs64(AF_ATIME, this->P.start);
-    this->rs64(AF_COMP, this->P.default_comp_delay);
+    this->rs64(AF_START_CASH, (*this->PP).starting_cash);
+    this->rs64(AF_CASH, (*this->PP).starting_cash);
+    this->rs64(AF_ATIME, (*this->PP).start);
+    this->rs64(AF_COMP, (*this->PP).default_comp_delay);
   }
   DEV i64 get_wake_time(RS& G, i64 open, i64 close) {  // util/util.py:35-58
     double u = rs_double(G);
@@ -1464,7 +1550,7 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
   }
   // expand every stream's init_genrand in parallel (lane = stream)
   DEV void seed_streams(int first) {
-    const MxaParams& P = this->P;
+    const MxaParams& P = (*this->PP);
     wfence();
     for (int b = first; b < P.n_streams; b += 64) {
       int s = b + this->lane;
@@ -1481,12 +1567,17 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
   }
 
   DEV void build(u32 seed) {
-    const MxaParams& P = this->P;
+    const MxaParams& P = (*this->PP);
     EnvHdr& h = this->h;
     h = EnvHdr();
-    h.hash = FNV_OFF;
-    h.status = ST_RUNNING;
-    h.cur = P.start;
+    this->hash = FNV_OFF;
+    this->status = ST_RUNNING;
+    this->err = 0;
+    this->pops = 0;
+    this->ocnt = 0;
+    this->seq = 0;
+    this->qcount = 0;
+    this->cur = P.start;
     for (int s = 0; s < 4; s++) h.rs_pos[s] = MXA_MT_N;
     this->mk = KEY_EMPTY;
     this->ms = 0xFFFFFFFFu;
@@ -1623,9 +1714,8 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
     // kernelStarting (every agent wakes at startTime, in id order)
     h.last_trade = (i64)P.o_rbar;
     h.last_trade_float = 1;
-    h.cur = P.start;
+    this->cur = P.start;
     for (int a = 0; a < n; a++) this->wakeup_at(a, P.start);
-    h.cur = P.start;
     this->save();
     // zero the history-epoch entry counts and the transaction ring
     if (this->lane < 16) this->ep_entries()[this->lane] = 0;
@@ -1646,8 +1736,9 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
 // kernels (one wavefront per env; grid = n_envs)
 // ------------------------------------------------------------------------------------
 template <int SQ, int SO, bool PL_LDS>
-__global__ __launch_bounds__(64) void mxa_build_kernel(MxaParams P, char* base, const uint32_t* seeds, const uint8_t* mask) {
+__global__ __launch_bounds__(64) void mxa_build_kernel(const MxaParams* __restrict__ Pg, char* base, const uint32_t* seeds, const uint8_t* mask) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  const MxaParams& P = *Pg;
   int env = blockIdx.x;
   if (env >= P.n_envs) return;
   if (mask && !mask[env]) return;
@@ -1655,9 +1746,10 @@ __global__ __launch_bounds__(64) void mxa_build_kernel(MxaParams P, char* base, 
   b.build(seeds[env]);
 }
 
-template <int SQ, int SO, bool PL_LDS>
-__global__ __launch_bounds__(64) void mxa_run_kernel(MxaParams P, char* base, int64_t max_pops) {
+template <int SQ, int SO, bool PL_LDS, int WAVES>
+__global__ __launch_bounds__(64, WAVES) void mxa_run_kernel(const MxaParams* __restrict__ Pg, char* base, int64_t max_pops) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  const MxaParams& P = *Pg;
   int env = blockIdx.x;
   if (env >= P.n_envs) return;
   char* e = base + (size_t)env * P.L.env_stride;
@@ -1698,9 +1790,11 @@ __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y
 }
 
 // explicit instantiations per supported configuration
-#define MXA_INST(SQ, SO, PL)                                                                              \
-  template __global__ void mxa_build_kernel<SQ, SO, PL>(MxaParams, char*, const uint32_t*, const uint8_t*); \
-  template __global__ void mxa_run_kernel<SQ, SO, PL>(MxaParams, char*, int64_t);
-MXA_INST(4, 2, true)     // rmsc03
-MXA_INST(8, 2, true)     // sparse_zi_100
-MXA_INST(48, 16, false)  // sparse_zi_1000
+#define MXA_INST(SQ, SO, PL, W)                                                                           \
+  template __global__ void mxa_build_kernel<SQ, SO, PL>(const MxaParams*, char*, const uint32_t*, const uint8_t*); \
+  template __global__ void mxa_run_kernel<SQ, SO, PL, W>(const MxaParams*, char*, int64_t);
+MXA_INST(4, 2, true, MXA_MIN_WAVES)     // rmsc03
+#ifndef MXA_ONLY_RMSC03
+MXA_INST(8, 2, true, 2)     // sparse_zi_100
+MXA_INST(48, 16, false, 1)  // sparse_zi_1000
+#endif

@@ -7,7 +7,7 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libmxa.so")
+LIB_PATH = os.environ.get("MXA_LIB") or os.path.join(PKG_ROOT, "lib", "libmxa.so")
 
 MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000 = 0, 1, 2
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000}
@@ -30,7 +30,8 @@ class AgentState(ctypes.Structure):
 
 EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_read_summary", "mxa_read_agents",
            "mxa_read_book", "mxa_read_trace", "mxa_n_agents", "mxa_n_envs", "mxa_env_bytes", "mxa_set_stream",
-           "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe"]
+           "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe",
+           "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout"]
 
 _lib = None
 
@@ -67,6 +68,10 @@ def load():
     L.mxa_last_error.restype = ctypes.c_char_p
     L.mxa_destroy.argtypes = [P]
     L.mxa_destroy.restype = None
+    L.mxa_set_seeds.argtypes = [P, P]
+    L.mxa_read_raw.argtypes = [P, I32, I64, I64, P]
+    L.mxa_layout.argtypes = [P, P]
+    L.mxa_write_results.argtypes = [P, P]
     L.mxa_rng_probe.argtypes = [I32, U32, I32, D, D, I32, P]
     L.mxa_math_probe.argtypes = [I32, I32, P, P, P, I64]
     _lib = L

@@ -43,6 +43,20 @@ class VecMarket:
             m = np.ascontiguousarray(mask, dtype=np.uint8)
         self._check(self.L.mxa_reset(self._h, m.ctypes.data if m is not None else None), "mxa_reset")
 
+    def set_seeds(self, seeds):
+        self.seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
+        assert len(self.seeds) == self.n_envs
+        self._check(self.L.mxa_set_seeds(self._h, self.seeds.ctypes.data), "mxa_set_seeds")
+
+    def set_stream(self, stream_ptr):
+        """Run on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
+        self._check(self.L.mxa_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None),
+                    "mxa_set_stream")
+
+    def write_results(self, device_ptr):
+        """Per-env (events, hash, status, current_time) int64 rows into device memory."""
+        self._check(self.L.mxa_write_results(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_results")
+
     def launch(self, max_pops):
         self._check(self.L.mxa_launch(self._h, max_pops), "mxa_launch")
 
@@ -66,10 +80,8 @@ class VecMarket:
     def summary(self):
         arr = (_lib.EnvSummary * self.n_envs)()
         self._check(self.L.mxa_read_summary(self._h, arr), "mxa_read_summary")
-        names = [f[0] for f in _lib.EnvSummary._fields_]
-        out = {k: np.array([getattr(a, k) for a in arr]) for k in names}
-        out["hash"] = out["hash"].astype(np.uint64)
-        return out
+        dt = {ctypes.c_int32: np.int32, ctypes.c_int64: np.int64, ctypes.c_uint64: np.uint64}
+        return {k: np.array([getattr(a, k) for a in arr], dtype=dt[t]) for k, t in _lib.EnvSummary._fields_}
 
     def agents(self, env):
         arr = (_lib.AgentState * self.n_agents)()
@@ -90,6 +102,16 @@ class VecMarket:
             else:
                 levels.append([o])
         return levels
+
+    def layout(self):
+        o = np.zeros(8, dtype=np.int64)
+        self._check(self.L.mxa_layout(self._h, o.ctypes.data), "mxa_layout")
+        return dict(zip(["ag", "open", "rng", "lat", "q", "book", "tx", "trace"], o.tolist()))
+
+    def raw(self, env, offset, nbytes):
+        buf = np.zeros(nbytes, dtype=np.uint8)
+        self._check(self.L.mxa_read_raw(self._h, env, offset, nbytes, buf.ctypes.data), "mxa_read_raw")
+        return buf
 
     def trace(self, env):
         if not self.trace_cap:
