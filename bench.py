@@ -117,7 +117,8 @@ def main():
                                    "09:30-09:45 session + 1 min tail), seeds %d+global_env" % (args.config, n, SEED0),
                        "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": m.n_agents,
                        "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
-                       "env_errors": n_err},
+                       "env_errors": n_err, "device": torch.cuda.get_device_name(local),
+                       "cus": torch.cuda.get_device_properties(local).multi_processor_count},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "mxa_run_kernel<4,2,true>", "avg_launch_ms": avg_launch_ms,

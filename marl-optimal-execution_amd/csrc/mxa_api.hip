@@ -16,21 +16,17 @@
 
 namespace {
 
-constexpr int64_t NS = 1000000000LL;
-constexpr int64_t MIN = 60 * NS;
-constexpr int64_t HOUR = 60 * MIN;
+typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*);
+typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t);
 
-typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, const MxaParams*, char*, const uint32_t*, const uint8_t*);
-typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, const MxaParams*, char*, int64_t);
-
-template <int SQ, int SO, bool PL>
-void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, const MxaParams* P, char* base, const uint32_t* seeds,
+template <int CFG>
+void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, const uint32_t* seeds,
                   const uint8_t* mask) {
-  hipLaunchKernelGGL((mxa_build_kernel<SQ, SO, PL>), g, b, lds, s, P, base, seeds, mask);
+  hipLaunchKernelGGL((mxa_build_kernel<CFG>), g, b, lds, s, base, stride, n, seeds, mask);
 }
-template <int SQ, int SO, bool PL, int W>
-void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, const MxaParams* P, char* base, int64_t max_pops) {
-  hipLaunchKernelGGL((mxa_run_kernel<SQ, SO, PL, W>), g, b, lds, s, P, base, max_pops);
+template <int CFG>
+void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops) {
+  hipLaunchKernelGGL((mxa_run_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops);
 }
 
 __global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int n, int* out) {
@@ -52,7 +48,6 @@ __global__ void mxa_results_kernel(const char* base, uint64_t stride, int n, int
 
 struct mxa_handle {
   MxaParams P;
-  MxaParams* d_P = nullptr;  // device copy read by the kernels (s_load)
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
   char* d_env = nullptr;
@@ -77,158 +72,11 @@ static int hip_fail(mxa_handle* h, hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail(h, _e, #x); \
   } while (0)
 
-// ------------------------------------------------------------------ config restatements
-static void base_params(MxaParams& P) {
-  memset(&P, 0, sizeof P);
-  P.o_rbar = 1e5;
-  P.o_kappa = 1.67e-12;
-  P.o_fundvol = 1e-4;
-  P.o_lambda = 2.77778e-13;
-  P.o_msmean = 1e3;
-  P.o_msvar = 5e4;
-  P.starting_cash = 10000000;
-  P.ex_pipeline = 0;
-  P.ex_comp = 0;
-  P.stream_history = 10;
-  P.mkt_open = 9 * HOUR + 30 * MIN;
-}
-
-// config/rmsc03.py:55-235 (defaults of its argparse options)
-static void params_rmsc03(MxaParams& P, int& sq, int& so, bool& pl) {
-  base_params(P);
-  P.config = MXA_CFG_RMSC03;
-  P.mkt_close = 9 * HOUR + 45 * MIN;
-  P.start = P.mkt_open;
-  P.stop = P.mkt_close + MIN;
-  P.default_comp_delay = 0;
-  P.lat_mode = 0;
-  P.noise_len = 1;
-  P.first_noise = 1;
-  P.n_noise = 50;
-  P.first_value = 51;
-  P.n_value = 10;
-  P.first_mm = 61;
-  P.n_mm = 1;
-  P.first_mom = 62;
-  P.n_mom = 2;
-  P.n_agents = 64;
-  P.v_sigma_n = 1e5 / 10;
-  P.v_rbar = 1e5;
-  P.v_kappa = 1.67e-15;
-  P.v_sigma_s = 100000;
-  P.v_lambda = 7e-11;
-  P.v_percent_aggr = 0.1;
-  P.v_depth_spread = 2;
-  P.noise_open = 9 * HOUR;
-  P.noise_close = 16 * HOUR;
-  P.mm_pov = 0.05;
-  P.mm_min_size = 20;
-  P.mm_window = 5;
-  P.mm_ticks = 20;
-  P.mm_wake = NS;
-  P.mom_min = 1;
-  P.mom_max = 10;
-  P.mom_wake = 20 * NS;
-  P.L.open_cap = 128;
-  P.L.tx_cap = 256;
-  P.L.lat_len = 0;
-  sq = 4;
-  so = 2;
-  pl = true;
-}
-
-// config/sparse_zi_100.py:73-334 and sparse_zi_1000.py
-static void params_sparse_zi(MxaParams& P, bool big, int& sq, int& so, bool& pl) {
-  base_params(P);
-  P.config = big ? MXA_CFG_SPARSE_ZI_1000 : MXA_CFG_SPARSE_ZI_100;
-  P.mkt_close = 16 * HOUR;
-  P.start = 0;
-  P.stop = 17 * HOUR;
-  P.default_comp_delay = 1000000000;
-  static const int n100[7] = {15, 15, 14, 14, 14, 14, 14};
-  static const int n1000[7] = {143, 143, 143, 143, 143, 143, 142};
-  static const int rmin[7] = {0, 0, 0, 0, 0, 250, 250};
-  static const int rmax[7] = {250, 500, 1000, 1000, 2000, 500, 500};
-  static const double eta[7] = {1, 1, 0.8, 1, 0.8, 0.8, 1};
-  P.zi_ngroups = 7;
-  int n = 0;
-  for (int g = 0; g < 7; g++) {
-    P.zi_group_count[g] = big ? n1000[g] : n100[g];
-    P.zi_rmin[g] = rmin[g];
-    P.zi_rmax[g] = rmax[g];
-    P.zi_eta[g] = eta[g];
-    n += P.zi_group_count[g];
-  }
-  P.first_zi = 1;
-  P.n_zi = n;
-  P.n_agents = 1 + n;
-  P.zi_sigma_n = 1000000.0;
-  P.zi_rbar = 1e5;
-  P.zi_kappa = 1.67e-15;
-  P.zi_sigma_s = 1e-4;
-  P.zi_lambda = 1e-12;
-  P.zi_sigma_pv = 5e6;
-  P.zi_qmax = 10;
-  if (!big) {
-    P.lat_mode = 2;
-    P.jitter = 0.3;
-    P.clip = 0.05;
-    P.unit = 5;
-    P.lat_lo = 21000;
-    P.lat_hi = 100000;
-    P.L.lat_len = 2 * P.n_agents;
-    sq = 8;
-    so = 2;
-    pl = true;
-  } else {
-    P.lat_mode = 1;
-    P.noise_len = 6;
-    P.lat_lo = 21000;
-    P.lat_hi = 13000000;
-    P.L.lat_len = P.n_agents;
-    sq = 48;
-    so = 16;
-    pl = false;
-  }
-  P.L.open_cap = 8;
-  P.L.tx_cap = 256;
-}
-
-static uint32_t align_up(uint64_t x, uint64_t a) { return (uint32_t)((x + a - 1) / a * a); }
-
-static void layout(MxaParams& P, int sq, int so, bool pl, int trace_cap) {
-  Layout& L = P.L;
-  P.n_streams = 4 + P.n_agents;
-  L.n_agents = P.n_agents;
-  L.n_streams = P.n_streams;
-  L.qcap = sq * 64;
-  L.ocap = so * 64;
-  L.trace_cap = trace_cap;
-  uint64_t off = align_up(sizeof(EnvHdr), 256);
-  L.off_ag = (uint32_t)off;
-  off = align_up(off + (uint64_t)P.n_agents * 512, 256);
-  L.off_open = (uint32_t)off;
-  off = align_up(off + (uint64_t)P.n_agents * L.open_cap * sizeof(OpenOrder), 256);
-  L.off_rng = (uint32_t)off;
-  off = align_up(off + (uint64_t)P.n_streams * MXA_RNG_WORDS * 4, 256);
-  L.off_lat = (uint32_t)off;
-  off = align_up(off + (uint64_t)L.lat_len * 8, 256);
-  L.off_q = (uint32_t)off;
-  off = align_up(off + (uint64_t)L.qcap * sizeof(SavedEvent) + (pl ? 0 : (uint64_t)L.qcap * 24), 256);
-  L.off_book = (uint32_t)off;
-  off = align_up(off + (uint64_t)L.ocap * sizeof(SavedOrder), 256);
-  L.off_tx = (uint32_t)off;
-  off = align_up(off + 64 + (uint64_t)L.tx_cap * sizeof(TxRec), 256);
-  L.off_trace = (uint32_t)off;
-  off = align_up(off + (uint64_t)trace_cap * MXA_TRACE_WORDS * 8, 256);
-  L.env_stride = off;
-}
-
-template <int SQ, int SO, bool PL, int W>
+template <int CFG>
 static void bind(mxa_handle* h) {
-  h->build = launch_build<SQ, SO, PL>;
-  h->run = launch_run<SQ, SO, PL, W>;
-  h->lds = (size_t)SQ * 64 * (12 + (PL ? 24 : 0)) + 512;  // queue + EnvHdr
+  h->build = launch_build<CFG>;
+  h->run = launch_run<CFG>;
+  h->lds = mxa_cfg::lds_bytes(CFG);
 }
 
 extern "C" {
@@ -237,22 +85,21 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
                mxa_handle** out) {
   if (!out || n_envs <= 0 || !seeds || trace_cap < 0) return MXA_EINVAL;
   mxa_handle* h = new mxa_handle();
-  int sq = 0, so = 0;
-  bool pl = true;
-  if (config == MXA_RMSC03) params_rmsc03(h->P, sq, so, pl);
-  else if (config == MXA_SPARSE_ZI_100) params_sparse_zi(h->P, false, sq, so, pl);
-  else if (config == MXA_SPARSE_ZI_1000) params_sparse_zi(h->P, true, sq, so, pl);
+  static_assert(MXA_RMSC03 == MXA_CFG_RMSC03 && MXA_SPARSE_ZI_100 == MXA_CFG_SPARSE_ZI_100 &&
+                MXA_SPARSE_ZI_1000 == MXA_CFG_SPARSE_ZI_1000, "config ids");
+  if (config == MXA_RMSC03) bind<MXA_CFG_RMSC03>(h);
+#ifndef MXA_ONLY_RMSC03
+  else if (config == MXA_SPARSE_ZI_100) bind<MXA_CFG_SPARSE_ZI_100>(h);
+  else if (config == MXA_SPARSE_ZI_1000) bind<MXA_CFG_SPARSE_ZI_1000>(h);
+#endif
   else {
     delete h;
     return MXA_EINVAL;
   }
+  h->P = mxa_cfg::params(config);
   h->P.n_envs = n_envs;
-  layout(h->P, sq, so, pl, trace_cap);
-  if (sq == 4 && so == 2 && pl) bind<4, 2, true, MXA_MIN_WAVES>(h);
-#ifndef MXA_ONLY_RMSC03
-  else if (sq == 8 && so == 2 && pl) bind<8, 2, true, 2>(h);
-  else bind<48, 16, false, 1>(h);
-#endif
+  h->P.L.trace_cap = trace_cap;
+  h->P.L.env_stride = mxa_cfg::env_stride(config, trace_cap);
   h->device = device;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
@@ -269,8 +116,6 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   HIPCHK(h, hipMalloc(&h->d_seeds, sizeof(uint32_t) * n_envs));
   HIPCHK(h, hipMalloc(&h->d_mask, n_envs));
   HIPCHK(h, hipMalloc(&h->d_count, sizeof(int)));
-  HIPCHK(h, hipMalloc(&h->d_P, sizeof(MxaParams)));
-  HIPCHK(h, hipMemcpyAsync(h->d_P, &h->P, sizeof(MxaParams), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(h->d_env, 0, bytes, h->stream));
   HIPCHK(h, hipMemcpyAsync(h->d_seeds, seeds, sizeof(uint32_t) * n_envs, hipMemcpyHostToDevice, h->stream));
   return mxa_reset(h, nullptr);
@@ -284,7 +129,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
     HIPCHK(h, hipMemcpyAsync(h->d_mask, mask, h->P.n_envs, hipMemcpyHostToDevice, h->stream));
     dm = h->d_mask;
   }
-  h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_P, h->d_env, h->d_seeds, dm);
+  h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_seeds, dm);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;
@@ -292,7 +137,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
 
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
   if (!h) return MXA_EINVAL;
-  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_P, h->d_env, max_pops);
+  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, max_pops);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
 }
@@ -311,7 +156,7 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   for (;;) {
     if (max_launches > 0 && launches >= max_launches) break;
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_P, h->d_env, chunk);
+    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, chunk);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     launches++;
@@ -459,7 +304,6 @@ void mxa_destroy(mxa_handle* h) {
   if (h->d_seeds) hipFree(h->d_seeds);
   if (h->d_mask) hipFree(h->d_mask);
   if (h->d_count) hipFree(h->d_count);
-  if (h->d_P) hipFree(h->d_P);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
   if (h->own) hipStreamDestroy(h->own);

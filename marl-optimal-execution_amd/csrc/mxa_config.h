@@ -1,0 +1,189 @@
+// mxa_config.h — the reference configurations as compile-time constants.
+//
+// Each reference config script (config/rmsc03.py, config/sparse_zi_100.py,
+// config/sparse_zi_1000.py) is a fixed set of constants once its argparse defaults are
+// taken.  They are restated here as constexpr MxaParams so the device engine is
+// instantiated per configuration with every parameter folded into immediates: no
+// parameter loads and no registers pinned for them in the event loop.  The host side
+// (mxa_api.hip) uses the same functions for the layout and the readers, then adds the
+// per-handle runtime values (n_envs, trace capacity, env stride).
+#pragma once
+#include "mxa_layout.h"
+
+namespace mxa_cfg {
+
+constexpr int64_t NS = 1000000000LL;
+constexpr int64_t MIN = 60 * NS;
+constexpr int64_t HOUR = 60 * MIN;
+
+// engine shape per configuration: queue slots per lane (SQ), book slots per lane (SO),
+// payload in LDS (PL), run-kernel waves per SIMD the register budget targets (W)
+struct Shape {
+  int sq, so;
+  bool pl;
+  int waves;
+};
+#ifndef MXA_RMSC03_WAVES
+#define MXA_RMSC03_WAVES 4
+#endif
+constexpr Shape shape(int cfg) {
+  return cfg == MXA_CFG_RMSC03 ? Shape{4, 2, true, MXA_RMSC03_WAVES}
+       : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2}
+                                      : Shape{48, 16, false, 1};
+}
+constexpr size_t lds_bytes(int cfg) {
+  return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 24 : 0)) + 512;  // queue + EnvHdr
+}
+
+constexpr void base_params(MxaParams& P) {
+  P.o_rbar = 1e5;
+  P.o_kappa = 1.67e-12;
+  P.o_fundvol = 1e-4;
+  P.o_lambda = 2.77778e-13;
+  P.o_msmean = 1e3;
+  P.o_msvar = 5e4;
+  P.starting_cash = 10000000;
+  P.ex_pipeline = 0;
+  P.ex_comp = 0;
+  P.stream_history = 10;
+  P.mkt_open = 9 * HOUR + 30 * MIN;
+}
+
+// config/rmsc03.py:55-235 (defaults of its argparse options)
+constexpr void params_rmsc03(MxaParams& P) {
+  base_params(P);
+  P.config = MXA_CFG_RMSC03;
+  P.mkt_close = 9 * HOUR + 45 * MIN;
+  P.start = P.mkt_open;
+  P.stop = P.mkt_close + MIN;
+  P.default_comp_delay = 0;
+  P.lat_mode = 0;
+  P.noise_len = 1;
+  P.first_noise = 1;
+  P.n_noise = 50;
+  P.first_value = 51;
+  P.n_value = 10;
+  P.first_mm = 61;
+  P.n_mm = 1;
+  P.first_mom = 62;
+  P.n_mom = 2;
+  P.n_agents = 64;
+  P.v_sigma_n = 1e5 / 10;
+  P.v_rbar = 1e5;
+  P.v_kappa = 1.67e-15;
+  P.v_sigma_s = 100000;
+  P.v_lambda = 7e-11;
+  P.v_percent_aggr = 0.1;
+  P.v_depth_spread = 2;
+  P.noise_open = 9 * HOUR;
+  P.noise_close = 16 * HOUR;
+  P.mm_pov = 0.05;
+  P.mm_min_size = 20;
+  P.mm_window = 5;
+  P.mm_ticks = 20;
+  P.mm_wake = NS;
+  P.mom_min = 1;
+  P.mom_max = 10;
+  P.mom_wake = 20 * NS;
+  P.L.open_cap = 128;
+  P.L.tx_cap = 256;
+  P.L.lat_len = 0;
+}
+
+// config/sparse_zi_100.py:73-334 and config/sparse_zi_1000.py
+constexpr void params_sparse_zi(MxaParams& P, bool big) {
+  base_params(P);
+  P.config = big ? MXA_CFG_SPARSE_ZI_1000 : MXA_CFG_SPARSE_ZI_100;
+  P.mkt_close = 16 * HOUR;
+  P.start = 0;
+  P.stop = 17 * HOUR;
+  P.default_comp_delay = 1000000000;
+  constexpr int n100[7] = {15, 15, 14, 14, 14, 14, 14};
+  constexpr int n1000[7] = {143, 143, 143, 143, 143, 143, 142};
+  constexpr int rmin[7] = {0, 0, 0, 0, 0, 250, 250};
+  constexpr int rmax[7] = {250, 500, 1000, 1000, 2000, 500, 500};
+  constexpr double eta[7] = {1, 1, 0.8, 1, 0.8, 0.8, 1};
+  P.zi_ngroups = 7;
+  int n = 0;
+  for (int g = 0; g < 7; g++) {
+    P.zi_group_count[g] = big ? n1000[g] : n100[g];
+    P.zi_rmin[g] = rmin[g];
+    P.zi_rmax[g] = rmax[g];
+    P.zi_eta[g] = eta[g];
+    n += P.zi_group_count[g];
+  }
+  P.first_zi = 1;
+  P.n_zi = n;
+  P.n_agents = 1 + n;
+  P.zi_sigma_n = 1000000.0;
+  P.zi_rbar = 1e5;
+  P.zi_kappa = 1.67e-15;
+  P.zi_sigma_s = 1e-4;
+  P.zi_lambda = 1e-12;
+  P.zi_sigma_pv = 5e6;
+  P.zi_qmax = 10;
+  if (!big) {
+    P.lat_mode = 2;
+    P.jitter = 0.3;
+    P.clip = 0.05;
+    P.unit = 5;
+    P.lat_lo = 21000;
+    P.lat_hi = 100000;
+    P.L.lat_len = 2 * P.n_agents;
+  } else {
+    P.lat_mode = 1;
+    P.noise_len = 6;
+    P.lat_lo = 21000;
+    P.lat_hi = 13000000;
+    P.L.lat_len = P.n_agents;
+  }
+  P.L.open_cap = 8;
+  P.L.tx_cap = 256;
+}
+
+constexpr uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// per-env HBM block: header, agent records, open orders, RNG streams, latency row/col,
+// saved queue, saved book, transaction ring, then the optional trace (runtime-sized, last)
+constexpr void layout(MxaParams& P, int cfg) {
+  const Shape S = shape(cfg);
+  Layout& L = P.L;
+  P.n_streams = 4 + P.n_agents;
+  L.n_agents = P.n_agents;
+  L.n_streams = P.n_streams;
+  L.qcap = S.sq * 64;
+  L.ocap = S.so * 64;
+  L.trace_cap = 0;
+  uint64_t off = align_up(sizeof(EnvHdr), 256);
+  L.off_ag = (uint32_t)off;
+  off = align_up(off + (uint64_t)P.n_agents * 512, 256);
+  L.off_open = (uint32_t)off;
+  off = align_up(off + (uint64_t)P.n_agents * L.open_cap * sizeof(OpenOrder), 256);
+  L.off_rng = (uint32_t)off;
+  off = align_up(off + (uint64_t)P.n_streams * MXA_RNG_WORDS * 4, 256);
+  L.off_lat = (uint32_t)off;
+  off = align_up(off + (uint64_t)L.lat_len * 8, 256);
+  L.off_q = (uint32_t)off;
+  off = align_up(off + (uint64_t)L.qcap * sizeof(SavedEvent) + (S.pl ? 0 : (uint64_t)L.qcap * 24), 256);
+  L.off_book = (uint32_t)off;
+  off = align_up(off + (uint64_t)L.ocap * sizeof(SavedOrder), 256);
+  L.off_tx = (uint32_t)off;
+  off = align_up(off + 64 + (uint64_t)L.tx_cap * sizeof(TxRec), 256);
+  L.off_trace = (uint32_t)off;
+  L.env_stride = off;  // without trace; the handle adds trace_cap records
+}
+
+constexpr MxaParams params(int cfg) {
+  MxaParams P{};
+  if (cfg == MXA_CFG_RMSC03) params_rmsc03(P);
+  else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
+  layout(P, cfg);
+  return P;
+}
+
+// runtime stride of one env block with `trace_cap` trace records
+constexpr uint64_t env_stride(int cfg, int trace_cap) {
+  return align_up(params(cfg).L.off_trace + (uint64_t)trace_cap * MXA_TRACE_WORDS * 8, 256);
+}
+
+}  // namespace mxa_cfg

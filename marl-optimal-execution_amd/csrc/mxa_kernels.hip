@@ -23,10 +23,8 @@
 
 #include "glibc_math.h"
 #include "mxa_layout.h"
+#include "mxa_config.h"
 
-#ifndef MXA_MIN_WAVES
-#define MXA_MIN_WAVES 4  // waves per SIMD the run kernel is register-budgeted for
-#endif
 
 typedef uint64_t u64;
 typedef int64_t i64;
@@ -122,50 +120,52 @@ DEV u64 as_u(double x) { return __builtin_bit_cast(u64, x); }
 // ------------------------------------------------------------------------------------
 // numpy legacy RandomState (numpy/random/src/mt19937, distributions/legacy)
 // ------------------------------------------------------------------------------------
-struct RS {
+// Stream storage: TWO 624-word MT blocks (double buffer, 1280 words per stream).  Output
+// index p lives in block p/624 at word (p/624 & 1)*624 + p%624; block b is generated from
+// block b-1 (mt19937_gen) into the other half.  The run kernel keeps one block of look-ahead
+// materialized at every event boundary (rs_maint, one code instance in the event loop), so
+// the draw sites inside the agent handlers never contain the twist; the build kernel
+// (BUILD = true) materializes blocks on demand instead.
+template <bool BUILD>
+struct RSt {
   u32* key;
-  i32 pos, hasg;
+  i32 p;      // absolute output index since seeding (first output: p = 624)
+  i32 m;      // highest materialized block
+  i32 hasg;   // bit0: cached second gauss (legacy_gauss); bit1: look-ahead overrun
   double gauss;
 };
 
-// cooperative MT19937 generation step (mt19937_gen) over the wave, in four dependency
-// phases: [0,227) reads only old words; [227,454) reads phase-1 words at i-227;
-// [454,623) reads [227,396); 623 reads key[0] and key[396].
-DEV void mt_twist(u32* key) {
+// materialize block b (>= 1) from block b-1, cooperatively over the wave in the four
+// dependency phases of mt19937_gen: [0,227) reads A only; [227,454) reads B[i-227] of
+// phase 1; [454,623) reads B[227..396); 623 reads B[0], B[396].
+DEV void mt_gen_block(u32* key, int b) {
   const int lane = laneid();
-  for (int b = 0; b < 227; b += 64) {
-    int i = b + lane;
-    if (i < 227) {
-      u32 y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
-      key[i] = key[i + 397] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
-    }
+  const u32* A = key + ((b - 1) & 1) * MXA_MT_N;
+  u32* B = key + (b & 1) * MXA_MT_N;
+  for (int i = lane; i < 227; i += 64) {
+    u32 y = (A[i] & 0x80000000u) | (A[i + 1] & 0x7fffffffu);
+    B[i] = A[i + 397] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
   }
   wfence();
-  for (int b = 227; b < 454; b += 64) {
-    int i = b + lane;
-    if (i < 454) {
-      u32 y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
-      key[i] = key[i - 227] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
-    }
+  for (int i = 227 + lane; i < 454; i += 64) {
+    u32 y = (A[i] & 0x80000000u) | (A[i + 1] & 0x7fffffffu);
+    B[i] = B[i - 227] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
   }
   wfence();
-  for (int b = 454; b < 623; b += 64) {
-    int i = b + lane;
-    if (i < 623) {
-      u32 y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
-      key[i] = key[i - 227] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
-    }
+  for (int i = 454 + lane; i < 623; i += 64) {
+    u32 y = (A[i] & 0x80000000u) | (A[i + 1] & 0x7fffffffu);
+    B[i] = B[i - 227] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
   }
   wfence();
   if (lane == 0) {
-    u32 y = (key[623] & 0x80000000u) | (key[0] & 0x7fffffffu);
-    key[623] = key[396] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    u32 y = (A[623] & 0x80000000u) | (B[0] & 0x7fffffffu);
+    B[623] = B[396] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
   }
   wfence();
 }
 
-// init_genrand (numpy _legacy_seeding with an int): every lane runs the recurrence,
-// lane (i % 64) stores word i.
+// init_genrand (numpy _legacy_seeding with an int) into block 0: every lane runs the
+// recurrence, lane (i % 64) stores word i.
 DEV void mt_seed(u32* key, u32 s) {
   const int lane = laneid();
   for (int i = 0; i < MXA_MT_N; i++) {
@@ -175,25 +175,33 @@ DEV void mt_seed(u32* key, u32 s) {
   wfence();
 }
 
-DEV u32 rs_u32(RS& r) {
-  if (r.pos >= MXA_MT_N) {
-    mt_twist(r.key);
-    r.pos = 0;
+template <bool B>
+DEV u32 rs_u32(RSt<B>& r) {
+  int blk = r.p / MXA_MT_N;
+  if (B) {
+    while (r.m < blk) {
+      mt_gen_block(r.key, r.m + 1);
+      r.m++;
+    }
+  } else if (blk > r.m) {
+    r.hasg |= 2;  // more than one block of draws inside one event: flagged, never silent
   }
-  u32 y = r.key[r.pos];
-  r.pos++;
+  u32 y = r.key[(blk & 1) * MXA_MT_N + (r.p - blk * MXA_MT_N)];
+  r.p++;
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680u;
   y ^= (y << 15) & 0xefc60000u;
   y ^= (y >> 18);
   return y;
 }
-DEV double rs_double(RS& r) {
+template <bool B>
+DEV double rs_double(RSt<B>& r) {
   i32 a = (i32)(rs_u32(r) >> 5);
   i32 b = (i32)(rs_u32(r) >> 6);
   return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
 }
-DEV i64 rs_randint(RS& r, i64 lo, i64 hi) {
+template <bool B>
+DEV i64 rs_randint(RSt<B>& r, i64 lo, i64 hi) {
   u64 rng = (u64)(hi - lo - 1);
   if (rng == 0) return lo;
   if (rng == 0xFFFFFFFFull) return lo + (i64)rs_u32(r);
@@ -205,10 +213,11 @@ DEV i64 rs_randint(RS& r, i64 lo, i64 hi) {
   } while (v > (u32)rng);
   return lo + (i64)v;
 }
-DEV double rs_gauss(RS& r) {
-  if (r.hasg) {
+template <bool B>
+DEV double rs_gauss(RSt<B>& r) {
+  if (r.hasg & 1) {
     double t = r.gauss;
-    r.hasg = 0;
+    r.hasg &= ~1;
     r.gauss = 0.0;
     return t;
   }
@@ -220,23 +229,31 @@ DEV double rs_gauss(RS& r) {
   } while (r2 >= 1.0 || r2 == 0.0);
   f = __builtin_sqrt(-2.0 * gm_log(r2) / r2);
   r.gauss = f * x1;
-  r.hasg = 1;
+  r.hasg |= 1;
   return f * x2;
 }
-DEV double rs_normal(RS& r, double loc, double scale) { return loc + scale * rs_gauss(r); }
-DEV double rs_exponential(RS& r, double scale) { return scale * -gm_log(1.0 - rs_double(r)); }
-DEV double rs_uniform(RS& r, double lo, double hi) { return lo + (hi - lo) * rs_double(r); }
-// advance a stream by k 32-bit outputs without tempering them (whole blocks = one twist)
-DEV void rs_skip_words(RS& r, i64 k) {
-  while (k > 0) {
-    if (r.pos >= MXA_MT_N) {
-      mt_twist(r.key);
-      r.pos = 0;
-    }
-    i64 step = MXA_MT_N - r.pos;
-    if (step > k) step = k;
-    r.pos += (i32)step;
-    k -= step;
+template <bool B>
+DEV double rs_normal(RSt<B>& r, double loc, double scale) { return loc + scale * rs_gauss(r); }
+template <bool B>
+DEV double rs_exponential(RSt<B>& r, double scale) { return scale * -gm_log(1.0 - rs_double(r)); }
+template <bool B>
+DEV double rs_uniform(RSt<B>& r, double lo, double hi) { return lo + (hi - lo) * rs_double(r); }
+// advance by k outputs without tempering them (build kernel only)
+DEV void rs_skip_words(RSt<true>& r, i64 k) {
+  i64 target = (i64)r.p + k;
+  while ((i64)r.m < target / MXA_MT_N) {
+    mt_gen_block(r.key, r.m + 1);
+    r.m++;
+  }
+  r.p = (i32)target;
+}
+// keep one block of look-ahead materialized (called at event boundaries)
+template <bool B>
+DEV void rs_maint(RSt<B>& r) {
+  int b = r.p / MXA_MT_N;
+  while (r.m < b + 1) {
+    mt_gen_block(r.key, r.m + 1);
+    r.m++;
   }
 }
 
@@ -347,22 +364,29 @@ DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
 // ------------------------------------------------------------------------------------
 // the engine: one instance per wave (= per env), lives in registers / LDS
 // ------------------------------------------------------------------------------------
-template <int SQ, int SO, bool PL_LDS>
+#define LDSP __attribute__((address_space(3)))
+template <int CFG, bool BUILD = false>
 struct Eng {
+  // every configuration constant is an immediate (mxa_config.h)
+  static constexpr MxaParams PC = mxa_cfg::params(CFG);
+  static constexpr int SQ = mxa_cfg::shape(CFG).sq;
+  static constexpr int SO = mxa_cfg::shape(CFG).so;
+  static constexpr bool PL_LDS = mxa_cfg::shape(CFG).pl;
+  typedef RSt<BUILD> RS;
+  typedef typename std::conditional<PL_LDS, LDSP u32*, u32*>::type PlPtr;
   static constexpr int QCAP = SQ * 64;
-  const MxaParams* PP;  // kernarg; re-laundered every event so LICM cannot pin its fields in SGPRs
   char* env;
   int lane;
-  EnvHdr& h;  // cold header fields live in LDS for the duration of a launch
+  LDSP EnvHdr& h;  // cold header fields live in LDS for the duration of a launch
   // hot header fields in SGPRs
   i64 cur, pops, ocnt;
   u64 hash;
   u32 seq;
   i32 status, err, qcount;
   // event queue: keys in LDS, payload in LDS (PL_LDS) or HBM; per-lane min cache
-  u64* qk;
-  u32* qs;
-  u32* qpl;
+  LDSP u64* qk;
+  LDSP u32* qs;
+  PlPtr qpl;
   u64 mk;
   u32 ms;
   i32 mj;
@@ -374,26 +398,30 @@ struct Eng {
   u32 rlo, rhi;
   i32 cur_agent;
   i64 add_delay;
+  u32 dirty;  // RNG streams touched by this event: bits 0-3 G/O/K/L, bit 4 the agent's own
   i64* trace;
+  i32 trace_cap;
 
   static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 24 : 0));
-  DEV Eng(const MxaParams& p, char* e, char* lds) : PP(&p), env(e), h(*(EnvHdr*)(lds + LDS_Q)) {
+  DEV Eng(char* e, char* lds, i32 tcap) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
     lane = laneid();
-    qk = (u64*)lds;
-    qs = (u32*)(lds + 8 * QCAP);
-    if (PL_LDS) qpl = (u32*)(lds + 12 * QCAP);
-    else qpl = (u32*)(env + PP->L.off_q + sizeof(SavedEvent) * QCAP);
-    trace = PP->L.trace_cap ? (i64*)(env + PP->L.off_trace) : nullptr;
+    qk = (LDSP u64*)lds;
+    qs = (LDSP u32*)(lds + 8 * QCAP);
+    if constexpr (PL_LDS) qpl = (LDSP u32*)(lds + 12 * QCAP);
+    else qpl = (u32*)(env + PC.L.off_q + sizeof(SavedEvent) * QCAP);
+    dirty = 0;
+    trace_cap = tcap;
+    trace = tcap ? (i64*)(env + PC.L.off_trace) : nullptr;
   }
 
   // ---------------- env block accessors
   DEV EnvHdr* hdr() { return (EnvHdr*)env; }
-  DEV u64* agent_ptr(int a) { return (u64*)(env + PP->L.off_ag + (size_t)a * 512); }
-  DEV OpenOrder* open_ptr(int a) { return (OpenOrder*)(env + PP->L.off_open + (size_t)a * PP->L.open_cap * sizeof(OpenOrder)); }
-  DEV u32* rng_key(int s) { return (u32*)(env + PP->L.off_rng + (size_t)s * MXA_RNG_WORDS * 4); }
-  DEV double* lat() { return (double*)(env + PP->L.off_lat); }
-  DEV i32* ep_entries() { return (i32*)(env + PP->L.off_tx); }               // 16 x i32
-  DEV TxRec* txr() { return (TxRec*)(env + PP->L.off_tx + 64); }
+  DEV u64* agent_ptr(int a) { return (u64*)(env + PC.L.off_ag + (size_t)a * 512); }
+  DEV OpenOrder* open_ptr(int a) { return (OpenOrder*)(env + PC.L.off_open + (size_t)a * PC.L.open_cap * sizeof(OpenOrder)); }
+  DEV u32* rng_key(int s) { return (u32*)(env + PC.L.off_rng + (size_t)s * MXA_RNG_WORDS * 4); }
+  DEV double* lat() { return (double*)(env + PC.L.off_lat); }
+  DEV i32* ep_entries() { return (i32*)(env + PC.L.off_tx); }               // 16 x i32
+  DEV TxRec* txr() { return (TxRec*)(env + PC.L.off_tx + 64); }
 
   DEV void fail(int code) {
     if (status != ST_ERROR) {
@@ -414,17 +442,23 @@ struct Eng {
   DEV i32 rgi(int f) { return (i32)rg(f); }
   DEV i64 rg64(int f) { return (i64)(((u64)rdl(rhi, f >> 1) << 32) | rdl(rlo, f >> 1)); }
   DEV double rgd(int f) { return as_d((u64)rg64(f)); }
+  // record writes are lane selects (v_cndmask), not divergent branches
   DEV void rs(int f, u32 v) {
+#ifdef MXA_DIVERGENT_RS
     if (lane == (f >> 1)) {
       if (f & 1) rhi = v;
       else rlo = v;
     }
+#else
+    bool me = lane == (f >> 1);
+    if (f & 1) rhi = me ? v : rhi;
+    else rlo = me ? v : rlo;
+#endif
   }
   DEV void rs64(int f, i64 v) {
-    if (lane == (f >> 1)) {
-      rlo = (u32)(u64)v;
-      rhi = (u32)((u64)v >> 32);
-    }
+    bool me = lane == (f >> 1);
+    rlo = me ? (u32)(u64)v : rlo;
+    rhi = me ? (u32)((u64)v >> 32) : rhi;
   }
   DEV void rsd(int f, double v) { rs64(f, (i64)as_u(v)); }
   DEV u32 flags() { return rg(AF_FLAGS); }
@@ -438,33 +472,55 @@ struct Eng {
   DEV RS agent_rs() {
     RS r;
     r.key = rng_key(4 + cur_agent);
-    r.pos = rgi(AF_RS_POS);
+    r.p = rgi(AF_RS_POS);
+    r.m = rgi(AF_RS_M);
     r.hasg = rgi(AF_RS_HASG);
     r.gauss = rgd(AF_RS_GAUSS);
     return r;
   }
   DEV void agent_rs_put(const RS& r) {
-    rs(AF_RS_POS, (u32)r.pos);
+    rs(AF_RS_POS, (u32)r.p);
+    rs(AF_RS_M, (u32)r.m);
     rs(AF_RS_HASG, (u32)r.hasg);
     rsd(AF_RS_GAUSS, r.gauss);
+    dirty |= 16;
   }
   // global streams: 0 = G (np.random), 1 = O (oracle symbol), 2 = K (kernel), 3 = L (latency)
   DEV RS grs(int s) {
     RS r;
     r.key = rng_key(s);
-    r.pos = h.rs_pos[s];
+    r.p = h.rs_pos[s];
+    r.m = h.rs_m[s];
     r.hasg = h.rs_has_gauss[s];
     r.gauss = h.rs_gauss[s];
     return r;
   }
   DEV void grs_put(int s, const RS& r) {
-    h.rs_pos[s] = r.pos;
+    h.rs_pos[s] = r.p;
+    h.rs_m[s] = r.m;
     h.rs_has_gauss[s] = r.hasg;
     h.rs_gauss[s] = r.gauss;
+    dirty |= 1u << s;
+  }
+  // event boundary: keep one MT block of look-ahead for every stream this event drew from
+  DEV void rng_maint() {
+#pragma unroll 1
+    for (int k = 0; k < 5; k++) {
+      if (!((dirty >> k) & 1)) continue;
+      RS r = k < 4 ? grs(k) : agent_rs();
+      if (r.hasg & 2) fail(ERR_RNG_OVERRUN);
+      rs_maint(r);
+      if (k < 4) {
+        h.rs_m[k] = r.m;
+      } else {
+        rs(AF_RS_M, (u32)r.m);
+      }
+    }
+    dirty = 0;
   }
 
   // ---------------- event queue
-  DEV void q_rescan() {  // lane-local: recompute this lane's min over its slots
+  DEV void q_rescan() {  // recompute this lane's min over its own slots
     u64 bk = KEY_EMPTY;
     u32 bs = 0xFFFFFFFFu;
     i32 bj = -1;
@@ -532,6 +588,7 @@ struct Eng {
     int j = rdli(mj, L);
     return j * 64 + L;
   }
+#ifdef MXA_DIVERGENT_Q
   DEV void q_remove(int slot) {
     if (lane == (slot & 63)) {
       qk[slot] = KEY_EMPTY;
@@ -547,26 +604,55 @@ struct Eng {
       q_rescan();
     }
   }
+#else
+  DEV void q_remove(int slot) {
+    if (lane == (slot & 63)) {
+      qk[slot] = KEY_EMPTY;
+      qs[slot] = 0xFFFFFFFFu;
+    }
+    qfree |= (lane == (slot & 63)) ? (1ull << (slot >> 6)) : 0ull;
+    u64 k0 = mk;
+    u32 s0 = ms;
+    i32 j0 = mj;
+    q_rescan();  // every lane rescans (no divergence); only the owner lane keeps the result
+    bool me = lane == (slot & 63);
+    mk = me ? mk : k0;
+    ms = me ? ms : s0;
+    mj = me ? mj : j0;
+    qcount--;
+  }
+  DEV void q_rekey(int slot, u64 key) {
+    if (lane == (slot & 63)) qk[slot] = key;
+    u64 k0 = mk;
+    u32 s0 = ms;
+    i32 j0 = mj;
+    q_rescan();
+    bool me = lane == (slot & 63);
+    mk = me ? mk : k0;
+    ms = me ? ms : s0;
+    mj = me ? mj : j0;
+  }
+#endif
 
   // ---------------- kernel services
   // Kernel.sendMessage (Kernel.py:347-425)
   DEV void send(int recipient, const Msg& m, i64 delay) {
     i64 sent = cur + rg64(AF_COMP) + add_delay + delay;
     i64 deliver;
-    if (PP->lat_mode == 2) {
+    if (PC.lat_mode == 2) {
       RS L = grs(3);
-      double x = rs_uniform(L, PP->clip, 1.0);
+      double x = rs_uniform(L, PC.clip, 1.0);
       grs_put(3, L);
-      double mn = cur_agent == 0 ? lat()[recipient] : lat()[PP->n_agents + cur_agent];
-      double l = mn + ((PP->jitter / gm_pow(x, 3.0)) * (mn / PP->unit));
+      double mn = cur_agent == 0 ? lat()[recipient] : lat()[PC.n_agents + cur_agent];
+      double l = mn + ((PC.jitter / gm_pow(x, 3.0)) * (mn / PC.unit));
       deliver = sent + (i64)l;
     } else {
       double l = 0.0;
-      if (PP->lat_mode == 1) l = lat()[cur_agent == 0 ? recipient : cur_agent];
+      if (PC.lat_mode == 1) l = lat()[cur_agent == 0 ? recipient : cur_agent];
       i64 noise = 0;
-      if (PP->noise_len > 1) {
+      if (PC.noise_len > 1) {
         RS K = grs(2);
-        noise = rs_randint(K, 0, PP->noise_len);
+        noise = rs_randint(K, 0, PC.noise_len);
         grs_put(2, K);
       }
       deliver = sent + (i64)(l + (double)noise);
@@ -589,7 +675,7 @@ struct Eng {
   // ---------------- SparseMeanRevertingOracle (SMRO:88-227)
   DEV double o_compute(i64 ts, double v_adj, i64 pt, double pv) {
     i64 d = ts - pt;
-    double mu = PP->o_rbar, gamma = PP->o_kappa, theta = PP->o_fundvol;
+    double mu = PC.o_rbar, gamma = PC.o_kappa, theta = PC.o_fundvol;
     double loc = mu + (pv - mu) * gm_exp(-gamma * (double)d);
     double scale = (gm_pow(theta, 2.0) / (2 * gamma)) * (1 - gm_exp(-2 * gamma * (double)d));
     RS O = grs(1);
@@ -611,17 +697,17 @@ struct Eng {
       pt = h.o_mst;
       pv = v;
       RS G = grs(0);
-      h.o_mst = pt + (i64)rs_exponential(G, 1.0 / PP->o_lambda);
+      h.o_mst = pt + (i64)rs_exponential(G, 1.0 / PC.o_lambda);
       grs_put(0, G);
       RS O = grs(1);
-      double msv = rs_normal(O, PP->o_msmean, __builtin_sqrt(PP->o_msvar));
+      double msv = rs_normal(O, PC.o_msmean, __builtin_sqrt(PC.o_msvar));
       h.o_msv = rs_randint(O, 0, 2) == 0 ? msv : -msv;
       grs_put(1, O);
     }
     return o_compute(t, 0, pt, pv);
   }
   DEV i64 o_observe(i64 t, double sigma_n) {
-    double r_t = t >= PP->mkt_close ? o_advance(PP->mkt_close - 1) : o_advance(t);
+    double r_t = t >= PC.mkt_close ? o_advance(PC.mkt_close - 1) : o_advance(t);
     if (sigma_n == 0) return (i64)r_t;
     RS A = agent_rs();
     i64 obs = py_round(rs_normal(A, r_t, __builtin_sqrt(sigma_n)));
@@ -707,11 +793,11 @@ struct Eng {
   // ---------------- OrderBook.history transaction ring (OrderBook.py:146-149, 227-237, 400-436)
   DEV void tx_add(i64 t, i32 q, i32 ep) {
     TxRec* R = txr();
-    int cap = PP->L.tx_cap;
+    int cap = PC.L.tx_cap;
     int pos = h.tx_head % cap;
     if (h.tx_head >= cap) {  // overwriting the oldest record: it must be dead
       TxRec old = R[pos];
-      if (old.epoch >= h.epoch - PP->stream_history) {
+      if (old.epoch >= h.epoch - PC.stream_history) {
         fail(ERR_TX_FULL);
         return;
       }
@@ -726,13 +812,13 @@ struct Eng {
     h.tx_head++;
   }
   DEV i64 transacted_volume(i64 lookback, int* perr) {
-    int lo_ep = h.epoch - PP->stream_history;
+    int lo_ep = h.epoch - PC.stream_history;
     i32 entries = 0;
     i32* EP = ep_entries();
     for (int e = lo_ep < 0 ? 0 : lo_ep; e <= h.epoch; e++) entries += EP[e & 15];
     if (entries == 0) return 0;
     TxRec* R = txr();
-    int cap = PP->L.tx_cap;
+    int cap = PC.L.tx_cap;
     int n = h.tx_head < cap ? h.tx_head : cap;
     int first = h.tx_head - n;
     i64 start = cur - lookback;
@@ -770,7 +856,7 @@ struct Eng {
   DEV void ex_notify(int recipient, const Msg& m) {
     // ExchangeAgent.sendMessage: ORDER_* notifications carry the pipeline delay
     u32 k = m_kind(m);
-    i64 d = (k == MK_ACCEPTED || k == MK_CANCELLED || k == MK_EXECUTED) ? PP->ex_pipeline : 0;
+    i64 d = (k == MK_ACCEPTED || k == MK_CANCELLED || k == MK_EXECUTED) ? PC.ex_pipeline : 0;
     send(recipient, m, d);
   }
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
@@ -799,7 +885,7 @@ struct Eng {
         }
         // history: taker logs its pre-match remaining qty; maker its matched qty if retained
         tx_add(cur, qty, h.epoch);
-        if (hh >= h.epoch - PP->stream_history) tx_add(cur, mq, hh);
+        if (hh >= h.epoch - PC.stream_history) tx_add(cur, mq, hh);
         qty -= mq;
         Msg mt = msg_order(MK_EXECUTED, oid, agent, is_buy, mq, price, best);
         ex_notify(agent, mt);
@@ -836,10 +922,10 @@ struct Eng {
 
   // ExchangeAgent.receiveMessage (ExchangeAgent.py:129-340)
   DEV void ex_receive(const Msg& m) {
-    rs64(AF_COMP, PP->ex_comp);
+    rs64(AF_COMP, PC.ex_comp);
     u32 k = m_kind(m);
     i32 sender = m_agent(m);
-    bool closed = cur > PP->mkt_close;
+    bool closed = cur > PC.mkt_close;
     if (closed) {
       if (k == MK_LIMIT || k == MK_CANCEL || k == MK_MODIFY) {
         ex_notify(sender, msg_make(MK_MKT_CLOSED, 0));
@@ -855,7 +941,7 @@ struct Eng {
     case MK_WHEN_CLOSE_REQ: {
       rs64(AF_COMP, 0);
       Msg r = msg_make(k == MK_WHEN_OPEN_REQ ? MK_WHEN_OPEN : MK_WHEN_CLOSE, 0);
-      i64 d = k == MK_WHEN_OPEN_REQ ? PP->mkt_open : PP->mkt_close;
+      i64 d = k == MK_WHEN_OPEN_REQ ? PC.mkt_open : PC.mkt_close;
       r.w[0] |= 1u << 11;
       r.w[1] = (u32)(u64)d;
       r.w[2] = (u32)((u64)d >> 32);
@@ -933,7 +1019,7 @@ struct Eng {
     i64 oid = next_order_id();
     if (qty > 0) {
       i32 n = rgi(AF_NORD);
-      if (n >= PP->L.open_cap) {
+      if (n >= PC.L.open_cap) {
         fail(ERR_OPEN_FULL);
         return;
       }
@@ -1009,8 +1095,8 @@ struct Eng {
     return (f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE) && !(f & FL_MKT_CLOSED);
   }
   DEV i64 wake_frequency(int type) {
-    if (type == AG_POVMM) return PP->mm_wake;
-    if (type == AG_MOMENTUM) return PP->mom_wake;
+    if (type == AG_POVMM) return PC.mm_wake;
+    if (type == AG_MOMENTUM) return PC.mom_wake;
     RS A = agent_rs();
     i64 v = rs_randint(A, 0, 100);
     agent_rs_put(A);
@@ -1131,7 +1217,7 @@ struct Eng {
     fl_set(FL_TRADING, true);
     if (fl(FL_MKT_CLOSED) && fl(FL_DAILY_CLOSE)) return;
     RS A = agent_rs();
-    double dt = rs_exponential(A, 1.0 / PP->zi_lambda);
+    double dt = rs_exponential(A, 1.0 / PC.zi_lambda);
     agent_rs_put(A);
     wakeup_at(cur_agent, cur + py_round(dt));
     if (fl(FL_MKT_CLOSED) && !fl(FL_DAILY_CLOSE)) {
@@ -1144,28 +1230,28 @@ struct Eng {
     rs(AF_STATE, AS_AWAITING_SPREAD);
   }
   DEV void zi_place() {
-    i64 obs = o_observe(cur, PP->zi_sigma_n);
+    i64 obs = o_observe(cur, PC.zi_sigma_n);
     i64 q = (i64)((double)rg64(AF_SHARES) / 100);
     int buy;
-    if (q >= PP->zi_qmax) buy = 0;
-    else if (q <= -PP->zi_qmax) buy = 1;
+    if (q >= PC.zi_qmax) buy = 0;
+    else if (q <= -PC.zi_qmax) buy = 1;
     else {
       RS A = agent_rs();
       buy = (int)rs_randint(A, 0, 2);
       agent_rs_put(A);
     }
-    i64 r_T = bayes_r_T(obs, PP->zi_kappa, PP->zi_rbar, PP->zi_sigma_n, PP->zi_sigma_s);
-    q += PP->zi_qmax - 1;
+    i64 r_T = bayes_r_T(obs, PC.zi_kappa, PC.zi_rbar, PC.zi_sigma_n, PC.zi_sigma_s);
+    q += PC.zi_qmax - 1;
     i64 idx = buy ? q + 1 : q;
-    if (idx < 0) idx += 2 * PP->zi_qmax;
-    if (idx < 0 || idx >= 2 * PP->zi_qmax) {
+    if (idx < 0) idx += 2 * PC.zi_qmax;
+    if (idx < 0 || idx >= 2 * PC.zi_qmax) {
       fail(ERR_THETA_INDEX);
       return;
     }
     i64 v = r_T + (i64)rgi(AF_THETA + (int)idx);
     int g = rgi(AF_GROUP);
     RS A = agent_rs();
-    i64 R = rs_randint(A, PP->zi_rmin[g], (i64)PP->zi_rmax[g] + 1);
+    i64 R = rs_randint(A, PC.zi_rmin[g], (i64)PC.zi_rmax[g] + 1);
     agent_rs_put(A);
     i64 p = buy ? v - R : v + R;
     i32 bid = 0, ask = 0;
@@ -1174,10 +1260,10 @@ struct Eng {
     ask = rgi(AF_ASK);
     if (buy && ask_vol > 0) {
       i64 R_ask = v - ask;
-      if ((double)R_ask >= PP->zi_eta[g] * (double)R) p = ask;
+      if ((double)R_ask >= PC.zi_eta[g] * (double)R) p = ask;
     } else if (!buy && bid_vol > 0) {
       i64 R_bid = bid - v;
-      if ((double)R_bid >= PP->zi_eta[g] * (double)R) p = bid;
+      if ((double)R_bid >= PC.zi_eta[g] * (double)R) p = bid;
     }
     place_limit(100, buy, p);
   }
@@ -1198,7 +1284,7 @@ struct Eng {
     fl_set(FL_TRADING, true);
     if (fl(FL_MKT_CLOSED) && fl(FL_DAILY_CLOSE)) return;
     RS A = agent_rs();
-    double dt = rs_exponential(A, 1.0 / PP->v_lambda);
+    double dt = rs_exponential(A, 1.0 / PC.v_lambda);
     agent_rs_put(A);
     wakeup_at(cur_agent, cur + py_round(dt));
     if (fl(FL_MKT_CLOSED) && !fl(FL_DAILY_CLOSE)) {
@@ -1211,8 +1297,8 @@ struct Eng {
     rs(AF_STATE, AS_AWAITING_SPREAD);
   }
   DEV void value_place() {
-    i64 obs = o_observe(cur, PP->v_sigma_n);
-    i64 r_T = bayes_r_T(obs, PP->v_kappa, PP->v_rbar, PP->v_sigma_n, PP->v_sigma_s);
+    i64 obs = o_observe(cur, PC.v_sigma_n);
+    i64 r_T = bayes_r_T(obs, PC.v_kappa, PC.v_rbar, PC.v_sigma_n, PC.v_sigma_s);
     i32 bid, ask;
     bool hb = known_bid(bid), ha = known_ask(ask);
     int buy;
@@ -1223,8 +1309,8 @@ struct Eng {
       i64 spread = (i64)ask - bid;
       if (spread < 0) spread = -spread;
       i64 adj;
-      if (rs_double(G) < PP->v_percent_aggr) adj = 0;
-      else adj = rs_randint(G, 0, PP->v_depth_spread * spread);
+      if (rs_double(G) < PC.v_percent_aggr) adj = 0;
+      else adj = rs_randint(G, 0, PC.v_depth_spread * spread);
       if (r_T < mid) {
         buy = 0;
         p = bid + adj;
@@ -1279,7 +1365,7 @@ struct Eng {
   DEV void mm_wakeup() {
     if (ta_wakeup()) {
       get_spread(1);
-      get_tv(PP->mm_wake);
+      get_tv(PC.mm_wake);
     }
   }
   DEV void mm_receive(const Msg& m) {
@@ -1287,8 +1373,8 @@ struct Eng {
     i64 mid = rg64(AF_LAST_MID);
     u32 k = m_kind(m);
     if (k == MK_TV && fl(FL_AW_TV)) {
-      i64 qty = py_round(PP->mm_pov * (double)rg64(AF_TV));
-      rs(AF_ORDER_SIZE, (u32)(qty >= PP->mm_min_size ? qty : PP->mm_min_size));
+      i64 qty = py_round(PC.mm_pov * (double)rg64(AF_TV));
+      rs(AF_ORDER_SIZE, (u32)(qty >= PC.mm_min_size ? qty : PC.mm_min_size));
       fl_set(FL_AW_TV, false);
     }
     if (k == MK_SPREAD && fl(FL_AW_SPREAD)) {
@@ -1303,14 +1389,14 @@ struct Eng {
     }
     if (!fl(FL_AW_SPREAD) && !fl(FL_AW_TV)) {
       cancel_all();
-      i64 hb = mid - 1, la = mid + PP->mm_window;
-      i64 lb = hb - PP->mm_ticks, ha = la + PP->mm_ticks;
+      i64 hb = mid - 1, la = mid + PC.mm_window;
+      i64 lb = hb - PC.mm_ticks, ha = la + PC.mm_ticks;
       i64 sz = rgi(AF_ORDER_SIZE);
       for (i64 p = lb; p <= hb; p++) place_limit(sz, 1, p);
       for (i64 p = la; p <= ha; p++) place_limit(sz, 0, p);
       fl_set(FL_AW_SPREAD, true);
       fl_set(FL_AW_TV, true);
-      wakeup_at(cur_agent, cur + PP->mm_wake);
+      wakeup_at(cur_agent, cur + PC.mm_wake);
     }
   }
 
@@ -1351,7 +1437,7 @@ struct Eng {
           else place_limit(rgi(AF_SIZE), 0, bid);
         }
       }
-      wakeup_at(cur_agent, cur + PP->mom_wake);
+      wakeup_at(cur_agent, cur + PC.mom_wake);
       rs(AF_STATE, AS_AWAITING_WAKEUP);
     }
   }
@@ -1413,7 +1499,7 @@ struct Eng {
   }
   DEV void load() {
     hdr_from_global();
-    SavedEvent* sq = (SavedEvent*)(env + PP->L.off_q);
+    SavedEvent* sq = (SavedEvent*)(env + PC.L.off_q);
     qfree = 0;
     for (int j = 0; j < SQ; j++) {
       int slot = j * 64 + lane;
@@ -1425,7 +1511,7 @@ struct Eng {
       if (e.key == KEY_EMPTY) qfree |= 1ull << j;
     }
     q_rescan();
-    SavedOrder* so = (SavedOrder*)(env + PP->L.off_book);
+    SavedOrder* so = (SavedOrder*)(env + PC.L.off_book);
     for (int j = 0; j < SO; j++) {
       SavedOrder o = so[j * 64 + lane];
       bp[j] = o.price;
@@ -1437,7 +1523,7 @@ struct Eng {
     }
   }
   DEV void save() {
-    SavedEvent* sq = (SavedEvent*)(env + PP->L.off_q);
+    SavedEvent* sq = (SavedEvent*)(env + PC.L.off_q);
     for (int j = 0; j < SQ; j++) {
       int slot = j * 64 + lane;
       SavedEvent e;
@@ -1447,7 +1533,7 @@ struct Eng {
       for (int i = 0; i < 6; i++) e.pl[i] = PL_LDS ? qpl[slot * 6 + i] : 0u;
       sq[slot] = e;
     }
-    SavedOrder* so = (SavedOrder*)(env + PP->L.off_book);
+    SavedOrder* so = (SavedOrder*)(env + PC.L.off_book);
     for (int j = 0; j < SO; j++) {
       SavedOrder o;
       o.price = bp[j];
@@ -1465,19 +1551,20 @@ struct Eng {
   // ---------------- Kernel.runner event loop (Kernel.py:190-292)
   DEV void run(i64 max_pops) {
     for (i64 n = 0; n < max_pops && status == ST_RUNNING; n++) {
-      {  // opaque per event: params are re-read (s_load) instead of pinned in SGPRs by LICM
-        u64 pv = (u64)PP;
+#ifndef MXA_NO_LAUNDER_ENV
+      {  // opaque per event: env-derived addresses are recomputed, not pinned in SGPRs by LICM
+         // (without this the event loop hoists ~1000 SGPRs of addresses and spills them)
+        u64 pv = (u64)env;
         u32 plo = (u32)__builtin_amdgcn_readfirstlane((int)(u32)pv);
         u32 phi = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(pv >> 32));
-#ifndef MXA_NO_LAUNDER
         asm volatile("" : "+s"(plo), "+s"(phi));
-#endif
-        PP = (const MxaParams*)(((u64)phi << 32) | plo);
+        env = (char*)(__attribute__((address_space(1))) char*)(((u64)phi << 32) | plo);
       }
+#endif
       u64 key;
       u32 eseq;
       int slot = q_peek(key, eseq);
-      if (slot < 0 || !(cur <= PP->stop)) {
+      if (slot < 0 || !(cur <= PC.stop)) {
         status = ST_DONE;
         break;
       }
@@ -1491,7 +1578,7 @@ struct Eng {
       u64 hs = hash;
       for (int i = 0; i < 10; i++) hs = (hs ^ (u64)rec[i]) * FNV_PRIME;
       hash = hs;
-      if (trace && h.trace_len < PP->L.trace_cap) {
+      if (trace && h.trace_len < trace_cap) {
         if (lane < 10) {
           i64 v = 0;
           for (int i = 0; i < 10; i++)
@@ -1511,6 +1598,7 @@ struct Eng {
       q_remove(slot);
       rs64(AF_ATIME, t);
       dispatch(rgi(AF_TYPE), type == MT_WAKEUP, m);
+      if (dirty) rng_maint();
       rs64(AF_ATIME, t + rg64(AF_COMP) + add_delay);
       rec_store();
     }
@@ -1520,10 +1608,11 @@ struct Eng {
 // ------------------------------------------------------------------------------------
 // env construction (config scripts' global-RNG draw order)
 // ------------------------------------------------------------------------------------
-template <int SQ, int SO, bool PL_LDS>
-struct Builder : Eng<SQ, SO, PL_LDS> {
-  typedef Eng<SQ, SO, PL_LDS> E;
-  DEV Builder(const MxaParams& p, char* e, char* lds) : E(p, e, lds) {}
+template <int CFG>
+struct Builder : Eng<CFG, true> {
+  typedef Eng<CFG, true> E;
+  typedef typename E::RS RS;
+  DEV Builder(char* e, char* lds) : E(e, lds, 0) {}
 
   DEV u32 g_seed(RS& G) { return (u32)rs_randint(G, 0, 4294967296LL); }
   DEV void set_seed(int stream, u32 s) {
@@ -1535,10 +1624,11 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
     this->rs(AF_TYPE, (u32)type);
     this->rs(AF_FLAGS, FL_FIRST_WAKE | FL_AW_SPREAD | FL_AW_TV);
     this->rs(AF_RS_POS, MXA_MT_N);
-    this->rs64(AF_START_CASH, (*this->PP).starting_cash);
-    this->rs64(AF_CASH, (*this->PP).starting_cash);
-    this->rs64(AF_ATIME, (*this->PP).start);
-    this->rs64(AF_COMP, (*this->PP).default_comp_delay);
+    this->rs(AF_RS_M, 0);
+    this->rs64(AF_START_CASH, E::PC.starting_cash);
+    this->rs64(AF_CASH, E::PC.starting_cash);
+    this->rs64(AF_ATIME, E::PC.start);
+    this->rs64(AF_COMP, E::PC.default_comp_delay);
   }
   DEV i64 get_wake_time(RS& G, i64 open, i64 close) {  // util/util.py:35-58
     double u = rs_double(G);
@@ -1550,7 +1640,7 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
   }
   // expand every stream's init_genrand in parallel (lane = stream)
   DEV void seed_streams(int first) {
-    const MxaParams& P = (*this->PP);
+    const MxaParams& P = E::PC;
     wfence();
     for (int b = first; b < P.n_streams; b += 64) {
       int s = b + this->lane;
@@ -1567,9 +1657,13 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
   }
 
   DEV void build(u32 seed) {
-    const MxaParams& P = (*this->PP);
-    EnvHdr& h = this->h;
-    h = EnvHdr();
+    const MxaParams& P = E::PC;
+    LDSP EnvHdr& h = this->h;
+    {
+      LDSP u32* hw = (LDSP u32*)&h;
+      for (int i = this->lane; i < (int)(sizeof(EnvHdr) / 4); i += 64) hw[i] = 0;
+      wfence();
+    }
     this->hash = FNV_OFF;
     this->status = ST_RUNNING;
     this->err = 0;
@@ -1578,16 +1672,19 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
     this->seq = 0;
     this->qcount = 0;
     this->cur = P.start;
-    for (int s = 0; s < 4; s++) h.rs_pos[s] = MXA_MT_N;
+    for (int s = 0; s < 4; s++) {
+      h.rs_pos[s] = MXA_MT_N;
+      h.rs_m[s] = 0;
+    }
     this->mk = KEY_EMPTY;
     this->ms = 0xFFFFFFFFu;
     this->mj = -1;
-    this->qfree = SQ >= 64 ? ~0ull : ((1ull << SQ) - 1ull);
-    for (int j = 0; j < SQ; j++) {
+    this->qfree = E::SQ >= 64 ? ~0ull : ((1ull << E::SQ) - 1ull);
+    for (int j = 0; j < E::SQ; j++) {
       this->qk[j * 64 + this->lane] = KEY_EMPTY;
       this->qs[j * 64 + this->lane] = 0xFFFFFFFFu;
     }
-    for (int j = 0; j < SO; j++) this->bm[j] = -1;
+    for (int j = 0; j < E::SO; j++) this->bm[j] = -1;
     mt_seed(this->rng_key(0), seed);
     RS G = this->grs(0);
     int n = P.n_agents;
@@ -1671,6 +1768,7 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
     // expand all other streams, then the per-stream config-time draws
     seed_streams(1);
     h.rs_pos[1] = h.rs_pos[2] = h.rs_pos[3] = MXA_MT_N;
+    h.rs_m[1] = h.rs_m[2] = h.rs_m[3] = 0;
     {  // oracle first megashock (SMRO:71-72)
       RS O = this->grs(1);
       double msv = rs_normal(O, P.o_msmean, __builtin_sqrt(P.o_msvar));
@@ -1710,6 +1808,19 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
       this->agent_rs_put(A);
       this->rec_store();
     }
+    // run-kernel invariant: every stream has the block after its current one materialized
+    for (int k = 0; k < 4; k++) {
+      RS r = this->grs(k);
+      rs_maint(r);
+      this->grs_put(k, r);
+    }
+    for (int a = 0; a < n; a++) {
+      this->rec_load(a);
+      RS A = this->agent_rs();
+      rs_maint(A);
+      this->agent_rs_put(A);
+      this->rec_store();
+    }
     // Kernel.runner: kernelInitializing (exchange opening price = r_bar, a python float),
     // kernelStarting (every agent wakes at startTime, in id order)
     h.last_trade = (i64)P.o_rbar;
@@ -1735,26 +1846,24 @@ struct Builder : Eng<SQ, SO, PL_LDS> {
 // ------------------------------------------------------------------------------------
 // kernels (one wavefront per env; grid = n_envs)
 // ------------------------------------------------------------------------------------
-template <int SQ, int SO, bool PL_LDS>
-__global__ __launch_bounds__(64) void mxa_build_kernel(const MxaParams* __restrict__ Pg, char* base, const uint32_t* seeds, const uint8_t* mask) {
+template <int CFG>
+__global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stride, int n_envs, const uint32_t* seeds, const uint8_t* mask) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const MxaParams& P = *Pg;
   int env = blockIdx.x;
-  if (env >= P.n_envs) return;
+  if (env >= n_envs) return;
   if (mask && !mask[env]) return;
-  mxa::Builder<SQ, SO, PL_LDS> b(P, base + (size_t)env * P.L.env_stride, lds);
+  mxa::Builder<CFG> b(base + (size_t)env * stride, lds);
   b.build(seeds[env]);
 }
 
-template <int SQ, int SO, bool PL_LDS, int WAVES>
-__global__ __launch_bounds__(64, WAVES) void mxa_run_kernel(const MxaParams* __restrict__ Pg, char* base, int64_t max_pops) {
+template <int CFG>
+__global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const MxaParams& P = *Pg;
   int env = blockIdx.x;
-  if (env >= P.n_envs) return;
-  char* e = base + (size_t)env * P.L.env_stride;
+  if (env >= n_envs) return;
+  char* e = base + (size_t)env * stride;
   if (((EnvHdr*)e)->status != ST_RUNNING) return;
-  mxa::Eng<SQ, SO, PL_LDS> g(P, e, lds);
+  mxa::Eng<CFG> g(e, lds, trace_cap);
   g.load();
   g.run(max_pops);
   g.save();
@@ -1764,9 +1873,10 @@ __global__ __launch_bounds__(64, WAVES) void mxa_run_kernel(const MxaParams* __r
 // these through the C-ABI; they exercise exactly the device functions the engine uses)
 __global__ __launch_bounds__(64) void mxa_rng_probe_kernel(uint32_t seed, int mode, double a, double b, int n, double* out, uint32_t* scratch) {
   mxa::mt_seed(scratch, seed);
-  mxa::RS r;
+  mxa::RSt<true> r;
   r.key = scratch;
-  r.pos = MXA_MT_N;
+  r.p = MXA_MT_N;
+  r.m = 0;
   r.hasg = 0;
   r.gauss = 0;
   for (int i = 0; i < n; i++) {
@@ -1790,11 +1900,11 @@ __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y
 }
 
 // explicit instantiations per supported configuration
-#define MXA_INST(SQ, SO, PL, W)                                                                           \
-  template __global__ void mxa_build_kernel<SQ, SO, PL>(const MxaParams*, char*, const uint32_t*, const uint8_t*); \
-  template __global__ void mxa_run_kernel<SQ, SO, PL, W>(const MxaParams*, char*, int64_t);
-MXA_INST(4, 2, true, MXA_MIN_WAVES)     // rmsc03
+#define MXA_INST(CFG)                                                                                      \
+  template __global__ void mxa_build_kernel<CFG>(char*, uint64_t, int, const uint32_t*, const uint8_t*); \
+  template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t);
+MXA_INST(MXA_CFG_RMSC03)
 #ifndef MXA_ONLY_RMSC03
-MXA_INST(8, 2, true, 2)     // sparse_zi_100
-MXA_INST(48, 16, false, 1)  // sparse_zi_1000
+MXA_INST(MXA_CFG_SPARSE_ZI_100)
+MXA_INST(MXA_CFG_SPARSE_ZI_1000)
 #endif

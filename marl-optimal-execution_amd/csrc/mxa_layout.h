@@ -13,7 +13,7 @@
 #define MXA_MAX_AGENTS 2047  // 11-bit recipient field in the event key
 #define MXA_MT_N 624
 #define MXA_MT_M 397
-#define MXA_RNG_WORDS 640     // 624 key words + pos/has_gauss/gauss/pad (2560 B per stream)
+#define MXA_RNG_WORDS 1280    // two 624-word MT blocks (double buffer) + pad (5120 B per stream)
 
 enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2 };
 
@@ -34,7 +34,8 @@ enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_
 enum { ST_RUNNING = 0, ST_DONE = 1, ST_ERROR = 2 };
 enum {
   ERR_NONE = 0, ERR_QUEUE_FULL = 1, ERR_BOOK_FULL = 2, ERR_OPEN_FULL = 3, ERR_TX_FULL = 4,
-  ERR_PANDAS_NO_TX = 5, ERR_WAKEUP_PAST = 6, ERR_THETA_INDEX = 7, ERR_BAD_CONFIG = 8
+  ERR_PANDAS_NO_TX = 5, ERR_WAKEUP_PAST = 6, ERR_THETA_INDEX = 7, ERR_BAD_CONFIG = 8,
+  ERR_RNG_OVERRUN = 9
 };
 
 // per-env scalar header (first bytes of the env block)
@@ -54,14 +55,15 @@ typedef struct {
   // oracle (SparseMeanRevertingOracle)
   int64_t o_pt, o_mst;
   double o_pv, o_msv;
-  // global RNG streams G, O, K, L: pos / gauss cache
+  // global RNG streams G, O, K, L: output index / materialized block / gauss cache
   int32_t rs_pos[4], rs_has_gauss[4];
   double rs_gauss[4];
+  int32_t rs_m[4];
   int32_t q_count, b_count;      // saved queue / book occupancy
   int64_t trace_len;
   int64_t ex_comp_delay;         // exchange's current computation delay
   int32_t max_q, max_book;       // capacity high-water marks (diagnostics)
-  int64_t pad1[3];
+  int64_t pad1[1];
 } EnvHdr;
 
 // one event slot as saved between launches (and payload as pushed)
@@ -105,6 +107,7 @@ enum {
   AF_ORDER_SIZE = 38, AF_NMID = 39, AF_N20 = 40, AF_N50 = 41, AF_AVG20 = 42, AF_AVG50 = 44,
   AF_THETA = 46,      // 20 x int32
   AF_MIDS = 66,       // 50 x int32 (2*mid ring), momentum
+  AF_RS_M = 116,      // highest materialized MT block of the agent's stream
   AF_ATIME = 120,     // Kernel.agentCurrentTimes[a]
   AF_COMP = 122,      // Kernel.agentComputationDelays[a]
   AF_END = 128
