@@ -24,9 +24,10 @@ import torch
 import torch.distributed as dist
 
 import mxabides
+from mxabides import shard
 
 METRIC = "env-steps/sec (whole node), rmsc03 100-agent market ×4096 envs, 1/2/4/8 GPUs"
-SEED0 = 123456789
+SEED0 = shard.SEED0
 ALGO_BYTES_PER_EVENT = 256  # nominal algorithmic HBM bytes per event
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
@@ -52,14 +53,12 @@ def main():
     n = args.envs
 
     def seeds_for(step):
-        first = SEED0 + (step * world + rank) * n
-        return (np.arange(first, first + n, dtype=np.int64)) & 0xFFFFFFFF
+        return shard.env_seeds(step, rank, world, n)
 
     m = mxabides.VecMarket(args.config, seeds_for(0), device=local)
     stream = torch.cuda.current_stream()
     m.set_stream(stream.cuda_stream)
     res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-    gathered = torch.zeros((world * n, 4), dtype=torch.int64, device="cuda") if world > 1 else res
 
     kernel_ms, launches = [0.0], [0]
 
@@ -69,8 +68,7 @@ def main():
         launches[0] += m.run(chunk=args.chunk)
         kernel_ms[0] += m.last_kernel_ms
         m.write_results(res.data_ptr())
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, res)  # episode records over RCCL/xGMI
+        shard.gather_records(res, world)  # episode records over RCCL/xGMI (the only collective)
         return res[:, 0].sum()
 
     for k in range(args.warmup):

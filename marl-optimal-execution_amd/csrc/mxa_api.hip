@@ -81,6 +81,16 @@ static void bind(mxa_handle* h) {
 
 extern "C" {
 
+#ifdef MXA_PROF
+// diagnostics build only (not in include/mxa.h): phase cycle totals, then cleared
+int mxa_prof_read(uint64_t* out32) {
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mxa::g_mxa_prof), 32 * 8) != hipSuccess) return MXA_EHIP;
+  static const uint64_t z[32] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(mxa::g_mxa_prof), z, 32 * 8) != hipSuccess) return MXA_EHIP;
+  return MXA_OK;
+}
+#endif
+
 int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device, int32_t trace_cap,
                mxa_handle** out) {
   if (!out || n_envs <= 0 || !seeds || trace_cap < 0) return MXA_EINVAL;

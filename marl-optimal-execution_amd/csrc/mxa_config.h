@@ -32,7 +32,11 @@ constexpr Shape shape(int cfg) {
                                       : Shape{48, 16, false, 1};
 }
 constexpr size_t lds_bytes(int cfg) {
-  return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 24 : 0)) + 512;  // queue + EnvHdr
+  return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 24 : 0)) + 512  // queue + EnvHdr
+#ifdef MXA_PROF
+         + 256  // phase counters
+#endif
+      ;
 }
 
 constexpr void base_params(MxaParams& P) {

@@ -365,6 +365,24 @@ DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
 // the engine: one instance per wave (= per env), lives in registers / LDS
 // ------------------------------------------------------------------------------------
 #define LDSP __attribute__((address_space(3)))
+#ifdef MXA_PROF
+// diagnostics build only: per-phase shader-cycle totals over all envs (tools/prof_phases.py)
+__device__ unsigned long long g_mxa_prof[32];
+DEV u64 stamp() {
+  u64 t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define PROF_T(v) u64 v = stamp()
+#define PROF_ADD(b, v) do { u64 _t = stamp(); if (lane == 0) prof[b] += _t - (v); v = _t; } while (0)
+#define PROF_CNT(b) do { if (lane == 0) prof[b] += 1; } while (0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(b, v)
+#define PROF_CNT(b)
+#endif
 template <int CFG, bool BUILD = false>
 struct Eng {
   // every configuration constant is an immediate (mxa_config.h)
@@ -401,6 +419,9 @@ struct Eng {
   u32 dirty;  // RNG streams touched by this event: bits 0-3 G/O/K/L, bit 4 the agent's own
   i64* trace;
   i32 trace_cap;
+#ifdef MXA_PROF
+  LDSP u64* prof;
+#endif
 
   static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 24 : 0));
   DEV Eng(char* e, char* lds, i32 tcap) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
@@ -411,6 +432,10 @@ struct Eng {
     else qpl = (u32*)(env + PC.L.off_q + sizeof(SavedEvent) * QCAP);
     dirty = 0;
     trace_cap = tcap;
+#ifdef MXA_PROF
+    prof = (LDSP u64*)(lds + LDS_Q + sizeof(EnvHdr));
+    if (lane < 32) prof[lane] = 0;
+#endif
     trace = tcap ? (i64*)(env + PC.L.off_trace) : nullptr;
   }
 
@@ -1443,26 +1468,32 @@ struct Eng {
   }
 
   // ---------------- dispatch
+  // agent classes absent from the configuration are compiled out
   DEV void dispatch(int type, bool wake, const Msg& m) {
     if (wake) {
-      switch (type) {
-      case AG_ZI: zi_wakeup(); break;
-      case AG_NOISE: noise_wakeup(); break;
-      case AG_VALUE: value_wakeup(); break;
-      case AG_POVMM: mm_wakeup(); break;
-      case AG_MOMENTUM: mom_wakeup(); break;
-      default: break;  // ExchangeAgent: Agent.wakeup does nothing
-      }
+      if constexpr (PC.n_zi > 0)
+        if (type == AG_ZI) return zi_wakeup();
+      if constexpr (PC.n_noise > 0)
+        if (type == AG_NOISE) return noise_wakeup();
+      if constexpr (PC.n_value > 0)
+        if (type == AG_VALUE) return value_wakeup();
+      if constexpr (PC.n_mm > 0)
+        if (type == AG_POVMM) return mm_wakeup();
+      if constexpr (PC.n_mom > 0)
+        if (type == AG_MOMENTUM) return mom_wakeup();
+      // ExchangeAgent: Agent.wakeup does nothing
     } else {
-      switch (type) {
-      case AG_EXCHANGE: ex_receive(m); break;
-      case AG_ZI: zi_receive(m); break;
-      case AG_NOISE: noise_receive(m); break;
-      case AG_VALUE: value_receive(m); break;
-      case AG_POVMM: mm_receive(m); break;
-      case AG_MOMENTUM: mom_receive(m); break;
-      default: break;
-      }
+      if (type == AG_EXCHANGE) return ex_receive(m);
+      if constexpr (PC.n_zi > 0)
+        if (type == AG_ZI) return zi_receive(m);
+      if constexpr (PC.n_noise > 0)
+        if (type == AG_NOISE) return noise_receive(m);
+      if constexpr (PC.n_value > 0)
+        if (type == AG_VALUE) return value_receive(m);
+      if constexpr (PC.n_mm > 0)
+        if (type == AG_POVMM) return mm_receive(m);
+      if constexpr (PC.n_mom > 0)
+        if (type == AG_MOMENTUM) return mom_receive(m);
     }
   }
 
@@ -1559,8 +1590,13 @@ struct Eng {
         u32 phi = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(pv >> 32));
         asm volatile("" : "+s"(plo), "+s"(phi));
         env = (char*)(__attribute__((address_space(1))) char*)(((u64)phi << 32) | plo);
+#ifndef MXA_NO_LAUNDER_LANE
+        // lane-derived masks (lane == field/2 ...) are rebuilt per use, not hoisted
+        asm volatile("" : "+v"(lane));
+#endif
       }
 #endif
+      PROF_T(t0);
       u64 key;
       u32 eseq;
       int slot = q_peek(key, eseq);
@@ -1591,16 +1627,25 @@ struct Eng {
       add_delay = 0;
       rec_load(rcp);
       i64 at = rg64(AF_ATIME);
+      PROF_ADD(0, t0);
       if (at > t) {  // agent in the future: requeue unchanged (same uniq)
         q_rekey(slot, ((u64)at << 13) | (key & 0x1FFF));
+        PROF_ADD(1, t0);
         continue;
       }
       q_remove(slot);
       rs64(AF_ATIME, t);
+#ifdef MXA_PROF
+      int pb = 2 + 2 * (rgi(AF_TYPE) & 7) + (type == MT_WAKEUP);
+#endif
       dispatch(rgi(AF_TYPE), type == MT_WAKEUP, m);
+      PROF_ADD(pb, t0);
+      PROF_CNT(pb + 14);
       if (dirty) rng_maint();
+      PROF_ADD(30, t0);
       rs64(AF_ATIME, t + rg64(AF_COMP) + add_delay);
       rec_store();
+      PROF_ADD(31, t0);
     }
   }
 };
@@ -1867,6 +1912,9 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
   g.load();
   g.run(max_pops);
   g.save();
+#ifdef MXA_PROF
+  if (g.lane < 32) atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
+#endif
 }
 
 // parity helpers: numpy-legacy RNG draws and glibc math on the device (tests only call
