@@ -119,7 +119,7 @@ def main():
                        "cus": torch.cuda.get_device_properties(local).multi_processor_count},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mxa_run_kernel<4,2,true>", "avg_launch_ms": avg_launch_ms,
+                         "kernel": "mxa_run_kernel<%d> (%s)" % (mxabides.CONFIG_IDS[args.config], args.config), "avg_launch_ms": avg_launch_ms,
                          "launches": launches[0], "algo_bytes_per_event": ALGO_BYTES_PER_EVENT},
         }
         if not args.no_cpu:
@@ -129,8 +129,8 @@ def main():
             cev, _, csec = pyoracle.run_batch(args.config, cseeds.astype(np.uint32), threads)
             out["cpu_baseline"] = {"value": float(cev.sum()) / csec, "unit": "env-steps/s", "cores": threads,
                                    "kind": "port",
-                                   "sample": "%d %s envs (seeds %d..), full episodes, C oracle, %d threads, %.1f s wall"
-                                             % (args.cpu_envs, args.config, SEED0, threads, csec)}
+                                   "sample": "%d %s envs (seeds %d..), full episodes, C oracle, %d threads, %.1f s wall "
+                                             "(~%.0f core-s)" % (args.cpu_envs, args.config, SEED0, threads, csec, csec * threads)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
