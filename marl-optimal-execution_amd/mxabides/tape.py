@@ -1,0 +1,62 @@
+"""Replay-tape ingestion: LOBSTER message files -> the packed per-record arrays the replay
+agent consumes.
+
+`load_lobster` restates LOBSTEROrdersProcessor.processOrders (MarketReplayAgent.py:178-220)
+on the CSV path (the reference's processed-pickle cache is never read): columns
+TIMESTAMP (seconds after midnight), EVENT_TYPE (ignored, as in the reference), ORDER_ID,
+SIZE, PRICE (1e-4 $), BUY_SELL_FLAG (1 buy / -1 sell); time = date + 09:30 + (s - 09:30)
+via pandas Timedelta; PRICE / 100 truncated to int (cents); keep 09:30 <= time < 16:00;
+records grouped by time in file order (`groupby(level=0)`).
+"""
+import numpy as np
+
+OPEN = "09:30:00"
+CLOSE = "16:00:00"
+
+
+class Tape:
+    """Time-sorted replay records: t (ns since midnight), oid, price (cents), size, buy."""
+
+    def __init__(self, t, oid, price, size, buy):
+        self.t = np.ascontiguousarray(t, dtype=np.int64)
+        self.oid = np.ascontiguousarray(oid, dtype=np.int64)
+        self.price = np.ascontiguousarray(price, dtype=np.int64)
+        self.size = np.ascontiguousarray(size, dtype=np.int64)
+        self.buy = np.ascontiguousarray(buy, dtype=np.int8)
+        n = len(self.t)
+        if not (len(self.oid) == len(self.price) == len(self.size) == len(self.buy) == n) or n == 0:
+            raise ValueError("tape arrays must be non-empty and of equal length")
+        if (np.diff(self.t) < 0).any():
+            raise ValueError("tape must be time-sorted")
+        if (self.oid <= 0).any():
+            # Order(order_id=0) falls back to the global auto-id counter (Order.py:26), which
+            # interleaves tape and agent ids; not supported by this build.
+            raise ValueError("tape records with ORDER_ID 0 are not supported")
+
+    def __len__(self):
+        return len(self.t)
+
+    def save(self, path):
+        np.savez_compressed(path, t=self.t, oid=self.oid, price=self.price, size=self.size, buy=self.buy)
+
+    @classmethod
+    def load(cls, path):
+        z = np.load(path, allow_pickle=False)
+        return cls(z["t"], z["oid"], z["price"], z["size"], z["buy"])
+
+
+def load_lobster(path, date):
+    import pandas as pd
+
+    df = pd.read_csv(path, names=["TIMESTAMP", "EVENT_TYPE", "ORDER_ID", "SIZE", "PRICE", "BUY_SELL_FLAG"])
+    day = pd.Timestamp(date)
+    start, end = day + pd.to_timedelta(OPEN), day + pd.to_timedelta(CLOSE)
+    ts = start + pd.to_timedelta(df["TIMESTAMP"], "s") - pd.to_timedelta(OPEN)
+    keep = ((ts >= start) & (ts < end)).to_numpy()
+    t = (ts - day).to_numpy().astype("timedelta64[ns]").astype(np.int64)[keep]
+    oid = df["ORDER_ID"].to_numpy().astype(np.int64)[keep]
+    size = df["SIZE"].astype(int).to_numpy().astype(np.int64)[keep]
+    price = (df["PRICE"].astype(float) / 100).astype(int).to_numpy().astype(np.int64)[keep]
+    buy = (df["BUY_SELL_FLAG"].astype(int) == 1).to_numpy()[keep]
+    order = np.argsort(t, kind="stable")
+    return Tape(t[order], oid[order], price[order], size[order], buy[order])

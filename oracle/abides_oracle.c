@@ -151,7 +151,11 @@ typedef struct {
     int depth, mkt_closed;
     int nb, na;
     int64_t bpx, bq, apx, aq;
+    int64_t b2px, a2px; /* second level prices (depth >= 2 replies; DummyRL metrics) */
     int64_t lookback;
+    /* MODIFY_ORDER: the agent's current copy of the order (the new order is oid/qty/price) */
+    int64_t ooid, oqty, oprice;
+    int obuy, oagent2;
 } msg_t;
 
 typedef struct {
@@ -194,7 +198,7 @@ typedef struct {
 /* ------------------------------------------------------------------------- */
 /* agents                                                                     */
 /* ------------------------------------------------------------------------- */
-enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM };
+enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL };
 enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE };
 
 typedef struct {
@@ -287,6 +291,35 @@ struct ora_env {
     int64_t st_max_heap, st_max_resting, st_max_open, st_resting, st_max_hist_tx;
     char* report;
     int64_t report_len;
+    int ex_has_last; /* OrderBook.last_trade is not None */
+    /* ---- marketreplay / ABIDESEnv (GymKernel) ---- */
+    int gym;
+    int end_step, has_obs, finished;
+    double obs[9];
+    /* LOBSTER tape (LOBSTEROrdersProcessor output), grouped by timestamp */
+    int64_t *tp_t, *tp_oid, *tp_price, *tp_size;
+    int8_t* tp_buy;
+    int tp_n;
+    int64_t* tm;  /* distinct timestamps */
+    int* tm_start; /* first record of each group (ntm + 1 entries) */
+    int ntm, mr_wi;
+    /* replay agent's open orders: open-addressing map oid -> slot */
+    int64_t* mr_key;
+    int32_t* mr_val;
+    int mr_cap, mr_used;
+    aord_t* mr_ord;
+    int mr_nord, mr_capord;
+    /* DummyRLExecutionAgent + ABIDESEnvMetrics */
+    int64_t rl_quantity, rl_exec_sum, rl_rem;
+    int rl_trade;
+    int64_t* hz;
+    int nhz;
+    int m_cnt, m_head;               /* deque(maxlen=100), index 0 = most recent */
+    int64_t m_bid[100], m_ask[100], m_data[100];
+    int m_nb[100], m_na[100], m_dnone[100];
+    int64_t m_bq, m_aq, m_b2, m_a2;  /* most recent LOB: level-1 qtys, level-2 prices */
+    int64_t p0;
+    int p0_none, ph_none, ph_n;
 };
 
 #define NS_SEC 1000000000LL
@@ -472,9 +505,10 @@ static void encode(const ora_env* e, const ev_t* v, int64_t rec[10]) {
         f[0] = m->data;
         f[5] = m->mkt_closed ? 1 : 0;
         break;
-    case K_LIMIT: case K_ACCEPTED: case K_CANCELLED: case K_MODIFY: case K_MODIFIED:
+    case K_LIMIT: case K_ACCEPTED: case K_CANCELLED: case K_MODIFY:
         f[0] = m->oid; f[1] = m->oagent; f[2] = m->is_buy; f[3] = m->qty; f[4] = m->price;
         break;
+    case K_MODIFIED: /* quantity left out: the reference message aliases the live book order */
     case K_CANCEL:
         f[0] = m->oid; f[1] = m->oagent; f[2] = m->is_buy; f[3] = 0; f[4] = m->price;
         break;
@@ -668,6 +702,7 @@ static void handle_limit_order(ora_env* e, bord_t order) {
     if (executed) {
         e->last_trade = py_round((double)ex_pq / (double)ex_q);
         e->last_trade_float = 0;
+        e->ex_has_last = 1;
         hist_shift(e);
     }
 }
@@ -688,6 +723,28 @@ static void cancel_order(ora_env* e, const msg_t* req) {
                 order_msg(&m, K_CANCELLED, &c);
                 ex_send(e, req->oagent, &m);
                 return;
+            }
+        }
+    }
+}
+
+/* modifyOrder (OrderBook.py:341-372).  Reference quirk kept: every order at the level
+ * whose id matches replaces the level HEAD (book[i][0] = new_order), not itself, and one
+ * ORDER_MODIFIED goes to the requester per history epoch that holds the id. */
+static void modify_order(ora_env* e, const msg_t* req) {
+    side_t* book = &e->book[req->obuy ? 0 : 1];
+    bord_t nw = {req->oid, req->oagent, req->is_buy, req->qty, req->price};
+    for (int i = 0; i < book->n; i++) {
+        level_t* L = &book->lv[i];
+        if (L->o[0].price != req->oprice) continue;
+        for (int j = 0; j < L->n; j++) {
+            if (L->o[j].id != req->ooid) continue;
+            L->o[0] = nw;
+            for (int h = 0; h < e->nhist; h++) {
+                if (!hist_find(&e->hist[h], nw.id)) continue;
+                msg_t m;
+                order_msg(&m, K_MODIFIED, &nw);
+                k_send(e, 0, req->oagent2, &m, 0);
             }
         }
     }
@@ -759,7 +816,7 @@ static void ex_receive(ora_env* e, const msg_t* m) {
         r.kind = K_LAST;
         r.data = e->last_trade;
         r.data_float = e->last_trade_float;
-        r.has_data = 1;
+        r.has_data = e->ex_has_last;
         r.mkt_closed = closed;
         ex_send(e, m->sender, &r);
         break;
@@ -778,9 +835,11 @@ static void ex_receive(ora_env* e, const msg_t* m) {
             r.apx = a->lv[0].o[0].price;
             for (int j = 0; j < a->lv[0].n; j++) r.aq += a->lv[0].o[j].qty;
         }
+        if (r.nb > 1) r.b2px = b->lv[1].o[0].price;
+        if (r.na > 1) r.a2px = a->lv[1].o[0].price;
         r.data = e->last_trade;
         r.data_float = e->last_trade_float;
-        r.has_data = 1;
+        r.has_data = e->ex_has_last;
         r.mkt_closed = closed;
         ex_send(e, m->sender, &r);
         break;
@@ -806,6 +865,9 @@ static void ex_receive(ora_env* e, const msg_t* m) {
     }
     case K_CANCEL:
         cancel_order(e, m);
+        break;
+    case K_MODIFY:
+        modify_order(e, m);
         break;
     default:
         break;
@@ -879,6 +941,38 @@ static void del_ord(agent_t* a, int i) {
     a->nord--;
 }
 
+/* open-order lookups: the replay agent keeps thousands of orders (hash map), everybody
+ * else a short insertion-ordered list */
+static int mr_slot(const ora_env* e, int64_t oid, int insert) {
+    uint64_t h = (uint64_t)oid * 0x9E3779B97F4A7C15ull;
+    int mask = e->mr_cap - 1, tomb = -1;
+    for (int i = (int)(h >> 40) & mask;; i = (i + 1) & mask) {
+        if (e->mr_key[i] == oid) return i;
+        if (e->mr_key[i] == -2 && tomb < 0) tomb = i;
+        if (e->mr_key[i] == -1) return insert ? (tomb >= 0 ? tomb : i) : -1;
+    }
+}
+static aord_t* ord_get(ora_env* e, agent_t* a, int64_t oid) {
+    if (a->type == AG_REPLAY) {
+        int i = mr_slot(e, oid, 0);
+        return i >= 0 ? &e->mr_ord[i] : NULL;
+    }
+    int i = find_ord(a, oid);
+    return i >= 0 ? &a->ord[i] : NULL;
+}
+static void ord_del(ora_env* e, agent_t* a, int64_t oid) {
+    if (a->type == AG_REPLAY) {
+        int i = mr_slot(e, oid, 0);
+        if (i >= 0) {
+            e->mr_key[i] = -2;
+            e->mr_nord--;
+        }
+        return;
+    }
+    int i = find_ord(a, oid);
+    if (i >= 0) del_ord(a, i);
+}
+
 /* TradingAgent.wakeup (TradingAgent.py:142-158); returns "ready to trade" */
 static int ta_wakeup(ora_env* e, agent_t* a) {
     a->cur_time = e->cur;
@@ -898,6 +992,8 @@ static int64_t wake_frequency(agent_t* a) {
     switch (a->type) {
     case AG_POVMM: return a->wake_freq;
     case AG_MOMENTUM: return a->wake_freq;
+    case AG_REPLAY: return a->wake_freq;  /* first tape time - mkt_open (MarketReplayAgent.py:94-96) */
+    case AG_DUMMYRL: return a->wake_freq; /* horizon[0] - mkt_open (execution_agent.py:129-130) */
     default: return rs_randint(&a->rs, 0, 100);
     }
 }
@@ -920,19 +1016,17 @@ static void ta_receive(ora_env* e, agent_t* a, const msg_t* m) {
         int64_t q = m->is_buy ? m->qty : -m->qty;
         a->shares += q;
         a->cash -= q * m->fill;
-        int i = find_ord(a, m->oid);
-        if (i >= 0) {
-            if (m->qty >= a->ord[i].qty) del_ord(a, i);
-            else a->ord[i].qty -= m->qty;
+        aord_t* o = ord_get(e, a, m->oid);
+        if (o) {
+            if (m->qty >= o->qty) ord_del(e, a, m->oid);
+            else o->qty -= m->qty;
         }
         break;
     }
     case K_ACCEPTED: break;
-    case K_CANCELLED: {
-        int i = find_ord(a, m->oid);
-        if (i >= 0) del_ord(a, i);
+    case K_CANCELLED:
+        ord_del(e, a, m->oid);
         break;
-    }
     case K_MKT_CLOSED: a->mkt_closed = 1; break;
     case K_LAST:
         if (m->mkt_closed) a->mkt_closed = 1;
@@ -941,6 +1035,7 @@ static void ta_receive(ora_env* e, agent_t* a, const msg_t* m) {
     case K_SPREAD:
         if (m->mkt_closed) a->mkt_closed = 1;
         query_last_trade(a, m);
+        a->has_last_trade = m->has_data;
         a->has_known = 1;
         a->nb = m->nb;
         a->na = m->na;
@@ -1197,6 +1292,243 @@ static void mom_receive(ora_env* e, agent_t* a, const msg_t* m) {
     }
 }
 
+
+/* ------------------------ marketreplay / ABIDESEnv -------------------------- */
+/* MarketReplayAgent.placeOrder (MarketReplayAgent.py:69-91) for one tape record */
+static void mr_place(ora_env* e, agent_t* a, int r) {
+    int64_t oid = e->tp_oid[r], size = e->tp_size[r], price = e->tp_price[r];
+    int buy = e->tp_buy[r];
+    int slot = mr_slot(e, oid, 0);
+    msg_t m;
+    memset(&m, 0, sizeof m);
+    m.fill = -1;
+    if (slot < 0 && size > 0) { /* placeLimitOrder(..., order_id=ORDER_ID) */
+        int i = mr_slot(e, oid, 1);
+        e->mr_key[i] = oid;
+        aord_t o = {oid, buy, size, price};
+        e->mr_ord[i] = o;
+        if (++e->mr_nord > e->st_max_open) e->st_max_open = e->mr_nord;
+        m.kind = K_LIMIT;
+        m.oid = oid;
+        m.oagent = a->id;
+        m.is_buy = buy;
+        m.qty = size;
+        m.price = price;
+        ta_send_ex(e, a, &m);
+    } else if (slot >= 0 && size == 0) { /* cancelOrder(existing_order) */
+        aord_t* o = &e->mr_ord[slot];
+        m.kind = K_CANCEL;
+        m.oid = o->id;
+        m.oagent = a->id;
+        m.is_buy = o->is_buy;
+        m.qty = o->qty;
+        m.price = o->price;
+        ta_send_ex(e, a, &m);
+    } else if (slot >= 0) { /* modifyOrder(existing_order, LimitOrder(..., order_id)) */
+        aord_t* o = &e->mr_ord[slot];
+        m.kind = K_MODIFY;
+        m.oid = oid;
+        m.oagent = a->id;
+        m.is_buy = buy;
+        m.qty = size;
+        m.price = price;
+        m.ooid = o->id;
+        m.oqty = o->qty;
+        m.oprice = o->price;
+        m.obuy = o->is_buy;
+        m.oagent2 = a->id;
+        ta_send_ex(e, a, &m);
+    }
+}
+/* MarketReplayAgent.wakeup (MarketReplayAgent.py:50-61).  The wakeup list starts with the
+ * first tape time, which is also the first wake time: that group is submitted twice and the
+ * last group never (both reference behaviour). */
+static void mr_wakeup(ora_env* e, agent_t* a) {
+    ta_wakeup(e, a);
+    if (!(a->has_open && a->has_close)) return;
+    if (e->mr_wi >= e->ntm) return; /* IndexError: all orders submitted */
+    k_wakeup(e, a->id, e->tm[e->mr_wi]);
+    e->mr_wi++;
+    int lo = 0, hi = e->ntm - 1, g = -1;
+    while (lo <= hi) {
+        int mid = (lo + hi) / 2;
+        if (e->tm[mid] == e->cur) { g = mid; break; }
+        if (e->tm[mid] < e->cur) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    if (g < 0) {
+        fail(e, -7, "MarketReplayAgent: no tape orders at wake time (KeyError)");
+        return;
+    }
+    for (int r = e->tm_start[g]; r < e->tm_start[g + 1]; r++) mr_place(e, a, r);
+}
+static void mr_receive(ora_env* e, agent_t* a, const msg_t* m) { ta_receive(e, a, m); }
+
+/* GymKernel.setCancelOrder (GymKernel.py:364-389) via DummyRL.setCancelOrder: the requested
+ * time minus pd.Timedelta(0.5), which truncates to 0 ns */
+static void k_cancel_order(ora_env* e, int sender, int64_t t) {
+    if (t < e->cur) {
+        fail(e, -3, "setCancelOrder() called with requested time not in future");
+        return;
+    }
+    ev_t v = {t, sender, T_CANCEL_ORDER, e->seq++, -1};
+    heap_push(e, v);
+}
+/* DummyRLExecutionAgent.wakeup (dummy_rl_execution_agent.py:181-213) */
+static void rl_wakeup(ora_env* e, agent_t* a) {
+    if (!ta_wakeup(e, a)) return;
+    if (e->rl_trade) {
+        int k = -1;
+        for (int i = 0; i < e->nhz; i++)
+            if (e->hz[i] > e->cur) { k = i; break; }
+        if (k >= 0) k_cancel_order(e, a->id, e->hz[k]);
+        else e->rl_trade = 0;
+    }
+    if (e->rl_trade) { /* effective_time_horizon = execution_time_horizon[:-1] */
+        int k = -1;
+        for (int i = 0; i < e->nhz - 1; i++)
+            if (e->hz[i] > e->cur) { k = i; break; }
+        if (k >= 0) k_wakeup(e, a->id, e->hz[k]);
+        else e->rl_trade = 0;
+    }
+    get_spread(e, a, 500);
+    a->state = ST_AWAITING_SPREAD;
+}
+/* ABIDESEnvMetrics.addLOB (ABIDESEnvMetrics.py:68-94): deque(maxlen=100), newest first */
+static void metrics_add(ora_env* e, const msg_t* m) {
+    if (e->ph_n == 0) {
+        e->p0 = m->data;
+        e->p0_none = !m->has_data;
+    }
+    e->m_head = (e->m_head + 99) % 100;
+    int s = e->m_head;
+    e->m_bid[s] = m->bpx;
+    e->m_ask[s] = m->apx;
+    e->m_nb[s] = m->nb;
+    e->m_na[s] = m->na;
+    e->m_data[s] = m->data;
+    e->m_dnone[s] = !m->has_data;
+    if (e->m_cnt < 100) e->m_cnt++;
+    e->m_bq = m->bq;
+    e->m_aq = m->aq;
+    e->m_b2 = m->b2px;
+    e->m_a2 = m->a2px;
+    e->ph_n++;
+    if (!m->has_data) e->ph_none = 1;
+}
+/* DummyRL.receiveMessage (dummy_rl_execution_agent.py:222-240); the execution handler is
+ * ExecutionAgent's because of the reference's `hanldeOrderExecution` typo (dummy_rl:273) */
+static void rl_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    if (m->kind == K_EXECUTED) {
+        e->rl_exec_sum += m->qty;
+        e->rl_rem = e->rl_quantity - e->rl_exec_sum;
+    }
+    if (e->rl_rem > 0 && a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        a->state = ST_AWAITING_WAKEUP;
+        metrics_add(e, m);
+    }
+}
+/* numpy pairwise summation (loops_utils.h pairwise_sum) for n <= 128 */
+static double np_pairwise(const double* a, int n) {
+    if (n < 8) {
+        double r = 0.;
+        for (int i = 0; i < n; i++) r += a[i];
+        return r;
+    }
+    double r[8];
+    for (int j = 0; j < 8; j++) r[j] = a[j];
+    int i;
+    for (i = 8; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; j++) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; i++) res += a[i];
+    return res;
+}
+static double np_std(const double* x, int n) {
+    double mean = np_pairwise(x, n) / n, sq[100];
+    for (int i = 0; i < n; i++) {
+        double d = x[i] - mean;
+        sq[i] = d * d;
+    }
+    return sqrt(np_pairwise(sq, n) / n);
+}
+static int m_slot(const ora_env* e, int idx) { /* python index into the deque (negative ok) */
+    if (idx < 0) idx += e->m_cnt;
+    return (e->m_head + idx) % 100;
+}
+/* DummyRL.get_observation (dummy_rl_execution_agent.py:291-312) with ABIDESEnvMetrics */
+static void rl_observe(ora_env* e) {
+    int64_t fl = (e->cur / (30 * NS_SEC)) * (30 * NS_SEC); /* currentTime.floor("30S") */
+    int rem = e->nhz;
+    for (int i = 0; i < e->nhz; i++)
+        if (e->hz[i] == fl) { rem = e->nhz - 1 - i; break; }
+    double* o = e->obs;
+    o[0] = rem;
+    o[1] = (double)e->rl_rem;
+    if (e->m_cnt == 0) { fail(e, -8, "get_observation: no LOB stored (IndexError)"); return; }
+    int s0 = m_slot(e, 0);
+    if (e->m_dnone[s0] || e->p0_none) { fail(e, -8, "get_observation: last trade is None (TypeError)"); return; }
+    o[2] = log((double)e->m_data[s0] / (double)e->p0);
+    for (int i = 0; i < e->m_cnt; i++) {
+        int si = m_slot(e, i);
+        if (!e->m_nb[si] || !e->m_na[si]) { fail(e, -8, "get_observation: empty book side (ValueError)"); return; }
+    }
+    int64_t bid = e->m_bid[s0], ask = e->m_ask[s0], bv = e->m_bq, av = e->m_aq;
+    o[3] = (double)(ask - bid);
+    o[4] = (double)(bv - av) / (double)(bv + av);
+    o[5] = tanh((double)ask / (double)av - (double)bid / (double)bv);
+    double lm[100];
+    for (int i = 0; i < e->m_cnt; i++) {
+        int si = m_slot(e, i);
+        double mid = (double)(e->m_bid[si] + e->m_ask[si]) / 2;
+        lm[i] = log(mid / (double)e->p0);
+    }
+    o[6] = np_std(lm, e->m_cnt);
+    double mt = (double)(bid + ask) / 2;
+    int64_t pt = e->m_data[s0];
+    int d;
+    if ((double)pt > mt) d = 1;
+    else if ((double)pt < mt) d = -1;
+    else { /* idx - 1 = -1: the oldest stored LOB */
+        int sl = m_slot(e, -1);
+        double ml = (double)(e->m_bid[sl] + e->m_ask[sl]) / 2;
+        d = mt > ml ? 1 : -1;
+    }
+    o[7] = d;
+    o[8] = (double)(2 * d) * ((double)pt - mt) / mt;
+    e->has_obs = 1;
+}
+/* DummyRL.process_action + place_orders (dummy_rl_execution_agent.py:138-179) */
+static void rl_place_orders(ora_env* e, const double* act) {
+    agent_t* a = &e->ag[2];
+    double q0 = (double)e->rl_quantity, q = q0; /* metrics.rem_quantity is never updated */
+    double x = act[0], sum = 0.0 + act[1] + act[2], oh0, oh1;
+    if (sum == 0.0) oh0 = oh1 = 0.5;
+    else { oh0 = act[1] / sum; oh1 = act[2] / sum; }
+    double qh = q / q0;
+    double total = rint(q0 * qh * pow(x, pow(qh, 0.5)));
+    double o0 = rint(total * oh0);
+    double o1 = total - (0.0 + o0);
+    double ol[2] = {o0, o1};
+    for (int l = 0; l < 2; l++) {
+        if (e->m_cnt == 0) continue; /* getBookCount on empty metrics raises */
+        int s0 = m_slot(e, 0);
+        int nb = e->m_nb[s0], na = e->m_na[s0];
+        if (nb == 0 || na == 0) continue;       /* ValueError */
+        if (l >= nb || l >= na) continue;       /* IndexError */
+        int64_t price = l == 0 ? e->m_bid[s0] : e->m_b2; /* BUY: bid of level l+1 */
+        place_limit(e, a, (int64_t)ol[l], 1, price);
+    }
+}
+/* GymKernel CANCEL_ORDER branch (GymKernel.py:244-249): get_reward, then cancelAllOrders */
+static void rl_kernel_cancel(ora_env* e) {
+    agent_t* a = &e->ag[2];
+    if (e->m_cnt == 0) { fail(e, -8, "get_reward: no LOB stored (IndexError)"); return; }
+    if (e->ph_none) { fail(e, -8, "get_reward: None in price history (TypeError)"); return; }
+    cancel_all(e, a);
+}
+
 /* ------------------------------- dispatch ---------------------------------- */
 static void dispatch_wakeup(ora_env* e, int id) {
     agent_t* a = &e->ag[id];
@@ -1207,6 +1539,8 @@ static void dispatch_wakeup(ora_env* e, int id) {
     case AG_VALUE: value_wakeup(e, a); break;
     case AG_POVMM: mm_wakeup(e, a); break;
     case AG_MOMENTUM: mom_wakeup(e, a); break;
+    case AG_REPLAY: mr_wakeup(e, a); break;
+    case AG_DUMMYRL: rl_wakeup(e, a); break;
     }
 }
 static void dispatch_message(ora_env* e, int id, const msg_t* m) {
@@ -1218,7 +1552,47 @@ static void dispatch_message(ora_env* e, int id, const msg_t* m) {
     case AG_VALUE: value_receive(e, a, m); break;
     case AG_POVMM: mm_receive(e, a, m); break;
     case AG_MOMENTUM: mom_receive(e, a, m); break;
+    case AG_REPLAY: mr_receive(e, a, m); break;
+    case AG_DUMMYRL:
+        rl_receive(e, a, m);
+        if (m->kind == K_SPREAD) { /* GymKernel: the step ends at the RL agent's spread reply */
+            rl_observe(e);
+            e->end_step = 1;
+        }
+        break;
     }
+}
+
+/* one pop of Kernel.runner (Kernel.py:190-292) / GymKernel.stepRunner (GymKernel.py:158-306) */
+static void pop_one(ora_env* e) {
+        ev_t v = heap_pop(e);
+        e->cur = v.t;
+        e->have_cur = 1;
+        int64_t rec[10];
+        encode(e, &v, rec);
+        for (int i = 0; i < 10; i++) e->hash = (e->hash ^ (uint64_t)rec[i]) * FNV_PRIME;
+        if (e->trace && e->trace_len < e->trace_cap) memcpy(e->trace + 10 * e->trace_len++, rec, sizeof rec);
+        e->pops++;
+        e->add_delay = 0;
+        int a = v.rcp;
+        if (v.type == T_CANCEL_ORDER) { /* no busy check, no delay accounting */
+            rl_kernel_cancel(e);
+            return;
+        }
+        if (e->agent_time[a] > e->cur) { /* agent in the future: requeue unchanged */
+            v.t = e->agent_time[a];
+            heap_push(e, v);
+            return;
+        }
+        e->agent_time[a] = e->cur;
+        if (v.type == T_WAKEUP) {
+            dispatch_wakeup(e, a);
+        } else {
+            msg_t m = e->msgs[v.mi];
+            msg_free(e, v.mi);
+            dispatch_message(e, a, &m);
+        }
+        e->agent_time[a] += e->comp_delay[a] + e->add_delay;
 }
 
 /* Kernel.runner event loop (Kernel.py:190-292) */
@@ -1230,33 +1604,28 @@ int64_t ora_run(ora_env* e, int64_t max_pops) {
             e->done = 1;
             break;
         }
-        ev_t v = heap_pop(e);
-        e->cur = v.t;
-        e->have_cur = 1;
-        int64_t rec[10];
-        encode(e, &v, rec);
-        for (int i = 0; i < 10; i++) e->hash = (e->hash ^ (uint64_t)rec[i]) * FNV_PRIME;
-        if (e->trace && e->trace_len < e->trace_cap) memcpy(e->trace + 10 * e->trace_len++, rec, sizeof rec);
-        e->pops++;
+        pop_one(e);
         done++;
-        e->add_delay = 0;
-        int a = v.rcp;
-        if (e->agent_time[a] > e->cur) { /* agent in the future: requeue unchanged */
-            v.t = e->agent_time[a];
-            heap_push(e, v);
-            continue;
-        }
-        e->agent_time[a] = e->cur;
-        if (v.type == T_WAKEUP) {
-            dispatch_wakeup(e, a);
-        } else {
-            msg_t m = e->msgs[v.mi];
-            msg_free(e, v.mi);
-            dispatch_message(e, a, &m);
-        }
-        e->agent_time[a] += e->comp_delay[a] + e->add_delay;
     }
     return done;
+}
+
+/* ABIDESEnv.step (ABIDESEnv.py:30-49) = GymKernel.stepRunner: place the action's orders,
+ * run until the RL agent's spread reply (or the end), return obs and done. */
+int ora_gym_step(ora_env* e, const double* action, double* obs_out, int* has_obs, int* done_out) {
+    if (!e->gym) return -1;
+    rl_place_orders(e, action);
+    e->end_step = 0;
+    while (!e->end_step && !e->err && e->nheap > 0 && e->cur <= e->stop) pop_one(e);
+    if (!e->err && (e->nheap == 0 || e->cur > e->stop) && !e->finished) {
+        e->finished = 1; /* terminateRunner -> ExecutionAgent.kernelStopping */
+        e->done = 1;
+        if (e->rl_trade) fail(e, -8, "ExecutionAgent.kernelStopping: arrival_price is None (TypeError)");
+    }
+    *done_out = !(e->nheap > 0 && e->cur <= e->stop);
+    memcpy(obs_out, e->obs, sizeof e->obs);
+    *has_obs = e->has_obs;
+    return e->err ? e->err : 0;
 }
 
 /* ------------------------------- reporting --------------------------------- */
@@ -1513,6 +1882,89 @@ static int build_rmsc03(ora_env* e, uint32_t seed) {
     return 0;
 }
 
+/* ABIDESEnv.initAgents / initKernel (ABIDESEnv.py:59-103; agent_config.py:30-160):
+ * Exchange (id 0), MarketReplayAgent (1) on a LOBSTER tape, DummyRLExecutionAgent (2);
+ * GymKernel start = midnight, stop = 16:10, compute delays 0, latencies 0, noise [1.0].
+ * Nothing in this composition draws from an RNG. */
+int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                  const int8_t* buy, int n, ora_env** out) {
+    if (n <= 0) return -1;
+    ora_env* e = (ora_env*)calloc(1, sizeof(ora_env));
+    snprintf(e->config, sizeof e->config, "marketreplay");
+    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
+    agent_t* x = add_agent(e, AG_EXCHANGE);
+    snprintf(x->name, sizeof x->name, "0_EXCHANGE_AGENT");
+    e->ex_open = open;
+    e->ex_close = close;
+    e->ex_pipeline = 0;
+    e->ex_comp = 0;
+    e->stream_history = 10;
+    agent_t* a = add_agent(e, AG_REPLAY);
+    trading_init(a, 0);
+    snprintf(a->name, sizeof a->name, "1_MARKET_REPLAY_AGENT");
+    agent_t* r = add_agent(e, AG_DUMMYRL);
+    trading_init(r, 0);
+    snprintf(r->name, sizeof r->name, "2_DUMMY_RL_EXECUTION_AGENT");
+    e->tp_n = n;
+    e->tp_t = (int64_t*)malloc(sizeof(int64_t) * n);
+    e->tp_oid = (int64_t*)malloc(sizeof(int64_t) * n);
+    e->tp_price = (int64_t*)malloc(sizeof(int64_t) * n);
+    e->tp_size = (int64_t*)malloc(sizeof(int64_t) * n);
+    e->tp_buy = (int8_t*)malloc(n);
+    memcpy(e->tp_t, t, sizeof(int64_t) * n);
+    memcpy(e->tp_oid, oid, sizeof(int64_t) * n);
+    memcpy(e->tp_price, price, sizeof(int64_t) * n);
+    memcpy(e->tp_size, size, sizeof(int64_t) * n);
+    memcpy(e->tp_buy, buy, n);
+    e->tm = (int64_t*)malloc(sizeof(int64_t) * n);
+    e->tm_start = (int*)malloc(sizeof(int) * (n + 1));
+    for (int i = 0; i < n; i++) {
+        if (i > 0 && t[i] < t[i - 1]) { free(e); return -2; } /* tape must be time-sorted */
+        if (i == 0 || t[i] != t[i - 1]) {
+            e->tm[e->ntm] = t[i];
+            e->tm_start[e->ntm++] = i;
+        }
+    }
+    e->tm_start[e->ntm] = n;
+    e->mr_cap = 1;
+    while (e->mr_cap < 2 * n + 64) e->mr_cap <<= 1;
+    e->mr_key = (int64_t*)malloc(sizeof(int64_t) * e->mr_cap);
+    for (int i = 0; i < e->mr_cap; i++) e->mr_key[i] = -1;
+    e->mr_ord = (aord_t*)calloc(e->mr_cap, sizeof(aord_t));
+    a = &e->ag[1]; /* add_agent reallocs: re-fetch */
+    r = &e->ag[2];
+    a->wake_freq = e->tm[0] - open;
+    /* execution_time_horizon = pd.date_range(09:40, 16:00, freq="30S") */
+    e->nhz = 761;
+    e->hz = (int64_t*)malloc(sizeof(int64_t) * e->nhz);
+    for (int i = 0; i < e->nhz; i++) e->hz[i] = 9 * NS_HOUR + 40 * NS_MIN + (int64_t)i * 30 * NS_SEC;
+    r->wake_freq = e->hz[0] - open;
+    e->rl_quantity = 100000;
+    e->rl_rem = 100000;
+    e->rl_trade = 1;
+    e->gym = 1;
+    e->start = 0;
+    e->stop = 16 * NS_HOUR + 10 * NS_MIN;
+    e->lat_mode = 0;
+    e->noise_len = 1;
+    e->agent_time = (int64_t*)calloc(e->n, sizeof(int64_t));
+    e->comp_delay = (int64_t*)calloc(e->n, sizeof(int64_t));
+    e->nhist = 1;
+    e->hash = FNV_OFF;
+    e->ex_has_last = 0; /* no oracle: getDailyOpenPrice raises AttributeError, last_trade None */
+    for (int i = 0; i < e->n; i++) k_wakeup(e, i, e->start);
+    e->cur = e->start;
+    *out = e;
+    return 0;
+}
+int ora_rl_state(const ora_env* e, int64_t* out4) {
+    out4[0] = e->rl_rem;
+    out4[1] = e->rl_exec_sum;
+    out4[2] = e->rl_trade;
+    out4[3] = e->mr_nord;
+    return 0;
+}
+
 int ora_create(const char* config, uint32_t seed, ora_env** out) {
     ora_env* e = (ora_env*)calloc(1, sizeof(ora_env));
     snprintf(e->config, sizeof e->config, "%s", config);
@@ -1530,6 +1982,7 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     /* kernelInitializing: exchange opening price = oracle.getDailyOpenPrice = r_bar (a float) */
     e->last_trade = (int64_t)e->o_rbar;
     e->last_trade_float = 1;
+    e->ex_has_last = 1;
     /* kernelStarting: every agent requests a wakeup at startTime, in id order */
     for (int i = 0; i < e->n; i++) k_wakeup(e, i, e->start);
     e->cur = e->start; /* Kernel.runner: currentTime = startTime before the loop */
@@ -1556,6 +2009,16 @@ void ora_destroy(ora_env* e) {
     free(e->msgs);
     free(e->freem);
     free(e->report);
+    free(e->tp_t);
+    free(e->tp_oid);
+    free(e->tp_price);
+    free(e->tp_size);
+    free(e->tp_buy);
+    free(e->tm);
+    free(e->tm_start);
+    free(e->mr_key);
+    free(e->mr_ord);
+    free(e->hz);
     free(e);
 }
 
@@ -1576,7 +2039,7 @@ int ora_agent_state(const ora_env* e, int id, int64_t* cash, int64_t* shares, in
     if (id < 0 || id >= e->n) return -1;
     *cash = e->ag[id].cash;
     *shares = e->ag[id].shares;
-    *n_open = e->ag[id].nord;
+    *n_open = e->ag[id].type == AG_REPLAY ? e->mr_nord : e->ag[id].nord;
     return 0;
 }
 int64_t ora_book(const ora_env* e, int side, int64_t* buf, int64_t cap) {

@@ -18,10 +18,15 @@
  *   SparseMeanRevertingOracle ................. util/oracle/SparseMeanRevertingOracle.py:36-227
  *   LatencyModel (cubic) ...................... model/LatencyModel.py:109-140
  *   configs sparse_zi_100 / sparse_zi_1000 / rmsc03 (global-RNG draw order)
+ *   ABIDESEnv / GymKernel step loop ........... ABIDESEnv.py:8-103, GymKernel.py:158-389
+ *   MarketReplayAgent + OrderBook.modifyOrder .. agent/examples/MarketReplayAgent.py:50-96,
+ *                                               util/OrderBook.py:341-372
+ *   DummyRLExecutionAgent + ABIDESEnvMetrics ... agent/execution/rl/dummy_rl_execution_agent.py,
+ *                                               ABIDESEnvMetrics.py, execution_agent.py
  *   numpy legacy RandomState (MT19937 + legacy_gauss/exponential/bounded ints), numpy 2.2.6
  *   transcendental math: the host glibc libm (the same libm the reference ran on).
  *
- * Parity is pinned by tests/golden/* (traces produced by the reference itself) and by
+ * Parity is pinned by the fixtures in tests/golden/ (traces produced by the reference itself) and by
  * the reference's own known-answer file tests/sparse_zi_1000.txt.
  */
 #ifndef ABIDES_ORACLE_H
@@ -59,6 +64,16 @@ int64_t ora_last_trade(const ora_env* e);
 void ora_stats(const ora_env* e, int64_t* out);
 /* stdout restatement after ora_finish: "Final holdings ..." lines then "Mean..." lines */
 int64_t ora_report(const ora_env* e, char* buf, int64_t cap);
+
+/* marketreplay / ABIDESEnv: a LOBSTER tape as parsed by
+ * LOBSTEROrdersProcessor (MarketReplayAgent.py:162-220): per record the time (ns since
+ * midnight), order id, price (cents), size, side; time-sorted, file order within a time. */
+int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                  const int8_t* buy, int n, ora_env** out);
+/* ABIDESEnv.step(action[3]): obs_out[9] (valid when *has_obs), *done; returns 0 or an error */
+int ora_gym_step(ora_env* e, const double* action, double* obs_out, int* has_obs, int* done_out);
+/* DummyRL: remaining quantity, executed quantity, trade flag; replay agent's open orders */
+int ora_rl_state(const ora_env* e, int64_t* out4);
 
 /* CPU baseline: n independent envs (seeds[i]) over `threads` OS threads, one env per task.
  * Each env runs at most max_pops pops (<0: to completion). Returns 0 on success. */

@@ -53,6 +53,9 @@ def lib():
         L.ora_report.argtypes = [P, ctypes.c_char_p, I64]
         L.ora_report.restype = I64
         L.ora_destroy.argtypes = [P]
+        L.ora_create_mr.argtypes = [ctypes.c_void_p] * 5 + [I32, ctypes.POINTER(P)]
+        L.ora_gym_step.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(I32), ctypes.POINTER(I32)]
+        L.ora_rl_state.argtypes = [P, ctypes.c_void_p]
         L.ora_run_batch.argtypes = [ctypes.c_char_p, ctypes.c_void_p, I32, I32, I64, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         L.ora_rs_new.argtypes = [ctypes.c_uint32]
@@ -170,6 +173,36 @@ def run_batch(config, seeds, threads, max_pops=-1):
     if rc:
         raise RuntimeError("oracle batch failed")
     return ev, hs, sec.value
+
+
+class OracleGymEnv(OracleEnv):
+    """ABIDESEnv restatement (Exchange + MarketReplayAgent + DummyRL on a LOBSTER tape)."""
+
+    def __init__(self, tape, trace_cap=0):
+        L = lib()
+        self._h = ctypes.c_void_p()
+        self._tape = tape
+        rc = L.ora_create_mr(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
+                             tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), ctypes.byref(self._h))
+        if rc:
+            raise ValueError("oracle: bad tape (%d)" % rc)
+        self.trace_buf = None
+        if trace_cap:
+            self.trace_buf = np.zeros((trace_cap, 10), dtype=np.int64)
+            L.ora_set_trace(self._h, self.trace_buf.ctypes.data, trace_cap)
+
+    def step(self, action):
+        """-> (obs float64[9] or None, done, rc)"""
+        a = np.ascontiguousarray(action, dtype=np.float64)
+        obs = np.zeros(9, dtype=np.float64)
+        has, done = ctypes.c_int(), ctypes.c_int()
+        rc = lib().ora_gym_step(self._h, a.ctypes.data, obs.ctypes.data, ctypes.byref(has), ctypes.byref(done))
+        return (obs if has.value else None), bool(done.value), rc
+
+    def rl_state(self):
+        out = np.zeros(4, dtype=np.int64)
+        lib().ora_rl_state(self._h, out.ctypes.data)
+        return out
 
 
 class RandomState:

@@ -147,7 +147,9 @@ def encode(t_rel, recipient, mtype, msg):
         kind = KIND[m]
     elif m == "ORDER_MODIFIED":
         kind = KIND[m]
-        f[:5] = _order_fields(b["new_order"])
+        # the message aliases the order object now resting in the book (OrderBook.py:366),
+        # whose quantity can change before delivery; the replay agent ignores the message
+        f[:5] = _order_fields(b["new_order"], with_qty=False)
     elif m == "MARKET_DATA":
         kind = KIND[m]
     else:
