@@ -17,6 +17,12 @@
  *   mxa_read_agents .... TradingAgent.holdings / orders (TradingAgent.py:45-46, 112-138)
  *   mxa_read_book ...... OrderBook.bids / asks (util/OrderBook.py:24-25, 377-398)
  *   mxa_read_trace ..... (parity tooling; no reference equivalent)
+ *   mxa_create_replay .. ABIDESEnv.__init__/reset (ABIDESEnv.py:8-57, 59-103), agent_config.py
+ *                        Agents (Exchange, MarketReplayAgent on a LOBSTER tape, DummyRL),
+ *                        LOBSTEROrdersProcessor output (MarketReplayAgent.py:162-220)
+ *   mxa_step ........... ABIDESEnv.step (ABIDESEnv.py:30-49) = GymKernel.stepRunner
+ *                        (GymKernel.py:158-306) with DummyRL.place_orders/get_observation
+ *                        (dummy_rl_execution_agent.py:138-179, 291-312)
  */
 #ifndef MXA_H
 #define MXA_H
@@ -27,7 +33,7 @@ extern "C" {
 
 typedef struct mxa_handle mxa_handle;
 
-enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2 };
+enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKETREPLAY = 3 };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };
@@ -86,6 +92,18 @@ int mxa_set_stream(mxa_handle* h, void* stream);
 double mxa_last_kernel_ms(const mxa_handle* h);
 const char* mxa_last_error(const mxa_handle* h);
 void mxa_destroy(mxa_handle* h);
+
+/* ABIDESEnv on a replay tape: n_rec time-sorted records (ns since midnight, order id > 0,
+ * price in cents < 2^20, size, side 1 = buy), as LOBSTEROrdersProcessor produces them.  One
+ * env per handle slot; envs differ only by the actions they are stepped with. */
+int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                      const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
+                      mxa_handle** out);
+/* one ABIDESEnv.step per env: actions [n][3] (float64) -> obs [n][9] (float64) and flags [n]
+ * (bit0 done, bit1 observation valid, bit2 env error).  Host arrays; synchronous. */
+int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags);
+/* the same on device arrays, asynchronous on the handle's stream */
+int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32_t* d_flags);
 
 /* parity probes: device numpy-legacy RNG (mode 0 u32, 1 double, 2 randint(a,b),
  * 3 normal(a,b), 4 exponential(a), 5 uniform(a,b)) and device glibc math

@@ -16,17 +16,19 @@
 
 namespace {
 
-typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*);
-typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t);
+typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*,
+                         const RpCtx*);
+typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*);
 
 template <int CFG>
 void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, const uint32_t* seeds,
-                  const uint8_t* mask) {
-  hipLaunchKernelGGL((mxa_build_kernel<CFG>), g, b, lds, s, base, stride, n, seeds, mask);
+                  const uint8_t* mask, const RpCtx* ctx) {
+  hipLaunchKernelGGL((mxa_build_kernel<CFG>), g, b, lds, s, base, stride, n, seeds, mask, ctx);
 }
 template <int CFG>
-void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops) {
-  hipLaunchKernelGGL((mxa_run_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops);
+void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
+                const RpCtx* ctx) {
+  hipLaunchKernelGGL((mxa_run_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx);
 }
 
 __global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int n, int* out) {
@@ -60,6 +62,15 @@ struct mxa_handle {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
   std::string err;
+  // marketreplay / ABIDESEnv handles
+  bool replay = false;
+  RpCtx ctx{};             // host copy (pointers are device pointers)
+  RpCtx* d_ctx = nullptr;
+  char* d_tape = nullptr;
+  double *d_act = nullptr, *d_obs = nullptr;
+  int32_t* d_flags = nullptr;
+  std::vector<char> tape_blob;  // host staging of the tape (uploaded by create_common)
+  size_t tb_t, tb_oid, tb_dense, tb_price, tb_size, tb_buy, tb_tm, tb_tm0;
 };
 
 static int hip_fail(mxa_handle* h, hipError_t e, const char* what) {
@@ -71,6 +82,8 @@ static int hip_fail(mxa_handle* h, hipError_t e, const char* what) {
     hipError_t _e = (x);                             \
     if (_e != hipSuccess) return hip_fail(h, _e, #x); \
   } while (0)
+
+static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, int32_t device, mxa_handle** out);
 
 template <int CFG>
 static void bind(mxa_handle* h) {
@@ -110,6 +123,10 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   h->P.n_envs = n_envs;
   h->P.L.trace_cap = trace_cap;
   h->P.L.env_stride = mxa_cfg::env_stride(config, trace_cap);
+  return create_common(h, n_envs, seeds, device, out);
+}
+
+static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, int32_t device, mxa_handle** out) {
   h->device = device;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
@@ -128,7 +145,142 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   HIPCHK(h, hipMalloc(&h->d_count, sizeof(int)));
   HIPCHK(h, hipMemsetAsync(h->d_env, 0, bytes, h->stream));
   HIPCHK(h, hipMemcpyAsync(h->d_seeds, seeds, sizeof(uint32_t) * n_envs, hipMemcpyHostToDevice, h->stream));
+  if (h->replay) {
+    HIPCHK(h, hipMalloc(&h->d_tape, h->tape_blob.size()));
+    HIPCHK(h, hipMemcpyAsync(h->d_tape, h->tape_blob.data(), h->tape_blob.size(), hipMemcpyHostToDevice, h->stream));
+    h->ctx.t = (const int64_t*)(h->d_tape + h->tb_t);
+    h->ctx.oid = (const int32_t*)(h->d_tape + h->tb_oid);
+    h->ctx.dense = (const int32_t*)(h->d_tape + h->tb_dense);
+    h->ctx.price = (const int32_t*)(h->d_tape + h->tb_price);
+    h->ctx.size = (const int32_t*)(h->d_tape + h->tb_size);
+    h->ctx.buy = (const int8_t*)(h->d_tape + h->tb_buy);
+    h->ctx.tm = (const int64_t*)(h->d_tape + h->tb_tm);
+    h->ctx.tm0 = (const int32_t*)(h->d_tape + h->tb_tm0);
+    HIPCHK(h, hipMalloc(&h->d_ctx, sizeof(RpCtx)));
+    HIPCHK(h, hipMemcpyAsync(h->d_ctx, &h->ctx, sizeof(RpCtx), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMalloc(&h->d_act, sizeof(double) * 3 * n_envs));
+    HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 9 * n_envs));
+    HIPCHK(h, hipMalloc(&h->d_flags, sizeof(int32_t) * n_envs));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
   return mxa_reset(h, nullptr);
+}
+
+// ABIDESEnv on a LOBSTER tape (agent_config.py / ABIDESEnv.py); see include/mxa.h
+int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                      const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
+                      mxa_handle** out) {
+  if (!out || !t || !oid || !price || !size || !buy || n_rec <= 0 || n_envs <= 0 || trace_cap < 0) return MXA_EINVAL;
+#ifdef MXA_ONLY_RMSC03
+  return MXA_EINVAL;
+#else
+  int64_t pmin = INT64_MAX, pmax = INT64_MIN;
+  for (int i = 0; i < n_rec; i++) {
+    if ((i && t[i] < t[i - 1]) || oid[i] <= 0 || oid[i] >= INT32_MAX || size[i] < 0 || size[i] >= INT32_MAX ||
+        price[i] < 0 || price[i] >= (1 << 20))
+      return MXA_EINVAL;  // unsorted tape, ORDER_ID 0 (auto-id) records, or out-of-range fields
+    pmin = std::min(pmin, price[i]);
+    pmax = std::max(pmax, price[i]);
+  }
+  mxa_handle* h = new mxa_handle();
+  bind<MXA_CFG_MARKETREPLAY>(h);
+  h->replay = true;
+  h->P = mxa_cfg::params(MXA_CFG_MARKETREPLAY);
+  h->P.n_envs = n_envs;
+  h->P.L.trace_cap = trace_cap;
+  // dense order-id index in first-appearance order; distinct times and their first records
+  std::vector<int32_t> dense(n_rec), tm0;
+  std::vector<int64_t> tm;
+  std::vector<std::pair<int64_t, int32_t>> ids(n_rec);
+  for (int i = 0; i < n_rec; i++) ids[i] = {oid[i], i};
+  std::sort(ids.begin(), ids.end());
+  std::vector<int32_t> first(n_rec);
+  int n_ids = 0;
+  for (int i = 0; i < n_rec; i++) {
+    if (i == 0 || ids[i].first != ids[i - 1].first) n_ids++;
+    dense[ids[i].second] = n_ids - 1;
+  }
+  for (int i = 0; i < n_rec; i++)
+    if (i == 0 || t[i] != t[i - 1]) {
+      tm.push_back(t[i]);
+      tm0.push_back(i);
+    }
+  tm0.push_back(n_rec);
+  const int ntm = (int)tm.size();
+  const int C = n_rec + h->P.rl_ids;  // every placement could rest at once
+  h->ctx.L = mxa_cfg::replay_layout(mxa_cfg::env_stride(MXA_CFG_MARKETREPLAY, trace_cap), (int)pmin, (int)(pmax - pmin + 1), C,
+                                    n_ids, h->P.rl_ids, ntm, n_rec);
+  h->P.L.env_stride = h->ctx.L.end;
+  // tape blob: t, oid, dense, price, size, buy, tm, tm0 (256-B aligned pieces)
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  size_t off = 0;
+  h->tb_t = off;
+  off = al(off + 8ull * n_rec);
+  h->tb_oid = off;
+  off = al(off + 4ull * n_rec);
+  h->tb_dense = off;
+  off = al(off + 4ull * n_rec);
+  h->tb_price = off;
+  off = al(off + 4ull * n_rec);
+  h->tb_size = off;
+  off = al(off + 4ull * n_rec);
+  h->tb_buy = off;
+  off = al(off + n_rec);
+  h->tb_tm = off;
+  off = al(off + 8ull * ntm);
+  h->tb_tm0 = off;
+  off = al(off + 4ull * (ntm + 1));
+  h->tape_blob.assign(off, 0);
+  char* b = h->tape_blob.data();
+  for (int i = 0; i < n_rec; i++) {
+    ((int64_t*)(b + h->tb_t))[i] = t[i];
+    ((int32_t*)(b + h->tb_oid))[i] = (int32_t)oid[i];
+    ((int32_t*)(b + h->tb_dense))[i] = dense[i];
+    ((int32_t*)(b + h->tb_price))[i] = (int32_t)price[i];
+    ((int32_t*)(b + h->tb_size))[i] = (int32_t)size[i];
+    ((int8_t*)(b + h->tb_buy))[i] = buy[i] ? 1 : 0;
+  }
+  memcpy(b + h->tb_tm, tm.data(), 8ull * ntm);
+  memcpy(b + h->tb_tm0, tm0.data(), 4ull * (ntm + 1));
+  std::vector<uint32_t> seeds(n_envs, 0u);  // nothing in this composition draws
+  return create_common(h, n_envs, seeds.data(), device, out);
+#endif
+}
+
+// ABIDESEnv.step for every env: actions [n][3] -> obs [n][9], flags [n] (all host arrays)
+int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags) {
+  if (!h || !h->replay || !actions || !obs || !flags) return MXA_EINVAL;
+#ifdef MXA_ONLY_RMSC03
+  return MXA_EINVAL;
+#else
+  HIPCHK(h, hipSetDevice(h->device));
+  int n = h->P.n_envs;
+  HIPCHK(h, hipMemcpyAsync(h->d_act, actions, sizeof(double) * 3 * n, hipMemcpyHostToDevice, h->stream));
+  int rc = mxa_step_device(h, h->d_act, h->d_obs, h->d_flags);
+  if (rc) return rc;
+  HIPCHK(h, hipMemcpyAsync(obs, h->d_obs, sizeof(double) * 9 * n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(flags, h->d_flags, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  float ms = 0;
+  HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  h->last_ms = ms;
+  return MXA_OK;
+#endif
+}
+
+// the same with device arrays (e.g. torch tensors), asynchronous on the handle's stream
+int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32_t* d_flags) {
+  if (!h || !h->replay) return MXA_EINVAL;
+#ifdef MXA_ONLY_RMSC03
+  return MXA_EINVAL;
+#else
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  hipLaunchKernelGGL(mxa_step_kernel, dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride,
+                     h->P.n_envs, h->P.L.trace_cap, (int64_t)1 << 40, (const RpCtx*)h->d_ctx, d_actions, d_obs, d_flags);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  return MXA_OK;
+#endif
 }
 
 int mxa_reset(mxa_handle* h, const uint8_t* mask) {
@@ -139,15 +291,17 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
     HIPCHK(h, hipMemcpyAsync(h->d_mask, mask, h->P.n_envs, hipMemcpyHostToDevice, h->stream));
     dm = h->d_mask;
   }
-  h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_seeds, dm);
+  h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_seeds, dm,
+           h->d_ctx);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;
 }
 
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
-  if (!h) return MXA_EINVAL;
-  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, max_pops);
+  if (!h || h->replay) return MXA_EINVAL;  // replay handles advance by mxa_step
+  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, max_pops,
+         h->d_ctx);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
 }
@@ -159,14 +313,15 @@ int mxa_sync(mxa_handle* h) {
 }
 
 int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launches_out) {
-  if (!h || chunk <= 0) return MXA_EINVAL;
+  if (!h || chunk <= 0 || h->replay) return MXA_EINVAL;
   HIPCHK(h, hipSetDevice(h->device));
   int launches = 0;
   float total = 0;
   for (;;) {
     if (max_launches > 0 && launches >= max_launches) break;
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, chunk);
+    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, chunk,
+           h->d_ctx);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     launches++;
@@ -223,12 +378,44 @@ int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t ca
     out[a].last_trade = g64(AF_LAST_TRADE);
     out[a].type = (int32_t)r[AF_TYPE];
     out[a].flags = (int32_t)r[AF_FLAGS];
+    if (h->replay && out[a].type == AG_REPLAY) {  // MarketReplayAgent.orders lives in the dense table
+      std::vector<RpOrder> mo(h->ctx.L.D);
+      HIPCHK(h, hipMemcpy(mo.data(), h->d_env + (size_t)env * h->P.L.env_stride + h->ctx.L.off_mro,
+                          sizeof(RpOrder) * mo.size(), hipMemcpyDeviceToHost));
+      int64_t c = 0;
+      for (auto& o : mo) c += o.present ? 1 : 0;
+      out[a].n_open = c;
+    }
   }
   return n;
 }
 
 int mxa_read_book(mxa_handle* h, int32_t env, int32_t side, int64_t* out4, int32_t cap) {
   if (!h || env < 0 || env >= h->P.n_envs) return MXA_ERANGE;
+  if (h->replay) {  // price ladder: levels best-first, FIFO lists
+    const RpLayout& L = h->ctx.L;
+    char* e = h->d_env + (size_t)env * h->P.L.env_stride;
+    std::vector<int32_t> cnt(L.P), head(L.P);
+    std::vector<RpEntry> pool(L.C);
+    HIPCHK(h, hipMemcpy(cnt.data(), e + L.off_lvc + 4ull * side * L.P, 4ull * L.P, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(head.data(), e + L.off_lvh + 4ull * side * L.P, 4ull * L.P, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(pool.data(), e + L.off_pool, sizeof(RpEntry) * L.C, hipMemcpyDeviceToHost));
+    int n = 0;
+    for (int k = 0; k < L.P; k++) {
+      int x = side == 0 ? L.P - 1 - k : k;
+      if (!cnt[x]) continue;
+      for (int q = head[x]; q >= 0; q = pool[q].next) {
+        if (n < cap) {
+          out4[4 * n + 0] = pool[q].oid;
+          out4[4 * n + 1] = pool[q].meta >> 1;
+          out4[4 * n + 2] = pool[q].qty;
+          out4[4 * n + 3] = pool[q].price;
+        }
+        n++;
+      }
+    }
+    return n;
+  }
   int oc = h->P.L.ocap;
   std::vector<SavedOrder> so(oc);
   HIPCHK(h, hipMemcpy(so.data(), h->d_env + (size_t)env * h->P.L.env_stride + h->P.L.off_book,
@@ -314,6 +501,11 @@ void mxa_destroy(mxa_handle* h) {
   if (h->d_seeds) hipFree(h->d_seeds);
   if (h->d_mask) hipFree(h->d_mask);
   if (h->d_count) hipFree(h->d_count);
+  if (h->d_tape) hipFree(h->d_tape);
+  if (h->d_ctx) hipFree(h->d_ctx);
+  if (h->d_act) hipFree(h->d_act);
+  if (h->d_obs) hipFree(h->d_obs);
+  if (h->d_flags) hipFree(h->d_flags);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
   if (h->own) hipStreamDestroy(h->own);

@@ -8,6 +8,7 @@
 // (mxa_api.hip) uses the same functions for the layout and the readers, then adds the
 // per-handle runtime values (n_envs, trace capacity, env stride).
 #pragma once
+#include <stddef.h>
 #include "mxa_layout.h"
 
 namespace mxa_cfg {
@@ -22,17 +23,19 @@ struct Shape {
   int sq, so;
   bool pl;
   int waves;
+  int pw;  // message payload words kept in the queue
 };
 #ifndef MXA_RMSC03_WAVES
 #define MXA_RMSC03_WAVES 4
 #endif
 constexpr Shape shape(int cfg) {
-  return cfg == MXA_CFG_RMSC03 ? Shape{4, 2, true, MXA_RMSC03_WAVES}
-       : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2}
-                                      : Shape{48, 16, false, 1};
+  return cfg == MXA_CFG_RMSC03 ? Shape{4, 2, true, MXA_RMSC03_WAVES, 6}
+       : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6}
+       : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6}
+                                       : Shape{1, 1, true, 2, 8};  // marketreplay: book in HBM
 }
 constexpr size_t lds_bytes(int cfg) {
-  return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 24 : 0)) + 512  // queue + EnvHdr
+  return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
 #ifdef MXA_PROF
          + 256  // phase counters
 #endif
@@ -145,6 +148,35 @@ constexpr void params_sparse_zi(MxaParams& P, bool big) {
   P.L.tx_cap = 256;
 }
 
+// ABIDESEnv composition (ABIDESEnv.py:59-103, agent_config.py): Exchange, MarketReplayAgent,
+// DummyRLExecutionAgent; GymKernel start midnight, stop 16:10, compute delays 0, latency 0,
+// noise [1.0] (no draw).  Nothing draws from an RNG.
+constexpr void params_marketreplay(MxaParams& P) {
+  base_params(P);
+  P.config = MXA_CFG_MARKETREPLAY;
+  P.mkt_close = 16 * HOUR;
+  P.start = 0;
+  P.stop = 16 * HOUR + 10 * MIN;
+  P.default_comp_delay = 0;
+  P.lat_mode = 0;
+  P.noise_len = 1;
+  P.starting_cash = 0;
+  P.first_replay = 1;
+  P.n_replay = 1;
+  P.first_rl = 2;
+  P.n_rl = 1;
+  P.n_agents = 3;
+  P.rl_quantity = 100000;
+  P.rl_h0 = 9 * HOUR + 40 * MIN;
+  P.rl_hstep = 30 * NS;
+  P.rl_nh = 761;      // pd.date_range(09:40, 16:00, freq="30S")
+  P.rl_depth = 500;   // getCurrentSpread(depth=500)
+  P.rl_ids = 4096;    // DummyRL order ids (2 per step at most)
+  P.L.open_cap = 64;
+  P.L.tx_cap = 64;
+  P.L.lat_len = 0;
+}
+
 constexpr uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 // per-env HBM block: header, agent records, open orders, RNG streams, latency row/col,
@@ -168,7 +200,7 @@ constexpr void layout(MxaParams& P, int cfg) {
   L.off_lat = (uint32_t)off;
   off = align_up(off + (uint64_t)L.lat_len * 8, 256);
   L.off_q = (uint32_t)off;
-  off = align_up(off + (uint64_t)L.qcap * sizeof(SavedEvent) + (S.pl ? 0 : (uint64_t)L.qcap * 24), 256);
+  off = align_up(off + (uint64_t)L.qcap * sizeof(SavedEvent) + (S.pl ? 0 : (uint64_t)L.qcap * 4 * S.pw), 256);
   L.off_book = (uint32_t)off;
   off = align_up(off + (uint64_t)L.ocap * sizeof(SavedOrder), 256);
   L.off_tx = (uint32_t)off;
@@ -180,6 +212,7 @@ constexpr void layout(MxaParams& P, int cfg) {
 constexpr MxaParams params(int cfg) {
   MxaParams P{};
   if (cfg == MXA_CFG_RMSC03) params_rmsc03(P);
+  else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;
@@ -188,6 +221,45 @@ constexpr MxaParams params(int cfg) {
 // runtime stride of one env block with `trace_cap` trace records
 constexpr uint64_t env_stride(int cfg, int trace_cap) {
   return align_up(params(cfg).L.off_trace + (uint64_t)trace_cap * MXA_TRACE_WORDS * 8, 256);
+}
+
+// replay sections appended after the trace: header, ladder (count/head/tail/qty per side),
+// entry pool + free stack, per-dense-id live-entry chain heads and entry epochs, the replay
+// agent's orders, the RL metrics deque
+inline RpLayout replay_layout(uint64_t base, int pmin, int P, int C, int n_ids, int agent_ids, int ntm, int nrec) {
+  RpLayout L{};
+  L.pmin = pmin;
+  L.P = P;
+  L.C = C;
+  L.n_ids = n_ids;
+  L.D = n_ids + agent_ids;
+  L.ntm = ntm;
+  L.nrec = nrec;
+  uint64_t off = align_up(base, 256);
+  L.off_rh = off;
+  off = align_up(off + sizeof(RpHdr), 256);
+  L.off_lvc = off;
+  off = align_up(off + 2ull * P * 4, 256);
+  L.off_lvh = off;
+  off = align_up(off + 2ull * P * 4, 256);
+  L.off_lvt = off;
+  off = align_up(off + 2ull * P * 4, 256);
+  L.off_lvq = off;
+  off = align_up(off + 2ull * P * 8, 256);
+  L.off_pool = off;
+  off = align_up(off + (uint64_t)C * sizeof(RpEntry), 256);
+  L.off_free = off;
+  off = align_up(off + (uint64_t)C * 4, 256);
+  L.off_idh = off;
+  off = align_up(off + (uint64_t)L.D * 4, 256);
+  L.off_idep = off;
+  off = align_up(off + (uint64_t)L.D * 8, 256);
+  L.off_mro = off;
+  off = align_up(off + (uint64_t)L.D * sizeof(RpOrder), 256);
+  L.off_ring = off;
+  off = align_up(off + 100 * sizeof(RpLob), 256);
+  L.end = off;
+  return L;
 }
 
 }  // namespace mxa_cfg

@@ -258,10 +258,11 @@ DEV void rs_maint(RSt<B>& r) {
 }
 
 // ------------------------------------------------------------------------------------
-// message payload (24 B)
+// message payload: w0 = kind | buy<<6 | closed<<7 | dfloat<<8 | nb<<9 | na<<10 | hasdata<<11
+// | agent<<16, w1..w5 fields; w6/w7 only in the marketreplay config (24 B / 32 B queued)
 // ------------------------------------------------------------------------------------
 struct Msg {
-  u32 w[6];
+  u32 w[8];
 };
 DEV u32 m_kind(const Msg& m) { return m.w[0] & 63u; }
 DEV int m_buy(const Msg& m) { return (m.w[0] >> 6) & 1; }
@@ -279,12 +280,14 @@ DEV u32 msel(const Msg& m, int i) {
   v = i == 3 ? m.w[3] : v;
   v = i == 4 ? m.w[4] : v;
   v = i == 5 ? m.w[5] : v;
+  v = i == 6 ? m.w[6] : v;
+  v = i == 7 ? m.w[7] : v;
   return v;
 }
 DEV Msg msg_make(u32 kind, i32 agent) {
   Msg m;
   m.w[0] = kind | ((u32)agent << 16);
-  m.w[1] = m.w[2] = m.w[3] = m.w[4] = m.w[5] = 0;
+  m.w[1] = m.w[2] = m.w[3] = m.w[4] = m.w[5] = m.w[6] = m.w[7] = 0;
   return m;
 }
 DEV Msg msg_order(u32 kind, i32 oid, i32 agent, int is_buy, i32 qty, i32 price, i32 fill) {
@@ -297,7 +300,9 @@ DEV Msg msg_order(u32 kind, i32 oid, i32 agent, int is_buy, i32 qty, i32 price, 
   return m;
 }
 
-// the 10-word parity record (tests/golden/gen_fixtures.py encode())
+// the 10-word parity record (tests/golden/gen_fixtures.py encode()).  WIDE: spread replies
+// carry level counts (w6/w7 >> 20) instead of the 0/1 flags (depth-500 queries)
+template <bool WIDE>
 DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
   for (int i = 0; i < 10; i++) rec[i] = 0;
   rec[0] = (i64)(key >> 13);
@@ -323,7 +328,7 @@ DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
     f[1] = (i32)m.w[1];
     break;
   case MK_SPREAD: {
-    int nb = m_nb(m), na = m_na(m);
+    int nb = WIDE ? (int)(m.w[6] >> 20) : m_nb(m), na = WIDE ? (int)(m.w[7] >> 20) : m_na(m);
     i64 d = (i32)m.w[5];
     f[0] = nb ? (i64)(i32)m.w[1] : -1;
     f[1] = nb ? (i64)(i32)m.w[2] : 0;
@@ -352,7 +357,7 @@ DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
     f[0] = (i32)m.w[1];
     f[1] = m_agent(m);
     f[2] = m_buy(m);
-    f[3] = k == MK_CANCEL ? 0 : (i64)(i32)m.w[2];
+    f[3] = (k == MK_CANCEL || k == MK_MODIFIED) ? 0 : (i64)(i32)m.w[2];  // (see gen_fixtures)
     f[4] = (i32)m.w[3];
     if (k == MK_EXECUTED) f[5] = (i32)m.w[4];
     break;
@@ -365,6 +370,15 @@ DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
 // the engine: one instance per wave (= per env), lives in registers / LDS
 // ------------------------------------------------------------------------------------
 #define LDSP __attribute__((address_space(3)))
+// uniform view of a value the compiler cannot prove wave-uniform (loads of a wave-uniform
+// address): moves it to SGPRs so the arithmetic on it is scalar
+DEV i32 U(i32 v) { return __builtin_amdgcn_readfirstlane(v); }
+DEV u32 U(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((i32)v); }
+DEV i64 U(i64 v) {
+  u32 lo = (u32)__builtin_amdgcn_readfirstlane((i32)(u32)(u64)v);
+  u32 hi = (u32)__builtin_amdgcn_readfirstlane((i32)(u32)((u64)v >> 32));
+  return (i64)(((u64)hi << 32) | lo);
+}
 #ifdef MXA_PROF
 // diagnostics build only: per-phase shader-cycle totals over all envs (tools/prof_phases.py)
 __device__ unsigned long long g_mxa_prof[32];
@@ -390,6 +404,8 @@ struct Eng {
   static constexpr int SQ = mxa_cfg::shape(CFG).sq;
   static constexpr int SO = mxa_cfg::shape(CFG).so;
   static constexpr bool PL_LDS = mxa_cfg::shape(CFG).pl;
+  static constexpr int PW = mxa_cfg::shape(CFG).pw;           // payload words queued
+  static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY;     // ABIDESEnv / replay composition
   typedef RSt<BUILD> RS;
   typedef typename std::conditional<PL_LDS, LDSP u32*, u32*>::type PlPtr;
   static constexpr int QCAP = SQ * 64;
@@ -419,17 +435,21 @@ struct Eng {
   u32 dirty;  // RNG streams touched by this event: bits 0-3 G/O/K/L, bit 4 the agent's own
   i64* trace;
   i32 trace_cap;
+  const RpCtx* rx;  // marketreplay: tape + runtime layout (nullptr otherwise)
+  i32 end_step;     // GymKernel: the RL agent's spread reply ends a step
 #ifdef MXA_PROF
   LDSP u64* prof;
 #endif
 
-  static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 24 : 0));
-  DEV Eng(char* e, char* lds, i32 tcap) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
+  static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 4 * PW : 0));
+  DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
+    rx = ctx;
+    end_step = 0;
     lane = laneid();
     qk = (LDSP u64*)lds;
     qs = (LDSP u32*)(lds + 8 * QCAP);
     if constexpr (PL_LDS) qpl = (LDSP u32*)(lds + 12 * QCAP);
-    else qpl = (u32*)(env + PC.L.off_q + sizeof(SavedEvent) * QCAP);
+    else qpl = (u32*)(env + PC.L.off_q + sizeof(SavedEvent) * QCAP);  // [QCAP][PW] after the saved queue
     dirty = 0;
     trace_cap = tcap;
 #ifdef MXA_PROF
@@ -564,11 +584,12 @@ struct Eng {
     mj = bj;
   }
   DEV void pl_write(int slot, const Msg& m) {
-    for (int i = 0; i < 6; i++) qpl[slot * 6 + i] = m.w[i];
+    for (int i = 0; i < PW; i++) qpl[slot * PW + i] = m.w[i];
   }
   DEV Msg pl_read(int slot) {
     Msg m;
-    for (int i = 0; i < 6; i++) m.w[i] = qpl[slot * 6 + i];
+    for (int i = 0; i < PW; i++) m.w[i] = qpl[slot * PW + i];
+    for (int i = PW; i < 8; i++) m.w[i] = 0;
     return m;
   }
   DEV void q_push(u64 key, u32 seq, const Msg& m) {
@@ -595,7 +616,7 @@ struct Eng {
       if (PL_LDS) pl_write(slot, m);
     }
     if (!PL_LDS) {
-      if (lane < 6) qpl[slot * 6 + lane] = msel(m, lane);
+      if (lane < PW) qpl[slot * PW + lane] = msel(m, lane);
     }
     qcount++;
     if (qcount > h.max_q) h.max_q = qcount;
@@ -961,6 +982,12 @@ struct Eng {
         return;
       }
     }
+    if constexpr (RP) {
+      if (k == MK_LIMIT) return rp_handle_limit(m);
+      if (k == MK_CANCEL) return rp_cancel(m);
+      if (k == MK_MODIFY) return rp_modify(m);
+      if (k == MK_SPREAD_REQ) return rp_spread(m, closed);
+    }
     switch (k) {
     case MK_WHEN_OPEN_REQ:
     case MK_WHEN_CLOSE_REQ: {
@@ -975,7 +1002,9 @@ struct Eng {
     }
     case MK_LAST_REQ: {
       Msg r = msg_make(MK_LAST, 0);
-      r.w[0] |= (1u << 11) | ((u32)h.last_trade_float << 8) | ((u32)closed << 7);
+      u32 hasd = 1;
+      if constexpr (RP) hasd = (u32)U(rh()->ex_has_last);
+      r.w[0] |= (hasd << 11) | ((u32)h.last_trade_float << 8) | ((u32)closed << 7);
       r.w[5] = (u32)h.last_trade;
       ex_notify(sender, r);
       break;
@@ -1058,7 +1087,9 @@ struct Eng {
         oo[n] = o;
       }
       rs(AF_NORD, (u32)(n + 1));
-      send_ex(msg_order(MK_LIMIT, (i32)oid, cur_agent, is_buy, (i32)qty, (i32)price, 0));
+      Msg lm = msg_order(MK_LIMIT, (i32)oid, cur_agent, is_buy, (i32)qty, (i32)price, 0);
+      if constexpr (RP) lm.w[5] = (u32)agent_dense(oid);
+      send_ex(lm);
     }
   }
   // cancelOrder for every open order in dict (= ascending order id) order
@@ -1072,7 +1103,9 @@ struct Eng {
       int cnt = n - b < 64 ? n - b : 64;
       for (int i = 0; i < cnt; i++) {
         i32 oid = rdli(my.oid, i), ib = rdli(my.is_buy, i), q = rdli(my.qty, i), p = rdli(my.price, i);
-        send_ex(msg_order(MK_CANCEL, oid, cur_agent, ib, q, p, 0));
+        Msg cm = msg_order(MK_CANCEL, oid, cur_agent, ib, q, p, 0);
+        if constexpr (RP) cm.w[5] = (u32)agent_dense(oid);
+        send_ex(cm);
       }
     }
   }
@@ -1122,6 +1155,10 @@ struct Eng {
   DEV i64 wake_frequency(int type) {
     if (type == AG_POVMM) return PC.mm_wake;
     if (type == AG_MOMENTUM) return PC.mom_wake;
+    if constexpr (RP) {
+      if (type == AG_REPLAY) return U(rx->tm[0]) - PC.mkt_open;  // MarketReplayAgent.py:94-96
+      if (type == AG_DUMMYRL) return PC.rl_h0 - PC.mkt_open;     // execution_agent.py:129-130
+    }
     RS A = agent_rs();
     i64 v = rs_randint(A, 0, 100);
     agent_rs_put(A);
@@ -1151,6 +1188,16 @@ struct Eng {
       i64 q = m_buy(m) ? (i64)(i32)m.w[2] : -(i64)(i32)m.w[2];
       rs64(AF_SHARES, rg64(AF_SHARES) + q);
       rs64(AF_CASH, rg64(AF_CASH) - q * (i64)(i32)m.w[4]);
+      if constexpr (RP) {
+        if (type == AG_REPLAY) {  // MarketReplayAgent.orders: dense-indexed table
+          RpOrder* o = mro() + (i32)m.w[5];
+          if (U(o->present)) {  // all lanes store the same value
+            if ((i32)m.w[2] >= U(o->qty)) o->present = 0;
+            else o->qty = U(o->qty) - (i32)m.w[2];
+          }
+          break;
+        }
+      }
       OpenOrder o;
       int idx = find_open((i32)m.w[1], o);
       if (idx >= 0) {
@@ -1160,6 +1207,12 @@ struct Eng {
       break;
     }
     case MK_CANCELLED: {
+      if constexpr (RP) {
+        if (type == AG_REPLAY) {
+          mro()[(i32)m.w[5]].present = 0;
+          break;
+        }
+      }
       OpenOrder o;
       int idx = find_open((i32)m.w[1], o);
       if (idx >= 0) del_open(idx);
@@ -1468,6 +1521,580 @@ struct Eng {
   }
 
   // ---------------- dispatch
+  // =====================================================================================
+  // marketreplay / ABIDESEnv.  Compiled only into the
+  // marketreplay instantiation (member templates are instantiated on use).
+  // The book is a price ladder in HBM: per side and price level a FIFO list of entries
+  // (count, head, tail, total qty); entries come from a per-env pool; the live entries of one
+  // order id are chained so cancel/modify find them without walking a level.
+  // =====================================================================================
+  DEV RpHdr* rh() { return (RpHdr*)(env + rx->L.off_rh); }
+  DEV i32* lv_cnt(int s) { return (i32*)(env + rx->L.off_lvc) + (size_t)s * U(rx->L.P); }
+  DEV i32* lv_head(int s) { return (i32*)(env + rx->L.off_lvh) + (size_t)s * U(rx->L.P); }
+  DEV i32* lv_tail(int s) { return (i32*)(env + rx->L.off_lvt) + (size_t)s * U(rx->L.P); }
+  DEV i64* lv_qty(int s) { return (i64*)(env + rx->L.off_lvq) + (size_t)s * U(rx->L.P); }
+  DEV RpEntry* pool() { return (RpEntry*)(env + rx->L.off_pool); }
+  DEV i32* freel() { return (i32*)(env + rx->L.off_free); }
+  DEV i32* idh() { return (i32*)(env + rx->L.off_idh); }
+  DEV i32* idep() { return (i32*)(env + rx->L.off_idep); }
+  DEV RpOrder* mro() { return (RpOrder*)(env + rx->L.off_mro); }
+  DEV RpLob* ring() { return (RpLob*)(env + rx->L.off_ring); }
+  // DummyRL order ids (the global counter) map after the tape's dense ids
+  DEV i32 agent_dense(i64 oid) {
+    i32 d = U(rx->L.n_ids) + (i32)oid;
+    if (oid < 0 || d >= U(rx->L.D)) {
+      fail(ERR_RP_IDS);
+      return 0;
+    }
+    return d;
+  }
+  DEV i32 lvl_index(i32 price) {
+    i32 x = price - U(rx->L.pmin);
+    if (x < 0 || x >= U(rx->L.P)) {
+      fail(ERR_RP_PRICE);
+      return -1;
+    }
+    return x;
+  }
+  // first non-empty level from `from` toward worse prices (bids down, asks up); wave-parallel
+  DEV i32 lvl_next(int side, i32 from) {
+    const i32* c = lv_cnt(side);
+    const i32 P = U(rx->L.P);
+    for (i32 b = from; side == 0 ? b >= 0 : b < P; b += side == 0 ? -64 : 64) {
+      i32 x = side == 0 ? b - lane : b + lane;
+      bool ok = x >= 0 && x < P && c[x] > 0;
+      u64 m = bal(ok);
+      if (m) return side == 0 ? b - ffs64(m) : b + ffs64(m);
+    }
+    return -1;
+  }
+  DEV void id_link(i32 d, i32 e) {
+    RpEntry* E = pool();
+    i32 hd = U(idh()[d]);
+    {  // every lane stores the same (uniform) value
+      E[e].idprev = -1;
+      E[e].idnext = hd;
+      if (hd >= 0) E[hd].idprev = e;
+      idh()[d] = e;
+    }
+  }
+  DEV void id_unlink(i32 d, i32 e) {
+    RpEntry* E = pool();
+    i32 p = U(E[e].idprev), n = U(E[e].idnext);
+    {  // every lane stores the same (uniform) value
+      if (p >= 0) E[p].idnext = n;
+      else idh()[d] = n;
+      if (n >= 0) E[n].idprev = p;
+    }
+  }
+  // enterOrder (OrderBook.py:256-282): append to the level FIFO
+  DEV void rp_enter(i32 oid, i32 d, i32 agent, int buy, i32 qty, i32 price) {
+    RpHdr* R = rh();
+    const int side = buy ? 0 : 1;
+    i32 x = lvl_index(price);
+    if (x < 0) return;
+    i32 top = U(R->free_top);
+    if (top <= 0) {
+      fail(ERR_RP_POOL);
+      return;
+    }
+    i32 e = U(freel()[top - 1]);
+    u32 arr = h.arrival++;
+    i32 tl = U(lv_tail(side)[x]);
+    i32 cnt = U(lv_cnt(side)[x]);
+    RpEntry* E = pool();
+    {  // every lane stores the same (uniform) value
+      R->free_top = top - 1;
+      RpEntry n;
+      n.price = price;
+      n.qty = qty;
+      n.oid = oid;
+      n.dense = d;
+      n.meta = (agent << 1) | buy;
+      n.arrival = arr;
+      n.prev = tl;
+      n.next = -1;
+      n.idprev = -1;
+      n.idnext = -1;
+      n.pad[0] = n.pad[1] = 0;
+      E[e] = n;
+      if (tl >= 0) E[tl].next = e;
+      else lv_head(side)[x] = e;
+      lv_tail(side)[x] = e;
+      lv_cnt(side)[x] = cnt + 1;
+      lv_qty(side)[x] += qty;
+    }
+    if (cnt == 0) {
+      i32 nl = U(R->nlev[side]);
+      i32 b = U(R->best[side]);
+      {  // every lane stores the same (uniform) value
+        R->nlev[side] = nl + 1;
+        if (b < 0 || (side == 0 ? x > b : x < b)) R->best[side] = x;
+      }
+    }
+    id_link(d, e);
+    h.b_count++;
+    if (h.b_count > h.max_book) h.max_book = h.b_count;
+  }
+  // remove entry e (level x of `side`) from the book
+  DEV void rp_unlink(int side, i32 x, i32 e) {
+    RpHdr* R = rh();
+    RpEntry* E = pool();
+    i32 p = U(E[e].prev), n = U(E[e].next), q = U(E[e].qty), d = U(E[e].dense);
+    i32 cnt = U(lv_cnt(side)[x]);
+    i32 top = U(R->free_top);
+    {  // every lane stores the same (uniform) value
+      if (p >= 0) E[p].next = n;
+      else lv_head(side)[x] = n;
+      if (n >= 0) E[n].prev = p;
+      else lv_tail(side)[x] = p;
+      lv_cnt(side)[x] = cnt - 1;
+      lv_qty(side)[x] -= q;
+      freel()[top] = e;
+      R->free_top = top + 1;
+    }
+    id_unlink(d, e);
+    h.b_count--;
+    if (cnt == 1) {
+      i32 nl = U(R->nlev[side]);
+      i32 b = U(R->best[side]);
+      i32 nb = b;
+      if (b == x) {
+        __threadfence_block();
+        nb = lvl_next(side, side == 0 ? x - 1 : x + 1);
+      }
+      {  // every lane stores the same (uniform) value
+        R->nlev[side] = nl - 1;
+        R->best[side] = nb;
+      }
+    }
+  }
+  DEV void rp_note_entry_epoch(i32 d, i32 ep) {  // history[0][order_id] = ... (OrderBook.py:51-60)
+    i32* E = idep() + 2 * (size_t)d;
+    i32 e0 = U(E[0]);
+    if (e0 != ep) {  // all lanes store the same value
+      E[1] = e0;
+      E[0] = ep;
+    }
+  }
+  // handleLimitOrder / executeOrder (OrderBook.py:38-254) on the ladder
+  DEV void rp_handle_limit(const Msg& m) {
+    i32 oid = (i32)m.w[1], qty = (i32)m.w[2], price = (i32)m.w[3], d = (i32)m.w[5];
+    i32 agent = m_agent(m);
+    int buy = m_buy(m);
+    if (qty <= 0) return;
+    const i32 hep = h.epoch;
+    rp_note_entry_epoch(d, hep);
+    RpHdr* R = rh();
+    RpEntry* E = pool();
+    const i32 pmin = U(rx->L.pmin);
+    i64 ex_q = 0, ex_pq = 0;
+    bool executed = false;
+    for (;;) {
+      const int opp = buy ? 1 : 0;
+      __threadfence_block();
+      i32 b = U(R->best[opp]);
+      bool match = b >= 0 && (buy ? price >= pmin + b : price <= pmin + b);
+      if (!match) {
+        rp_enter(oid, d, agent, buy, qty, price);
+        Msg ma = msg_order(MK_ACCEPTED, oid, agent, buy, qty, price, 0);
+        ma.w[5] = (u32)d;
+        ex_notify(agent, ma);
+        break;
+      }
+      i32 e = U(lv_head(opp)[b]);
+      i32 hq = U(E[e].qty), ho = U(E[e].oid), hd = U(E[e].dense), hm = U(E[e].meta), hp = U(E[e].price);
+      i32 mq;
+      if (qty >= hq) {
+        mq = hq;
+        rp_unlink(opp, b, e);
+      } else {
+        mq = qty;
+        {  // every lane stores the same (uniform) value
+          E[e].qty = hq - qty;
+          lv_qty(opp)[b] -= qty;
+        }
+      }
+      qty -= mq;
+      Msg mt = msg_order(MK_EXECUTED, oid, agent, buy, mq, price, hp);
+      mt.w[5] = (u32)d;
+      ex_notify(agent, mt);
+      Msg mm = msg_order(MK_EXECUTED, ho, hm >> 1, hm & 1, mq, hp, hp);
+      mm.w[5] = (u32)hd;
+      ex_notify(hm >> 1, mm);
+      ex_q += mq;
+      ex_pq += (i64)hp * mq;
+      executed = true;
+      if (qty <= 0 || status == ST_ERROR) break;
+    }
+    if (executed) {
+      h.last_trade = py_round((double)ex_pq / (double)ex_q);
+      h.last_trade_float = 0;
+      h.epoch = hep + 1;
+      R->ex_has_last = 1;
+    }
+  }
+  // cancelOrder (OrderBook.py:284-339): first live entry of the id at the request's level
+  DEV void rp_cancel(const Msg& m) {
+    i32 oid = (i32)m.w[1], price = (i32)m.w[3], d = (i32)m.w[5];
+    const int side = m_buy(m) ? 0 : 1;
+    i32 x = price - U(rx->L.pmin);
+    if (x < 0 || x >= U(rx->L.P)) return;
+    RpEntry* E = pool();
+    i32 best = -1;
+    u32 ba = 0xFFFFFFFFu;
+    i32 guard = 0;
+    for (i32 e = U(idh()[d]); e >= 0 && guard < (1 << 16); e = U(E[e].idnext), guard++) {
+      bool at = U(E[e].price) == price && (U(E[e].meta) & 1) == (side == 0) && U(E[e].oid) == oid;
+      u32 a = U(E[e].arrival);
+      if (at && a < ba) {
+        ba = a;
+        best = e;
+      }
+    }
+    if (best < 0) return;
+    i32 q = U(E[best].qty), mt = U(E[best].meta);
+    rp_unlink(side, x, best);
+    Msg r = msg_order(MK_CANCELLED, oid, mt >> 1, mt & 1, q, price, 0);
+    r.w[5] = (u32)d;
+    ex_notify(m_agent(m), r);
+  }
+  // modifyOrder (OrderBook.py:341-372): each entry of the id at the level replaces the level
+  // HEAD with the new order; one ORDER_MODIFIED per match per history epoch holding the id
+  DEV void rp_modify(const Msg& m) {
+    i32 oid = (i32)m.w[1], qty = (i32)m.w[2], price = (i32)m.w[3], oprice = (i32)m.w[4], d = (i32)m.w[5];
+    const int buy = m_buy(m), side = buy ? 0 : 1;
+    i32 agent = m_agent(m);
+    i32 x = oprice - U(rx->L.pmin);
+    if (x < 0 || x >= U(rx->L.P)) return;
+    if (U(lv_cnt(side)[x]) == 0) return;
+    if (price != oprice) {
+      fail(ERR_RP_MODIFY);
+      return;
+    }
+    RpEntry* E = pool();
+    int matches = 0;
+    i32 guard = 0;
+    for (i32 e = U(idh()[d]); e >= 0 && guard < (1 << 16); e = U(E[e].idnext), guard++)
+      if (U(E[e].price) == oprice && (U(E[e].meta) & 1) == buy && U(E[e].oid) == oid) matches++;
+    if (matches == 0) return;
+    i32 hd = U(lv_head(side)[x]);
+    i32 hq = U(E[hd].qty), hdense = U(E[hd].dense);
+    if (hdense != d) {
+      id_unlink(hdense, hd);
+      id_link(d, hd);
+    }
+    {  // every lane stores the same (uniform) value
+      E[hd].oid = oid;
+      E[hd].dense = d;
+      E[hd].qty = qty;
+      E[hd].meta = (agent << 1) | buy;
+      lv_qty(side)[x] += (i64)(qty - hq);
+    }
+    const i32* EP = idep() + 2 * (size_t)d;
+    const i32 lo = h.epoch - PC.stream_history;
+    int neps = (U(EP[0]) >= lo ? 1 : 0) + (U(EP[1]) >= lo && U(EP[1]) != U(EP[0]) ? 1 : 0);
+    for (int k = 0; k < matches * neps; k++) {
+      Msg r = msg_order(MK_MODIFIED, oid, agent, buy, qty, price, 0);
+      r.w[5] = (u32)d;
+      ex_notify(agent, r);
+    }
+  }
+  // QUERY_SPREAD reply with `depth` levels (ExchangeAgent.py:215-245): level-1 price/qty,
+  // level-2 prices and the level counts (w6/w7 = price2 | count << 20)
+  DEV void rp_spread(const Msg& m, bool closed) {
+    RpHdr* R = rh();
+    const i32 pmin = U(rx->L.pmin);
+    i32 depth = (i32)m.w[1];
+    i32 nb = U(R->nlev[0]), na = U(R->nlev[1]);
+    nb = nb < depth ? nb : depth;
+    na = na < depth ? na : depth;
+    Msg r = msg_make(MK_SPREAD, 0);
+    i32 bb = U(R->best[0]), ab = U(R->best[1]);
+    if (nb > 0) {
+      r.w[1] = (u32)(pmin + bb);
+      r.w[2] = (u32)U(lv_qty(0)[bb]);
+    }
+    if (na > 0) {
+      r.w[3] = (u32)(pmin + ab);
+      r.w[4] = (u32)U(lv_qty(1)[ab]);
+    }
+    i32 b2 = 0, a2 = 0;
+    if (nb > 1) b2 = pmin + lvl_next(0, bb - 1);
+    if (na > 1) a2 = pmin + lvl_next(1, ab + 1);
+    r.w[6] = (u32)b2 | ((u32)nb << 20);
+    r.w[7] = (u32)a2 | ((u32)na << 20);
+    r.w[5] = (u32)h.last_trade;
+    u32 hasd = (u32)U(R->ex_has_last);
+    r.w[0] |= ((u32)(nb > 0) << 9) | ((u32)(na > 0) << 10) | (hasd << 11) | ((u32)closed << 7);
+    ex_notify(m_agent(m), r);
+  }
+
+  // ---------------- MarketReplayAgent (MarketReplayAgent.py:50-96)
+  DEV void mr_place_record(i32 r) {
+    const i32 oid = U(rx->oid[r]), d = U(rx->dense[r]), price = U(rx->price[r]), size = U(rx->size[r]);
+    const int buy = (int)U((i32)rx->buy[r]);
+    RpOrder* O = mro() + d;
+    const i32 present = U(O->present);
+    if (!present && size > 0) {  // placeLimitOrder(..., order_id=ORDER_ID)
+      {  // every lane stores the same (uniform) value
+        RpOrder o;
+        o.qty = size;
+        o.price = price;
+        o.is_buy = buy;
+        o.present = 1;
+        *O = o;
+      }
+      Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, size, price, 0);
+      lm.w[5] = (u32)d;
+      send_ex(lm);
+    } else if (present && size == 0) {  // cancelOrder(existing_order)
+      Msg cm = msg_order(MK_CANCEL, oid, cur_agent, U(O->is_buy), U(O->qty), U(O->price), 0);
+      cm.w[5] = (u32)d;
+      send_ex(cm);
+    } else if (present) {  // modifyOrder(existing_order, LimitOrder(..., order_id))
+      if (buy != U(O->is_buy)) {
+        fail(ERR_RP_MODIFY);
+        return;
+      }
+      Msg mm = msg_order(MK_MODIFY, oid, cur_agent, buy, size, price, U(O->price));
+      mm.w[5] = (u32)d;
+      send_ex(mm);
+    }
+  }
+  DEV void mr_wakeup() {
+    ta_wakeup();
+    u32 f = flags();
+    if (!((f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE))) return;
+    RpHdr* R = rh();
+    i32 wi = U(R->mr_wi);
+    const i32 ntm = U(rx->L.ntm);
+    if (wi >= ntm) return;  // IndexError: every order submitted (the last group never is)
+    wakeup_at(cur_agent, U(rx->tm[wi]));
+    R->mr_wi = wi + 1;
+    i32 lo = 0, hi = ntm - 1, g = -1;
+    while (lo <= hi) {
+      i32 mid = (lo + hi) >> 1;
+      i64 tv = U(rx->tm[mid]);
+      if (tv == cur) {
+        g = mid;
+        break;
+      }
+      if (tv < cur) lo = mid + 1;
+      else hi = mid - 1;
+    }
+    if (g < 0) {
+      fail(ERR_RP_KEYERROR);
+      return;
+    }
+    const i32 r1 = U(rx->tm0[g + 1]);
+    for (i32 r = U(rx->tm0[g]); r < r1; r++) mr_place_record(r);
+  }
+  DEV void mr_receive(const Msg& m) { ta_receive(m, AG_REPLAY); }
+
+  // ---------------- DummyRLExecutionAgent (dummy_rl_execution_agent.py) + GymKernel hooks
+  DEV void kcancel_at(i64 t) {  // GymKernel.setCancelOrder(sender, t - Timedelta(0.5) = t)
+    if (t < cur) {
+      fail(ERR_WAKEUP_PAST);
+      return;
+    }
+    Msg m = msg_make(MK_KCANCEL, 0);
+    u64 key = ((u64)t << 13) | ((u64)cur_agent << 2) | MT_CANCEL_ORDER;
+    q_push(key, seq++, m);
+  }
+  DEV void rl_wakeup() {
+    if (!ta_wakeup()) return;
+    RpHdr* R = rh();
+    // first horizon time strictly after now
+    i32 k = cur < PC.rl_h0 ? 0 : (i32)((cur - PC.rl_h0) / PC.rl_hstep) + 1;
+    i32 trade = U(R->rl_trade);
+    if (trade) {
+      if (k < PC.rl_nh) kcancel_at(PC.rl_h0 + (i64)k * PC.rl_hstep);
+      else trade = 0;
+    }
+    if (trade) {  // effective_time_horizon = execution_time_horizon[:-1]
+      if (k < PC.rl_nh - 1) wakeup_at(cur_agent, PC.rl_h0 + (i64)k * PC.rl_hstep);
+      else trade = 0;
+    }
+    R->rl_trade = trade;
+    get_spread(PC.rl_depth);
+    rs(AF_STATE, AS_AWAITING_SPREAD);
+  }
+  // ABIDESEnvMetrics.addLOB: deque(maxlen=100), newest first
+  DEV void rl_add_lob(const Msg& m) {
+    RpHdr* R = rh();
+    const i32 nb = (i32)(m.w[6] >> 20), na = (i32)(m.w[7] >> 20);
+    const int dnone = !m_hasdata(m);
+    i32 ph = U(R->ph_n), cnt = U(R->m_cnt), hd = U(R->m_head);
+    hd = (hd + 99) % 100;
+    {  // every lane stores the same (uniform) value
+      if (ph == 0) {
+        R->p0 = (i32)m.w[5];
+        R->p0_none = dnone;
+      }
+      RpLob l;
+      l.bid = (i32)m.w[1];
+      l.ask = (i32)m.w[3];
+      l.data = (i32)m.w[5];
+      l.flags = (nb > 0 ? 1 : 0) | (na > 0 ? 2 : 0) | (dnone ? 4 : 0);
+      ring()[hd] = l;
+      R->m_head = hd;
+      R->m_cnt = cnt < 100 ? cnt + 1 : 100;
+      R->m_nb = nb;
+      R->m_na = na;
+      R->m_bq = (i32)m.w[2];
+      R->m_aq = (i32)m.w[4];
+      R->m_b2 = (i32)(m.w[6] & 0xFFFFFu);
+      R->m_a2 = (i32)(m.w[7] & 0xFFFFFu);
+      R->ph_n = ph + 1;
+      if (dnone) R->ph_none = 1;
+    }
+  }
+  DEV void rl_receive(const Msg& m) {
+    ta_receive(m, AG_DUMMYRL);
+    RpHdr* R = rh();
+    const u32 k = m_kind(m);
+    if (k == MK_EXECUTED) {  // ExecutionAgent.handleOrderExecution (the DummyRL override is misspelt)
+      i64 ex = U(R->rl_exec) + (i32)m.w[2];
+      {  // every lane stores the same (uniform) value
+        R->rl_exec = ex;
+        R->rl_rem = PC.rl_quantity - ex;
+      }
+    }
+    __threadfence_block();
+    if (U(R->rl_rem) > 0 && rgi(AF_STATE) == AS_AWAITING_SPREAD && k == MK_SPREAD) {
+      rs(AF_STATE, AS_AWAITING_WAKEUP);
+      rl_add_lob(m);
+    }
+    if (k == MK_SPREAD) {  // GymKernel.stepRunner: observation, end of step
+      __threadfence_block();
+      rl_observe();
+      end_step = 1;
+    }
+  }
+  // numpy pairwise summation (n <= 128) and np.std
+  DEV static double np_pairwise(const double* a, int n) {
+    if (n < 8) {
+      double r = 0.;
+      for (int i = 0; i < n; i++) r += a[i];
+      return r;
+    }
+    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    int i;
+    for (i = 8; i < n - (n % 8); i += 8) {
+      r0 += a[i];
+      r1 += a[i + 1];
+      r2 += a[i + 2];
+      r3 += a[i + 3];
+      r4 += a[i + 4];
+      r5 += a[i + 5];
+      r6 += a[i + 6];
+      r7 += a[i + 7];
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; i++) res += a[i];
+    return res;
+  }
+  // DummyRL.get_observation (dummy_rl:291-312): float64[9] into the replay header
+  DEV void rl_observe() {
+    RpHdr* R = rh();
+    const i64 fl = (cur / PC.rl_hstep) * PC.rl_hstep;  // currentTime.floor("30S")
+    i32 rem = PC.rl_nh;
+    if (fl >= PC.rl_h0 && (fl - PC.rl_h0) / PC.rl_hstep < PC.rl_nh) rem = PC.rl_nh - 1 - (i32)((fl - PC.rl_h0) / PC.rl_hstep);
+    const i32 cnt = U(R->m_cnt), hd = U(R->m_head);
+    double o[9];
+    o[0] = (double)rem;
+    o[1] = (double)U(R->rl_rem);
+    if (cnt == 0) {
+      fail(ERR_RP_OBS);
+      return;
+    }
+    const RpLob* L = ring();
+    const i32 f0 = U(L[hd].flags);
+    if ((f0 & 4) || U(R->p0_none)) {
+      fail(ERR_RP_OBS);
+      return;
+    }
+    const i64 p0 = U(R->p0), pt = U(L[hd].data);
+    const i64 bid = U(L[hd].bid), ask = U(L[hd].ask), bv = U(R->m_bq), av = U(R->m_aq);
+    double lm[100];
+    for (int i = 0; i < cnt; i++) {
+      const RpLob li = L[(hd + i) % 100];
+      if ((U(li.flags) & 3) != 3) {
+        fail(ERR_RP_OBS);
+        return;
+      }
+      double mid = (double)((i64)U(li.bid) + U(li.ask)) / 2;
+      lm[i] = gm_log(mid / (double)p0);
+    }
+    o[2] = gm_log((double)pt / (double)p0);
+    o[3] = (double)(ask - bid);
+    o[4] = (double)(bv - av) / (double)(bv + av);
+    o[5] = tanh((double)ask / (double)av - (double)bid / (double)bv);
+    double mean = np_pairwise(lm, cnt) / cnt;
+    for (int i = 0; i < cnt; i++) {
+      double dd = lm[i] - mean;
+      lm[i] = dd * dd;
+    }
+    o[6] = __builtin_sqrt(np_pairwise(lm, cnt) / cnt);
+    const double mt = (double)(bid + ask) / 2;
+    int dir;
+    if ((double)pt > mt) dir = 1;
+    else if ((double)pt < mt) dir = -1;
+    else {  // idx - 1 == -1: the oldest stored LOB
+      const RpLob ll = L[(hd + cnt - 1) % 100];
+      double ml = (double)((i64)U(ll.bid) + U(ll.ask)) / 2;
+      dir = mt > ml ? 1 : -1;
+    }
+    o[7] = (double)dir;
+    o[8] = (double)(2 * dir) * ((double)pt - mt) / mt;
+    {  // every lane stores the same (uniform) value
+      for (int i = 0; i < 9; i++) R->obs[i] = o[i];
+      R->has_obs = 1;
+    }
+  }
+  // DummyRL.process_action + place_orders (dummy_rl:138-179), called by the step kernel
+  DEV void rl_place_orders(const double* act) {
+    RpHdr* R = rh();
+    rec_load(PC.first_rl);
+    const double q0 = (double)PC.rl_quantity, q = q0;  // metrics.rem_quantity is never updated
+    const double x = act[0], sum = 0.0 + act[1] + act[2];
+    double oh0 = 0.5, oh1 = 0.5;
+    if (sum != 0.0) {
+      oh0 = act[1] / sum;
+      oh1 = act[2] / sum;
+    }
+    const double qh = q / q0;
+    const double total = __builtin_rint(q0 * qh * gm_pow(x, gm_pow(qh, 0.5)));
+    const double o0 = __builtin_rint(total * oh0);
+    const double o1 = total - (0.0 + o0);
+    const i32 cnt = U(R->m_cnt), hd = U(R->m_head), nb = U(R->m_nb), na = U(R->m_na);
+    for (int l = 0; l < 2; l++) {
+      if (cnt == 0 || nb == 0 || na == 0 || l >= nb || l >= na) continue;  // raises: skipped
+      i32 price = l == 0 ? U(ring()[hd].bid) : U(R->m_b2);                  // BUY at bid level l+1
+      place_limit((i64)(l == 0 ? o0 : o1), 1, price);
+    }
+    rec_store();
+  }
+  // GymKernel CANCEL_ORDER branch (GymKernel.py:244-249): get_reward (None), cancelAllOrders
+  DEV void rl_kernel_cancel() {
+    RpHdr* R = rh();
+    if (U(R->m_cnt) == 0 || U(R->ph_none)) {
+      fail(ERR_RP_OBS);
+      return;
+    }
+    rec_load(PC.first_rl);
+    cancel_all();
+    rec_store();
+  }
+  // GymKernel.terminateRunner -> ExecutionAgent.kernelStopping (execution_agent.py:45-58)
+  DEV void rp_terminate() {
+    RpHdr* R = rh();
+    if (U(R->finished)) return;
+    R->finished = 1;
+    if (U(R->rl_trade)) fail(ERR_RP_STOPPING);
+  }
+
   // agent classes absent from the configuration are compiled out
   DEV void dispatch(int type, bool wake, const Msg& m) {
     if (wake) {
@@ -1481,6 +2108,10 @@ struct Eng {
         if (type == AG_POVMM) return mm_wakeup();
       if constexpr (PC.n_mom > 0)
         if (type == AG_MOMENTUM) return mom_wakeup();
+      if constexpr (RP) {
+        if (type == AG_REPLAY) return mr_wakeup();
+        if (type == AG_DUMMYRL) return rl_wakeup();
+      }
       // ExchangeAgent: Agent.wakeup does nothing
     } else {
       if (type == AG_EXCHANGE) return ex_receive(m);
@@ -1494,6 +2125,10 @@ struct Eng {
         if (type == AG_POVMM) return mm_receive(m);
       if constexpr (PC.n_mom > 0)
         if (type == AG_MOMENTUM) return mom_receive(m);
+      if constexpr (RP) {
+        if (type == AG_REPLAY) return mr_receive(m);
+        if (type == AG_DUMMYRL) return rl_receive(m);
+      }
     }
   }
 
@@ -1538,7 +2173,7 @@ struct Eng {
       qk[slot] = e.key;
       qs[slot] = e.seq;
       if (PL_LDS)
-        for (int i = 0; i < 6; i++) qpl[slot * 6 + i] = e.pl[i];
+        for (int i = 0; i < PW; i++) qpl[slot * PW + i] = e.pl[i];
       if (e.key == KEY_EMPTY) qfree |= 1ull << j;
     }
     q_rescan();
@@ -1561,7 +2196,7 @@ struct Eng {
       e.key = qk[slot];
       e.seq = qs[slot];
       e.pad = 0;
-      for (int i = 0; i < 6; i++) e.pl[i] = PL_LDS ? qpl[slot * 6 + i] : 0u;
+      for (int i = 0; i < 8; i++) e.pl[i] = (PL_LDS && i < PW) ? qpl[slot * PW + i] : 0u;
       sq[slot] = e;
     }
     SavedOrder* so = (SavedOrder*)(env + PC.L.off_book);
@@ -1582,6 +2217,9 @@ struct Eng {
   // ---------------- Kernel.runner event loop (Kernel.py:190-292)
   DEV void run(i64 max_pops) {
     for (i64 n = 0; n < max_pops && status == ST_RUNNING; n++) {
+      if constexpr (RP) {
+        if (end_step) break;  // GymKernel.stepRunner: `while not end_step and ...`
+      }
 #ifndef MXA_NO_LAUNDER_ENV
       {  // opaque per event: env-derived addresses are recomputed, not pinned in SGPRs by LICM
          // (without this the event loop hoists ~1000 SGPRs of addresses and spills them)
@@ -1610,7 +2248,7 @@ struct Eng {
       int type = (int)(key & 3);
       cur = t;
       i64 rec[10];
-      encode(key, m, rec);
+      encode<PW == 8>(key, m, rec);
       u64 hs = hash;
       for (int i = 0; i < 10; i++) hs = (hs ^ (u64)rec[i]) * FNV_PRIME;
       hash = hs;
@@ -1625,6 +2263,14 @@ struct Eng {
       }
       pops++;
       add_delay = 0;
+      if constexpr (RP) {
+        if (type == MT_CANCEL_ORDER) {  // GymKernel CANCEL_ORDER: no busy check, no delay
+          q_remove(slot);
+          rl_kernel_cancel();
+          if (dirty) rng_maint();
+          continue;
+        }
+      }
       rec_load(rcp);
       i64 at = rg64(AF_ATIME);
       PROF_ADD(0, t0);
@@ -1657,7 +2303,7 @@ template <int CFG>
 struct Builder : Eng<CFG, true> {
   typedef Eng<CFG, true> E;
   typedef typename E::RS RS;
-  DEV Builder(char* e, char* lds) : E(e, lds, 0) {}
+  DEV Builder(char* e, char* lds, const RpCtx* ctx = nullptr) : E(e, lds, 0, ctx) {}
 
   DEV u32 g_seed(RS& G) { return (u32)rs_randint(G, 0, 4294967296LL); }
   DEV void set_seed(int stream, u32 s) {
@@ -1701,6 +2347,64 @@ struct Builder : Eng<CFG, true> {
     wfence();
   }
 
+  // ABIDESEnv.reset (ABIDESEnv.py:51-103): agents, empty ladder book, kernelStarting wakeups.
+  // No RNG stream is ever drawn in this composition.
+  DEV void build_replay() {
+    const MxaParams& P = E::PC;
+    const RpLayout& L = this->rx->L;
+    const i32 Pn = U(L.P), C = U(L.C), D = U(L.D);
+    for (int s = 0; s < 2; s++) {
+      i32 *c = this->lv_cnt(s), *hd = this->lv_head(s), *tl = this->lv_tail(s);
+      i64* q = this->lv_qty(s);
+      for (i32 i = this->lane; i < Pn; i += 64) {
+        c[i] = 0;
+        hd[i] = -1;
+        tl[i] = -1;
+        q[i] = 0;
+      }
+    }
+    i32* fr = this->freel();
+    for (i32 i = this->lane; i < C; i += 64) fr[i] = C - 1 - i;
+    i32 *ih = this->idh(), *ie = this->idep();
+    RpOrder* mo = this->mro();
+    for (i32 i = this->lane; i < D; i += 64) {
+      ih[i] = -1;
+      ie[2 * i] = INT32_MIN;
+      ie[2 * i + 1] = INT32_MIN;
+      RpOrder z;
+      z.qty = z.price = z.is_buy = z.present = 0;
+      mo[i] = z;
+    }
+    RpLob* rg = this->ring();
+    for (int i = this->lane; i < 100; i += 64) {
+      RpLob z;
+      z.bid = z.ask = z.data = z.flags = 0;
+      rg[i] = z;
+    }
+    u32* rw = (u32*)this->rh();
+    for (int i = this->lane; i < (int)(sizeof(RpHdr) / 4); i += 64) rw[i] = 0;
+    __threadfence_block();
+    RpHdr* R = this->rh();
+    R->best[0] = R->best[1] = -1;
+    R->free_top = C;
+    R->rl_trade = 1;
+    R->rl_rem = P.rl_quantity;
+    R->ex_has_last = 0;  // no oracle: getDailyOpenPrice raises, last_trade stays None
+    rec_init(0, AG_EXCHANGE);
+    this->rs64(AF_COMP, P.default_comp_delay);
+    this->rec_store();
+    rec_init(P.first_replay, AG_REPLAY);
+    this->rec_store();
+    rec_init(P.first_rl, AG_DUMMYRL);
+    this->rec_store();
+    this->h.last_trade = 0;
+    this->h.last_trade_float = 0;
+    this->cur = P.start;
+    for (int a = 0; a < P.n_agents; a++) this->wakeup_at(a, P.start);
+    this->save();
+    __threadfence_block();
+  }
+
   DEV void build(u32 seed) {
     const MxaParams& P = E::PC;
     LDSP EnvHdr& h = this->h;
@@ -1730,6 +2434,10 @@ struct Builder : Eng<CFG, true> {
       this->qs[j * 64 + this->lane] = 0xFFFFFFFFu;
     }
     for (int j = 0; j < E::SO; j++) this->bm[j] = -1;
+    if constexpr (E::RP) {
+      build_replay();
+      return;
+    }
     mt_seed(this->rng_key(0), seed);
     RS G = this->grs(0);
     int n = P.n_agents;
@@ -1892,23 +2600,25 @@ struct Builder : Eng<CFG, true> {
 // kernels (one wavefront per env; grid = n_envs)
 // ------------------------------------------------------------------------------------
 template <int CFG>
-__global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stride, int n_envs, const uint32_t* seeds, const uint8_t* mask) {
+__global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stride, int n_envs, const uint32_t* seeds, const uint8_t* mask,
+                                                       const RpCtx* ctx) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int env = blockIdx.x;
   if (env >= n_envs) return;
   if (mask && !mask[env]) return;
-  mxa::Builder<CFG> b(base + (size_t)env * stride, lds);
+  mxa::Builder<CFG> b(base + (size_t)env * stride, lds, ctx);
   b.build(seeds[env]);
 }
 
 template <int CFG>
-__global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops) {
+__global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops,
+                                                                              const RpCtx* ctx) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int env = blockIdx.x;
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
   if (((EnvHdr*)e)->status != ST_RUNNING) return;
-  mxa::Eng<CFG> g(e, lds, trace_cap);
+  mxa::Eng<CFG> g(e, lds, trace_cap, ctx);
   g.load();
   g.run(max_pops);
   g.save();
@@ -1916,6 +2626,45 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
   if (g.lane < 32) atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
 #endif
 }
+
+#ifndef MXA_ONLY_RMSC03
+// ABIDESEnv.step for every env: DummyRL.place_orders(action), then the GymKernel loop until
+// the RL agent's spread reply (end of step) or the end of the episode.  obs [n][9] float64;
+// flags [n]: bit0 done, bit1 observation valid, bit2 env error.
+__global__ __launch_bounds__(64, mxa_cfg::shape(MXA_CFG_MARKETREPLAY).waves) void mxa_step_kernel(
+    char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops, const RpCtx* ctx, const double* actions,
+    double* obs, int32_t* flags) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int env = blockIdx.x;
+  if (env >= n_envs) return;
+  char* e = base + (size_t)env * stride;
+  mxa::Eng<MXA_CFG_MARKETREPLAY> g(e, lds, trace_cap, ctx);
+  g.load();
+  if (g.status == ST_RUNNING) {
+    double a[3];
+    for (int i = 0; i < 3; i++) a[i] = actions[3 * (size_t)env + i];
+    g.rl_place_orders(a);
+    g.end_step = 0;
+    g.run(max_pops);
+    if (g.status == ST_RUNNING) {  // after the loop: terminateRunner if the queue ran dry / past stop
+      u64 key;
+      u32 s;
+      if (g.q_peek(key, s) < 0 || g.cur > mxa::Eng<MXA_CFG_MARKETREPLAY>::PC.stop) g.status = ST_DONE;
+    }
+    if (g.status == ST_DONE) g.rp_terminate();
+  }
+  g.save();
+  RpHdr* R = g.rh();
+  if (g.lane < 9) obs[9 * (size_t)env + g.lane] = R->obs[g.lane];
+  u64 key;
+  u32 sq;
+  const bool pending = g.q_peek(key, sq) >= 0;  // all lanes: DPP reduction
+  // ABIDESEnv.step: done = not (queue non-empty and currentTime <= stopTime)
+  const int done = !(pending && g.cur <= mxa::Eng<MXA_CFG_MARKETREPLAY>::PC.stop) || g.status != ST_RUNNING;
+  const int hobs = mxa::U(R->has_obs);
+  if (g.lane == 0) flags[env] = done | (hobs ? 2 : 0) | (g.status == ST_ERROR ? 4 : 0);
+}
+#endif
 
 // parity helpers: numpy-legacy RNG draws and glibc math on the device (tests only call
 // these through the C-ABI; they exercise exactly the device functions the engine uses)
@@ -1949,10 +2698,11 @@ __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y
 
 // explicit instantiations per supported configuration
 #define MXA_INST(CFG)                                                                                      \
-  template __global__ void mxa_build_kernel<CFG>(char*, uint64_t, int, const uint32_t*, const uint8_t*); \
-  template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t);
+  template __global__ void mxa_build_kernel<CFG>(char*, uint64_t, int, const uint32_t*, const uint8_t*, const RpCtx*); \
+  template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*);
 MXA_INST(MXA_CFG_RMSC03)
 #ifndef MXA_ONLY_RMSC03
 MXA_INST(MXA_CFG_SPARSE_ZI_100)
 MXA_INST(MXA_CFG_SPARSE_ZI_1000)
+MXA_INST(MXA_CFG_MARKETREPLAY)
 #endif

@@ -15,7 +15,7 @@
 #define MXA_MT_M 397
 #define MXA_RNG_WORDS 1280    // two 624-word MT blocks (double buffer) + pad (5120 B per stream)
 
-enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2 };
+enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -28,14 +28,22 @@ enum {
 enum { MT_MESSAGE = 1, MT_WAKEUP = 2, MT_CANCEL_ORDER = 3 };
 
 // agent classes
-enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_MOMENTUM = 5 };
+enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_MOMENTUM = 5, AG_REPLAY = 6, AG_DUMMYRL = 7 };
 
 // env status flags (EnvHdr::status)
 enum { ST_RUNNING = 0, ST_DONE = 1, ST_ERROR = 2 };
 enum {
   ERR_NONE = 0, ERR_QUEUE_FULL = 1, ERR_BOOK_FULL = 2, ERR_OPEN_FULL = 3, ERR_TX_FULL = 4,
   ERR_PANDAS_NO_TX = 5, ERR_WAKEUP_PAST = 6, ERR_THETA_INDEX = 7, ERR_BAD_CONFIG = 8,
-  ERR_RNG_OVERRUN = 9
+  ERR_RNG_OVERRUN = 9,
+  // marketreplay / ABIDESEnv: reference crash paths and capacity limits
+  ERR_RP_PRICE = 10,      // tape/agent price outside the ladder
+  ERR_RP_POOL = 11,       // book entry pool exhausted
+  ERR_RP_IDS = 12,        // agent order ids beyond the dense-id capacity
+  ERR_RP_KEYERROR = 13,   // MarketReplayAgent: no tape group at the wake time
+  ERR_RP_OBS = 14,        // get_observation / get_reward on missing or None data
+  ERR_RP_STOPPING = 15,   // ExecutionAgent.kernelStopping with trade still on (arrival_price None)
+  ERR_RP_MODIFY = 16      // modify changing price or side (head-replace would re-key the level)
 };
 
 // per-env scalar header (first bytes of the env block)
@@ -71,8 +79,8 @@ typedef struct {
   uint64_t key;   // t << 13 | recipient << 2 | type
   uint32_t seq;
   uint32_t pad;
-  uint32_t pl[6]; // payload
-} SavedEvent;   // 32 B
+  uint32_t pl[8]; // payload (6 words used except by the marketreplay config)
+} SavedEvent;   // 48 B
 
 // book slot as saved between launches
 typedef struct {
@@ -90,6 +98,53 @@ typedef struct {  // transaction record of OrderBook.history (util/OrderBook.py:
 typedef struct {  // TradingAgent.orders entry (agent's copy of an open order)
   int32_t oid, is_buy, qty, price;
 } OpenOrder;
+
+// ---- marketreplay / ABIDESEnv (runtime-sized sections after the fixed layout) ----
+typedef struct {  // one resting order of the price-ladder book (OrderBook level entries)
+  int32_t price, qty, oid, dense;  // dense = order-id index (tape ids, then agent ids)
+  int32_t meta;                    // agent << 1 | is_buy
+  uint32_t arrival;                // FIFO position stamp
+  int32_t prev, next;              // level list
+  int32_t idprev, idnext;          // live entries of the same order id
+  int32_t pad[2];
+} RpEntry;        // 48 B
+typedef struct {  // MarketReplayAgent.orders (agent copy) per dense id
+  int32_t qty, price, is_buy, present;
+} RpOrder;
+typedef struct {  // ABIDESEnvMetrics deque entry (level-1 book + last trade of one LOB)
+  int32_t bid, ask, data, flags;   // flags: 1 has bids, 2 has asks, 4 data is None
+} RpLob;
+typedef struct {  // per-env replay / gym state
+  int32_t best[2];      // best level index per side (bids max, asks min), -1 = empty
+  int32_t nlev[2];      // non-empty levels per side
+  int32_t free_top, mr_wi, ex_has_last, rl_trade;
+  int64_t rl_exec, rl_rem;
+  int32_t m_cnt, m_head, m_nb, m_na;
+  int64_t m_bq, m_aq;
+  int32_t m_b2, m_a2, p0, p0_none;
+  int32_t ph_n, ph_none, end_step, has_obs;
+  double obs[9];
+  int32_t finished, pad[5];
+} RpHdr;          // 208 B
+typedef struct {  // runtime layout of the replay sections (offsets from the env block)
+  int32_t pmin, P;      // price ladder [pmin, pmin + P)
+  int32_t C, D;         // entry capacity, dense-id capacity
+  int32_t n_ids;        // dense ids used by the tape (agent ids start here)
+  int32_t ntm, nrec, pad;
+  uint64_t off_rh, off_lvc, off_lvh, off_lvt, off_lvq, off_pool, off_free, off_idh, off_idep, off_mro, off_ring,
+      end;
+} RpLayout;
+typedef struct {  // device-resident tape (shared by all envs of a handle)
+  const int64_t* t;     // [nrec] ns since midnight, time-sorted
+  const int32_t* oid;   // [nrec]
+  const int32_t* dense; // [nrec]
+  const int32_t* price; // [nrec] cents
+  const int32_t* size;  // [nrec]
+  const int8_t* buy;    // [nrec]
+  const int64_t* tm;    // [ntm] distinct times
+  const int32_t* tm0;   // [ntm + 1] first record of each time group
+  RpLayout L;
+} RpCtx;
 
 typedef struct {
   uint64_t env_stride;
@@ -148,6 +203,10 @@ typedef struct {
   int32_t mom_min, mom_max;
   int64_t mom_wake;
   double lat_lo, lat_hi;   // G.uniform bounds of the latency matrix
+  // marketreplay / ABIDESEnv composition (agent_config.py:30-160)
+  int32_t first_replay, n_replay, first_rl, n_rl;
+  int64_t rl_quantity, rl_h0, rl_hstep;   // DummyRL: BUY 1e5 over date_range(h0, ..., hstep)
+  int32_t rl_nh, rl_depth, rl_ids, pad3;  // horizon length, spread depth, agent-id capacity
   Layout L;
 } MxaParams;
 

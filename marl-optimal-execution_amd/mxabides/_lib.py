@@ -9,12 +9,16 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MXA_LIB") or os.path.join(PKG_ROOT, "lib", "libmxa.so")
 
-MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000 = 0, 1, 2
+MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000, MXA_MARKETREPLAY = 0, 1, 2, 3
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000}
 ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
 ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",
              4: "transaction history capacity", 5: "get_transacted_volume without transactions (pandas error)",
-             6: "setWakeup in the past", 7: "ZI theta index (IndexError)", 8: "bad config"}
+             6: "setWakeup in the past", 7: "ZI theta index (IndexError)", 8: "bad config",
+             9: "RNG look-ahead overrun", 10: "price outside the replay ladder", 11: "book entry pool capacity",
+             12: "agent order-id capacity", 13: "MarketReplayAgent KeyError (no tape group at wake time)",
+             14: "get_observation/get_reward on missing or None data", 15: "kernelStopping with trade on (TypeError)",
+             16: "modify changing price or side"}
 
 
 class EnvSummary(ctypes.Structure):
@@ -31,7 +35,8 @@ class AgentState(ctypes.Structure):
 EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_read_summary", "mxa_read_agents",
            "mxa_read_book", "mxa_read_trace", "mxa_n_agents", "mxa_n_envs", "mxa_env_bytes", "mxa_set_stream",
            "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe",
-           "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout"]
+           "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout", "mxa_create_replay", "mxa_step",
+           "mxa_step_device"]
 
 _lib = None
 
@@ -74,5 +79,8 @@ def load():
     L.mxa_write_results.argtypes = [P, P]
     L.mxa_rng_probe.argtypes = [I32, U32, I32, D, D, I32, P]
     L.mxa_math_probe.argtypes = [I32, I32, P, P, P, I64]
+    L.mxa_create_replay.argtypes = [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)]
+    L.mxa_step.argtypes = [P, P, P, P]
+    L.mxa_step_device.argtypes = [P, P, P, P]
     _lib = L
     return L

@@ -1,0 +1,139 @@
+"""ABIDESEnv on MI355X: the Gym surface of the reference (ABIDESEnv.py:7-57) over libmxa.
+
+`VecABIDESEnv` steps n independent copies of the reference's ABIDESEnv composition
+(ExchangeAgent + MarketReplayAgent on a LOBSTER tape + DummyRLExecutionAgent, with the
+GymKernel step loop) in one kernel launch per step; envs differ by the actions they are fed.
+`ABIDESEnv` is the single-env drop-in with the reference's signature and return values:
+reset() -> None, step(action) -> (obs float64[9] or [] , reward None, done 0|1, info None).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from .tape import Tape, load_lobster
+
+OBS_SIZE = 9      # get_observation returns 9 values (the declared space says 10: dummy_rl:317-322)
+ACTION_SIZE = 3   # order_level 2 -> [total volume, level-1 share, level-2 share]
+
+
+class VecABIDESEnv:
+    def __init__(self, tape, n_envs, device=0, trace_cap=0):
+        if not isinstance(tape, Tape):
+            raise TypeError("tape must be an mxabides.tape.Tape")
+        self.L = _lib.load()
+        self.tape = tape
+        self.n_envs = int(n_envs)
+        self.trace_cap = trace_cap
+        self._h = ctypes.c_void_p()
+        rc = self.L.mxa_create_replay(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
+                                      tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), self.n_envs, device,
+                                      trace_cap, ctypes.byref(self._h))
+        self._check(rc, "mxa_create_replay")
+        self.obs = np.zeros((self.n_envs, OBS_SIZE), dtype=np.float64)
+        self.flags = np.zeros(self.n_envs, dtype=np.int32)
+
+    def _check(self, rc, what):
+        if rc < 0:
+            msg = self.L.mxa_last_error(self._h).decode() if self._h else ""
+            raise _lib.MxaError("%s failed (%d): %s" % (what, rc, msg))
+        return rc
+
+    def reset(self):
+        self._check(self.L.mxa_reset(self._h, None), "mxa_reset")
+        self.obs[:] = 0
+        self.flags[:] = 0
+
+    def step(self, actions):
+        """actions [n][3] -> (obs [n][9], done [n] bool, valid [n] bool, error [n] bool)"""
+        a = np.ascontiguousarray(np.asarray(actions, dtype=np.float64).reshape(self.n_envs, ACTION_SIZE))
+        self._check(self.L.mxa_step(self._h, a.ctypes.data, self.obs.ctypes.data, self.flags.ctypes.data), "mxa_step")
+        f = self.flags
+        return self.obs.copy(), (f & 1) != 0, (f & 2) != 0, (f & 4) != 0
+
+    def step_device(self, d_actions, d_obs, d_flags):
+        """Asynchronous step on device buffers (e.g. torch tensors' data_ptr())."""
+        self._check(self.L.mxa_step_device(self._h, ctypes.c_void_p(d_actions), ctypes.c_void_p(d_obs),
+                                           ctypes.c_void_p(d_flags)), "mxa_step_device")
+
+    def summary(self):
+        n = self.n_envs
+        buf = (_lib.EnvSummary * n)()
+        self._check(self.L.mxa_read_summary(self._h, buf), "mxa_read_summary")
+        return {"events": np.array([b.events for b in buf], dtype=np.int64),
+                "hash": np.array([b.hash for b in buf], dtype=np.uint64),
+                "status": np.array([b.status for b in buf], dtype=np.int32),
+                "err": np.array([b.err for b in buf], dtype=np.int32),
+                "current_time": np.array([b.current_time for b in buf], dtype=np.int64),
+                "order_counter": np.array([b.order_counter for b in buf], dtype=np.int64)}
+
+    def agents(self, env):
+        buf = (_lib.AgentState * 3)()
+        self._check(self.L.mxa_read_agents(self._h, env, buf, 3), "mxa_read_agents")
+        return [(b.cash, b.shares, b.n_open) for b in buf]
+
+    def book(self, env, side):
+        """levels best-first, FIFO within level: [[order_id, agent_id, qty, price], ...] per level"""
+        n = self._check(self.L.mxa_read_book(self._h, env, side, None, 0), "mxa_read_book")
+        buf = np.zeros((max(n, 1), 4), dtype=np.int64)
+        self._check(self.L.mxa_read_book(self._h, env, side, buf.ctypes.data, n), "mxa_read_book")
+        levels = []
+        for o in buf[:n].tolist():
+            if levels and levels[-1][0][3] == o[3]:
+                levels[-1].append(o)
+            else:
+                levels.append([o])
+        return levels
+
+    def trace(self, env):
+        out = np.zeros((self.trace_cap, 10), dtype=np.int64)
+        n = ctypes.c_int64()
+        self._check(self.L.mxa_read_trace(self._h, env, out.ctypes.data, self.trace_cap, ctypes.byref(n)),
+                    "mxa_read_trace")
+        return out[:n.value]
+
+    @property
+    def last_kernel_ms(self):
+        return self.L.mxa_last_kernel_ms(self._h)
+
+    def close(self):
+        if self._h:
+            self.L.mxa_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ABIDESEnv:
+    """Drop-in for the reference ABIDESEnv(ticker, date, log_dir=None, seed=None) on a LOBSTER
+    message file `data/lobster/LOBSTER_SampleFile_{ticker}_1/{ticker}_{date}_34200000_57600000_message_1.csv`
+    under `data_root` (agent_config.py:57-60), or on an explicit Tape."""
+
+    def __init__(self, ticker, date, log_dir=None, seed=None, data_root=".", tape=None, device=0):
+        if tape is None:
+            f = "%s_%s_34200000_57600000_message_1.csv" % (ticker, date)
+            tape = load_lobster(os.path.join(data_root, "data", "lobster", "LOBSTER_SampleFile_%s_1" % ticker, f), date)
+        self.ticker, self.date, self.log_dir = ticker, date, log_dir
+        self.seed = np.random.randint(low=0, high=2 ** 31 - 1) if seed is None else seed  # agents draw nothing
+        self._v = VecABIDESEnv(tape, 1, device=device)
+        self.action_space = (np.zeros(ACTION_SIZE), np.ones(ACTION_SIZE))
+        self.observation_space = (np.zeros(10), np.zeros(10))  # as declared by the reference
+        self._obs = []
+
+    def reset(self):
+        self._v.reset()
+        self._obs = []
+
+    def step(self, action):
+        obs, done, valid, err = self._v.step(np.asarray(action, dtype=np.float64).reshape(1, ACTION_SIZE))
+        if err[0]:
+            s = self._v.summary()
+            raise _lib.MxaError("env error: %s" % _lib.ERR_NAMES.get(int(s["err"][0]), s["err"][0]))
+        if valid[0]:
+            self._obs = obs[0]
+        return self._obs, None, int(done[0]), None

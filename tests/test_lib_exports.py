@@ -22,7 +22,20 @@ def test_every_declared_symbol_is_exported():
     assert set(names) == set(mxabides._lib.EXPORTS)
 
 
-def test_layout_header_is_self_consistent():
-    # the 24-byte payload and the saved-slot structs are part of the env block contract
-    h = open(os.path.join(ROOT, "marl-optimal-execution_amd", "csrc", "mxa_layout.h")).read()
-    assert "SavedEvent;   // 32 B" in h and "SavedOrder;   // 32 B" in h
+def test_layout_header_is_self_consistent(tmp_path):
+    """the env-block structs shared by host and kernels have the sizes the layout assumes"""
+    import subprocess
+    src = tmp_path / "sz.cpp"
+    src.write_text("""#include "mxa_config.h"
+static_assert(sizeof(EnvHdr) == 288, "EnvHdr");
+static_assert(sizeof(SavedEvent) == 48, "SavedEvent");
+static_assert(sizeof(SavedOrder) == 32, "SavedOrder");
+static_assert(sizeof(RpEntry) == 48, "RpEntry");
+static_assert(sizeof(RpHdr) == 208, "RpHdr");
+static_assert(sizeof(RpOrder) == 16 && sizeof(RpLob) == 16, "replay tables");
+static_assert(mxa_cfg::params(MXA_CFG_RMSC03).n_agents == 64, "rmsc03");
+static_assert(mxa_cfg::params(MXA_CFG_MARKETREPLAY).n_agents == 3, "replay");
+int main() { return 0; }
+""")
+    inc = os.path.join(ROOT, "marl-optimal-execution_amd", "csrc")
+    subprocess.check_call(["g++", "-std=c++20", "-fsyntax-only", "-I", inc, str(src)])
