@@ -32,6 +32,82 @@ ALGO_BYTES_PER_EVENT = 256  # nominal algorithmic HBM bytes pe
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
+def replay_bench(args):
+    """ABIDESEnv / market replay (BASELINE configs[4] shape): n envs stepping the reference's
+    composition on the IBM 2003-01-14 LOBSTER tape with per-env random actions; one bench
+    step = one full episode (761 ABIDESEnv.step calls per env)."""
+    from mxabides import tape
+    from mxabides.gym import VecABIDESEnv
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    tp = tape.Tape.load(os.path.join(ROOT, "tests", "golden", "tape_IBM_2003-01-14.npz"))
+    n = args.envs
+    v = VecABIDESEnv(tp, n, device=local)
+    rs = np.random.RandomState(1000 + rank)
+
+    def episode():
+        v.reset()
+        steps, kms = 0, 0.0
+        while True:
+            a = np.stack([rs.uniform(0, 0.01, n), rs.uniform(0, 1, n), rs.uniform(0, 1, n)], 1)
+            obs, done, valid, err = v.step(a)
+            kms += v.last_kernel_ms
+            steps += 1
+            if done.all() or err.any():
+                break
+        s = v.summary()
+        return int(s["events"].sum()), steps, int((s["status"] == 2).sum()), kms
+
+    for _ in range(args.warmup):
+        episode()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ev = st = nerr = 0
+    kms = 0.0
+    for _ in range(args.steps):
+        e, s_, er, k = episode()
+        ev, st, nerr, kms = ev + e, st + s_, nerr + er, kms + k
+    el = time.perf_counter() - t0
+    tot = torch.tensor([ev, st * n], dtype=torch.float64, device="cuda")
+    elt = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot)
+        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+        el = float(elt.item())
+    if rank == 0:
+        out = {"metric": "env-steps/sec, ABIDESEnv market replay (IBM 2003-01-14 LOBSTER tape) x%d envs per GPU" % n,
+               "value": float(tot[0]) / el, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "LOBSTER sample tape + random actions",
+               "config": {"workload": "marketreplay x%d envs per GPU, full episode (761 ABIDESEnv.step) per bench step" % n,
+                          "gym_steps_per_s": float(tot[1]) / el, "env_errors": nerr,
+                          "kernel_ms_per_episode": kms / args.steps}}
+        if not args.no_cpu:
+            import pyoracle
+            k = 8
+            t1 = time.perf_counter()
+            cev = 0
+            for i in range(k):
+                e = pyoracle.OracleGymEnv(tp)
+                r2 = np.random.RandomState(i)
+                while True:
+                    _, d_, rc = e.step([r2.uniform(0, 0.01), r2.uniform(), r2.uniform()])
+                    if d_ or rc:
+                        break
+                cev += e.events
+            cs = time.perf_counter() - t1
+            out["cpu_baseline"] = {"value": cev / cs, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                                   "sample": "%d episodes, C oracle, 1 thread, %.1f s" % (k, cs)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -43,6 +119,8 @@ def main():
     ap.add_argument("--cpu-envs", type=int, default=2048, help="CPU-baseline sample size (envs)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    if args.config == "marketreplay":
+        return replay_bench(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
