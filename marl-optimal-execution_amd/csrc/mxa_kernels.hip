@@ -1078,14 +1078,17 @@ struct Eng {
         return;
       }
       OpenOrder* oo = open_ptr(cur_agent);
+      i32 u = rgi(AF_NUSED);
+      if (u >= PC.L.open_cap) u = open_compact();
       if (lane == 0) {
         OpenOrder o;
         o.oid = (i32)oid;
         o.is_buy = is_buy;
         o.qty = (i32)qty;
         o.price = (i32)price;
-        oo[n] = o;
+        oo[u] = o;
       }
+      rs(AF_NUSED, (u32)(u + 1));
       rs(AF_NORD, (u32)(n + 1));
       Msg lm = msg_order(MK_LIMIT, (i32)oid, cur_agent, is_buy, (i32)qty, (i32)price, 0);
       if constexpr (RP) lm.w[5] = (u32)agent_dense(oid);
@@ -1093,16 +1096,24 @@ struct Eng {
     }
   }
   // cancelOrder for every open order in dict (= ascending order id) order
+  // TradingAgent.orders (dict, insertion order) as an append-only list in HBM: deletions leave
+  // a tombstone (oid -1), the list is compacted when its slots run out
+  static constexpr int OC = (PC.L.open_cap + 63) / 64;
+  // cancelOrder for every open order in dict (= list) order
   DEV void cancel_all() {
-    i32 n = rgi(AF_NORD);
+    const i32 u = rgi(AF_NUSED);
     OpenOrder* oo = open_ptr(cur_agent);
-    for (int b = 0; b < n; b += 64) {
-      OpenOrder my;
-      int k = b + lane;
-      if (k < n) my = oo[k];
-      int cnt = n - b < 64 ? n - b : 64;
-      for (int i = 0; i < cnt; i++) {
-        i32 oid = rdli(my.oid, i), ib = rdli(my.is_buy, i), q = rdli(my.qty, i), p = rdli(my.price, i);
+    OpenOrder my[OC];
+    for (int j = 0; j < OC; j++) {
+      my[j].oid = -1;
+      if (j * 64 + lane < u) my[j] = oo[j * 64 + lane];
+    }
+    for (int j = 0; j < OC; j++) {
+      u64 b = bal(my[j].oid != -1);
+      while (b) {
+        int L = ffs64(b);
+        b &= b - 1;
+        i32 oid = rdli(my[j].oid, L), ib = rdli(my[j].is_buy, L), q = rdli(my[j].qty, L), p = rdli(my[j].price, L);
         Msg cm = msg_order(MK_CANCEL, oid, cur_agent, ib, q, p, 0);
         if constexpr (RP) cm.w[5] = (u32)agent_dense(oid);
         send_ex(cm);
@@ -1110,35 +1121,53 @@ struct Eng {
     }
   }
   DEV int find_open(i32 oid, OpenOrder& out) {
-    i32 n = rgi(AF_NORD);
+    const i32 u = rgi(AF_NUSED);
     OpenOrder* oo = open_ptr(cur_agent);
-    for (int b = 0; b < n; b += 64) {
-      int k = b + lane;
-      OpenOrder my;
-      my.oid = -1;
-      if (k < n) my = oo[k];
-      u64 hit = bal(k < n && my.oid == oid);
+    OpenOrder my[OC];
+    for (int j = 0; j < OC; j++) {  // all chunks in flight at once
+      my[j].oid = -1;
+      if (j * 64 + lane < u) my[j] = oo[j * 64 + lane];
+    }
+    for (int j = 0; j < OC; j++) {
+      u64 hit = bal(my[j].oid == oid);
       if (hit) {
         int L = ffs64(hit);
         out.oid = oid;
-        out.is_buy = rdli(my.is_buy, L);
-        out.qty = rdli(my.qty, L);
-        out.price = rdli(my.price, L);
-        return b + L;
+        out.is_buy = rdli(my[j].is_buy, L);
+        out.qty = rdli(my[j].qty, L);
+        out.price = rdli(my[j].price, L);
+        return j * 64 + L;
       }
     }
     return -1;
   }
   DEV void del_open(int idx) {
-    i32 n = rgi(AF_NORD);
     OpenOrder* oo = open_ptr(cur_agent);
-    for (int b = idx; b < n - 1; b += 64) {
-      int k = b + lane;
-      OpenOrder nx;
-      if (k < n - 1) nx = oo[k + 1];
-      if (k < n - 1) oo[k] = nx;
+    if (lane == 0) oo[idx].oid = -1;
+    i32 n = rgi(AF_NORD) - 1;
+    rs(AF_NORD, (u32)n);
+    if (n == 0) rs(AF_NUSED, 0u);
+  }
+  DEV i32 open_compact() {  // keep live entries in order; returns the new used count
+    OpenOrder* oo = open_ptr(cur_agent);
+    const i32 u = rgi(AF_NUSED);
+    OpenOrder my[OC];
+    for (int j = 0; j < OC; j++) {
+      my[j].oid = -1;
+      if (j * 64 + lane < u) my[j] = oo[j * 64 + lane];
     }
-    rs(AF_NORD, (u32)(n - 1));
+    __threadfence_block();
+    i32 base = 0;
+    for (int j = 0; j < OC; j++) {
+      bool live = my[j].oid != -1;
+      u64 b = bal(live);
+      i32 r = base + (i32)__builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
+      if (live) oo[r] = my[j];
+      base += __popcll(b);
+    }
+    __threadfence_block();
+    rs(AF_NUSED, (u32)base);
+    return base;
   }
 
   // TradingAgent.wakeup (TradingAgent.py:142-158)

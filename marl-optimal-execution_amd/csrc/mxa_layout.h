@@ -163,6 +163,7 @@ enum {
   AF_THETA = 46,      // 20 x int32
   AF_MIDS = 66,       // 50 x int32 (2*mid ring), momentum
   AF_RS_M = 116,      // highest materialized MT block of the agent's stream
+  AF_NUSED = 117,     // open-order list slots used (live + tombstones); AF_NORD = live
   AF_ATIME = 120,     // Kernel.agentCurrentTimes[a]
   AF_COMP = 122,      // Kernel.agentComputationDelays[a]
   AF_END = 128
