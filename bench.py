@@ -185,12 +185,13 @@ def main():
                 p = json.load(f)
             if p.get("config") == args.config and p.get("envs") == n:
                 traffic = p.get("bytes_per_launch")
+        metric = METRIC if args.config == "rmsc03" else "env-steps/sec, %s x%d envs per GPU" % (args.config, n)
         out = {
-            "metric": METRIC, "value": events / elapsed, "unit": "env-steps/s", "n_gpus": world,
+            "metric": metric, "value": events / elapsed, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
             "config": {"workload": "%s x%d envs per GPU, full episode per step (config build from seeds + "
-                                   "09:30-09:45 session + 1 min tail), seeds %d+global_env" % (args.config, n, SEED0),
+                                   "the config's session), seeds %d+global_env" % (args.config, n, SEED0),
                        "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": m.n_agents,
                        "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
                        "env_errors": n_err, "device": torch.cuda.get_device_name(local),

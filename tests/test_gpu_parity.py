@@ -109,6 +109,30 @@ def test_gpu_batch_equals_oracle(mx, cfg, n):
     assert (s["hash"] == hs).all()
 
 
+def test_gpu_bench_workload_equals_oracle(mx):
+    """the exact bench.py workload (rmsc03 x4096, seeds 123456789 + env) is bit-exact per env"""
+    from mxabides import shard
+    seeds = shard.env_seeds(0, 0, 1, 4096)
+    m = mx.VecMarket("rmsc03", seeds)
+    m.run()
+    s = m.summary()
+    ev, hs, _ = pyoracle.run_batch("rmsc03", seeds, threads=min(16, os.cpu_count() or 1))
+    assert (s["status"] == 1).all()
+    assert (s["events"] == ev).all()
+    assert (s["hash"] == hs).all()
+
+
+@pytest.mark.parametrize("cfg,n", [("sparse_zi_1000", 8)])
+def test_gpu_wide_config_equals_oracle(mx, cfg, n):
+    seeds = (np.arange(n, dtype=np.int64) * 104729 + 3) & 0xFFFFFFFF
+    m = mx.VecMarket(cfg, seeds)
+    m.run()
+    s = m.summary()
+    ev, hs, _ = pyoracle.run_batch(cfg, seeds.astype(np.uint32), threads=8)
+    assert (s["events"] == ev).all()
+    assert (s["hash"] == hs).all()
+
+
 def test_gpu_chunked_launches_equal_single(mx):
     seeds = [3, 5, 123456789, 1008]
     a = mx.VecMarket("rmsc03", seeds)
