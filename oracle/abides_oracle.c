@@ -311,7 +311,7 @@ struct ora_env {
     int mr_nord, mr_capord;
     /* DummyRLExecutionAgent + ABIDESEnvMetrics */
     int64_t rl_quantity, rl_exec_sum, rl_rem;
-    int rl_trade;
+    int rl_trade, rl_id; /* DummyRL agent id (2 in ABIDESEnv, 64 in rmsc03_rl) */
     int64_t* hz;
     int nhz;
     int m_cnt, m_head;               /* deque(maxlen=100), index 0 = most recent */
@@ -1501,7 +1501,7 @@ static void rl_observe(ora_env* e) {
 }
 /* DummyRL.process_action + place_orders (dummy_rl_execution_agent.py:138-179) */
 static void rl_place_orders(ora_env* e, const double* act) {
-    agent_t* a = &e->ag[2];
+    agent_t* a = &e->ag[e->rl_id];
     double q0 = (double)e->rl_quantity, q = q0; /* metrics.rem_quantity is never updated */
     double x = act[0], sum = 0.0 + act[1] + act[2], oh0, oh1;
     if (sum == 0.0) oh0 = oh1 = 0.5;
@@ -1523,7 +1523,7 @@ static void rl_place_orders(ora_env* e, const double* act) {
 }
 /* GymKernel CANCEL_ORDER branch (GymKernel.py:244-249): get_reward, then cancelAllOrders */
 static void rl_kernel_cancel(ora_env* e) {
-    agent_t* a = &e->ag[2];
+    agent_t* a = &e->ag[e->rl_id];
     if (e->m_cnt == 0) { fail(e, -8, "get_reward: no LOB stored (IndexError)"); return; }
     if (e->ph_none) { fail(e, -8, "get_reward: None in price history (TypeError)"); return; }
     cancel_all(e, a);
@@ -1641,7 +1641,7 @@ static void rep_append(ora_env* e, const char* s) {
 /* TradingAgent.kernelStopping (TradingAgent.py:112-138) + Kernel mean print (Kernel.py:337-341) */
 int ora_finish(ora_env* e) {
     char line[512];
-    const char* sym = strcmp(e->config, "rmsc03") == 0 ? "ABM" : "JPM";
+    const char* sym = strncmp(e->config, "rmsc03", 6) == 0 ? "ABM" : "JPM";
     char tnames[16][96];
     long long gains[16];
     int counts[16], nt = 0;
@@ -1882,6 +1882,35 @@ static int build_rmsc03(ora_env* e, uint32_t seed) {
     return 0;
 }
 
+/* rmsc03 + DummyRL (BASELINE.json configs[3]; tests/golden/gen_rl_fixtures.py): config/rmsc03.py's
+ * 64 agents, oracle and kernel RandomState, plus DummyRLExecutionAgent 64 (agent_config.py:115-137
+ * parameters: BUY 1e5, freq 30 s, order_level 2) with execution_time_horizon =
+ * pd.date_range(09:31, 09:44, "30S"), run by a GymKernel with rmsc03's start/stop, latency
+ * zeros(65, 65), noise [0.0] and compute delay 0.  The DummyRL draws nothing. */
+static int build_rmsc03_rl(ora_env* e, uint32_t seed) {
+    int rc = build_rmsc03(e, seed);
+    if (rc) return rc;
+    agent_t* r = add_agent(e, AG_DUMMYRL);
+    trading_init(r, 0);
+    snprintf(r->name, sizeof r->name, "%d_DUMMY_RL_EXECUTION_AGENT", r->id);
+    snprintf(r->tname, sizeof r->tname, "DummyRLExecutionAgent");
+    e->rl_id = r->id;
+    e->nhz = 27;
+    e->hz = (int64_t*)malloc(sizeof(int64_t) * e->nhz);
+    for (int i = 0; i < e->nhz; i++) e->hz[i] = 9 * NS_HOUR + 31 * NS_MIN + (int64_t)i * 30 * NS_SEC;
+    r->wake_freq = e->hz[0] - e->ex_open;
+    e->rl_quantity = 100000;
+    e->rl_rem = 100000;
+    e->rl_trade = 1;
+    e->gym = 1;
+    int n = e->n;
+    e->agent_time = (int64_t*)realloc(e->agent_time, sizeof(int64_t) * n);
+    e->comp_delay = (int64_t*)realloc(e->comp_delay, sizeof(int64_t) * n);
+    e->agent_time[n - 1] = e->start;
+    e->comp_delay[n - 1] = 0;
+    return 0;
+}
+
 /* ABIDESEnv.initAgents / initKernel (ABIDESEnv.py:59-103; agent_config.py:30-160):
  * Exchange (id 0), MarketReplayAgent (1) on a LOBSTER tape, DummyRLExecutionAgent (2);
  * GymKernel start = midnight, stop = 16:10, compute delays 0, latencies 0, noise [1.0].
@@ -1942,6 +1971,7 @@ int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, co
     e->rl_quantity = 100000;
     e->rl_rem = 100000;
     e->rl_trade = 1;
+    e->rl_id = 2;
     e->gym = 1;
     e->start = 0;
     e->stop = 16 * NS_HOUR + 10 * NS_MIN;
@@ -1972,6 +2002,7 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     if (!strcmp(config, "sparse_zi_100")) rc = build_sparse_zi(e, seed, 0);
     else if (!strcmp(config, "sparse_zi_1000")) rc = build_sparse_zi(e, seed, 1);
     else if (!strcmp(config, "rmsc03")) rc = build_rmsc03(e, seed);
+    else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
     else rc = -1;
     if (rc) {
         free(e);

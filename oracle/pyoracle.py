@@ -176,16 +176,20 @@ def run_batch(config, seeds, threads, max_pops=-1):
 
 
 class OracleGymEnv(OracleEnv):
-    """ABIDESEnv restatement (Exchange + MarketReplayAgent + DummyRL on a LOBSTER tape)."""
+    """GymKernel restatement: ABIDESEnv (Exchange + MarketReplayAgent + DummyRL on a LOBSTER tape),
+    or with `tape=None, seed=s` the rmsc03 + DummyRL composition (config "rmsc03_rl")."""
 
-    def __init__(self, tape, trace_cap=0):
+    def __init__(self, tape=None, trace_cap=0, seed=None):
         L = lib()
         self._h = ctypes.c_void_p()
         self._tape = tape
-        rc = L.ora_create_mr(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
-                             tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), ctypes.byref(self._h))
+        if tape is None:
+            rc = L.ora_create(b"rmsc03_rl", int(seed) & 0xFFFFFFFF, ctypes.byref(self._h))
+        else:
+            rc = L.ora_create_mr(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
+                                 tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), ctypes.byref(self._h))
         if rc:
-            raise ValueError("oracle: bad tape (%d)" % rc)
+            raise ValueError("oracle: bad tape or config (%d)" % rc)
         self.trace_buf = None
         if trace_cap:
             self.trace_buf = np.zeros((trace_cap, 10), dtype=np.int64)
