@@ -20,6 +20,8 @@
  *   mxa_create_replay .. ABIDESEnv.__init__/reset (ABIDESEnv.py:8-57, 59-103), agent_config.py
  *                        Agents (Exchange, MarketReplayAgent on a LOBSTER tape, DummyRL),
  *                        LOBSTEROrdersProcessor output (MarketReplayAgent.py:162-220)
+ *   mxa_create(MXA_RMSC03_RL) config/rmsc03.py agents + DummyRLExecutionAgent
+ *                        (dummy_rl_execution_agent.py:77-137) + GymKernel.initRunner (GymKernel.py:24-156)
  *   mxa_step ........... ABIDESEnv.step (ABIDESEnv.py:30-49) = GymKernel.stepRunner
  *                        (GymKernel.py:158-306) with DummyRL.place_orders/get_observation
  *                        (dummy_rl_execution_agent.py:138-179, 291-312)
@@ -33,7 +35,10 @@ extern "C" {
 
 typedef struct mxa_handle mxa_handle;
 
-enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKETREPLAY = 3 };
+/* MXA_RMSC03_RL: rmsc03's 64 agents + DummyRLExecutionAgent 64 under a GymKernel (BASELINE.json
+ * configs[3]; composition of tests/golden/gen_rl_fixtures.py).  Created by mxa_create like
+ * the plain configs (per-env seeds), advanced by mxa_step / mxa_step_device like a replay handle. */
+enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKETREPLAY = 3, MXA_RMSC03_RL = 4 };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };
@@ -70,7 +75,8 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
 int mxa_read_summary(mxa_handle* h, mxa_env_summary* out /* [n_envs] */);
 int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t cap);
 /* book side 0 bids / 1 asks: levels best-first, FIFO within level; each order is
- * (order_id, agent_id, quantity, price).  Returns the number of orders (<= cap). */
+ * (order_id, agent_id, quantity, price).  Returns the total number of orders on the side;
+ * min(total, cap) are written (cap 0 / out4 NULL: count only). */
 int mxa_read_book(mxa_handle* h, int32_t env, int32_t side, int64_t* out4, int32_t cap);
 int mxa_read_trace(mxa_handle* h, int32_t env, int64_t* out /* [cap][10] */, int64_t cap, int64_t* n);
 /* replace the per-env seeds used by the next mxa_reset (n_envs values) */
@@ -99,7 +105,7 @@ void mxa_destroy(mxa_handle* h);
 int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                       const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
                       mxa_handle** out);
-/* one ABIDESEnv.step per env: actions [n][3] (float64) -> obs [n][9] (float64) and flags [n]
+/* (replay and MXA_RMSC03_RL handles) one ABIDESEnv.step per env: actions [n][3] (float64) -> obs [n][9] (float64) and flags [n]
  * (bit0 done, bit1 observation valid, bit2 env error).  Host arrays; synchronous. */
 int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags);
 /* the same on device arrays, asynchronous on the handle's stream */

@@ -19,6 +19,8 @@ namespace {
 typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*,
                          const RpCtx*);
 typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*);
+typedef void (*step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, const double*,
+                        double*, int32_t*);
 
 template <int CFG>
 void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, const uint32_t* seeds,
@@ -30,6 +32,14 @@ void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t 
                 const RpCtx* ctx) {
   hipLaunchKernelGGL((mxa_run_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx);
 }
+
+#ifndef MXA_ONLY_RMSC03
+template <int CFG>
+void launch_step(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
+                 const RpCtx* ctx, const double* act, double* obs, int32_t* flags) {
+  hipLaunchKernelGGL((mxa_step_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, act, obs, flags);
+}
+#endif
 
 __global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int n, int* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -59,11 +69,13 @@ struct mxa_handle {
   size_t lds = 0;
   build_fn build = nullptr;
   run_fn run = nullptr;
+  step_fn step = nullptr;  // GymKernel handles (replay, rmsc03_rl)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
   std::string err;
-  // marketreplay / ABIDESEnv handles
-  bool replay = false;
+  // GymKernel handles (ABIDESEnv replay, rmsc03 + DummyRL): stepped with actions
+  bool gym = false;
+  bool replay = false;  // the replay ladder book + tape
   RpCtx ctx{};             // host copy (pointers are device pointers)
   RpCtx* d_ctx = nullptr;
   char* d_tape = nullptr;
@@ -90,6 +102,12 @@ static void bind(mxa_handle* h) {
   h->build = launch_build<CFG>;
   h->run = launch_run<CFG>;
   h->lds = mxa_cfg::lds_bytes(CFG);
+#ifndef MXA_ONLY_RMSC03
+  if constexpr (CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL) {
+    h->step = launch_step<CFG>;
+    h->gym = true;
+  }
+#endif
 }
 
 extern "C" {
@@ -108,12 +126,15 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
                mxa_handle** out) {
   if (!out || n_envs <= 0 || !seeds || trace_cap < 0) return MXA_EINVAL;
   mxa_handle* h = new mxa_handle();
-  static_assert(MXA_RMSC03 == MXA_CFG_RMSC03 && MXA_SPARSE_ZI_100 == MXA_CFG_SPARSE_ZI_100 &&
-                MXA_SPARSE_ZI_1000 == MXA_CFG_SPARSE_ZI_1000, "config ids");
+  static_assert((int)MXA_RMSC03 == (int)MXA_CFG_RMSC03 && (int)MXA_SPARSE_ZI_100 == (int)MXA_CFG_SPARSE_ZI_100 &&
+                    (int)MXA_SPARSE_ZI_1000 == (int)MXA_CFG_SPARSE_ZI_1000 &&
+                    (int)MXA_MARKETREPLAY == (int)MXA_CFG_MARKETREPLAY && (int)MXA_RMSC03_RL == (int)MXA_CFG_RMSC03_RL,
+                "config ids");
   if (config == MXA_RMSC03) bind<MXA_CFG_RMSC03>(h);
 #ifndef MXA_ONLY_RMSC03
   else if (config == MXA_SPARSE_ZI_100) bind<MXA_CFG_SPARSE_ZI_100>(h);
   else if (config == MXA_SPARSE_ZI_1000) bind<MXA_CFG_SPARSE_ZI_1000>(h);
+  else if (config == MXA_RMSC03_RL) bind<MXA_CFG_RMSC03_RL>(h);
 #endif
   else {
     delete h;
@@ -123,6 +144,10 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   h->P.n_envs = n_envs;
   h->P.L.trace_cap = trace_cap;
   h->P.L.env_stride = mxa_cfg::env_stride(config, trace_cap);
+  if (h->gym) {  // the DummyRL metrics header + deque after the trace (no ladder, no tape)
+    h->ctx.L = mxa_cfg::replay_layout(h->P.L.env_stride, 0, 0, 0, 0, 0, 0, 0);
+    h->P.L.env_stride = h->ctx.L.end;
+  }
   return create_common(h, n_envs, seeds, device, out);
 }
 
@@ -156,6 +181,8 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
     h->ctx.buy = (const int8_t*)(h->d_tape + h->tb_buy);
     h->ctx.tm = (const int64_t*)(h->d_tape + h->tb_tm);
     h->ctx.tm0 = (const int32_t*)(h->d_tape + h->tb_tm0);
+  }
+  if (h->gym) {
     HIPCHK(h, hipMalloc(&h->d_ctx, sizeof(RpCtx)));
     HIPCHK(h, hipMemcpyAsync(h->d_ctx, &h->ctx, sizeof(RpCtx), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMalloc(&h->d_act, sizeof(double) * 3 * n_envs));
@@ -249,7 +276,7 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
 
 // ABIDESEnv.step for every env: actions [n][3] -> obs [n][9], flags [n] (all host arrays)
 int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags) {
-  if (!h || !h->replay || !actions || !obs || !flags) return MXA_EINVAL;
+  if (!h || !h->gym || !actions || !obs || !flags) return MXA_EINVAL;
 #ifdef MXA_ONLY_RMSC03
   return MXA_EINVAL;
 #else
@@ -270,13 +297,13 @@ int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags) 
 
 // the same with device arrays (e.g. torch tensors), asynchronous on the handle's stream
 int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32_t* d_flags) {
-  if (!h || !h->replay) return MXA_EINVAL;
+  if (!h || !h->gym) return MXA_EINVAL;
 #ifdef MXA_ONLY_RMSC03
   return MXA_EINVAL;
 #else
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipLaunchKernelGGL(mxa_step_kernel, dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride,
-                     h->P.n_envs, h->P.L.trace_cap, (int64_t)1 << 40, (const RpCtx*)h->d_ctx, d_actions, d_obs, d_flags);
+  h->step(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap,
+          (int64_t)1 << 40, (const RpCtx*)h->d_ctx, d_actions, d_obs, d_flags);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   return MXA_OK;
@@ -299,7 +326,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
 }
 
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
-  if (!h || h->replay) return MXA_EINVAL;  // replay handles advance by mxa_step
+  if (!h || h->gym) return MXA_EINVAL;  // GymKernel handles advance by mxa_step
   h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, max_pops,
          h->d_ctx);
   HIPCHK(h, hipGetLastError());
@@ -313,7 +340,7 @@ int mxa_sync(mxa_handle* h) {
 }
 
 int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launches_out) {
-  if (!h || chunk <= 0 || h->replay) return MXA_EINVAL;
+  if (!h || chunk <= 0 || h->gym) return MXA_EINVAL;
   HIPCHK(h, hipSetDevice(h->device));
   int launches = 0;
   float total = 0;
@@ -428,16 +455,13 @@ int mxa_read_book(mxa_handle* h, int32_t env, int32_t side, int64_t* out4, int32
     if (a.price != b.price) return buy ? a.price > b.price : a.price < b.price;
     return a.arrival < b.arrival;
   });
-  int n = 0;
-  for (auto& o : v) {
-    if (n >= cap) break;
-    out4[4 * n + 0] = o.oid;
-    out4[4 * n + 1] = o.meta >> 1;
-    out4[4 * n + 2] = o.qty;
-    out4[4 * n + 3] = o.price;
-    n++;
+  for (int n = 0; n < (int)v.size() && n < cap; n++) {
+    out4[4 * n + 0] = v[n].oid;
+    out4[4 * n + 1] = v[n].meta >> 1;
+    out4[4 * n + 2] = v[n].qty;
+    out4[4 * n + 3] = v[n].price;
   }
-  return (int)v.size() <= cap ? (int)v.size() : n;
+  return (int)v.size();  // total on the side; min(total, cap) written
 }
 
 int mxa_read_trace(mxa_handle* h, int32_t env, int64_t* out, int64_t cap, int64_t* nout) {

@@ -30,6 +30,7 @@ struct Shape {
 #endif
 constexpr Shape shape(int cfg) {
   return cfg == MXA_CFG_RMSC03 ? Shape{4, 2, true, MXA_RMSC03_WAVES, 6}
+       : cfg == MXA_CFG_RMSC03_RL ? Shape{4, 2, true, 4, 8}  // wide spread replies (depth 500)
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6}
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6}
                                        : Shape{1, 1, true, 2, 8};  // marketreplay: book in HBM
@@ -177,6 +178,23 @@ constexpr void params_marketreplay(MxaParams& P) {
   P.L.lat_len = 0;
 }
 
+// rmsc03 + DummyRL (BASELINE.json configs[3]; tests/golden/gen_rl_fixtures.py): rmsc03's 64
+// agents under a GymKernel with DummyRLExecutionAgent 64 (agent_config.py:115-137 parameters:
+// BUY 1e5, 30 s, order_level 2, spread depth 500), horizon pd.date_range(09:31, 09:44, "30S").
+// The DummyRL draws nothing, so rmsc03's global draw order is unchanged.
+constexpr void params_rmsc03_rl(MxaParams& P) {
+  params_rmsc03(P);
+  P.config = MXA_CFG_RMSC03_RL;
+  P.first_rl = 64;
+  P.n_rl = 1;
+  P.n_agents = 65;
+  P.rl_quantity = 100000;
+  P.rl_h0 = 9 * HOUR + 31 * MIN;
+  P.rl_hstep = 30 * NS;
+  P.rl_nh = 27;
+  P.rl_depth = 500;
+}
+
 constexpr uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 // per-env HBM block: header, agent records, open orders, RNG streams, latency row/col,
@@ -212,6 +230,7 @@ constexpr void layout(MxaParams& P, int cfg) {
 constexpr MxaParams params(int cfg) {
   MxaParams P{};
   if (cfg == MXA_CFG_RMSC03) params_rmsc03(P);
+  else if (cfg == MXA_CFG_RMSC03_RL) params_rmsc03_rl(P);
   else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);

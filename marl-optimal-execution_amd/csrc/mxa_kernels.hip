@@ -406,6 +406,7 @@ struct Eng {
   static constexpr bool PL_LDS = mxa_cfg::shape(CFG).pl;
   static constexpr int PW = mxa_cfg::shape(CFG).pw;           // payload words queued
   static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY;     // ABIDESEnv / replay composition
+  static constexpr bool GYM = RP || CFG == MXA_CFG_RMSC03_RL;  // a GymKernel with a DummyRL agent
   typedef RSt<BUILD> RS;
   typedef typename std::conditional<PL_LDS, LDSP u32*, u32*>::type PlPtr;
   static constexpr int QCAP = SQ * 64;
@@ -812,6 +813,25 @@ struct Eng {
     }
     return -1;
   }
+  // OrderBook.getInsideBids/Asks(depth) level count (distinct prices, at most `cap`) from the best
+  // price `best` toward worse prices; the level-2 price in `second` (0 without one)
+  DEV i32 b_levels(int buy_side, i32 best, i32 cap, i32& second) {
+    i32 n = 1, p = best;
+    second = 0;
+    while (n < cap) {
+      i32 v = buy_side ? INT32_MIN : INT32_MAX;
+      for (int j = 0; j < SO; j++) {
+        bool m = bm[j] >= 0 && (bm[j] & 1) == buy_side && (buy_side ? bp[j] < p : bp[j] > p);
+        if (m) v = buy_side ? (bp[j] > v ? bp[j] : v) : (bp[j] < v ? bp[j] : v);
+      }
+      v = buy_side ? wmax_i32(v) : wmin_i32(v);
+      if (v == (buy_side ? INT32_MIN : INT32_MAX)) break;
+      if (n == 1) second = v;
+      n++;
+      p = v;
+    }
+    return n;
+  }
   DEV void b_enter(i32 oid, i32 agent, int is_buy, i32 qty, i32 price, i32 hep) {
     int s = b_free_slot();
     if (s < 0) {
@@ -1024,6 +1044,13 @@ struct Eng {
       }
       r.w[5] = (u32)h.last_trade;
       r.w[0] |= ((u32)hb << 9) | ((u32)ha << 10) | (1u << 11) | ((u32)h.last_trade_float << 8) | ((u32)closed << 7);
+      if constexpr (PW == 8) {  // level counts and level-2 prices (w6/w7 = price2 | count << 20)
+        i32 b2 = 0, a2 = 0;
+        i32 nb = hb ? b_levels(1, bb, depth, b2) : 0, na = ha ? b_levels(0, aa, depth, a2) : 0;
+        if ((u32)b2 >= (1u << 20) || (u32)a2 >= (1u << 20)) fail(ERR_RP_PRICE);
+        r.w[6] = (u32)b2 | ((u32)nb << 20);
+        r.w[7] = (u32)a2 | ((u32)na << 20);
+      }
       ex_notify(sender, r);
       break;
     }
@@ -1186,6 +1213,8 @@ struct Eng {
     if (type == AG_MOMENTUM) return PC.mom_wake;
     if constexpr (RP) {
       if (type == AG_REPLAY) return U(rx->tm[0]) - PC.mkt_open;  // MarketReplayAgent.py:94-96
+    }
+    if constexpr (GYM) {
       if (type == AG_DUMMYRL) return PC.rl_h0 - PC.mkt_open;     // execution_agent.py:129-130
     }
     RS A = agent_rs();
@@ -2139,6 +2168,8 @@ struct Eng {
         if (type == AG_MOMENTUM) return mom_wakeup();
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_wakeup();
+      }
+      if constexpr (GYM) {
         if (type == AG_DUMMYRL) return rl_wakeup();
       }
       // ExchangeAgent: Agent.wakeup does nothing
@@ -2156,6 +2187,8 @@ struct Eng {
         if (type == AG_MOMENTUM) return mom_receive(m);
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_receive(m);
+      }
+      if constexpr (GYM) {
         if (type == AG_DUMMYRL) return rl_receive(m);
       }
     }
@@ -2246,7 +2279,7 @@ struct Eng {
   // ---------------- Kernel.runner event loop (Kernel.py:190-292)
   DEV void run(i64 max_pops) {
     for (i64 n = 0; n < max_pops && status == ST_RUNNING; n++) {
-      if constexpr (RP) {
+      if constexpr (GYM) {
         if (end_step) break;  // GymKernel.stepRunner: `while not end_step and ...`
       }
 #ifndef MXA_NO_LAUNDER_ENV
@@ -2292,7 +2325,7 @@ struct Eng {
       }
       pops++;
       add_delay = 0;
-      if constexpr (RP) {
+      if constexpr (GYM) {
         if (type == MT_CANCEL_ORDER) {  // GymKernel CANCEL_ORDER: no busy check, no delay
           q_remove(slot);
           rl_kernel_cancel();
@@ -2376,6 +2409,24 @@ struct Builder : Eng<CFG, true> {
     wfence();
   }
 
+  // GymKernel-side state of the DummyRL agent: ABIDESEnvMetrics deque, trade flag, quantities
+  DEV void init_gym() {
+    RpLob* rg = this->ring();
+    for (int i = this->lane; i < 100; i += 64) {
+      RpLob z;
+      z.bid = z.ask = z.data = z.flags = 0;
+      rg[i] = z;
+    }
+    u32* rw = (u32*)this->rh();
+    for (int i = this->lane; i < (int)(sizeof(RpHdr) / 4); i += 64) rw[i] = 0;
+    __threadfence_block();
+    RpHdr* R = this->rh();
+    R->rl_trade = 1;
+    R->rl_rem = E::PC.rl_quantity;
+    R->ex_has_last = 1;
+    __threadfence_block();
+  }
+
   // ABIDESEnv.reset (ABIDESEnv.py:51-103): agents, empty ladder book, kernelStarting wakeups.
   // No RNG stream is ever drawn in this composition.
   DEV void build_replay() {
@@ -2404,20 +2455,10 @@ struct Builder : Eng<CFG, true> {
       z.qty = z.price = z.is_buy = z.present = 0;
       mo[i] = z;
     }
-    RpLob* rg = this->ring();
-    for (int i = this->lane; i < 100; i += 64) {
-      RpLob z;
-      z.bid = z.ask = z.data = z.flags = 0;
-      rg[i] = z;
-    }
-    u32* rw = (u32*)this->rh();
-    for (int i = this->lane; i < (int)(sizeof(RpHdr) / 4); i += 64) rw[i] = 0;
-    __threadfence_block();
+    init_gym();
     RpHdr* R = this->rh();
     R->best[0] = R->best[1] = -1;
     R->free_top = C;
-    R->rl_trade = 1;
-    R->rl_rem = P.rl_quantity;
     R->ex_has_last = 0;  // no oracle: getDailyOpenPrice raises, last_trade stays None
     rec_init(0, AG_EXCHANGE);
     this->rs64(AF_COMP, P.default_comp_delay);
@@ -2471,7 +2512,7 @@ struct Builder : Eng<CFG, true> {
     RS G = this->grs(0);
     int n = P.n_agents;
     u32 tmp;
-    if (P.config == MXA_CFG_RMSC03) {
+    if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_RL) {
       set_seed(1, g_seed(G));  // O
       h.o_pt = P.mkt_open;
       h.o_pv = P.o_rbar;
@@ -2505,6 +2546,13 @@ struct Builder : Eng<CFG, true> {
         set_seed(4 + a, g_seed(G));
         rec_init(a, AG_MOMENTUM);
         this->rec_store();
+      }
+      if constexpr (E::GYM) {  // DummyRLExecutionAgent 64: constructed after the config, draws nothing
+        rec_init(P.first_rl, AG_DUMMYRL);
+        this->rs64(AF_START_CASH, 0);  // starting_cash=0 (agent_config.py:115-137)
+        this->rs64(AF_CASH, 0);
+        this->rec_store();
+        init_gym();
       }
       set_seed(2, g_seed(G));  // K
     } else {
@@ -2660,14 +2708,15 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
 // ABIDESEnv.step for every env: DummyRL.place_orders(action), then the GymKernel loop until
 // the RL agent's spread reply (end of step) or the end of the episode.  obs [n][9] float64;
 // flags [n]: bit0 done, bit1 observation valid, bit2 env error.
-__global__ __launch_bounds__(64, mxa_cfg::shape(MXA_CFG_MARKETREPLAY).waves) void mxa_step_kernel(
+template <int CFG>
+__global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel(
     char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops, const RpCtx* ctx, const double* actions,
     double* obs, int32_t* flags) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int env = blockIdx.x;
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
-  mxa::Eng<MXA_CFG_MARKETREPLAY> g(e, lds, trace_cap, ctx);
+  mxa::Eng<CFG> g(e, lds, trace_cap, ctx);
   g.load();
   if (g.status == ST_RUNNING) {
     double a[3];
@@ -2678,7 +2727,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(MXA_CFG_MARKETREPLAY).waves) voi
     if (g.status == ST_RUNNING) {  // after the loop: terminateRunner if the queue ran dry / past stop
       u64 key;
       u32 s;
-      if (g.q_peek(key, s) < 0 || g.cur > mxa::Eng<MXA_CFG_MARKETREPLAY>::PC.stop) g.status = ST_DONE;
+      if (g.q_peek(key, s) < 0 || g.cur > mxa::Eng<CFG>::PC.stop) g.status = ST_DONE;
     }
     if (g.status == ST_DONE) g.rp_terminate();
   }
@@ -2689,7 +2738,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(MXA_CFG_MARKETREPLAY).waves) voi
   u32 sq;
   const bool pending = g.q_peek(key, sq) >= 0;  // all lanes: DPP reduction
   // ABIDESEnv.step: done = not (queue non-empty and currentTime <= stopTime)
-  const int done = !(pending && g.cur <= mxa::Eng<MXA_CFG_MARKETREPLAY>::PC.stop) || g.status != ST_RUNNING;
+  const int done = !(pending && g.cur <= mxa::Eng<CFG>::PC.stop) || g.status != ST_RUNNING;
   const int hobs = mxa::U(R->has_obs);
   if (g.lane == 0) flags[env] = done | (hobs ? 2 : 0) | (g.status == ST_ERROR ? 4 : 0);
 }
@@ -2734,4 +2783,9 @@ MXA_INST(MXA_CFG_RMSC03)
 MXA_INST(MXA_CFG_SPARSE_ZI_100)
 MXA_INST(MXA_CFG_SPARSE_ZI_1000)
 MXA_INST(MXA_CFG_MARKETREPLAY)
+MXA_INST(MXA_CFG_RMSC03_RL)
+#define MXA_INST_STEP(CFG) \
+  template __global__ void mxa_step_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*, const double*, double*, int32_t*);
+MXA_INST_STEP(MXA_CFG_MARKETREPLAY)
+MXA_INST_STEP(MXA_CFG_RMSC03_RL)
 #endif

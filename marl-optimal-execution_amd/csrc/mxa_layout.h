@@ -15,7 +15,8 @@
 #define MXA_MT_M 397
 #define MXA_RNG_WORDS 1280    // two 624-word MT blocks (double buffer) + pad (5120 B per stream)
 
-enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3 };
+enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3,
+                     MXA_CFG_RMSC03_RL = 4 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {

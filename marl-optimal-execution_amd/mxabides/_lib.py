@@ -9,7 +9,7 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MXA_LIB") or os.path.join(PKG_ROOT, "lib", "libmxa.so")
 
-MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000, MXA_MARKETREPLAY = 0, 1, 2, 3
+MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000, MXA_MARKETREPLAY, MXA_RMSC03_RL = 0, 1, 2, 3, 4
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000}
 ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
 ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",

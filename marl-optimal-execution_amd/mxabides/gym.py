@@ -3,6 +3,9 @@
 `VecABIDESEnv` steps n independent copies of the reference's ABIDESEnv composition
 (ExchangeAgent + MarketReplayAgent on a LOBSTER tape + DummyRLExecutionAgent, with the
 GymKernel step loop) in one kernel launch per step; envs differ by the actions they are fed.
+With `tape=None, seeds=[...]` it steps the rmsc03 + DummyRL composition instead (BASELINE.json
+configs[3]): rmsc03's 64 agents from each env's seed plus DummyRLExecutionAgent 64 under the
+same GymKernel step loop (libmxa config MXA_RMSC03_RL).
 `ABIDESEnv` is the single-env drop-in with the reference's signature and return values:
 reset() -> None, step(action) -> (obs float64[9] or [] , reward None, done 0|1, info None).
 """
@@ -19,18 +22,30 @@ ACTION_SIZE = 3   # order_level 2 -> [total volume, level-1 share, level-2 share
 
 
 class VecABIDESEnv:
-    def __init__(self, tape, n_envs, device=0, trace_cap=0):
-        if not isinstance(tape, Tape):
-            raise TypeError("tape must be an mxabides.tape.Tape")
+    def __init__(self, tape=None, n_envs=None, device=0, trace_cap=0, seeds=None):
         self.L = _lib.load()
         self.tape = tape
-        self.n_envs = int(n_envs)
         self.trace_cap = trace_cap
         self._h = ctypes.c_void_p()
-        rc = self.L.mxa_create_replay(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
-                                      tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), self.n_envs, device,
-                                      trace_cap, ctypes.byref(self._h))
-        self._check(rc, "mxa_create_replay")
+        if tape is None:  # rmsc03 + DummyRL, one env per seed
+            if seeds is None:
+                raise TypeError("either a Tape or seeds (rmsc03 + DummyRL) is required")
+            sd = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
+            if n_envs is not None and int(n_envs) != len(sd):
+                raise ValueError("n_envs must equal len(seeds)")
+            self.n_envs = len(sd)
+            rc = self.L.mxa_create(_lib.MXA_RMSC03_RL, self.n_envs, sd.ctypes.data, device, trace_cap,
+                                   ctypes.byref(self._h))
+            self._check(rc, "mxa_create")
+        else:
+            if not isinstance(tape, Tape):
+                raise TypeError("tape must be an mxabides.tape.Tape")
+            self.n_envs = int(n_envs)
+            rc = self.L.mxa_create_replay(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
+                                          tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), self.n_envs, device,
+                                          trace_cap, ctypes.byref(self._h))
+            self._check(rc, "mxa_create_replay")
+        self.n_agents = self.L.mxa_n_agents(self._h)
         self.obs = np.zeros((self.n_envs, OBS_SIZE), dtype=np.float64)
         self.flags = np.zeros(self.n_envs, dtype=np.int32)
 
@@ -40,7 +55,10 @@ class VecABIDESEnv:
             raise _lib.MxaError("%s failed (%d): %s" % (what, rc, msg))
         return rc
 
-    def reset(self):
+    def reset(self, seeds=None):
+        if seeds is not None:  # rmsc03 + DummyRL: new per-env seeds
+            sd = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
+            self._check(self.L.mxa_set_seeds(self._h, sd.ctypes.data), "mxa_set_seeds")
         self._check(self.L.mxa_reset(self._h, None), "mxa_reset")
         self.obs[:] = 0
         self.flags[:] = 0
@@ -69,8 +87,9 @@ class VecABIDESEnv:
                 "order_counter": np.array([b.order_counter for b in buf], dtype=np.int64)}
 
     def agents(self, env):
-        buf = (_lib.AgentState * 3)()
-        self._check(self.L.mxa_read_agents(self._h, env, buf, 3), "mxa_read_agents")
+        n = self.n_agents
+        buf = (_lib.AgentState * n)()
+        self._check(self.L.mxa_read_agents(self._h, env, buf, n), "mxa_read_agents")
         return [(b.cash, b.shares, b.n_open) for b in buf]
 
     def book(self, env, side):

@@ -96,6 +96,8 @@ class VecMarket:
         buf = np.zeros((cap, 4), dtype=np.int64)
         n = self._check(self.L.mxa_read_book(self._h, env, side, buf.ctypes.data, cap), "mxa_read_book")
         levels = []
+        if n > cap:
+            raise _lib.MxaError("book side holds %d orders (> %d)" % (n, cap))
         for o in buf[:n].tolist():
             if levels and levels[-1][0][3] == o[3]:
                 levels[-1].append(o)

@@ -12,6 +12,7 @@ the reference's own classes, nothing restated:
     noise [0.0], compute delay 0, rmsc03's start/stop and oracle;
   * env.step(action) = GymKernel.stepRunner(action); done as in ABIDESEnv.step.
 Recorded: actions, per-step obs / done / events, trace head, FNV hash, final book, holdings.
+A step on which the reference raises is recorded as {"error": exception type, "events"}.
 
 Usage: python tests/golden/gen_rl_fixtures.py SEED ACTION_SEED [XMAX]  (x ~ U(0, XMAX), default 0.002)
 """
@@ -103,7 +104,12 @@ def main():
             a = [float(rs.uniform(0, xmax)), float(rs.uniform()), float(rs.uniform())]
             actions.append(a)
             sys.stdout = io.StringIO()
-            rew, obs = kern.stepRunner(a)
+            try:
+                rew, obs = kern.stepRunner(a)
+            except Exception as exc:  # the reference raises mid-step (e.g. empty book side)
+                steps.append({"error": type(exc).__name__, "events": int(kern.ttl_messages),
+                              "t": int(kern.currentTime.value) - G.MIDNIGHT})
+                break
             done = 0 if (not kern.messages.empty() and kern.currentTime <= kern.stopTime) else 1
             steps.append({"obs": [float(x) for x in obs] if obs is not None and len(obs) else [], "done": done,
                           "events": int(kern.ttl_messages), "t": int(kern.currentTime.value) - G.MIDNIGHT})

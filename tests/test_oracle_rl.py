@@ -12,7 +12,8 @@ import pytest
 import pyoracle
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-FIXTURES = [("rl_rmsc03_123456789_1", 123456789), ("rl_rmsc03_2024_7", 2024)]
+# the third episode ends in the reference's own ValueError (get_observation on an empty book side)
+FIXTURES = [("rl_rmsc03_123456789_1", 123456789), ("rl_rmsc03_2024_7", 2024), ("rl_rmsc03_99991_3", 99991)]
 OBS_RTOL = 1e-9  # observations are float64 (numpy log/tanh/std vs glibc): north_star tolerance
 
 
@@ -30,11 +31,14 @@ def test_oracle_rl_episode_matches_reference(name, seed):
     for i, a in enumerate(actions):
         obs, done, rc = e.step(a)
         st = d["steps"][i]
-        assert rc == 0, e.error
         assert e.events == st["events"], i
+        if "error" in st:  # the reference raised on this step: the oracle stops with an error too
+            assert rc != 0 and i == len(actions) - 1
+            break
+        assert rc == 0, e.error
         assert int(done) == st["done"], i
         np.testing.assert_allclose(obs, st["obs"], rtol=OBS_RTOL, atol=1e-12, err_msg="step %d" % i)
-    assert done
+    assert done or "error" in d["steps"][-1]
     assert e.events == d["events"]
     assert "%016x" % e.hash == d["hash"]
     assert (e.trace() == trace).all()
