@@ -108,6 +108,117 @@ def replay_bench(args):
         dist.destroy_process_group()
 
 
+def rl_bench(args):
+    """rmsc03 + DummyRL under the GymKernel step loop (BASELINE configs[3]): n envs per GPU,
+    each an rmsc03 market from its own seed with DummyRLExecutionAgent 64 stepped every 30 s
+    (09:31-09:44, 27 ABIDESEnv.step calls per episode).  Actions (x ~ U(0, 0.01), level shares
+    U(0, 1)) are drawn on the device (torch Philox, per-rank seed) and stepped through mxa_step_device on torch's
+    stream, so nothing crosses PCIe inside the timed region.  One bench step = one full
+    episode of every env (config build from seeds + 27 gym steps) + the RCCL all-gather of the
+    per-env episode records."""
+    from mxabides.gym import ACTION_SIZE, OBS_SIZE, VecABIDESEnv
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n = args.envs
+    n_steps = 27  # pd.date_range(09:31, 09:44, "30S")
+    ACT_XMAX = 0.01  # total-volume action x ~ U(0, 0.01): up to 1,000 of the 1e5 shares per step
+    v = VecABIDESEnv(seeds=shard.env_seeds(0, rank, world, n), device=local)
+    stream = torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
+    torch.cuda.set_stream(stream)
+    v.set_stream(stream.cuda_stream)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1000 + rank)
+    act = torch.empty((n_steps, n, ACTION_SIZE), dtype=torch.float64, device="cuda")
+    obs = torch.empty((n, OBS_SIZE), dtype=torch.float64, device="cuda")
+    flags = torch.empty((n,), dtype=torch.int32, device="cuda")
+    res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    ev_pairs = []
+
+    def episode(k, timed):
+        v.reset(seeds=shard.env_seeds(k, rank, world, n))
+        torch.rand(act.shape, generator=gen, dtype=torch.float64, device="cuda", out=act)
+        act[:, :, 0] *= ACT_XMAX
+        for i in range(n_steps):
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            v.step_device(act[i].data_ptr(), obs.data_ptr(), flags.data_ptr())
+            if timed:
+                e1.record(stream)
+                ev_pairs.append((e0, e1))
+        v.write_results(res.data_ptr())
+        shard.gather_records(res, world)
+        return res[:, 0].sum(), flags
+
+    for k in range(args.warmup):
+        episode(k, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev = torch.zeros((), dtype=torch.int64, device="cuda")
+    done_all = torch.ones((), dtype=torch.bool, device="cuda")
+    for k in range(args.warmup, args.warmup + args.steps):
+        e, f = episode(k, True)
+        ev += e
+        done_all &= (((f & 1) != 0) | ((f & 4) != 0)).all()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    elt = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+    el = float(elt.item())
+    events = int(ev.item())
+    s = v.summary()
+    n_err = int((s["status"] == 2).sum())
+    if rank == 0:
+        kms = [a.elapsed_time(b) for a, b in ev_pairs]
+        avg_ms = sum(kms) / len(kms)
+        my_ev_per_launch = events / world / len(kms)
+        achieved = ALGO_BYTES_PER_EVENT * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
+        out = {"metric": "env-steps/sec, rmsc03 + DummyRL execution agent (GymKernel) x%d envs per GPU" % n,
+               "value": events / el, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic (seeds) + device-drawn actions x~U(0,0.01), shares~U(0,1)",
+               "config": {"workload": "rmsc03_rl x%d envs per GPU, full episode (config build + %d ABIDESEnv.step) per "
+                                      "bench step, seeds %d+global_env" % (n, n_steps, SEED0),
+                          "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": v.n_agents,
+                          "gym_steps_per_s": n * world * n_steps * args.steps / el,
+                          "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
+                          "env_errors": n_err, "all_done": bool(done_all.item())},
+               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                            "kernel": "mxa_step_kernel<4> (rmsc03_rl)", "avg_launch_ms": avg_ms, "launches": len(kms),
+                            "algo_bytes_per_event": ALGO_BYTES_PER_EVENT}}
+        if not args.no_cpu:
+            import pyoracle
+            k = 256  # ~10 s of one host core
+            t1 = time.perf_counter()
+            cev = 0
+            for i in range(k):
+                e = pyoracle.OracleGymEnv(seed=int(SEED0 + i))
+                r2 = np.random.RandomState(i)
+                while True:
+                    _, d_, rc = e.step([r2.uniform(0, 0.01), r2.uniform(), r2.uniform()])
+                    if d_ or rc:
+                        break
+                cev += e.events
+            cs = time.perf_counter() - t1
+            out["cpu_baseline"] = {"value": cev / cs, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                                   "sample": "%d rmsc03_rl episodes, C oracle, 1 thread, %.1f s" % (k, cs)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -121,6 +232,8 @@ def main():
     args = ap.parse_args()
     if args.config == "marketreplay":
         return replay_bench(args)
+    if args.config == "rmsc03_rl":
+        return rl_bench(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -134,7 +247,8 @@ def main():
         return shard.env_seeds(step, rank, world, n)
 
     m = mxabides.VecMarket(args.config, seeds_for(0), device=local)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
+    torch.cuda.set_stream(stream)
     m.set_stream(stream.cuda_stream)
     res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
 

@@ -75,6 +75,15 @@ class VecABIDESEnv:
         self._check(self.L.mxa_step_device(self._h, ctypes.c_void_p(d_actions), ctypes.c_void_p(d_obs),
                                            ctypes.c_void_p(d_flags)), "mxa_step_device")
 
+    def set_stream(self, stream_ptr):
+        """Step on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
+        self._check(self.L.mxa_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None),
+                    "mxa_set_stream")
+
+    def write_results(self, device_ptr):
+        """Per-env (events, hash, status, current_time) int64 rows into device memory."""
+        self._check(self.L.mxa_write_results(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_results")
+
     def summary(self):
         n = self.n_envs
         buf = (_lib.EnvSummary * n)()
