@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "mxa_api.hip")
 OUT = os.path.join(HERE, "lib", "libmxa.so")
-DEPS = ["mxa_api.hip", "mxa_kernels.hip", "mxa_layout.h", "glibc_math.h", "glibc_math_tables.h"]
+DEPS = ["mxa_api.hip", "mxa_kernels.hip", "mxa_layout.h", "mxa_config.h", "glibc_math.h", "glibc_math_tables.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
          "-Wno-unused-result", "-Wno-unused-value"]

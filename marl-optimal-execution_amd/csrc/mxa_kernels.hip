@@ -302,68 +302,85 @@ DEV Msg msg_order(u32 kind, i32 oid, i32 agent, int is_buy, i32 qty, i32 price, 
 
 // the 10-word parity record (tests/golden/gen_fixtures.py encode()).  WIDE: spread replies
 // carry level counts (w6/w7 >> 20) instead of the 0/1 flags (depth-500 queries)
+struct Rec {  // named scalars, not an array: a private i64[10] is promoted to a VGPR vector
+  i64 t, rcp, type, kind, f0, f1, f2, f3, f4, f5;
+  DEV i64 at(int i) const {
+    switch (i) {
+    case 0: return t; case 1: return rcp; case 2: return type; case 3: return kind;
+    case 4: return f0; case 5: return f1; case 6: return f2; case 7: return f3;
+    case 8: return f4; default: return f5;
+    }
+  }
+};
 template <bool WIDE>
-DEV void encode(u64 key, const Msg& m, i64 rec[10]) {
-  for (int i = 0; i < 10; i++) rec[i] = 0;
-  rec[0] = (i64)(key >> 13);
-  rec[1] = (i64)((key >> 2) & 0x7FF);
+DEV Rec encode(u64 key, const Msg& m) {
+  Rec r;
+  r.t = (i64)(key >> 13);
+  r.rcp = (i64)((key >> 2) & 0x7FF);
   i32 type = (i32)(key & 3);
-  rec[2] = type;
+  r.type = type;
+  r.f0 = r.f1 = r.f2 = r.f3 = r.f4 = r.f5 = 0;
   u32 k = m_kind(m);
   if (type != MT_MESSAGE) {
-    rec[3] = type == MT_WAKEUP ? MK_WAKEUP : MK_KCANCEL;
-    return;
+    r.kind = type == MT_WAKEUP ? MK_WAKEUP : MK_KCANCEL;
+    return r;
   }
-  rec[3] = k;
-  i64* f = rec + 4;
+  r.kind = k;
   switch (k) {
   case MK_WHEN_OPEN_REQ: case MK_WHEN_CLOSE_REQ: case MK_LAST_REQ:
-    f[0] = m_agent(m);
+    r.f0 = m_agent(m);
     break;
   case MK_WHEN_OPEN: case MK_WHEN_CLOSE:
-    f[0] = m_i64(m, 1);
+    r.f0 = m_i64(m, 1);
     break;
   case MK_SPREAD_REQ:
-    f[0] = m_agent(m);
-    f[1] = (i32)m.w[1];
+    r.f0 = m_agent(m);
+    r.f1 = (i32)m.w[1];
     break;
   case MK_SPREAD: {
     int nb = WIDE ? (int)(m.w[6] >> 20) : m_nb(m), na = WIDE ? (int)(m.w[7] >> 20) : m_na(m);
     i64 d = (i32)m.w[5];
-    f[0] = nb ? (i64)(i32)m.w[1] : -1;
-    f[1] = nb ? (i64)(i32)m.w[2] : 0;
-    f[2] = na ? (i64)(i32)m.w[3] : -1;
-    f[3] = na ? (i64)(i32)m.w[4] : 0;
-    f[4] = !m_hasdata(m) ? -1 : (m_dfloat(m) ? d * 10000 : d);
-    f[5] = (i64)m_closed(m) + 2 * (i64)nb + ((i64)1 << 20) * na;
+    r.f0 = nb ? (i64)(i32)m.w[1] : -1;
+    r.f1 = nb ? (i64)(i32)m.w[2] : 0;
+    r.f2 = na ? (i64)(i32)m.w[3] : -1;
+    r.f3 = na ? (i64)(i32)m.w[4] : 0;
+    r.f4 = !m_hasdata(m) ? -1 : (m_dfloat(m) ? d * 10000 : d);
+    r.f5 = (i64)m_closed(m) + 2 * (i64)nb + ((i64)1 << 20) * na;
     break;
   }
   case MK_LAST: {
     i64 d = (i32)m.w[5];
-    f[0] = !m_hasdata(m) ? -1 : (m_dfloat(m) ? d * 10000 : d);
-    f[5] = m_closed(m);
+    r.f0 = !m_hasdata(m) ? -1 : (m_dfloat(m) ? d * 10000 : d);
+    r.f5 = m_closed(m);
     break;
   }
   case MK_TV_REQ:
-    f[0] = m_agent(m);
-    f[1] = m_i64(m, 1);
+    r.f0 = m_agent(m);
+    r.f1 = m_i64(m, 1);
     break;
   case MK_TV:
-    f[0] = m_i64(m, 1);
-    f[5] = m_closed(m);
+    r.f0 = m_i64(m, 1);
+    r.f5 = m_closed(m);
     break;
   case MK_LIMIT: case MK_ACCEPTED: case MK_CANCELLED: case MK_MODIFY: case MK_MODIFIED:
   case MK_CANCEL: case MK_EXECUTED:
-    f[0] = (i32)m.w[1];
-    f[1] = m_agent(m);
-    f[2] = m_buy(m);
-    f[3] = (k == MK_CANCEL || k == MK_MODIFIED) ? 0 : (i64)(i32)m.w[2];  // (see gen_fixtures)
-    f[4] = (i32)m.w[3];
-    if (k == MK_EXECUTED) f[5] = (i32)m.w[4];
+    r.f0 = (i32)m.w[1];
+    r.f1 = m_agent(m);
+    r.f2 = m_buy(m);
+    r.f3 = (k == MK_CANCEL || k == MK_MODIFIED) ? 0 : (i64)(i32)m.w[2];  // (see gen_fixtures)
+    r.f4 = (i32)m.w[3];
+    if (k == MK_EXECUTED) r.f5 = (i32)m.w[4];
     break;
   default:
     break;
   }
+  return r;
+}
+DEV u64 fnv(u64 h, i64 v) { return (h ^ (u64)v) * FNV_PRIME; }
+DEV u64 rec_hash(u64 h, const Rec& r) {
+  h = fnv(h, r.t); h = fnv(h, r.rcp); h = fnv(h, r.type); h = fnv(h, r.kind);
+  h = fnv(h, r.f0); h = fnv(h, r.f1); h = fnv(h, r.f2); h = fnv(h, r.f3); h = fnv(h, r.f4);
+  return fnv(h, r.f5);
 }
 
 // ------------------------------------------------------------------------------------
@@ -466,7 +483,7 @@ struct Eng {
   DEV OpenOrder* open_ptr(int a) { return (OpenOrder*)(env + PC.L.off_open + (size_t)a * PC.L.open_cap * sizeof(OpenOrder)); }
   DEV u32* rng_key(int s) { return (u32*)(env + PC.L.off_rng + (size_t)s * MXA_RNG_WORDS * 4); }
   DEV double* lat() { return (double*)(env + PC.L.off_lat); }
-  DEV i32* ep_entries() { return (i32*)(env + PC.L.off_tx); }               // 16 x i32
+  DEV LDSP i32* ep_entries() { return h.ep_n; }  // header field: LDS for the launch
   DEV TxRec* txr() { return (TxRec*)(env + PC.L.off_tx + 64); }
 
   DEV void fail(int code) {
@@ -589,6 +606,7 @@ struct Eng {
   }
   DEV Msg pl_read(int slot) {
     Msg m;
+    // (readfirstlane'd SGPR copies of the words measured 3 % slower: r01 s3b)
     for (int i = 0; i < PW; i++) m.w[i] = qpl[slot * PW + i];
     for (int i = PW; i < 8; i++) m.w[i] = 0;
     return m;
@@ -623,6 +641,7 @@ struct Eng {
     if (qcount > h.max_q) h.max_q = qcount;
   }
   // lexicographic wave-min of the per-lane cached (key, seq); returns winning slot or -1
+#ifdef MXA_KEY96
   DEV int q_peek(u64& key, u32& seq) {
     u64 k = mk;
     u32 s = ms;
@@ -635,6 +654,29 @@ struct Eng {
     int j = rdli(mj, L);
     return j * 64 + L;
   }
+#else
+  // three 32-bit wave-mins (key high word, key low word, seq), each only while the previous
+  // word still ties across lanes: (key, seq) pairs are unique, so a single candidate lane
+  // after any phase is the winner
+  DEV int q_peek(u64& key, u32& seq) {
+    const u32 kh = (u32)(mk >> 32), kl = (u32)mk;
+    const u32 m1 = wmin_u32(kh);
+    if (m1 == (u32)(KEY_EMPTY >> 32)) return -1;
+    u64 b = bal(kh == m1);
+    if (__popcll(b) > 1) {
+      const u32 m2 = wmin_u32(kh == m1 ? kl : 0xFFFFFFFFu);
+      b = bal(kh == m1 && kl == m2);
+      if (__popcll(b) > 1) {
+        const u32 m3 = wmin_u32((kh == m1 && kl == m2) ? ms : 0xFFFFFFFFu);
+        b = bal(kh == m1 && kl == m2 && ms == m3);
+      }
+    }
+    const int L = ffs64(b);
+    key = ((u64)m1 << 32) | rdl(kl, L);
+    seq = rdl(ms, L);
+    return rdli(mj, L) * 64 + L;
+  }
+#endif
 #ifdef MXA_DIVERGENT_Q
   DEV void q_remove(int slot) {
     if (lane == (slot & 63)) {
@@ -880,7 +922,7 @@ struct Eng {
   DEV i64 transacted_volume(i64 lookback, int* perr) {
     int lo_ep = h.epoch - PC.stream_history;
     i32 entries = 0;
-    i32* EP = ep_entries();
+    LDSP i32* EP = ep_entries();
     for (int e = lo_ep < 0 ? 0 : lo_ep; e <= h.epoch; e++) entries += EP[e & 15];
     if (entries == 0) return 0;
     TxRec* R = txr();
@@ -928,7 +970,7 @@ struct Eng {
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
     if (qty <= 0) return;
     i32 hep = h.epoch;
-    i32* EP = ep_entries();
+    LDSP i32* EP = ep_entries();
     i32 ne = EP[h.epoch & 15] + 1;
     if (lane == 0) EP[h.epoch & 15] = ne;
     i64 ex_q = 0, ex_pq = 0;
@@ -2308,19 +2350,12 @@ struct Eng {
       i64 t = (i64)(key >> 13);
       int rcp = (int)((key >> 2) & 0x7FF);
       int type = (int)(key & 3);
+      rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
       cur = t;
-      i64 rec[10];
-      encode<PW == 8>(key, m, rec);
-      u64 hs = hash;
-      for (int i = 0; i < 10; i++) hs = (hs ^ (u64)rec[i]) * FNV_PRIME;
-      hash = hs;
+      const Rec rec = encode<PW == 8>(key, m);
+      hash = rec_hash(hash, rec);
       if (trace && h.trace_len < trace_cap) {
-        if (lane < 10) {
-          i64 v = 0;
-          for (int i = 0; i < 10; i++)
-            if (i == lane) v = rec[i];
-          trace[h.trace_len * 10 + lane] = v;
-        }
+        if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
         h.trace_len++;
       }
       pops++;
@@ -2333,7 +2368,6 @@ struct Eng {
           continue;
         }
       }
-      rec_load(rcp);
       i64 at = rg64(AF_ATIME);
       PROF_ADD(0, t0);
       if (at > t) {  // agent in the future: requeue unchanged (same uniq)
@@ -2658,8 +2692,7 @@ struct Builder : Eng<CFG, true> {
     this->cur = P.start;
     for (int a = 0; a < n; a++) this->wakeup_at(a, P.start);
     this->save();
-    // zero the history-epoch entry counts and the transaction ring
-    if (this->lane < 16) this->ep_entries()[this->lane] = 0;
+    // the transaction ring (the history-epoch entry counts are header fields, zeroed above)
     TxRec* R = this->txr();
     for (int i = this->lane; i < P.L.tx_cap; i += 64) {
       TxRec z;

@@ -60,7 +60,7 @@ typedef struct {
   int32_t tx_head;      // transaction ring write position (monotonic)
   int64_t last_trade;
   int32_t last_trade_float, pad0;
-  int32_t pad_ep[16];
+  int32_t ep_n[16];     // OrderBook.history: order entries per epoch (ring of 16 epochs)
   // oracle (SparseMeanRevertingOracle)
   int64_t o_pt, o_mst;
   double o_pv, o_msv;
