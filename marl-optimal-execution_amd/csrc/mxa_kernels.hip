@@ -422,6 +422,7 @@ struct Eng {
   static constexpr int SO = mxa_cfg::shape(CFG).so;
   static constexpr bool PL_LDS = mxa_cfg::shape(CFG).pl;
   static constexpr int PW = mxa_cfg::shape(CFG).pw;           // payload words queued
+  static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
   static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY;     // ABIDESEnv / replay composition
   static constexpr bool GYM = RP || CFG == MXA_CFG_RMSC03_RL;  // a GymKernel with a DummyRL agent
   typedef RSt<BUILD> RS;
@@ -458,6 +459,7 @@ struct Eng {
 #ifdef MXA_PROF
   LDSP u64* prof;
 #endif
+  LDSP u64* hotrec;  // [HOT][64]: the exchange's (and the market maker's) agent record
 
   static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 4 * PW : 0));
   DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
@@ -475,6 +477,11 @@ struct Eng {
     if (lane < 32) prof[lane] = 0;
 #endif
     trace = tcap ? (i64*)(env + PC.L.off_trace) : nullptr;
+#ifdef MXA_PROF
+    hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 256);
+#else
+    hotrec = (LDSP u64*)(lds + LDS_Q + 512);
+#endif
   }
 
   // ---------------- env block accessors
@@ -494,13 +501,29 @@ struct Eng {
   }
 
   // ---------------- agent record
+  // the exchange and the market maker take ~95 % of rmsc03's events: their records live in
+  // LDS for the launch (load()/save() move them), every other agent's comes from HBM
+  DEV int hot_slot(int a) {
+    if (HOT > 0 && a == 0) return 0;
+    if (HOT > 1 && PC.n_mm > 0 && a == PC.first_mm) return 1;
+    return -1;
+  }
   DEV void rec_load(int a) {
-    u64 v = agent_ptr(a)[lane];
+    const int hs = hot_slot(a);
+    u64 v;
+    if (hs >= 0) v = hotrec[hs * 64 + lane];
+    else v = agent_ptr(a)[lane];
     rlo = (u32)v;
     rhi = (u32)(v >> 32);
     cur_agent = a;
   }
-  DEV void rec_store() { agent_ptr(cur_agent)[lane] = ((u64)rhi << 32) | rlo; }
+  DEV void rec_store() {
+    const u64 v = ((u64)rhi << 32) | rlo;
+    const int hs = hot_slot(cur_agent);
+    if (hs >= 0) hotrec[hs * 64 + lane] = v;
+    else agent_ptr(cur_agent)[lane] = v;
+  }
+  DEV int hot_agent(int hs) { return hs == 0 ? 0 : PC.first_mm; }
   DEV u32 rg(int f) { return (f & 1) ? rdl(rhi, f >> 1) : rdl(rlo, f >> 1); }
   DEV i32 rgi(int f) { return (i32)rg(f); }
   DEV i64 rg64(int f) { return (i64)(((u64)rdl(rhi, f >> 1) << 32) | rdl(rlo, f >> 1)); }
@@ -2269,6 +2292,7 @@ struct Eng {
   }
   DEV void load() {
     hdr_from_global();
+    for (int hs = 0; hs < HOT; hs++) hotrec[hs * 64 + lane] = agent_ptr(hot_agent(hs))[lane];
     SavedEvent* sq = (SavedEvent*)(env + PC.L.off_q);
     qfree = 0;
     for (int j = 0; j < SQ; j++) {
@@ -2315,6 +2339,7 @@ struct Eng {
       o.pad[0] = o.pad[1] = 0;
       so[j * 64 + lane] = o;
     }
+    for (int hs = 0; hs < HOT; hs++) agent_ptr(hot_agent(hs))[lane] = hotrec[hs * 64 + lane];
     hdr_to_global();
   }
 

@@ -1,0 +1,32 @@
+"""Per-phase cycle breakdown of the run kernel (MXA_PROF build): one rmsc03 episode batch.
+usage: MXA_LIB=.../libmxa_prof.so python tools/prof_phases.py [config] [n_envs]"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "marl-optimal-execution_amd")]
+import numpy as np
+import mxabides
+from mxabides import _lib
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "rmsc03"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+m = mxabides.VecMarket(cfg, (123456789 + np.arange(n)) & 0xFFFFFFFF)
+buf = (ctypes.c_uint64 * 32)()
+lib = _lib.load()
+lib.mxa_prof_read(buf)  # clear
+m.reset()
+m.run()
+lib.mxa_prof_read(buf)
+v = list(buf)
+ev = int(m.summary()["events"].sum())
+names = ["pop+hash+rec_load", "requeue", "EX.other", "EX.wake", "EX.LIMIT", "EX.CANCEL", "NOISE.msg", "NOISE.wake", "VALUE.msg", "VALUE.wake", "MM.ACCEPTED", "MM.wake", "MOM.msg", "MM.EXECUTED", "MM.CANCELLED", "MM.SPREAD_TV"]
+tot = v[0] + v[1] + sum(v[2:16]) + v[30] + v[31]
+print("events %d  total cycles/event (sum over waves) %.0f" % (ev, tot / ev))
+print("%-20s %8s %10s %12s" % ("phase", "share", "cyc/event", "cyc/call"))
+for i, nm in enumerate(names[:16]):
+    c = v[16 + i - 2] if i >= 2 else 0
+    print("%-20s %7.1f%% %10.0f %12s" % (nm, 100 * v[i] / tot, v[i] / ev, ("%.0f (%d calls)" % (v[i] / c, c)) if c else ""))
+print("%-20s %7.1f%% %10.0f" % ("rng_maint", 100 * v[30] / tot, v[30] / ev))
+print("%-20s %7.1f%% %10.0f" % ("tail+rec_store", 100 * v[31] / tot, v[31] / ev))
