@@ -201,32 +201,46 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
 #ifdef MXA_ONLY_RMSC03
   return MXA_EINVAL;
 #else
-  int64_t pmin = INT64_MAX, pmax = INT64_MIN;
+  int64_t pmin = INT64_MAX, pmax = INT64_MIN, min_id = INT64_MAX;
+  int n_zero = 0;  // ORDER_ID 0 records: LimitOrder(order_id=0) takes an auto id (Order.py:26)
   for (int i = 0; i < n_rec; i++) {
-    if ((i && t[i] < t[i - 1]) || oid[i] <= 0 || oid[i] >= INT32_MAX || size[i] < 0 || size[i] >= INT32_MAX ||
+    if ((i && t[i] < t[i - 1]) || oid[i] < 0 || oid[i] >= INT32_MAX || size[i] < 0 || size[i] >= INT32_MAX ||
         price[i] < 0 || price[i] >= (1 << 20))
-      return MXA_EINVAL;  // unsorted tape, ORDER_ID 0 (auto-id) records, or out-of-range fields
+      return MXA_EINVAL;  // unsorted tape or out-of-range fields
     pmin = std::min(pmin, price[i]);
     pmax = std::max(pmax, price[i]);
+    if (oid[i] == 0) n_zero++;
+    else min_id = std::min(min_id, oid[i]);
   }
+  const MxaParams P0 = mxa_cfg::params(MXA_CFG_MARKETREPLAY);
+  // auto ids (DummyRL's orders and the tape's ORDER_ID 0 records) count up from 0 in one
+  // global sequence; Order.generateOrderId would skip explicit tape ids it met, which cannot
+  // happen while every auto id stays below the smallest tape id
+  const int64_t auto_cap = (int64_t)P0.rl_ids + n_zero;
+  if (min_id <= auto_cap) return MXA_EINVAL;
   mxa_handle* h = new mxa_handle();
   bind<MXA_CFG_MARKETREPLAY>(h);
   h->replay = true;
-  h->P = mxa_cfg::params(MXA_CFG_MARKETREPLAY);
+  h->P = P0;
   h->P.n_envs = n_envs;
   h->P.L.trace_cap = trace_cap;
   // dense order-id index in first-appearance order; distinct times and their first records
   std::vector<int32_t> dense(n_rec), tm0;
   std::vector<int64_t> tm;
-  std::vector<std::pair<int64_t, int32_t>> ids(n_rec);
-  for (int i = 0; i < n_rec; i++) ids[i] = {oid[i], i};
+  std::vector<std::pair<int64_t, int32_t>> ids;
+  ids.reserve(n_rec);
+  for (int i = 0; i < n_rec; i++)
+    if (oid[i] != 0) ids.push_back({oid[i], i});
   std::sort(ids.begin(), ids.end());
-  std::vector<int32_t> first(n_rec);
   int n_ids = 0;
-  for (int i = 0; i < n_rec; i++) {
+  for (size_t i = 0; i < ids.size(); i++) {
     if (i == 0 || ids[i].first != ids[i - 1].first) n_ids++;
     dense[ids[i].second] = n_ids - 1;
   }
+  // ORDER_ID 0 records look up `orders.get(0)`: the order whose auto id is 0, which sits at
+  // the first auto-id dense index
+  for (int i = 0; i < n_rec; i++)
+    if (oid[i] == 0) dense[i] = n_ids;
   for (int i = 0; i < n_rec; i++)
     if (i == 0 || t[i] != t[i - 1]) {
       tm.push_back(t[i]);
@@ -236,7 +250,7 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
   const int ntm = (int)tm.size();
   const int C = n_rec + h->P.rl_ids;  // every placement could rest at once
   h->ctx.L = mxa_cfg::replay_layout(mxa_cfg::env_stride(MXA_CFG_MARKETREPLAY, trace_cap), (int)pmin, (int)(pmax - pmin + 1), C,
-                                    n_ids, h->P.rl_ids, ntm, n_rec);
+                                    n_ids, (int)auto_cap, ntm, n_rec);
   h->P.L.env_stride = h->ctx.L.end;
   // tape blob: t, oid, dense, price, size, buy, tm, tm0 (256-B aligned pieces)
   auto al = [](size_t x) { return (x + 255) / 256 * 256; };

@@ -40,7 +40,7 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_RMSC03_RL ? Shape{3, 2, true, 4, 8, 2 * MXA_HOT_RECORDS}  // wide spread replies (depth 500)
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
-                                       : Shape{1, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM
+                                       : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
@@ -280,7 +280,7 @@ inline RpLayout replay_layout(uint64_t base, int pmin, int P, int C, int n_ids, 
   L.off_idh = off;
   off = align_up(off + (uint64_t)L.D * 4, 256);
   L.off_idep = off;
-  off = align_up(off + (uint64_t)L.D * 8, 256);
+  off = align_up(off + (uint64_t)L.D * MXA_ID_EPOCHS * 4, 256);
   L.off_mro = off;
   off = align_up(off + (uint64_t)L.D * sizeof(RpOrder), 256);
   L.off_ring = off;

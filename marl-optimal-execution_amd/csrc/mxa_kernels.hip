@@ -290,6 +290,7 @@ DEV Msg msg_make(u32 kind, i32 agent) {
   m.w[1] = m.w[2] = m.w[3] = m.w[4] = m.w[5] = m.w[6] = m.w[7] = 0;
   return m;
 }
+#define MF_NOT_SAME (1u << 12)  // MODIFY_ORDER whose new order carries another id
 DEV Msg msg_order(u32 kind, i32 oid, i32 agent, int is_buy, i32 qty, i32 price, i32 fill) {
   Msg m = msg_make(kind, agent);
   m.w[0] |= (u32)is_buy << 6;
@@ -1792,13 +1793,15 @@ struct Eng {
       }
     }
   }
-  DEV void rp_note_entry_epoch(i32 d, i32 ep) {  // history[0][order_id] = ... (OrderBook.py:51-60)
-    i32* E = idep() + 2 * (size_t)d;
-    i32 e0 = U(E[0]);
-    if (e0 != ep) {  // all lanes store the same value
-      E[1] = e0;
-      E[0] = ep;
-    }
+  // history[0][order_id] = ... (OrderBook.py:51-60): the id's distinct entry epochs, newest
+  // first, one per lane (lanes < MXA_ID_EPOCHS)
+  DEV void rp_note_entry_epoch(i32 d, i32 ep) {
+    static_assert(MXA_ID_EPOCHS > PC.stream_history, "the id's entry epochs must cover the history window");
+    i32* E = idep() + MXA_ID_EPOCHS * (size_t)d;
+    if (U(E[0]) == ep) return;
+    i32 v = 0;
+    if (lane < MXA_ID_EPOCHS) v = lane == 0 ? ep : E[lane - 1];
+    if (lane < MXA_ID_EPOCHS) E[lane] = v;  // every lane's load completed before the stores
   }
   // handleLimitOrder / executeOrder (OrderBook.py:38-254) on the ladder
   DEV void rp_handle_limit(const Msg& m) {
@@ -1885,6 +1888,7 @@ struct Eng {
   // modifyOrder (OrderBook.py:341-372): each entry of the id at the level replaces the level
   // HEAD with the new order; one ORDER_MODIFIED per match per history epoch holding the id
   DEV void rp_modify(const Msg& m) {
+    if (m.w[0] & MF_NOT_SAME) return;  // isSameOrder(order, new_order) is False
     i32 oid = (i32)m.w[1], qty = (i32)m.w[2], price = (i32)m.w[3], oprice = (i32)m.w[4], d = (i32)m.w[5];
     const int buy = m_buy(m), side = buy ? 0 : 1;
     i32 agent = m_agent(m);
@@ -1914,9 +1918,10 @@ struct Eng {
       E[hd].meta = (agent << 1) | buy;
       lv_qty(side)[x] += (i64)(qty - hq);
     }
-    const i32* EP = idep() + 2 * (size_t)d;
+    // one ORDER_MODIFIED per retained history epoch holding the id (OrderBook.py:352-355)
+    const i32* EP = idep() + MXA_ID_EPOCHS * (size_t)d;
     const i32 lo = h.epoch - PC.stream_history;
-    int neps = (U(EP[0]) >= lo ? 1 : 0) + (U(EP[1]) >= lo && U(EP[1]) != U(EP[0]) ? 1 : 0);
+    const int neps = __popcll(bal(lane < MXA_ID_EPOCHS && EP[lane < MXA_ID_EPOCHS ? lane : 0] >= lo));
     for (int k = 0; k < matches * neps; k++) {
       Msg r = msg_order(MK_MODIFIED, oid, agent, buy, qty, price, 0);
       r.w[5] = (u32)d;
@@ -1954,34 +1959,45 @@ struct Eng {
   }
 
   // ---------------- MarketReplayAgent (MarketReplayAgent.py:50-96)
+  // ORDER_ID 0 records: `orders.get(0)` finds the order whose auto id is 0 (dense index n_ids);
+  // placing or modifying builds LimitOrder(order_id=0), which takes the next auto id
+  // (Order.py:26), so a modify then fails isSameOrder at the exchange (OrderBook.py:343-344)
   DEV void mr_place_record(i32 r) {
     const i32 oid = U(rx->oid[r]), d = U(rx->dense[r]), price = U(rx->price[r]), size = U(rx->size[r]);
     const int buy = (int)U((i32)rx->buy[r]);
     RpOrder* O = mro() + d;
     const i32 present = U(O->present);
     if (!present && size > 0) {  // placeLimitOrder(..., order_id=ORDER_ID)
+      i32 id = oid, dd = d;
+      if (oid == 0) {
+        id = (i32)next_order_id();
+        dd = agent_dense(id);
+      }
       {  // every lane stores the same (uniform) value
         RpOrder o;
         o.qty = size;
         o.price = price;
         o.is_buy = buy;
         o.present = 1;
-        *O = o;
+        mro()[dd] = o;
       }
-      Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, size, price, 0);
-      lm.w[5] = (u32)d;
+      Msg lm = msg_order(MK_LIMIT, id, cur_agent, buy, size, price, 0);
+      lm.w[5] = (u32)dd;
       send_ex(lm);
     } else if (present && size == 0) {  // cancelOrder(existing_order)
       Msg cm = msg_order(MK_CANCEL, oid, cur_agent, U(O->is_buy), U(O->qty), U(O->price), 0);
       cm.w[5] = (u32)d;
       send_ex(cm);
     } else if (present) {  // modifyOrder(existing_order, LimitOrder(..., order_id))
-      if (buy != U(O->is_buy)) {
+      i32 id = oid;
+      if (oid == 0) id = (i32)next_order_id();
+      else if (buy != U(O->is_buy)) {
         fail(ERR_RP_MODIFY);
         return;
       }
-      Msg mm = msg_order(MK_MODIFY, oid, cur_agent, buy, size, price, U(O->price));
+      Msg mm = msg_order(MK_MODIFY, id, cur_agent, buy, size, price, U(O->price));
       mm.w[5] = (u32)d;
+      if (id != oid) mm.w[0] |= MF_NOT_SAME;
       send_ex(mm);
     }
   }
@@ -2508,8 +2524,7 @@ struct Builder : Eng<CFG, true> {
     RpOrder* mo = this->mro();
     for (i32 i = this->lane; i < D; i += 64) {
       ih[i] = -1;
-      ie[2 * i] = INT32_MIN;
-      ie[2 * i + 1] = INT32_MIN;
+      for (int k = 0; k < MXA_ID_EPOCHS; k++) ie[MXA_ID_EPOCHS * i + k] = INT32_MIN;
       RpOrder z;
       z.qty = z.price = z.is_buy = z.present = 0;
       mo[i] = z;

@@ -101,6 +101,9 @@ typedef struct {  // TradingAgent.orders entry (agent's copy of an open order)
 } OpenOrder;
 
 // ---- marketreplay / ABIDESEnv (runtime-sized sections after the fixed layout) ----
+// entry epochs kept per order id (replay book): the OrderBook.history window is
+// stream_history + 1 = 11 epochs, and an id re-entered after a cancel can sit in several
+#define MXA_ID_EPOCHS 12
 typedef struct {  // one resting order of the price-ladder book (OrderBook level entries)
   int32_t price, qty, oid, dense;  // dense = order-id index (tape ids, then agent ids)
   int32_t meta;                    // agent << 1 | is_buy

@@ -28,10 +28,11 @@ class Tape:
             raise ValueError("tape arrays must be non-empty and of equal length")
         if (np.diff(self.t) < 0).any():
             raise ValueError("tape must be time-sorted")
-        if (self.oid <= 0).any():
-            # Order(order_id=0) falls back to the global auto-id counter (Order.py:26), which
-            # interleaves tape and agent ids; not supported by this build.
-            raise ValueError("tape records with ORDER_ID 0 are not supported")
+        if (self.oid < 0).any():
+            raise ValueError("negative ORDER_ID")
+        # ORDER_ID 0 records (LOBSTER hidden executions) take auto ids from the global
+        # Order.order_id counter (Order.py:26) that DummyRL's orders also use
+        self.n_auto = int((self.oid == 0).sum())
 
     def __len__(self):
         return len(self.t)

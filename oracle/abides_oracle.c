@@ -732,6 +732,7 @@ static void cancel_order(ora_env* e, const msg_t* req) {
  * whose id matches replaces the level HEAD (book[i][0] = new_order), not itself, and one
  * ORDER_MODIFIED goes to the requester per history epoch that holds the id. */
 static void modify_order(ora_env* e, const msg_t* req) {
+    if (req->ooid != req->oid) return; /* isSameOrder(order, new_order) (OrderBook.py:343-344) */
     side_t* book = &e->book[req->obuy ? 0 : 1];
     bord_t nw = {req->oid, req->oagent, req->is_buy, req->qty, req->price};
     for (int i = 0; i < book->n; i++) {
@@ -1294,7 +1295,12 @@ static void mom_receive(ora_env* e, agent_t* a, const msg_t* m) {
 
 
 /* ------------------------ marketreplay / ABIDESEnv -------------------------- */
-/* MarketReplayAgent.placeOrder (MarketReplayAgent.py:69-91) for one tape record */
+/* MarketReplayAgent.placeOrder (MarketReplayAgent.py:69-91) for one tape record.
+ * ORDER_ID 0: `self.orders.get(0)` finds only an order whose auto id is 0, and
+ * LimitOrder(..., order_id=0) takes the next auto id (Order.py:26, generateOrderId), both when
+ * placing and when building the modify's new order (whose id then differs: isSameOrder fails
+ * at the exchange, OrderBook.py:343-344).  Auto ids never reach the tape's explicit ids here
+ * (the device host side checks that), so Order._order_ids needs no restating. */
 static void mr_place(ora_env* e, agent_t* a, int r) {
     int64_t oid = e->tp_oid[r], size = e->tp_size[r], price = e->tp_price[r];
     int buy = e->tp_buy[r];
@@ -1303,13 +1309,14 @@ static void mr_place(ora_env* e, agent_t* a, int r) {
     memset(&m, 0, sizeof m);
     m.fill = -1;
     if (slot < 0 && size > 0) { /* placeLimitOrder(..., order_id=ORDER_ID) */
-        int i = mr_slot(e, oid, 1);
-        e->mr_key[i] = oid;
-        aord_t o = {oid, buy, size, price};
+        int64_t id = oid ? oid : next_order_id(e);
+        int i = mr_slot(e, id, 1);
+        e->mr_key[i] = id;
+        aord_t o = {id, buy, size, price};
         e->mr_ord[i] = o;
         if (++e->mr_nord > e->st_max_open) e->st_max_open = e->mr_nord;
         m.kind = K_LIMIT;
-        m.oid = oid;
+        m.oid = id;
         m.oagent = a->id;
         m.is_buy = buy;
         m.qty = size;
@@ -1327,7 +1334,7 @@ static void mr_place(ora_env* e, agent_t* a, int r) {
     } else if (slot >= 0) { /* modifyOrder(existing_order, LimitOrder(..., order_id)) */
         aord_t* o = &e->mr_ord[slot];
         m.kind = K_MODIFY;
-        m.oid = oid;
+        m.oid = oid ? oid : next_order_id(e);
         m.oagent = a->id;
         m.is_buy = buy;
         m.qty = size;

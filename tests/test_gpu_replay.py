@@ -15,8 +15,10 @@ from mxabides.gym import VecABIDESEnv, ABIDESEnv
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-FIX = os.path.join(GOLD, "mr_IBM_2003-01-14_789_1")
 TAPE = os.path.join(GOLD, "tape_IBM_2003-01-14.npz")
+# (ticker, date): IBM 2003-01-14 has explicit ids only; GOOG 2012-06-21 has 3,913 ORDER_ID 0
+# records (hidden executions) that take auto ids interleaved with DummyRL's
+EPISODES = [("IBM", "2003-01-14"), ("GOOG", "2012-06-21")]
 OBS_RTOL = 1e-9
 
 
@@ -31,11 +33,13 @@ def _actions(n_envs, fixture_actions):
     return acts
 
 
-def test_gpu_replay_matches_reference_and_oracle():
-    with open(FIX + ".json") as f:
+@pytest.mark.parametrize("ticker,date", EPISODES)
+def test_gpu_replay_matches_reference_and_oracle(ticker, date):
+    fix = os.path.join(GOLD, "mr_%s_%s_789_1" % (ticker, date))
+    with open(fix + ".json") as f:
         d = json.load(f)
-    z = np.load(FIX + ".npz", allow_pickle=False)
-    tp = tape.Tape.load(TAPE)
+    z = np.load(fix + ".npz", allow_pickle=False)
+    tp = tape.Tape.load(os.path.join(GOLD, "tape_%s_%s.npz" % (ticker, date)))
     n_envs = 4
     acts = _actions(n_envs, z["actions"])
     v = VecABIDESEnv(tp, n_envs, trace_cap=len(z["trace"]))
@@ -66,7 +70,7 @@ def test_gpu_replay_matches_reference_and_oracle():
     assert v.book(0, 0) == d["bids"] and v.book(0, 1) == d["asks"]
     ag = v.agents(0)
     for k, ref in enumerate(d["agents"], start=1):
-        assert ag[k][0] == ref["holdings"]["CASH"] and ag[k][1] == ref["holdings"].get("IBM", 0)
+        assert ag[k][0] == ref["holdings"]["CASH"] and ag[k][1] == ref["holdings"].get(ticker, 0)
         assert ag[k][2] == len(ref["open_orders"])
     for e in range(1, n_envs):
         assert s["hash"][e] == oras[e].hash, e

@@ -1,7 +1,9 @@
-"""C oracle vs the reference ABIDESEnv (Exchange + MarketReplayAgent + DummyRL on the IBM
-2003-01-14 LOBSTER tape): every step's observation, done flag and event count, the event
-trace head, the whole-episode hash, the final book and holdings.  Fixture produced by
-tests/golden/gen_mr_fixtures.py from the reference itself."""
+"""C oracle vs the reference ABIDESEnv (Exchange + MarketReplayAgent + DummyRL on a LOBSTER
+tape): every step's observation, done flag and event count, the event trace head, the
+whole-episode hash, the final book and holdings.  Two episodes: IBM 2003-01-14 (explicit
+order ids only) and GOOG 2012-06-21 (3,913 ORDER_ID 0 records, which take auto ids from the
+counter DummyRL also uses).  Fixtures produced by tests/golden/gen_mr_fixtures.py from the
+reference itself (LOBSTER CSV path; the reference's processed pickles are never loaded)."""
 import json
 import os
 
@@ -12,18 +14,24 @@ import pyoracle
 from mxabides import tape
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-FIX = os.path.join(GOLD, "mr_IBM_2003-01-14_789_1")
 TAPE = os.path.join(GOLD, "tape_IBM_2003-01-14.npz")
-CSV = "/root/reference/data/lobster/LOBSTER_SampleFile_IBM_1/IBM_2003-01-14_34200000_57600000_message_1.csv"
+LOB = "/root/reference/data/lobster/LOBSTER_SampleFile_%s_1/%s_%s_34200000_57600000_message_1.csv"
+EPISODES = [("IBM", "2003-01-14"), ("GOOG", "2012-06-21")]
 OBS_RTOL = 1e-9  # observations are float64 (numpy log/tanh/std vs glibc): north_star tolerance
 
 
-@pytest.fixture(scope="module")
-def fx():
-    with open(FIX + ".json") as f:
+def _tape(ticker, date):
+    return os.path.join(GOLD, "tape_%s_%s.npz" % (ticker, date))
+
+
+@pytest.fixture(scope="module", params=EPISODES, ids=["%s_%s" % e for e in EPISODES])
+def fx(request):
+    ticker, date = request.param
+    fix = os.path.join(GOLD, "mr_%s_%s_789_1" % (ticker, date))
+    with open(fix + ".json") as f:
         d = json.load(f)
-    z = np.load(FIX + ".npz", allow_pickle=False)
-    return d, z["actions"], z["trace"]
+    z = np.load(fix + ".npz", allow_pickle=False)
+    return d, z["actions"], z["trace"], ticker, date
 
 
 def test_tape_fixture_well_formed():
@@ -31,16 +39,24 @@ def test_tape_fixture_well_formed():
     assert len(t) == 38311 and (np.diff(t.t) >= 0).all()
 
 
-@pytest.mark.skipif(not os.path.exists(CSV), reason="reference data not present (GPU box)")
-def test_tape_loader_matches_committed_tape():
-    a, b = tape.load_lobster(CSV, "2003-01-14"), tape.Tape.load(TAPE)
+@pytest.mark.parametrize("ticker,date", EPISODES)
+def test_tape_loader_matches_committed_tape(ticker, date):
+    csv = LOB % (ticker, ticker, date)
+    if not os.path.exists(csv):
+        pytest.skip("reference data not present (GPU box)")
+    a, b = tape.load_lobster(csv, date), tape.Tape.load(_tape(ticker, date))
     for k in ("t", "oid", "price", "size", "buy"):
         assert (getattr(a, k) == getattr(b, k)).all(), k
 
 
+def test_goog_tape_has_auto_id_records():
+    t = tape.Tape.load(_tape("GOOG", "2012-06-21"))
+    assert len(t) == 49482 and t.n_auto == 3913
+
+
 def test_oracle_replay_episode_matches_reference(fx):
-    d, actions, trace = fx
-    e = pyoracle.OracleGymEnv(tape.Tape.load(TAPE), trace_cap=len(trace))
+    d, actions, trace, ticker, date = fx
+    e = pyoracle.OracleGymEnv(tape.Tape.load(_tape(ticker, date)), trace_cap=len(trace))
     for i, a in enumerate(actions):
         obs, done, rc = e.step(a)
         st = d["steps"][i]
@@ -58,7 +74,7 @@ def test_oracle_replay_episode_matches_reference(fx):
     ag = e.agents()
     for k, ref in enumerate(d["agents"], start=1):
         assert ag[k][0] == ref["holdings"]["CASH"]
-        assert ag[k][1] == ref["holdings"].get("IBM", 0)
+        assert ag[k][1] == ref["holdings"].get(ticker, 0)
         assert ag[k][2] == len(ref["open_orders"])
     rl = e.rl_state()
     assert rl[0] == d["rl"]["rem_quantity"] and rl[2] == int(d["rl"]["trade"])
