@@ -128,13 +128,15 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   mxa_handle* h = new mxa_handle();
   static_assert((int)MXA_RMSC03 == (int)MXA_CFG_RMSC03 && (int)MXA_SPARSE_ZI_100 == (int)MXA_CFG_SPARSE_ZI_100 &&
                     (int)MXA_SPARSE_ZI_1000 == (int)MXA_CFG_SPARSE_ZI_1000 &&
-                    (int)MXA_MARKETREPLAY == (int)MXA_CFG_MARKETREPLAY && (int)MXA_RMSC03_RL == (int)MXA_CFG_RMSC03_RL,
+                    (int)MXA_MARKETREPLAY == (int)MXA_CFG_MARKETREPLAY && (int)MXA_RMSC03_RL == (int)MXA_CFG_RMSC03_RL &&
+                    (int)MXA_VALUE_NOISE == (int)MXA_CFG_VALUE_NOISE,
                 "config ids");
   if (config == MXA_RMSC03) bind<MXA_CFG_RMSC03>(h);
 #ifndef MXA_ONLY_RMSC03
   else if (config == MXA_SPARSE_ZI_100) bind<MXA_CFG_SPARSE_ZI_100>(h);
   else if (config == MXA_SPARSE_ZI_1000) bind<MXA_CFG_SPARSE_ZI_1000>(h);
   else if (config == MXA_RMSC03_RL) bind<MXA_CFG_RMSC03_RL>(h);
+  else if (config == MXA_VALUE_NOISE) bind<MXA_CFG_VALUE_NOISE>(h);
 #endif
   else {
     delete h;
@@ -419,6 +421,7 @@ int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t ca
     out[a].last_trade = g64(AF_LAST_TRADE);
     out[a].type = (int32_t)r[AF_TYPE];
     out[a].flags = (int32_t)r[AF_FLAGS];
+    out[a].starting_cash = g64(AF_START_CASH);
     if (h->replay && out[a].type == AG_REPLAY) {  // MarketReplayAgent.orders lives in the dense table
       std::vector<RpOrder> mo(h->ctx.L.D);
       HIPCHK(h, hipMemcpy(mo.data(), h->d_env + (size_t)env * h->P.L.env_stride + h->ctx.L.off_mro,

@@ -39,6 +39,7 @@ constexpr Shape shape(int cfg) {
   return cfg == MXA_CFG_RMSC03 ? Shape{3, 2, true, MXA_RMSC03_WAVES, 6, 2 * MXA_HOT_RECORDS}
        : cfg == MXA_CFG_RMSC03_RL ? Shape{3, 2, true, 4, 8, 2 * MXA_HOT_RECORDS}  // wide spread replies (depth 500)
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6, MXA_HOT_RECORDS}
+       : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, 2, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
@@ -91,6 +92,7 @@ constexpr void params_rmsc03(MxaParams& P) {
   P.v_lambda = 7e-11;
   P.v_percent_aggr = 0.1;
   P.v_depth_spread = 2;
+  P.v_starting_cash = 10000000;
   P.noise_open = 9 * HOUR;
   P.noise_close = 16 * HOUR;
   P.mm_pov = 0.05;
@@ -235,11 +237,45 @@ constexpr void layout(MxaParams& P, int cfg) {
   L.env_stride = off;  // without trace; the handle adds trace_cap records
 }
 
+// config/value_noise.py:45-200 (argparse defaults; obs_noise 1e6): 1 exchange, 100 noise and 50
+// value agents on JPM, market 09:30-10:30, kernel midnight-17:00, compute delay 1 s, latency
+// matrix U(21000, 13e6) symmetrised (only the exchange row is read), 6-way uniform noise.
+// ValueAgents take their default starting_cash (ValueAgent.py:17).
+constexpr void params_value_noise(MxaParams& P) {
+  base_params(P);
+  P.config = MXA_CFG_VALUE_NOISE;
+  P.mkt_close = 10 * HOUR + 30 * MIN;
+  P.start = 0;
+  P.stop = 17 * HOUR;
+  P.default_comp_delay = 1000000000;
+  P.lat_mode = 1;
+  P.noise_len = 6;
+  P.lat_lo = 21000;
+  P.lat_hi = 13000000;
+  P.first_noise = 1;
+  P.n_noise = 100;
+  P.first_value = 101;
+  P.n_value = 50;
+  P.n_agents = 151;
+  P.v_sigma_n = 1000000.0;
+  P.v_rbar = 1e5;
+  P.v_kappa = 1.67e-15;
+  P.v_sigma_s = 1e-4;
+  P.v_lambda = 1e-12;
+  P.v_percent_aggr = 0.1;
+  P.v_depth_spread = 2;
+  P.v_starting_cash = 100000;
+  P.L.open_cap = 8;
+  P.L.tx_cap = 256;
+  P.L.lat_len = P.n_agents;
+}
+
 constexpr MxaParams params(int cfg) {
   MxaParams P{};
   if (cfg == MXA_CFG_RMSC03) params_rmsc03(P);
   else if (cfg == MXA_CFG_RMSC03_RL) params_rmsc03_rl(P);
   else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);
+  else if (cfg == MXA_CFG_VALUE_NOISE) params_value_noise(P);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;

@@ -2453,8 +2453,9 @@ struct Builder : Eng<CFG, true> {
     this->rs(AF_FLAGS, FL_FIRST_WAKE | FL_AW_SPREAD | FL_AW_TV);
     this->rs(AF_RS_POS, MXA_MT_N);
     this->rs(AF_RS_M, 0);
-    this->rs64(AF_START_CASH, E::PC.starting_cash);
-    this->rs64(AF_CASH, E::PC.starting_cash);
+    const i64 cash = type == AG_VALUE ? E::PC.v_starting_cash : E::PC.starting_cash;
+    this->rs64(AF_START_CASH, cash);
+    this->rs64(AF_CASH, cash);
     this->rs64(AF_ATIME, E::PC.start);
     this->rs64(AF_COMP, E::PC.default_comp_delay);
   }
@@ -2629,6 +2630,43 @@ struct Builder : Eng<CFG, true> {
         init_gym();
       }
       set_seed(2, g_seed(G));  // K
+    } else if (P.config == MXA_CFG_VALUE_NOISE) {
+      // config/value_noise.py: O and K seeds (the kernel is built before the oracle), the
+      // oracle's first megashock time, the exchange; per noise agent its seed, its wakeup_time
+      // open + rand() * (close - open) (pandas float * Timedelta truncates), NoiseAgent's size;
+      // per value agent its seed and size; then the 151 x 151 latency matrix
+      set_seed(1, g_seed(G));  // O
+      set_seed(2, g_seed(G));  // K
+      h.o_pt = P.mkt_open;
+      h.o_pv = P.o_rbar;
+      h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
+      set_seed(4 + 0, g_seed(G));  // exchange
+      for (int a = P.first_noise; a < P.first_noise + P.n_noise; a++) {
+        set_seed(4 + a, g_seed(G));
+        const i64 wt = P.mkt_open + (i64)(rs_double(G) * (double)(P.mkt_close - P.mkt_open));
+        const i64 size = rs_randint(G, 20, 50);
+        rec_init(a, AG_NOISE);
+        this->rs64(AF_WAKEUP_TIME, wt);
+        this->rs(AF_SIZE, (u32)size);
+        this->rec_store();
+      }
+      for (int a = P.first_value; a < P.first_value + P.n_value; a++) {
+        set_seed(4 + a, g_seed(G));
+        const i64 size = rs_randint(G, 20, 50);
+        rec_init(a, AG_VALUE);
+        this->rs(AF_SIZE, (u32)size);
+        this->rsd(AF_R_T, P.v_rbar);
+        this->rec_store();
+      }
+      // symmetrised matrix: latency[a][0] = latency[0][a], so row 0 is all that is read
+      double* lat = this->lat();
+      const i64 total = (i64)n * n;
+      for (i64 d = 0; d < n; d++) {
+        double v = rs_uniform(G, P.lat_lo, P.lat_hi);
+        if (this->lane == 0) lat[d] = d == 0 ? 20000.0 : v;
+      }
+      rs_skip_words(G, 2 * (total - n));
+      wfence();
     } else {
       set_seed(1, g_seed(G));  // O
       set_seed(2, g_seed(G));  // K
@@ -2857,6 +2895,7 @@ MXA_INST(MXA_CFG_SPARSE_ZI_100)
 MXA_INST(MXA_CFG_SPARSE_ZI_1000)
 MXA_INST(MXA_CFG_MARKETREPLAY)
 MXA_INST(MXA_CFG_RMSC03_RL)
+MXA_INST(MXA_CFG_VALUE_NOISE)
 #define MXA_INST_STEP(CFG) \
   template __global__ void mxa_step_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*, const double*, double*, int32_t*);
 MXA_INST_STEP(MXA_CFG_MARKETREPLAY)

@@ -16,7 +16,7 @@
 #define MXA_RNG_WORDS 1280    // two 624-word MT blocks (double buffer) + pad (5120 B per stream)
 
 enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3,
-                     MXA_CFG_RMSC03_RL = 4 };
+                     MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -198,6 +198,7 @@ typedef struct {
   // ValueAgent
   double v_sigma_n, v_rbar, v_kappa, v_sigma_s, v_lambda, v_percent_aggr;
   int32_t v_depth_spread, pad1;
+  int64_t v_starting_cash;
   // NoiseAgent wake window
   int64_t noise_open, noise_close;
   // POVMarketMakerAgent

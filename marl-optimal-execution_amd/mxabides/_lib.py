@@ -9,8 +9,9 @@ import os
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MXA_LIB") or os.path.join(PKG_ROOT, "lib", "libmxa.so")
 
-MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000, MXA_MARKETREPLAY, MXA_RMSC03_RL = 0, 1, 2, 3, 4
-CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000}
+MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000, MXA_MARKETREPLAY, MXA_RMSC03_RL, MXA_VALUE_NOISE = 0, 1, 2, 3, 4, 5
+CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000,
+              "value_noise": MXA_VALUE_NOISE}
 ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
 ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",
              4: "transaction history capacity", 5: "get_transacted_volume without transactions (pandas error)",
@@ -29,7 +30,8 @@ class EnvSummary(ctypes.Structure):
 
 class AgentState(ctypes.Structure):
     _fields_ = [("cash", ctypes.c_int64), ("shares", ctypes.c_int64), ("n_open", ctypes.c_int64),
-                ("last_trade", ctypes.c_int64), ("type", ctypes.c_int32), ("flags", ctypes.c_int32)]
+                ("last_trade", ctypes.c_int64), ("type", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("starting_cash", ctypes.c_int64)]
 
 
 EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_read_summary", "mxa_read_agents",

@@ -1,6 +1,7 @@
 """Agent naming of the reference configs (used for the reference-format stdout report).
 
-config/rmsc03.py:95-197, config/sparse_zi_100.py:177-256, config/sparse_zi_1000.py.
+config/rmsc03.py:95-197, config/sparse_zi_100.py:177-256, config/sparse_zi_1000.py,
+config/value_noise.py:98-161 (every ValueAgent gets its own type string "ValueAgent {id}").
 """
 ZI_GROUPS = [(0, 250, "1"), (0, 500, "1"), (0, 1000, "0.8"), (0, 1000, "1"), (0, 2000, "0.8"), (250, 500, "0.8"),
              (250, 500, "1")]
@@ -12,6 +13,9 @@ def symbol_of(config):
 
 
 def agent_names(config):
+    if config == "value_noise":
+        return (["Exchange Agent 0"] + ["NoiseAgent %d" % j for j in range(1, 101)] +
+                ["Value Agent %d" % j for j in range(101, 151)])
     if config == "rmsc03":
         return (["EXCHANGE_AGENT"] + ["NoiseAgent %d" % j for j in range(1, 51)] +
                 ["Value Agent %d" % j for j in range(51, 61)] + ["POV_MARKET_MAKER_AGENT_61"] +
@@ -26,6 +30,8 @@ def agent_names(config):
 
 
 def agent_type_names(config):
+    if config == "value_noise":
+        return ["ExchangeAgent"] + ["NoiseAgent"] * 100 + ["ValueAgent %d" % j for j in range(101, 151)]
     if config == "rmsc03":
         return ["ExchangeAgent"] + ["NoiseAgent"] * 50 + ["ValueAgent"] * 10 + ["POVMarketMakerAgent"] + ["MomentumAgent"] * 2
     out = ["ExchangeAgent"]

@@ -87,7 +87,7 @@ class VecMarket:
         arr = (_lib.AgentState * self.n_agents)()
         self._check(self.L.mxa_read_agents(self._h, env, arr, self.n_agents), "mxa_read_agents")
         return [dict(cash=a.cash, shares=a.shares, n_open=a.n_open, last_trade=a.last_trade, type=a.type,
-                     flags=a.flags) for a in arr]
+                     flags=a.flags, starting_cash=a.starting_cash) for a in arr]
 
     def book(self, env, side):
         """OrderBook.bids (side 0) / asks (side 1): list of levels, each a FIFO list of
@@ -142,7 +142,7 @@ class VecMarket:
             if t not in gains:
                 gains[t], counts[t] = 0, 0
                 order.append(t)
-            gains[t] += mtm - 10000000
+            gains[t] += mtm - st["starting_cash"]
             counts[t] += 1
         means = ["%s: %d" % (t, int(round(gains[t] / counts[t]))) for t in order]
         return lines, means

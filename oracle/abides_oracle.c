@@ -1649,9 +1649,11 @@ static void rep_append(ora_env* e, const char* s) {
 int ora_finish(ora_env* e) {
     char line[512];
     const char* sym = strncmp(e->config, "rmsc03", 6) == 0 ? "ABM" : "JPM";
-    char tnames[16][96];
-    long long gains[16];
-    int counts[16], nt = 0;
+    /* one entry per distinct agent type string (value_noise names every ValueAgent's type apart) */
+    char (*tnames)[96] = (char (*)[96])malloc(sizeof(char[96]) * (size_t)e->n);
+    long long* gains = (long long*)malloc(sizeof(long long) * (size_t)e->n);
+    int* counts = (int*)malloc(sizeof(int) * (size_t)e->n);
+    int nt = 0;
     for (int i = 1; i < e->n; i++) {
         agent_t* a = &e->ag[i];
         char hold[128];
@@ -1682,6 +1684,9 @@ int ora_finish(ora_env* e) {
         snprintf(line, sizeof line, "%s: %lld", tnames[k], (long long)rint((double)gains[k] / (double)counts[k]));
         rep_append(e, line);
     }
+    free(tnames);
+    free(gains);
+    free(counts);
     return 0;
 }
 
@@ -1889,6 +1894,73 @@ static int build_rmsc03(ora_env* e, uint32_t seed) {
     return 0;
 }
 
+/* config/value_noise.py:45-200 (argparse defaults: obs_noise 1e6): 1 exchange, 100 noise and
+ * 50 value agents on JPM 2019-06-28, market 09:30-10:30, kernel midnight-17:00, compute delay
+ * 1 s, latency matrix U(21000, 13e6) symmetrised (diagonal 20000), 6-way uniform noise.
+ * Global draw order: O seed, K seed (kernel built before the oracle), oracle megashock
+ * exponential, exchange seed; per noise agent its seed, then wakeup_time = open + rand() *
+ * (close - open) (pandas float * Timedelta truncates to ns), then NoiseAgent.__init__'s
+ * size; per value agent its seed, then its size; then the 151 x 151 latency draws. */
+static int build_value_noise(ora_env* e, uint32_t seed) {
+    rs_seed(&e->G, seed);
+    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 10 * NS_HOUR + 30 * NS_MIN;
+    rs_seed(&e->O, seed_u32(&e->G));
+    rs_seed(&e->K, seed_u32(&e->G));
+    oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+    agent_t* ex = add_agent(e, AG_EXCHANGE);
+    rs_seed(&ex->rs, seed_u32(&e->G));
+    snprintf(ex->name, 96, "Exchange Agent 0");
+    snprintf(ex->tname, 96, "ExchangeAgent");
+    e->ex_open = open;
+    e->ex_close = close;
+    e->ex_pipeline = 0;
+    e->ex_comp = 0;
+    e->stream_history = 10;
+    for (int j = 0; j < 100; j++) {
+        agent_t* a = add_agent(e, AG_NOISE);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        a->wakeup_time = open + (int64_t)(rs_double(&e->G) * (double)(close - open));
+        a->size = rs_randint(&e->G, 20, 50);
+        snprintf(a->name, 96, "NoiseAgent %d", a->id);
+        snprintf(a->tname, 96, "NoiseAgent");
+        trading_init(a, 10000000);
+    }
+    for (int j = 0; j < 50; j++) {
+        agent_t* a = add_agent(e, AG_VALUE);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        a->size = rs_randint(&e->G, 20, 50);
+        snprintf(a->name, 96, "Value Agent %d", a->id);
+        snprintf(a->tname, 96, "ValueAgent %d", a->id);
+        trading_init(a, 100000); /* ValueAgent's default starting_cash */
+        a->sigma_n = 1000000.0;
+        a->r_bar = 1e5;
+        a->kappa = 1.67e-15;
+        a->sigma_s = 1e-4;
+        a->lambda_a = 1e-12;
+        a->r_t = 1e5;
+        a->sigma_t = 0;
+    }
+    int n = e->n;
+    e->lat = (double*)malloc(sizeof(double) * (size_t)n * n);
+    for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, 21000, 13000000);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            if (i > j) e->lat[(size_t)i * n + j] = e->lat[(size_t)j * n + i];
+            else if (i == j) e->lat[(size_t)i * n + j] = 20000;
+        }
+    e->lat_mode = 1;
+    e->noise_len = 6;
+    e->start = 0;
+    e->stop = 17 * NS_HOUR;
+    e->agent_time = (int64_t*)calloc(n, sizeof(int64_t));
+    e->comp_delay = (int64_t*)calloc(n, sizeof(int64_t));
+    for (int i = 0; i < n; i++) {
+        e->agent_time[i] = e->start;
+        e->comp_delay[i] = 1000000000;
+    }
+    return 0;
+}
+
 /* rmsc03 + DummyRL (BASELINE.json configs[3]; tests/golden/gen_rl_fixtures.py): config/rmsc03.py's
  * 64 agents, oracle and kernel RandomState, plus DummyRLExecutionAgent 64 (agent_config.py:115-137
  * parameters: BUY 1e5, freq 30 s, order_level 2) with execution_time_horizon =
@@ -2010,6 +2082,7 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     else if (!strcmp(config, "sparse_zi_1000")) rc = build_sparse_zi(e, seed, 1);
     else if (!strcmp(config, "rmsc03")) rc = build_rmsc03(e, seed);
     else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
+    else if (!strcmp(config, "value_noise")) rc = build_value_noise(e, seed);
     else rc = -1;
     if (rc) {
         free(e);

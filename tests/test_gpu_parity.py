@@ -97,7 +97,7 @@ def test_gpu_sparse_zi_1000_known_answer(mx):
     assert sorted(h) == sorted(holdings) and mm == means
 
 
-@pytest.mark.parametrize("cfg,n", [("rmsc03", 96), ("sparse_zi_100", 64)])
+@pytest.mark.parametrize("cfg,n", [("rmsc03", 96), ("sparse_zi_100", 64), ("value_noise", 1024)])
 def test_gpu_batch_equals_oracle(mx, cfg, n):
     seeds = (np.arange(n, dtype=np.int64) * 7919 + 11) & 0xFFFFFFFF
     m = mx.VecMarket(cfg, seeds)
