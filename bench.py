@@ -34,62 +34,97 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 def replay_bench(args):
     """ABIDESEnv / market replay (BASELINE configs[4] shape): n envs stepping the reference's
-    composition on the IBM 2003-01-14 LOBSTER tape with per-env random actions; one bench
-    step = one full episode (761 ABIDESEnv.step calls per env)."""
+    composition (Exchange + MarketReplayAgent + DummyRL) on a LOBSTER tape (IBM 2003-01-14 by
+    default; --tape GOOG_2012-06-21 has ORDER_ID 0 records) with per-env random actions.  One
+    bench step = one full episode: reset + the 761 ABIDESEnv.step calls of DummyRL's horizon
+    (09:40-16:00 every 30 s).  Actions x ~ U(0, 0.01), level shares U(0, 1) are drawn on the
+    device (torch Philox, per-rank seed) and stepped through mxa_step_device on the bench's
+    stream, so nothing crosses PCIe inside the timed region; envs that finish early stay
+    finished (the step kernel skips them)."""
     from mxabides import tape
-    from mxabides.gym import VecABIDESEnv
+    from mxabides.gym import ACTION_SIZE, OBS_SIZE, VecABIDESEnv
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    tp = tape.Tape.load(os.path.join(ROOT, "tests", "golden", "tape_IBM_2003-01-14.npz"))
+    tname = args.tape or "IBM_2003-01-14"
+    tp = tape.Tape.load(os.path.join(ROOT, "tests", "golden", "tape_%s.npz" % tname))
     n = args.envs
+    n_steps = 761  # pd.date_range(09:40, 16:00, freq="30S")
     v = VecABIDESEnv(tp, n, device=local)
-    rs = np.random.RandomState(1000 + rank)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    v.set_stream(stream.cuda_stream)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1000 + rank)
+    act = torch.empty((n_steps, n, ACTION_SIZE), dtype=torch.float64, device="cuda")
+    obs = torch.empty((n, OBS_SIZE), dtype=torch.float64, device="cuda")
+    flags = torch.empty((n,), dtype=torch.int32, device="cuda")
+    res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    ev_pairs = []
 
-    def episode():
+    def episode(timed):
         v.reset()
-        steps, kms = 0, 0.0
-        while True:
-            a = np.stack([rs.uniform(0, 0.01, n), rs.uniform(0, 1, n), rs.uniform(0, 1, n)], 1)
-            obs, done, valid, err = v.step(a)
-            kms += v.last_kernel_ms
-            steps += 1
-            if done.all() or err.any():
-                break
-        s = v.summary()
-        return int(s["events"].sum()), steps, int((s["status"] == 2).sum()), kms
+        torch.rand(act.shape, generator=gen, dtype=torch.float64, device="cuda", out=act)
+        act[:, :, 0] *= 0.01
+        for i in range(n_steps):
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            v.step_device(act[i].data_ptr(), obs.data_ptr(), flags.data_ptr())
+            if timed:
+                e1.record(stream)
+                ev_pairs.append((e0, e1))
+        v.write_results(res.data_ptr())
+        shard.gather_records(res, world)
+        return res[:, 0].sum()
 
     for _ in range(args.warmup):
-        episode()
+        episode(False)
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev = st = nerr = 0
-    kms = 0.0
+    ev = torch.zeros((), dtype=torch.int64, device="cuda")
     for _ in range(args.steps):
-        e, s_, er, k = episode()
-        ev, st, nerr, kms = ev + e, st + s_, nerr + er, kms + k
+        ev += episode(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     el = time.perf_counter() - t0
-    tot = torch.tensor([ev, st * n], dtype=torch.float64, device="cuda")
     elt = torch.tensor([el], dtype=torch.float64, device="cuda")
     if world > 1:
-        dist.all_reduce(tot)
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
-        el = float(elt.item())
+        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+    el = float(elt.item())
+    events = int(ev.item())
+    s = v.summary()
+    nerr = int((s["status"] == 2).sum())
     if rank == 0:
-        out = {"metric": "env-steps/sec, ABIDESEnv market replay (IBM 2003-01-14 LOBSTER tape) x%d envs per GPU" % n,
-               "value": float(tot[0]) / el, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        kms = [a.elapsed_time(b) for a, b in ev_pairs]
+        avg_ms = sum(kms) / len(kms)
+        achieved = ALGO_BYTES_PER_EVENT * (events / world / len(kms)) / (avg_ms * 1e-3) / 1e9
+        out = {"metric": "env-steps/sec, ABIDESEnv market replay (%s LOBSTER tape) x%d envs per GPU" % (tname, n),
+               "value": events / el, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "LOBSTER sample tape + random actions",
-               "config": {"workload": "marketreplay x%d envs per GPU, full episode (761 ABIDESEnv.step) per bench step" % n,
-                          "gym_steps_per_s": float(tot[1]) / el, "env_errors": nerr,
-                          "kernel_ms_per_episode": kms / args.steps}}
+               "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+               "data": "LOBSTER sample tape %s + device-drawn actions x~U(0,0.01), shares~U(0,1)" % tname,
+               "config": {"workload": "marketreplay x%d envs per GPU, full episode (reset + %d ABIDESEnv.step) per bench "
+                                      "step" % (n, n_steps),
+                          "envs_per_gpu": n, "global_envs": n * world, "tape_records": len(tp),
+                          "gym_steps_per_s": n * world * n_steps * args.steps / el,
+                          "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
+                          "env_errors": nerr},
+               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                            "kernel": "mxa_step_kernel<3> (marketreplay)", "avg_launch_ms": avg_ms,
+                            "launches": len(kms), "algo_bytes_per_event": ALGO_BYTES_PER_EVENT}}
         if not args.no_cpu:
             import pyoracle
-            k = 8
+            k = 512  # ~10 s of one host core (8.4 M env-steps/s, ~144 k events per IBM episode)
             t1 = time.perf_counter()
             cev = 0
             for i in range(k):
@@ -102,7 +137,7 @@ def replay_bench(args):
                 cev += e.events
             cs = time.perf_counter() - t1
             out["cpu_baseline"] = {"value": cev / cs, "unit": "env-steps/s", "cores": 1, "kind": "port",
-                                   "sample": "%d episodes, C oracle, 1 thread, %.1f s" % (k, cs)}
+                                   "sample": "%d %s episodes, C oracle, 1 thread, %.1f s" % (k, tname, cs)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -200,7 +235,7 @@ def rl_bench(args):
                             "algo_bytes_per_event": ALGO_BYTES_PER_EVENT}}
         if not args.no_cpu:
             import pyoracle
-            k = 256  # ~10 s of one host core
+            k = 1024  # ~12 s of one host core
             t1 = time.perf_counter()
             cev = 0
             for i in range(k):
@@ -229,6 +264,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=1 << 22, help="max pops per env per kernel launch")
     ap.add_argument("--cpu-envs", type=int, default=2048, help="CPU-baseline sample size (envs)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tape", default=None, help="marketreplay tape under tests/golden (IBM_2003-01-14, GOOG_2012-06-21)")
     args = ap.parse_args()
     if args.config == "marketreplay":
         return replay_bench(args)
