@@ -203,13 +203,11 @@ def run_config(cfg, seed, out, full):
     TradingAgent.getTransactedVolume = TradingAgent.get_transacted_volume  # SURVEY.md key finding 3
 
     date = {"sparse_zi_100": "2019-06-28", "sparse_zi_1000": "2019-06-28", "rmsc03": "2019-06-28",
-            "value_noise": "2019-06-28", "random_fund_value": "2019-06-28"}[cfg]
+            "value_noise": "2019-06-28"}[cfg]
     MIDNIGHT = int(pd.Timestamp(date).value)
     argv = ["abides.py", "-c", cfg, "-s", str(seed)]
     if cfg == "rmsc03":
         argv += ["-t", "ABM", "-d", "20190628"]
-    if cfg == "random_fund_value":
-        argv += ["-t", "JPM", "-d", "20190628"]
     sys.argv = argv
     buf = io.StringIO()
     real_stdout = sys.stdout
@@ -316,8 +314,7 @@ def main():
     rng_kats(os.path.join(HERE, "rng_kats.json"))
     jobs = [("sparse_zi_100", 123456789, True), ("rmsc03", 123456789, False),
             ("rmsc03", 1008, True), ("rmsc03", 7, False), ("sparse_zi_1000", 123456789, False),
-            ("value_noise", 123456789, True), ("value_noise", 7, False),
-            ("random_fund_value", 123456789, False)]
+            ("value_noise", 123456789, True), ("value_noise", 7, False)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2]]
     procs = []
