@@ -150,3 +150,28 @@ def test_gpu_reset_reproduces(mx):
     m.reset()
     m.run()
     assert (m.summary()["hash"] == h1).all()
+
+
+@pytest.mark.parametrize("n", [1, 257])
+def test_gpu_odd_env_counts_equal_oracle(mx, n):
+    """a single env and a batch that fills no CU evenly (grid = n_envs, one wave per env)"""
+    seeds = (np.arange(n, dtype=np.int64) * 15485863 + 99) & 0xFFFFFFFF
+    m = mx.VecMarket("rmsc03", seeds)
+    m.run()
+    s = m.summary()
+    ev, hs, _ = pyoracle.run_batch("rmsc03", seeds.astype(np.uint32), threads=8)
+    assert (s["status"] == 1).all()
+    assert (s["events"] == ev).all() and (s["hash"] == hs).all()
+
+
+def test_gpu_launch_budget_then_resume(mx):
+    """mxa_run with a launch cap stops mid-episode; later launches finish it bit-exactly"""
+    seeds = [123456789, 7]
+    m = mx.VecMarket("rmsc03", seeds)
+    m.run(chunk=5000, max_launches=3)
+    s = m.summary()
+    assert (s["status"] == 0).all() and (s["events"] == 15000).all()
+    m.run()
+    s = m.summary()
+    ev, hs, _ = pyoracle.run_batch("rmsc03", np.array(seeds, dtype=np.uint32), threads=2)
+    assert (s["events"] == ev).all() and (s["hash"] == hs).all()

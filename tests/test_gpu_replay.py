@@ -84,3 +84,34 @@ def test_gpu_abidesenv_surface():
     obs, rew, done, info = env.step([0.0, 0.5, 0.5])
     assert rew is None and info is None and done == 0 and len(obs) == 9
     assert obs[0] == 760.0 and obs[1] == 100000.0
+
+
+def test_gpu_replay_truncated_goog_tape_equals_oracle():
+    """a short tape (first 3,000 GOOG records, 217 of them ORDER_ID 0): the replay agent runs
+    out of records early and DummyRL keeps trading against what is left"""
+    full = tape.Tape.load(os.path.join(GOLD, "tape_GOOG_2012-06-21.npz"))
+    k = 3000
+    tp = tape.Tape(full.t[:k], full.oid[:k], full.price[:k], full.size[:k], full.buy[:k])
+    n_envs = 6
+    rs = np.random.RandomState(11)
+    acts = np.stack([rs.uniform(0, 0.03, (761, n_envs)), rs.uniform(0, 1, (761, n_envs)),
+                     rs.uniform(0, 1, (761, n_envs))], 2)
+    v = VecABIDESEnv(tp, n_envs)
+    oras = [pyoracle.OracleGymEnv(tp) for _ in range(n_envs)]
+    done_o = [False] * n_envs
+    for i in range(761):
+        obs, done, valid, err = v.step(acts[i])
+        for e in range(n_envs):
+            if done_o[e]:
+                continue
+            o_obs, o_done, rc = oras[e].step(acts[i, e])
+            assert bool(err[e]) == (rc != 0), (i, e)
+            done_o[e] = o_done or rc != 0
+            if o_obs is not None and not err[e]:
+                np.testing.assert_allclose(obs[e], o_obs, rtol=OBS_RTOL, atol=1e-12, err_msg="step %d env %d" % (i, e))
+        if all(done_o):
+            break
+    s = v.summary()
+    for e in range(n_envs):
+        assert s["events"][e] == oras[e].events and s["hash"][e] == oras[e].hash, e
+        assert v.book(e, 0) == oras[e].book(0) and v.book(e, 1) == oras[e].book(1), e
