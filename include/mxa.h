@@ -17,6 +17,8 @@
  *   mxa_read_agents .... TradingAgent.holdings / orders (TradingAgent.py:45-46, 112-138)
  *   mxa_read_book ...... OrderBook.bids / asks (util/OrderBook.py:24-25, 377-398)
  *   mxa_read_trace ..... (parity tooling; no reference equivalent)
+ *   mxa_finalize ....... Kernel.runner's kernelStopping loop (Kernel.py:305-312): agents'
+ *                        FINAL_VALUATION, the summary log of Kernel.writeSummaryLog (Kernel.py:549-565)
  *   mxa_create_replay .. ABIDESEnv.__init__/reset (ABIDESEnv.py:8-57, 59-103), agent_config.py
  *                        Agents (Exchange, MarketReplayAgent on a LOBSTER tape, DummyRL),
  *                        LOBSTEROrdersProcessor output (MarketReplayAgent.py:162-220)
@@ -64,6 +66,15 @@ typedef struct {
   int64_t starting_cash; /* TradingAgent.starting_cash (the base of Kernel's mean ending value) */
 } mxa_agent_state;
 
+/* one agent's kernelStopping valuation (Kernel.runner's after-loop pass, Kernel.py:305-312) */
+typedef struct {
+  int64_t final_fundamental; /* oracle.observePrice(sym, currentTime, sigma_n=0) (ZI, Value), else 0 */
+  int64_t valuation_int;     /* FINAL_VALUATION when the reference logs an int (ZeroIntelligenceAgent) */
+  double valuation;          /* FINAL_VALUATION when it logs a float (NoiseAgent, ValueAgent) */
+  int32_t kind;              /* 0 no FINAL_VALUATION, 1 int, 2 float */
+  int32_t err;               /* nonzero where the reference raises: 1 KeyError (no known quote), 2 IndexError */
+} mxa_agent_final;
+
 /* configuration id + per-env seeds (the reference config's -s/--seed) */
 int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device,
                int32_t trace_cap, mxa_handle** out);
@@ -74,6 +85,13 @@ int mxa_launch(mxa_handle* h, int64_t max_pops);
 int mxa_sync(mxa_handle* h);
 /* launches of `chunk` pops until every env is done/errored (or max_launches reached) */
 int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launches_out);
+/* Kernel.runner's kernelStopping pass for every env once the run is over: the agents'
+ * FINAL_VALUATION entries of the summary log (ZeroIntelligenceAgent.py:80-112, NoiseAgent.py:44-68,
+ * ValueAgent.py:66-86), observing the oracle in agent order.  Idempotent (state is not saved);
+ * plain Kernel.runner configs only (MXA_EINVAL for GymKernel handles). */
+int mxa_finalize(mxa_handle* h);
+/* env's rows of the last mxa_finalize, one per agent (row 0, the exchange, is empty) */
+int mxa_read_final(mxa_handle* h, int32_t env, mxa_agent_final* out, int32_t cap);
 int mxa_read_summary(mxa_handle* h, mxa_env_summary* out /* [n_envs] */);
 int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t cap);
 /* book side 0 bids / 1 asks: levels best-first, FIFO within level; each order is

@@ -19,6 +19,7 @@ namespace {
 typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*,
                          const RpCtx*);
 typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*);
+typedef void (*stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, mxa_agent_final*);
 typedef void (*step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, const double*,
                         double*, int32_t*);
 
@@ -31,6 +32,11 @@ template <int CFG>
 void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
                 const RpCtx* ctx) {
   hipLaunchKernelGGL((mxa_run_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx);
+}
+
+template <int CFG>
+void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, mxa_agent_final* out) {
+  hipLaunchKernelGGL((mxa_stop_kernel<CFG>), g, b, lds, s, base, stride, n, out);
 }
 
 #ifndef MXA_ONLY_RMSC03
@@ -70,6 +76,8 @@ struct mxa_handle {
   build_fn build = nullptr;
   run_fn run = nullptr;
   step_fn step = nullptr;  // GymKernel handles (replay, rmsc03_rl)
+  stop_fn stop = nullptr;  // kernelStopping pass (plain Kernel.runner configs)
+  mxa_agent_final* d_final = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
   std::string err;
@@ -101,6 +109,7 @@ template <int CFG>
 static void bind(mxa_handle* h) {
   h->build = launch_build<CFG>;
   h->run = launch_run<CFG>;
+  h->stop = launch_stop<CFG>;
   h->lds = mxa_cfg::lds_bytes(CFG);
 #ifndef MXA_ONLY_RMSC03
   if constexpr (CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL) {
@@ -385,6 +394,25 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   return MXA_OK;
 }
 
+int mxa_finalize(mxa_handle* h) {
+  if (!h || h->gym || !h->stop) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t rows = (size_t)h->P.n_envs * h->P.n_agents;
+  if (!h->d_final) HIPCHK(h, hipMalloc(&h->d_final, rows * sizeof(mxa_agent_final)));
+  h->stop(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_final);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_read_final(mxa_handle* h, int32_t env, mxa_agent_final* out, int32_t cap) {
+  if (!h || !h->d_final || env < 0 || env >= h->P.n_envs || !out || cap < h->P.n_agents) return MXA_EINVAL;
+  HIPCHK(h, hipMemcpyAsync(out, h->d_final + (size_t)env * h->P.n_agents, sizeof(mxa_agent_final) * h->P.n_agents,
+                           hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return h->P.n_agents;
+}
+
 int mxa_read_summary(mxa_handle* h, mxa_env_summary* out) {
   if (!h || !out) return MXA_EINVAL;
   int n = h->P.n_envs;
@@ -547,6 +575,7 @@ void mxa_destroy(mxa_handle* h) {
   if (h->d_act) hipFree(h->d_act);
   if (h->d_obs) hipFree(h->d_obs);
   if (h->d_flags) hipFree(h->d_flags);
+  if (h->d_final) hipFree(h->d_final);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
   if (h->own) hipStreamDestroy(h->own);

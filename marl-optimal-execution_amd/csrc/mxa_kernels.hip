@@ -2275,6 +2275,76 @@ struct Eng {
     }
   }
 
+  // ---------------- Kernel.runner after the loop: kernelStopping per agent in id order
+  // (Kernel.py:305-312).  FINAL_VALUATION of ZI (ZeroIntelligenceAgent.py:80-112), Noise
+  // (NoiseAgent.py:44-68) and Value (ValueAgent.py:66-86) agents; ZI and Value observe the
+  // oracle at their own currentTime (the last event they handled = agentCurrentTimes minus
+  // their computation delay) with sigma_n = 0, advancing it in agent order.
+  DEV static i64 round_hundreds(i64 x) {  // int(round(x, -2) / 100), Python half-to-even
+    i64 q = x / 100, r = x % 100;
+    if (r < 0) {
+      r += 100;
+      q -= 1;
+    }
+    if (r > 50 || (r == 50 && (q & 1))) q += 1;
+    return q;
+  }
+  DEV void stop(mxa_agent_final* out) {
+    for (int a = 1; a < PC.n_agents; a++) {
+      rec_load(a);
+      const int ty = rgi(AF_TYPE);
+      mxa_agent_final f;
+      f.final_fundamental = 0;
+      f.valuation_int = 0;
+      f.valuation = 0.0;
+      f.kind = 0;
+      f.err = 0;
+      const i64 cash = rg64(AF_CASH), start = rg64(AF_START_CASH);
+      const i64 H = round_hundreds(rg64(AF_SHARES));
+      const u32 fl = flags();
+      if (ty == AG_NOISE) {
+        f.kind = 2;
+        if (!(fl & FL_HAS_KNOWN)) {
+          f.err = 1;
+        } else if ((fl & FL_NB) && (fl & FL_NA) && rgi(AF_BID) != 0 && rgi(AF_ASK) != 0) {
+          const double rT = (double)((i64)rgi(AF_BID) + rgi(AF_ASK)) / 2.0;  // int(bid + ask) / 2
+          f.valuation = (rT * (double)H + (double)(cash - start)) / (double)start;
+        } else if (!(fl & FL_HAS_LAST)) {
+          f.err = 1;
+        } else if (fl & FL_LAST_FLOAT) {  // rT = last_trade[symbol], a python float
+          f.valuation = ((double)rg64(AF_LAST_TRADE) * (double)H + (double)(cash - start)) / (double)start;
+        } else {
+          f.valuation = (double)(rg64(AF_LAST_TRADE) * H + cash - start) / (double)start;
+        }
+      } else if (ty == AG_VALUE || ty == AG_ZI) {
+        const i64 rT = o_observe(rg64(AF_ATIME) - rg64(AF_COMP), 0.0);
+        if (dirty) rng_maint();
+        f.final_fundamental = rT;
+        if (ty == AG_VALUE) {
+          f.kind = 2;
+          f.valuation = (double)(rT * H + cash - start) / (double)start;
+        } else {
+          f.kind = 1;
+          const int nq = 2 * PC.zi_qmax;
+          i64 s = 0;
+          if (H > nq - PC.zi_qmax || H < -nq - PC.zi_qmax) {
+            f.err = 2;  // theta[x + q_max - 1] outside [-2 q_max, 2 q_max) (IndexError)
+          } else if (H > 0) {
+            for (i64 x = 1; x <= H; x++) s += rgi(AF_THETA + (int)(x + PC.zi_qmax - 1));
+          } else if (H < 0) {
+            for (i64 x = H + 1; x <= 0; x++) {
+              i64 i = x + PC.zi_qmax - 1;
+              s -= rgi(AF_THETA + (int)(i < 0 ? i + nq : i));  // Python negative indices wrap
+            }
+          }
+          f.valuation_int = s + rT * H + cash - start;
+        }
+      }
+      if (lane == 0) out[a] = f;
+    }
+    if (lane == 0) out[0] = mxa_agent_final{0, 0, 0.0, 0, 0};
+  }
+
   // ---------------- state save/restore around a launch
   DEV void hdr_from_global() {
     const u64* src = (const u64*)hdr();
@@ -2815,6 +2885,16 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
 #endif
 }
 
+template <int CFG>
+__global__ __launch_bounds__(64) void mxa_stop_kernel(char* base, uint64_t stride, int n_envs, mxa_agent_final* out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int env = blockIdx.x;
+  if (env >= n_envs) return;
+  mxa::Eng<CFG> g(base + (size_t)env * stride, lds, 0, nullptr);
+  g.load();
+  g.stop(out + (size_t)env * mxa::Eng<CFG>::PC.n_agents);  // no save(): the pass is idempotent
+}
+
 #ifndef MXA_ONLY_RMSC03
 // ABIDESEnv.step for every env: DummyRL.place_orders(action), then the GymKernel loop until
 // the RL agent's spread reply (end of step) or the end of the episode.  obs [n][9] float64;
@@ -2888,7 +2968,8 @@ __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y
 // explicit instantiations per supported configuration
 #define MXA_INST(CFG)                                                                                      \
   template __global__ void mxa_build_kernel<CFG>(char*, uint64_t, int, const uint32_t*, const uint8_t*, const RpCtx*); \
-  template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*);
+  template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*);               \
+  template __global__ void mxa_stop_kernel<CFG>(char*, uint64_t, int, mxa_agent_final*);
 MXA_INST(MXA_CFG_RMSC03)
 #ifndef MXA_ONLY_RMSC03
 MXA_INST(MXA_CFG_SPARSE_ZI_100)

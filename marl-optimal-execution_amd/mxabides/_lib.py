@@ -34,11 +34,16 @@ class AgentState(ctypes.Structure):
                 ("starting_cash", ctypes.c_int64)]
 
 
+class AgentFinal(ctypes.Structure):  # mxa_agent_final
+    _fields_ = [("final_fundamental", ctypes.c_int64), ("valuation_int", ctypes.c_int64), ("valuation", ctypes.c_double),
+                ("kind", ctypes.c_int32), ("err", ctypes.c_int32)]
+
+
 EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_read_summary", "mxa_read_agents",
            "mxa_read_book", "mxa_read_trace", "mxa_n_agents", "mxa_n_envs", "mxa_env_bytes", "mxa_set_stream",
            "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe",
            "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout", "mxa_create_replay", "mxa_step",
-           "mxa_step_device"]
+           "mxa_step_device", "mxa_finalize", "mxa_read_final"]
 
 _lib = None
 
@@ -84,5 +89,7 @@ def load():
     L.mxa_create_replay.argtypes = [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)]
     L.mxa_step.argtypes = [P, P, P, P]
     L.mxa_step_device.argtypes = [P, P, P, P]
+    L.mxa_finalize.argtypes = [P]
+    L.mxa_read_final.argtypes = [P, I32, P, I32]
     _lib = L
     return L

@@ -5,6 +5,7 @@ abides.py:19-29 -> config/<config>.py -> Kernel.runner, Kernel.py:50-345): every
 one reference simulation with its own seed, all simulated by libmxa's HIP kernels.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -38,6 +39,7 @@ class VecMarket:
 
     # ---- lifecycle
     def reset(self, mask=None):
+        self._finalized = False
         m = None
         if mask is not None:
             m = np.ascontiguousarray(mask, dtype=np.uint8)
@@ -64,6 +66,7 @@ class VecMarket:
         self._check(self.L.mxa_sync(self._h), "mxa_sync")
 
     def run(self, chunk=CHUNK_DEFAULT, max_launches=0):
+        self._finalized = False
         n = ctypes.c_int32()
         self._check(self.L.mxa_run(self._h, chunk, max_launches, ctypes.byref(n)), "mxa_run")
         return n.value
@@ -146,6 +149,53 @@ class VecMarket:
             counts[t] += 1
         means = ["%s: %d" % (t, int(round(gains[t] / counts[t]))) for t in order]
         return lines, means
+
+    SUMMARY_EVENTS = ("STARTING_CASH", "FINAL_CASH_POSITION", "ENDING_CASH", "FINAL_VALUATION")
+
+    def finalize(self):
+        """Kernel.runner's kernelStopping pass (Kernel.py:305-312) for every env, once the run is
+        over: the agents' FINAL_VALUATION (oracle observed in agent order).  Idempotent."""
+        self._check(self.L.mxa_finalize(self._h), "mxa_finalize")
+        self._finalized = True
+
+    def summary_log(self, env):
+        """Kernel.summaryLog (Kernel.py:549-554) of one env as the reference builds it: STARTING_CASH
+        of every trading agent (TradingAgent.kernelStarting, TradingAgent.py:101), then per agent
+        FINAL_CASH_POSITION and ENDING_CASH (TradingAgent.py:118-123) and the FINAL_VALUATION of
+        ZI / Noise / Value agents.  Rows are dicts AgentID, AgentStrategy, EventType, Event; Event
+        is an int or a float exactly where the reference logs one."""
+        if not getattr(self, "_finalized", False):
+            self.finalize()
+        fin = (_lib.AgentFinal * self.n_agents)()
+        self._check(self.L.mxa_read_final(self._h, env, fin, self.n_agents), "mxa_read_final")
+        tnames = agent_type_names(self.config)
+        ag = self.agents(env)
+        FL_LAST_FLOAT = 1024
+        rows = [dict(AgentID=a, AgentStrategy=tnames[a], EventType="STARTING_CASH", Event=int(ag[a]["starting_cash"]))
+                for a in range(1, self.n_agents)]
+        for a in range(1, self.n_agents):
+            st, f = ag[a], fin[a]
+            if f.err:
+                raise _lib.MxaError("env %d agent %d: the reference raises in kernelStopping (%s)"
+                                    % (env, a, "KeyError" if f.err == 1 else "IndexError"))
+            mtm = st["cash"] + (st["last_trade"] * st["shares"] if st["shares"] else 0)
+            flt = bool(st["shares"]) and bool(st["flags"] & FL_LAST_FLOAT)
+            rows.append(dict(AgentID=a, AgentStrategy=tnames[a], EventType="FINAL_CASH_POSITION", Event=int(st["cash"])))
+            rows.append(dict(AgentID=a, AgentStrategy=tnames[a], EventType="ENDING_CASH",
+                             Event=float(mtm) if flt else int(mtm)))
+            if f.kind:
+                rows.append(dict(AgentID=a, AgentStrategy=tnames[a], EventType="FINAL_VALUATION",
+                                 Event=int(f.valuation_int) if f.kind == 1 else float(f.valuation)))
+        return rows
+
+    def write_summary_log(self, env, log_dir):
+        """Kernel.writeSummaryLog (Kernel.py:556-565): log_dir/summary_log.bz2, a pandas DataFrame
+        pickled with bz2 compression, as cli/stats.py and cli/read_agent_logs.py read it."""
+        import pandas as pd
+        os.makedirs(log_dir, exist_ok=True)
+        path = os.path.join(log_dir, "summary_log.bz2")
+        pd.DataFrame(self.summary_log(env)).to_pickle(path, compression="bz2")
+        return path
 
     def close(self):
         if self._h:

@@ -291,6 +291,13 @@ struct ora_env {
     int64_t st_max_heap, st_max_resting, st_max_open, st_resting, st_max_hist_tx;
     char* report;
     int64_t report_len;
+    /* Kernel.summaryLog: (agent, event type, int or float value) rows */
+    int nsum;
+    int* sum_agent;
+    int* sum_type;  /* 0 STARTING_CASH, 1 FINAL_CASH_POSITION, 2 ENDING_CASH, 3 FINAL_VALUATION */
+    int* sum_isf;
+    int64_t* sum_i;
+    double* sum_f;
     int ex_has_last; /* OrderBook.last_trade is not None */
     /* ---- marketreplay / ABIDESEnv (GymKernel) ---- */
     int gym;
@@ -1645,6 +1652,76 @@ static void rep_append(ora_env* e, const char* s) {
     e->report[e->report_len] = 0;
 }
 
+/* Kernel.appendSummaryLog (Kernel.py:549-554) */
+static void sum_add(ora_env* e, int agent, int type, int isf, int64_t vi, double vf) {
+    int k = e->nsum++;
+    e->sum_agent = (int*)realloc(e->sum_agent, sizeof(int) * e->nsum);
+    e->sum_type = (int*)realloc(e->sum_type, sizeof(int) * e->nsum);
+    e->sum_isf = (int*)realloc(e->sum_isf, sizeof(int) * e->nsum);
+    e->sum_i = (int64_t*)realloc(e->sum_i, sizeof(int64_t) * e->nsum);
+    e->sum_f = (double*)realloc(e->sum_f, sizeof(double) * e->nsum);
+    e->sum_agent[k] = agent;
+    e->sum_type[k] = type;
+    e->sum_isf[k] = isf;
+    e->sum_i[k] = vi;
+    e->sum_f[k] = vf;
+}
+/* int(round(shares, -2) / 100): Python int rounding to hundreds, half to even */
+static int64_t round_hundreds(int64_t x) {
+    int64_t q = x / 100, r = x % 100;
+    if (r < 0) { r += 100; q -= 1; } /* floor divmod */
+    if (r > 50 || (r == 50 && (q & 1))) q += 1;
+    return q;
+}
+/* the FINAL_VALUATION of ZeroIntelligenceAgent.kernelStopping (ZeroIntelligenceAgent.py:80-112),
+ * NoiseAgent.kernelStopping (NoiseAgent.py:44-68) and ValueAgent.kernelStopping
+ * (ValueAgent.py:66-86), in Kernel.runner's agent order (the oracle advances as it goes) */
+static void final_valuation(ora_env* e, agent_t* a) {
+    int64_t H = round_hundreds(a->shares);
+    if (a->type == AG_NOISE) {
+        int64_t si;
+        double sf;
+        int isf;
+        if (!a->has_known) { fail(e, -9, "NoiseAgent.kernelStopping: no known quote (KeyError)"); return; }
+        if (a->nb && a->na && a->bid && a->ask) { /* rT = int(bid + ask) / 2 (a float) */
+            sf = (double)(a->bid + a->ask) / 2.0 * (double)H;
+            isf = 1;
+            si = 0;
+        } else { /* rT = last_trade[symbol] */
+            if (!a->has_last_trade) { fail(e, -9, "NoiseAgent.kernelStopping: no last trade (KeyError)"); return; }
+            isf = a->last_trade_float;
+            si = a->last_trade * H;
+            sf = (double)a->last_trade * (double)H;
+        }
+        double v = isf ? (sf + (double)(a->cash - a->starting_cash)) / (double)a->starting_cash
+                       : (double)(si + a->cash - a->starting_cash) / (double)a->starting_cash;
+        sum_add(e, a->id, 3, 1, 0, v);
+    } else if (a->type == AG_VALUE) {
+        int64_t rT = o_observe(e, a->cur_time, 0, NULL);
+        sum_add(e, a->id, 3, 1, 0, (double)(rT * H + a->cash - a->starting_cash) / (double)a->starting_cash);
+    } else if (a->type == AG_ZI) {
+        int64_t rT = o_observe(e, a->cur_time, 0, NULL);
+        int64_t s = 0;
+        int nq = 2 * a->q_max;
+        if (H > 0) {
+            for (int64_t x = 1; x <= H; x++) {
+                int64_t i = x + a->q_max - 1;
+                if (i >= nq) { fail(e, -10, "ZeroIntelligenceAgent.kernelStopping: theta index (IndexError)"); return; }
+                s += a->theta[i];
+            }
+        } else if (H < 0) {
+            for (int64_t x = H + 1; x <= 0; x++) {
+                int64_t i = x + a->q_max - 1;
+                if (i < -nq) { fail(e, -10, "ZeroIntelligenceAgent.kernelStopping: theta index (IndexError)"); return; }
+                s -= a->theta[i < 0 ? i + nq : i]; /* Python negative indices wrap */
+            }
+        }
+        s += rT * H;
+        s += a->cash - a->starting_cash;
+        sum_add(e, a->id, 3, 0, s, 0);
+    }
+}
+
 /* TradingAgent.kernelStopping (TradingAgent.py:112-138) + Kernel mean print (Kernel.py:337-341) */
 int ora_finish(ora_env* e) {
     char line[512];
@@ -1654,6 +1731,9 @@ int ora_finish(ora_env* e) {
     long long* gains = (long long*)malloc(sizeof(long long) * (size_t)e->n);
     int* counts = (int*)malloc(sizeof(int) * (size_t)e->n);
     int nt = 0;
+    /* TradingAgent.kernelStarting logged STARTING_CASH for every trading agent (TradingAgent.py:101) */
+    e->nsum = 0;
+    for (int i = 1; i < e->n; i++) sum_add(e, i, 0, 0, e->ag[i].starting_cash, 0);
     for (int i = 1; i < e->n; i++) {
         agent_t* a = &e->ag[i];
         char hold[128];
@@ -1665,6 +1745,9 @@ int ora_finish(ora_env* e) {
             mtm += (long long)a->last_trade * a->shares;
             mtm_float = a->last_trade_float;
         }
+        sum_add(e, i, 1, 0, a->cash, 0);
+        sum_add(e, i, 2, mtm_float, mtm, (double)mtm);
+        final_valuation(e, a);
         if (mtm_float) snprintf(line, sizeof line, "Final holdings for %s: %s.  Marked to market: %lld.0", a->name, hold, mtm);
         else snprintf(line, sizeof line, "Final holdings for %s: %s.  Marked to market: %lld", a->name, hold, mtm);
         rep_append(e, line);
@@ -2171,6 +2254,18 @@ int64_t ora_book(const ora_env* e, int side, int64_t* buf, int64_t cap) {
     return k;
 }
 int64_t ora_order_counter(const ora_env* e) { return e->order_counter; }
+const char* ora_agent_type_name(const ora_env* e, int id) { return id >= 0 && id < e->n ? e->ag[id].tname : ""; }
+/* Kernel.summaryLog rows after ora_finish; returns the row count (copies at most cap rows) */
+int ora_summary(const ora_env* e, int* agent, int* type, int* isf, int64_t* vi, double* vf, int cap) {
+    for (int k = 0; k < e->nsum && k < cap; k++) {
+        agent[k] = e->sum_agent[k];
+        type[k] = e->sum_type[k];
+        isf[k] = e->sum_isf[k];
+        vi[k] = e->sum_i[k];
+        vf[k] = e->sum_f[k];
+    }
+    return e->nsum;
+}
 /* capacity statistics: max pending events, max resting orders, max open orders of one agent,
  * max live transaction records */
 void ora_stats(const ora_env* e, int64_t* out) {

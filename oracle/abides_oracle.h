@@ -62,6 +62,10 @@ int64_t ora_book(const ora_env* e, int side, int64_t* buf, int64_t cap);
 int64_t ora_order_counter(const ora_env* e);
 int64_t ora_last_trade(const ora_env* e);
 void ora_stats(const ora_env* e, int64_t* out);
+/* Kernel.summaryLog after ora_finish: (agent, type 0 STARTING_CASH / 1 FINAL_CASH_POSITION /
+ * 2 ENDING_CASH / 3 FINAL_VALUATION, is-float, int value, float value); returns the row count */
+const char* ora_agent_type_name(const ora_env* e, int id); /* Agent.type (the summary's AgentStrategy) */
+int ora_summary(const ora_env* e, int* agent, int* type, int* isf, int64_t* vi, double* vf, int cap);
 /* stdout restatement after ora_finish: "Final holdings ..." lines then "Mean..." lines */
 int64_t ora_report(const ora_env* e, char* buf, int64_t cap);
 

@@ -148,6 +148,23 @@ class OracleEnv:
     def last_trade(self):
         return lib().ora_last_trade(self._h)
 
+    SUMMARY_EVENTS = ["STARTING_CASH", "FINAL_CASH_POSITION", "ENDING_CASH", "FINAL_VALUATION"]
+
+    def summary_log(self):
+        """Kernel.summaryLog rows after finish(): dicts with AgentID, AgentStrategy, EventType, Event
+        (Event an int or a float exactly as the reference logs it)."""
+        L = lib()
+        L.ora_summary.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5 + [ctypes.c_int]
+        L.ora_agent_type_name.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.ora_agent_type_name.restype = ctypes.c_char_p
+        n = L.ora_summary(self._h, None, None, None, None, None, 0)
+        ag, ty, isf = (np.zeros(n, dtype=np.int32) for _ in range(3))
+        vi, vf = np.zeros(n, dtype=np.int64), np.zeros(n, dtype=np.float64)
+        L.ora_summary(self._h, ag.ctypes.data, ty.ctypes.data, isf.ctypes.data, vi.ctypes.data, vf.ctypes.data, n)
+        return [{"AgentID": int(a), "AgentStrategy": L.ora_agent_type_name(self._h, int(a)).decode(),
+                 "EventType": self.SUMMARY_EVENTS[t], "Event": float(f) if s else int(i)}
+                for a, t, s, i, f in zip(ag, ty, isf, vi, vf)]
+
     def report(self):
         L = lib()
         n = L.ora_report(self._h, None, 0)

@@ -23,6 +23,7 @@ pandas 2 API renames (`pandas.io.json.json_normalize`, `SparseDataFrame`), and t
 bz2 log writers are no-ops.  None of them touches the simulated arithmetic.
 
 Usage:  python tests/golden/gen_fixtures.py all          (writes tests/golden/*.npz/json)
+        python tests/golden/gen_fixtures.py summaries    (only the *_summary.json summary logs)
         python tests/golden/gen_fixtures.py run CFG SEED OUT [--full]
 """
 import importlib
@@ -159,6 +160,7 @@ def encode(t_rel, recipient, mtype, msg):
 
 MIDNIGHT = 0
 TRACE = []
+SUMMARY_ONLY = False
 
 
 def install_stubs():
@@ -263,6 +265,14 @@ def run_config(cfg, seed, out, full):
             hs.append(h)
     final["hash"] = "%016x" % h
     final["hash_checkpoints"] = ["%016x" % x for x in hs]
+    # Kernel.summaryLog (Kernel.py:549-554): what writeSummaryLog pickles to summary_log.bz2
+    summary = [{"AgentID": int(r["AgentID"]), "AgentStrategy": r["AgentStrategy"], "EventType": r["EventType"],
+                "Event": r["Event"] if isinstance(r["Event"], (int, float)) else str(r["Event"])}
+               for r in kern.summaryLog]
+    with open(out + "_summary.json", "w") as f:
+        json.dump(summary, f, indent=0)
+    if SUMMARY_ONLY:
+        return
     with open(out + ".json", "w") as f:
         json.dump(final, f, indent=0)
     keep = tr if full else tr[:20000]
@@ -307,11 +317,19 @@ def rng_kats(path):
 
 
 def main():
+    global SUMMARY_ONLY
     if sys.argv[1] == "run":
+        SUMMARY_ONLY = "--summary-only" in sys.argv
         run_config(sys.argv[2], int(sys.argv[3]), sys.argv[4], "--full" in sys.argv)
         return
+    if sys.argv[1] == "summaries":  # only the summary logs (<cfg>_<seed>_summary.json)
+        sys.argv[1] = "all"
+        extra = ["--summary-only"]
+    else:
+        extra = []
     assert sys.argv[1] == "all"
-    rng_kats(os.path.join(HERE, "rng_kats.json"))
+    if not extra:
+        rng_kats(os.path.join(HERE, "rng_kats.json"))
     jobs = [("sparse_zi_100", 123456789, True), ("rmsc03", 123456789, False),
             ("rmsc03", 1008, True), ("rmsc03", 7, False), ("sparse_zi_1000", 123456789, False),
             ("value_noise", 123456789, True), ("value_noise", 7, False)]
@@ -320,7 +338,7 @@ def main():
     procs = []
     for cfg, seed, full in jobs:
         out = os.path.join(HERE, "%s_%d" % (cfg, seed))
-        cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out] + (["--full"] if full else [])
+        cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out] + (["--full"] if full else []) + extra
         wd = tempfile.mkdtemp(prefix="gf_")
         procs.append((cfg, seed, subprocess.Popen(cmd, cwd=wd, env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))))
     for cfg, seed, p in procs:

@@ -175,3 +175,37 @@ def test_gpu_launch_budget_then_resume(mx):
     s = m.summary()
     ev, hs, _ = pyoracle.run_batch("rmsc03", np.array(seeds, dtype=np.uint32), threads=2)
     assert (s["events"] == ev).all() and (s["hash"] == hs).all()
+
+
+@pytest.mark.parametrize("cfg,seed", FIXTURES)
+def test_gpu_summary_log_matches_reference(mx, cfg, seed, tmp_path):
+    """mxa_finalize (Kernel.runner's kernelStopping pass) + the host summary log equal the
+    reference's Kernel.summaryLog; the bz2 pickle round-trips as cli/stats.py reads it"""
+    import pandas as pd
+    with open(os.path.join(os.path.dirname(__file__), "golden", "%s_%d_summary.json" % (cfg, seed))) as f:
+        ref = json.load(f)
+    m = mx.VecMarket(cfg, [seed])
+    m.run()
+    got = m.summary_log(0)
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert a == b and type(a["Event"]) is type(b["Event"]), (a, b)
+    m.finalize()  # idempotent: the pass does not save the oracle's advance
+    assert m.summary_log(0) == got
+    df = pd.read_pickle(m.write_summary_log(0, str(tmp_path)), compression="bz2")
+    assert list(df.columns) == ["AgentID", "AgentStrategy", "EventType", "Event"] and len(df) == len(ref)
+
+
+@pytest.mark.parametrize("cfg,n", [("rmsc03", 64), ("sparse_zi_100", 16), ("value_noise", 64)])
+def test_gpu_summary_log_batch_equals_oracle(mx, cfg, n):
+    seeds = (np.arange(n, dtype=np.int64) * 7919 + 11) & 0xFFFFFFFF
+    m = mx.VecMarket(cfg, seeds)
+    m.run()
+    m.finalize()
+    for i, s in enumerate(seeds):
+        o = pyoracle.OracleEnv(cfg, int(s))
+        o.run()
+        o.finish()
+        ref = o.summary_log()
+        got = m.summary_log(i)
+        assert got == ref, (cfg, int(s))

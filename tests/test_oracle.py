@@ -72,3 +72,19 @@ def test_oracle_batch_runner_deterministic():
         e = pyoracle.OracleEnv("rmsc03", int(s))
         e.run()
         assert e.events == ev1[i] and e.hash == h1[i]
+
+
+@pytest.mark.parametrize("cfg,seed", FIXTURES)
+def test_oracle_summary_log_matches_reference(cfg, seed):
+    """Kernel.summaryLog (what writeSummaryLog pickles): STARTING_CASH, FINAL_CASH_POSITION,
+    ENDING_CASH and the agents' FINAL_VALUATION, int/float types included"""
+    with open(os.path.join(os.path.dirname(__file__), "golden", "%s_%d_summary.json" % (cfg, seed))) as f:
+        ref = json.load(f)
+    e = pyoracle.OracleEnv(cfg, seed)
+    e.run()
+    e.finish()
+    got = e.summary_log()
+    assert e.error[0] == 0
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert a == b and type(a["Event"]) is type(b["Event"]), (a, b)
