@@ -254,6 +254,91 @@ def rl_bench(args):
         dist.destroy_process_group()
 
 
+def ddqn_bench(args):
+    """rmsc03 + DummyRL (BASELINE configs[3]) with the DDQN execution learner in the loop
+    (mxabides.ddqn: the reference's DDQLearningExecutionAgent learner on PyTorch-ROCm): every
+    env's actions come from the shared Q-network (epsilon-greedy), transitions go to the device
+    replay ring and the learner trains every 5 periods, as the reference agent does. One bench
+    step = one full episode of every env (config build + 27 gym steps + learner) + the RCCL
+    all-gather of the episode records. Learner state persists across bench steps."""
+    from mxabides import ddqn
+    from mxabides.gym import VecABIDESEnv
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n = args.envs
+    v = VecABIDESEnv(seeds=shard.env_seeds(0, rank, world, n), device=local)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    v.set_stream(stream.cuda_stream)
+    learner = ddqn.DDQNLearner(device="cuda", seed=1000 + rank, batch_size=args.ddqn_batch)
+    task = ddqn.ExecutionTask(device="cuda")
+    res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    timing = []
+
+    def episode(k, timed):
+        r = ddqn.run_episode(v, learner, task, seeds=shard.env_seeds(k, rank, world, n),
+                             timing=timing if timed else None)
+        v.write_results(res.data_ptr())
+        shard.gather_records(res, world)
+        return res[:, 0].sum(), r["steps"]
+
+    for k in range(args.warmup):
+        episode(k, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    learns0 = learner.learn_step_counter
+    t0 = time.perf_counter()
+    ev = torch.zeros((), dtype=torch.int64, device="cuda")
+    gym_steps = 0
+    for k in range(args.warmup, args.warmup + args.steps):
+        e, ns = episode(k, True)
+        ev += e
+        gym_steps += ns
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    elt = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+    el = float(elt.item())
+    events = int(ev.item())
+    s = v.summary()
+    if rank == 0:
+        kms = [a.elapsed_time(b) for a, b in timing]
+        avg_ms = sum(kms) / len(kms)
+        my_ev_per_launch = events / world / len(kms)
+        achieved = ALGO_BYTES_PER_EVENT * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
+        out = {"metric": "env-steps/sec, rmsc03 + DDQN execution learner (GymKernel) x%d envs per GPU" % n,
+               "value": events / el, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "int64 (market), fp32 (Q-network)",
+               "data": "synthetic (seeds); actions from the DDQN learner",
+               "config": {"workload": "rmsc03_rl x%d envs per GPU + DDQN learner (NNModel_1, batch %d, train every "
+                                      "5 periods), full episode per bench step, seeds %d+global_env"
+                                      % (n, args.ddqn_batch, SEED0),
+                          "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": v.n_agents,
+                          "gym_steps_per_s": n * world * gym_steps / el,
+                          "learn_steps": learner.learn_step_counter - learns0,
+                          "step_kernel_ms_total": sum(kms), "wall_ms_total": 1000.0 * el,
+                          "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
+                          "env_errors": int((s["status"] == 2).sum())},
+               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                            "kernel": "mxa_step_kernel<4> (rmsc03_rl)", "avg_launch_ms": avg_ms, "launches": len(kms),
+                            "algo_bytes_per_event": ALGO_BYTES_PER_EVENT}}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,12 +349,15 @@ def main():
     ap.add_argument("--chunk", type=int, default=1 << 22, help="max pops per env per kernel launch")
     ap.add_argument("--cpu-envs", type=int, default=2048, help="CPU-baseline sample size (envs)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--ddqn-batch", type=int, default=32, help="rmsc03_ddqn: learner batch size (reference 32)")
     ap.add_argument("--tape", default=None, help="marketreplay tape under tests/golden (IBM_2003-01-14, GOOG_2012-06-21)")
     args = ap.parse_args()
     if args.config == "marketreplay":
         return replay_bench(args)
     if args.config == "rmsc03_rl":
         return rl_bench(args)
+    if args.config == "rmsc03_ddqn":
+        return ddqn_bench(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -130,6 +130,14 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
 int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags);
 /* the same on device arrays, asynchronous on the handle's stream */
 int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32_t* d_flags);
+/* the execution agent's state after the last step, for a learner on the device (the reward
+ * inputs of DDQLearningExecutionAgent.compute_reward, ddqlearning_execution_agent.py:409-446):
+ * DEVICE array [n_envs][MXA_RL_STATE_WORDS] float64 = (CASH, holdings, executed quantity,
+ * best bid, best ask, best-bid size, best-ask size, lob flags: 1 bids, 2 asks) of
+ * DummyRLExecutionAgent, the LOB being the newest ABIDESEnvMetrics entry (dummy_rl:294-315).
+ * Asynchronous on the handle's stream; GymKernel handles only. */
+#define MXA_RL_STATE_WORDS 8
+int mxa_write_rl_state(mxa_handle* h, double* device_out);
 
 /* parity probes: device numpy-legacy RNG (mode 0 u32, 1 double, 2 randint(a,b),
  * 3 normal(a,b), 4 exponential(a), 5 uniform(a,b)) and device glibc math

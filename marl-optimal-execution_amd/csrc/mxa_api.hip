@@ -62,6 +62,35 @@ __global__ void mxa_results_kernel(const char* base, uint64_t stride, int n, int
   out[4 * i + 3] = h->cur;
 }
 
+// execution-agent state after a step, for a learner on the device: [n][MXA_RL_STATE_WORDS]
+// doubles = (CASH, holdings, executed qty, best bid, best ask, bid size, ask size, lob flags)
+// of DummyRLExecutionAgent (TradingAgent.holdings, ExecutionAgent.executed quantity,
+// ABIDESEnvMetrics' newest LOB: dummy_rl:294-315, execution_agent.py:88-100)
+__global__ void mxa_rl_state_kernel(const char* base, uint64_t stride, int n, uint32_t off_rec, uint64_t off_rh,
+                                    uint64_t off_ring, double* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const char* e = base + (size_t)i * stride;
+  const uint32_t* r = (const uint32_t*)(e + off_rec);
+  const RpHdr* R = (const RpHdr*)(e + off_rh);
+  const RpLob* L = (const RpLob*)(e + off_ring);
+  auto g64 = [&](int f) { return (int64_t)(((uint64_t)r[f + 1] << 32) | r[f]); };
+  double* o = out + (size_t)MXA_RL_STATE_WORDS * i;
+  o[0] = (double)g64(AF_CASH);
+  o[1] = (double)g64(AF_SHARES);
+  o[2] = (double)R->rl_exec;
+  if (R->m_cnt > 0) {
+    const RpLob l = L[R->m_head];
+    o[3] = (double)l.bid;
+    o[4] = (double)l.ask;
+    o[5] = (double)R->m_bq;
+    o[6] = (double)R->m_aq;
+    o[7] = (double)(l.flags & 3);
+  } else {
+    o[3] = o[4] = o[5] = o[6] = o[7] = 0.0;
+  }
+}
+
 }  // namespace
 
 struct mxa_handle {
@@ -532,6 +561,16 @@ int mxa_write_results(mxa_handle* h, void* device_out) {
   int n = h->P.n_envs;
   hipLaunchKernelGGL(mxa_results_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env, h->P.L.env_stride,
                      n, (int64_t*)device_out);
+  HIPCHK(h, hipGetLastError());
+  return MXA_OK;
+}
+
+int mxa_write_rl_state(mxa_handle* h, double* device_out) {
+  if (!h || !device_out || !h->gym || h->P.n_rl != 1) return MXA_EINVAL;
+  int n = h->P.n_envs;
+  hipLaunchKernelGGL(mxa_rl_state_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env, h->P.L.env_stride,
+                     n, (uint32_t)(h->P.L.off_ag + 512u * (uint32_t)h->P.first_rl), h->ctx.L.off_rh, h->ctx.L.off_ring,
+                     device_out);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
 }

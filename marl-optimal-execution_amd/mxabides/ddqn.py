@@ -1,0 +1,328 @@
+"""DDQN optimal-execution learner on PyTorch-ROCm, fed by the MI355X market step.
+
+Restates the reference's DDQLearningExecutionAgent learner (agent/execution/qlearning/
+ddqlearning_execution_agent.py, TensorFlow 2.1 / Keras, requirements.txt:17) for thousands of
+parallel envs on one device:
+
+* the 24-action table: SIZE_ALLOCATION x SIZE_SCALE (ddqlearning_execution_agent.py:21-37);
+* the state: `discretize([time_remaining, qty_remaining, ...], grid)` on a 200 x 200 uniform grid
+  over [0, 1]^2 (:129, :301-331; agent/execution/util.py:5-40). `discretize` zips the six
+  features with the two grid axes, so the state is the two bin indices of time and quantity;
+* the Q-network NNModel_1 (util/model/QNets.py:7-27: Dense 32-64-128-128-64-32 ReLU, Dropout 0.1
+  after layers 2-6, linear 24-way head; Keras defaults glorot_uniform / zero bias), EvalModel and
+  TargetModel (QNets.py:54-60); NNModel_2 (:30-51) by name;
+* epsilon-greedy `choose_action` (:333-362): exploit when U < epsilon and enough experience,
+  else `randint(0, n_actions)`; epsilon = epsilon_max unless an increment is given (:100);
+* `train_neural_nets` (:448-515): uniform sampling with replacement, target copy every
+  `replace_target_iter` learn steps before the update, q_next AND q_eval4next both from the
+  TARGET net (so the "double" argmax is the target's own: kept as written), no terminal mask,
+  one Keras `train_on_batch` (MSE, RMSprop lr 0.01, rho 0.9, eps 1e-7 outside the sqrt,
+  TF 2.1 optimizer_v2), then the epsilon update that may overshoot epsilon_max by one step;
+* `compute_reward` (:409-446): per fill (1 - (fill - arrival)/arrival) * qty/q0 * 1e4 (BUY).
+
+The environment is the rmsc03 + DummyRL GymKernel composition on the device (BASELINE.json
+configs[3]; libmxa MXA_RMSC03_RL), which is a build-defined composition: the reference runs the
+DDQN agent only inside a Kernel config (config/execution/marketreplay/execution_marketreplay_ddqn.py)
+and never under ABIDESEnv. What the composition changes, and why:
+
+* actions go through DummyRL's action vector [x, level-1 share, level-2 share] (dummy_rl:138-158,
+  q/q0 == 1 by the reference's own quirk): `x = qty/q0` places exactly `qty`; allocation 1 ->
+  (1, 0), 2 -> (0.5, 0.5), 3 -> (0.34, 0.66) (levels 2-3 merged: order_level is 2); allocation 0
+  (a MARKET order in the reference) has no DummyRL counterpart and posts at the level-1 bid.
+  The last step (remaining_time == 1) places the whole remaining quantity (:388-390);
+* the reward of a step is the SUM of `compute_reward` over the step's fills, from the agent's
+  cash and executed-quantity change (sum_i q_i (2 - f_i/A) = 2 dq + dcash/A for a BUY); the
+  reference overwrites the experience reward per message (acceptance 0, execution r), an
+  artefact of message order that a per-step environment cannot see;
+* one learner serves every env (shared replay, one policy); `batch_size`, `train_every` and
+  `updates_per_train` default to the reference's 32, 5 and 1.
+
+Everything runs on the device stream the env steps on; the only host reads per step are the
+stored-transition count and the any-env-alive check.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+# ddqlearning_execution_agent.py:21-37
+SIZE_ALLOCATION = {1: [1, 0, 0, 0], 2: [0.5, 0.5, 0, 0], 3: [0.34, 0.33, 0.33, 0]}
+SIZE_SCALE = [0.1] + [i * 0.5 for i in range(1, 6)]
+
+
+def _action_table():
+    alloc = sorted(list(SIZE_ALLOCATION.keys()) + [0])
+    acts, k = {}, 0
+    for a in alloc:
+        for s in SIZE_SCALE:
+            acts[k] = (a, s)
+            k += 1
+    return acts
+
+
+ACTIONS = _action_table()
+N_ACTIONS = len(ACTIONS)  # 24 (execution_marketreplay_ddqn.py:244)
+GRID_BINS = (200, 200)    # create_uniform_grid(low=[0, 0], high=[1, 1], bins=(200, 200)), :129
+
+# DummyRL level shares per allocation type (levels >= 2 merged: order_level 2); 0 = MARKET -> level 1
+LEVEL_SHARES = {0: (1.0, 0.0), 1: (1.0, 0.0), 2: (0.5, 0.5), 3: (0.34, 0.66)}
+
+
+def create_uniform_grid(low, high, bins=(10, 10)):
+    """agent/execution/util.py:5-22: interior split points per dimension."""
+    return [np.linspace(low[d], high[d], bins[d] + 1)[1:-1] for d in range(len(bins))]
+
+
+def discretize(sample, grid):
+    """agent/execution/util.py:25-40: np.digitize per dimension (zip truncates to the grid)."""
+    return list(int(np.digitize(s, g)) for s, g in zip(sample, grid))
+
+
+class QNet(nn.Module):
+    """NNModel_1 / NNModel_2 (util/model/QNets.py:7-51) with Keras Dense defaults."""
+
+    WIDTHS = {"NNModel_1": (32, 64, 128, 128, 64, 32), "NNModel_2": (32, 64, 128, 256, 128, 64, 32)}
+
+    def __init__(self, n_in=2, n_actions=N_ACTIONS, model="NNModel_1", dropout=0.1, generator=None):
+        super().__init__()
+        w = self.WIDTHS[model]
+        dims = (n_in,) + w
+        self.hidden = nn.ModuleList(nn.Linear(dims[i], dims[i + 1]) for i in range(len(w)))
+        self.logits = nn.Linear(w[-1], n_actions)
+        self.p = dropout
+        with torch.no_grad():
+            for lin in list(self.hidden) + [self.logits]:  # glorot_uniform kernel, zero bias
+                lim = math.sqrt(6.0 / (lin.in_features + lin.out_features))
+                lin.weight.uniform_(-lim, lim, generator=generator)
+                lin.bias.zero_()
+
+    def forward(self, x):
+        for i, lin in enumerate(self.hidden):
+            x = torch.relu(lin(x))
+            if i >= 1 and self.p > 0:  # dropout after layers 2..n (QNets.py:22-26)
+                x = nn.functional.dropout(x, self.p, self.training)
+        return self.logits(x)
+
+
+class ReplayRing:
+    """Device-resident experience (s, a, s', r) of every env (the reference keeps one
+    OrderedDict per agent, :115-116). Valid rows are compacted with a prefix sum, no host loop."""
+
+    def __init__(self, capacity, n_state, device):
+        self.cap = int(capacity)
+        self.s = torch.zeros((self.cap, n_state), dtype=torch.float32, device=device)
+        self.s2 = torch.zeros_like(self.s)
+        self.a = torch.zeros(self.cap, dtype=torch.int64, device=device)
+        self.r = torch.zeros(self.cap, dtype=torch.float32, device=device)
+        self.n = 0  # rows written so far (host)
+
+    def add(self, s, a, s2, r, mask):
+        """append rows where mask; returns the number appended (one host read)."""
+        m = mask.to(torch.int64)
+        k = int(m.sum().item())
+        if k:
+            pos = (self.n + torch.cumsum(m, 0) - 1) % self.cap
+            sel = mask.nonzero(as_tuple=True)[0]
+            p = pos[sel]
+            self.s[p] = s[sel].float()
+            self.s2[p] = s2[sel].float()
+            self.a[p] = a[sel]
+            self.r[p] = r[sel].float()
+            self.n += k
+        return k
+
+    def __len__(self):
+        return min(self.n, self.cap)
+
+
+class DDQNLearner:
+    """DDQLearningExecutionAgent's learner (ddqlearning_execution_agent.py:40-131, 333-362, 448-515)."""
+
+    def __init__(self, n_state=2, n_actions=N_ACTIONS, replace_target_iter=5, batch_size=32, learning_rate=0.01,
+                 epsilon_increment=None, epsilon_max=0.9, reward_decay=0.98, mode="train", model="NNModel_1",
+                 dropout=0.1, capacity=1 << 20, device="cuda", seed=0):
+        self.device = torch.device(device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        cpu = torch.Generator()
+        cpu.manual_seed(seed)
+        self.eval_model = QNet(n_state, n_actions, model, dropout, cpu).to(self.device)
+        self.target_model = QNet(n_state, n_actions, model, dropout, cpu).to(self.device)
+        self.n_actions = n_actions
+        self.replace_target_iter = replace_target_iter
+        self.batch_size = batch_size
+        self.learning_rate = learning_rate
+        self.epsilon_increment = epsilon_increment
+        self.epsilon_max = epsilon_max
+        self.epsilon = 0 if epsilon_increment is not None else epsilon_max  # :100
+        self.reward_decay = reward_decay
+        self.mode = mode
+        self.learn_step_counter = 0
+        self.cost_hist = []
+        # Keras RMSprop (TF 2.1 optimizer_v2, momentum 0, not centered): rho 0.9, epsilon 1e-7
+        self.opt = torch.optim.RMSprop(self.eval_model.parameters(), lr=learning_rate, alpha=0.9, eps=1e-7)
+        self.memory = ReplayRing(capacity, n_state, self.device)
+
+    # ---- acting (choose_action, :333-362)
+    def q_values(self, s):
+        self.eval_model.eval()  # Keras predict(): training=False, no dropout
+        with torch.no_grad():
+            return self.eval_model(s.to(self.eval_model.logits.weight.dtype))
+
+    def choose_action(self, s):
+        """s [n, n_state] -> actions [n] int64 (epsilon-greedy per env in train mode)."""
+        n = s.shape[0]
+        greedy = torch.argmax(self.q_values(s), dim=1)
+        if self.mode == "test":
+            return greedy
+        u = torch.rand(n, generator=self.gen, device=self.device, dtype=torch.float64)
+        rnd = torch.randint(0, self.n_actions, (n,), generator=self.gen, device=self.device)
+        exploit = (u < self.epsilon) & (len(self.memory) + 1 > self.batch_size)
+        return torch.where(exploit, greedy, rnd)
+
+    # ---- learning (train_neural_nets, :448-515)
+    def q_target(self, s, a, s2, r):
+        """the reference's target: both q_next and q_eval4next from the target net."""
+        self.target_model.eval()
+        self.eval_model.eval()
+        with torch.no_grad():
+            q_next = self.target_model(s2)
+            q_eval4next = self.target_model(s2)
+            q_eval = self.eval_model(s)
+            tgt = q_eval.clone()
+            idx = torch.arange(s.shape[0], device=s.device)
+            best = torch.argmax(q_eval4next, dim=1)
+            tgt[idx, a] = r + self.reward_decay * q_next[idx, best]
+        return tgt
+
+    def learn_on(self, s, a, s2, r):
+        """one train_neural_nets update on a given batch; returns the cost (a device scalar)."""
+        if self.learn_step_counter % self.replace_target_iter == 0:
+            self.target_model.load_state_dict(self.eval_model.state_dict())
+        tgt = self.q_target(s, a, s2, r)
+        self.eval_model.train()  # train_on_batch: training=True (dropout active)
+        self.opt.zero_grad(set_to_none=True)
+        loss = torch.mean((self.eval_model(s) - tgt) ** 2)
+        loss.backward()
+        self.opt.step()
+        self.epsilon = self.epsilon + self.epsilon_increment if self.epsilon < self.epsilon_max else self.epsilon_max
+        self.learn_step_counter += 1
+        return loss.detach()
+
+    def learn(self):
+        """sample a batch with replacement (np.random.choice(current_size, batch)) and update."""
+        n = len(self.memory)
+        if n <= self.batch_size:
+            return None
+        idx = torch.randint(0, n, (self.batch_size,), generator=self.gen, device=self.device)
+        m = self.memory
+        cost = self.learn_on(m.s[idx], m.a[idx], m.s2[idx], m.r[idx])
+        self.cost_hist.append(cost)
+        return cost
+
+
+class ExecutionTask:
+    """Maps the rmsc03 + DummyRL env (obs float64[9], agent state) to the DDQN's state, action
+    and reward (ddqlearning_execution_agent.py:301-331, 364-407, 409-446).
+
+    obs[0] = remaining horizon steps, obs[1] = remaining quantity (dummy_rl:294-315); the
+    horizon has `n_horizon` points; the parent order is `quantity` shares BUY."""
+
+    def __init__(self, quantity=100000, n_horizon=27, device="cuda"):
+        self.q0 = float(quantity)
+        self.nh = int(n_horizon)
+        self.child = int(self.q0 / (self.nh - 1))  # generate_schedule: int(quantity / (len - 1))
+        g = create_uniform_grid([0, 0], [1.0, 1.0], GRID_BINS)
+        self.grid = [torch.tensor(x, dtype=torch.float64, device=device) for x in g]
+        tab = np.zeros((N_ACTIONS, 3))
+        for k, (alloc, scale) in ACTIONS.items():
+            tab[k] = (max(0, round(scale * self.child)) / self.q0,) + LEVEL_SHARES[alloc]
+        self.table = torch.tensor(tab, dtype=torch.float64, device=device)
+
+    def state(self, obs):
+        """discretize([2*rem_t/len - 1, 2*rem_q/q0 - 1]) -> float [n, 2] bin indices."""
+        tr = 2 * (obs[:, 0] / self.nh) - 1
+        qr = 2 * (obs[:, 1] / self.q0) - 1
+        # np.digitize(x, increasing bins) == torch.bucketize(x, bins, right=True)
+        return torch.stack([torch.bucketize(tr, self.grid[0], right=True),
+                            torch.bucketize(qr, self.grid[1], right=True)], 1).to(torch.float32)
+
+    def actions(self, a, obs):
+        """DDQN action index -> DummyRL action vector [n, 3] float64 (take_action, :364-407)."""
+        act = self.table[a].clone()
+        last = obs[:, 0] == 1  # remaining_time == 1: the whole remaining quantity, allocation 0
+        act[:, 0] = torch.where(last, obs[:, 1] / self.q0, act[:, 0])
+        act[:, 1] = torch.where(last, torch.ones_like(act[:, 1]), act[:, 1])
+        act[:, 2] = torch.where(last, torch.zeros_like(act[:, 2]), act[:, 2])
+        return act
+
+    @staticmethod
+    def reward(prev, cur, arrival, q0):
+        """sum over the step's fills of compute_reward (BUY): 1e4/q0 * (2 dq + dcash / A);
+        prev/cur are mxa_write_rl_state rows (CASH, holdings, executed, ...)."""
+        dq = cur[:, 2] - prev[:, 2]
+        dcash = cur[:, 0] - prev[:, 0]
+        return torch.where(dq > 0, 1e4 / q0 * (2 * dq + dcash / arrival), torch.zeros_like(dq))
+
+
+def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train=1, record=None, timing=None):
+    """One episode of every env of a VecABIDESEnv (rmsc03 + DummyRL) driven by the learner, all on
+    the current torch stream (the env must step on it: env.set_stream). Mirrors the agent's
+    per-period loop (place_order, :275-299): observe, choose, act, then store the completed
+    transition and train every `train_every` periods (train_step_counter % 5 == 0, :286-293).
+
+    Returns a dict of device tensors (rewards [steps, n], actions [steps, n], flags) and the
+    number of stored transitions. `record` (a list) receives the per-step action vectors;
+    `timing` (a list) receives a (start, end) torch.cuda.Event pair around every step launch."""
+    from .gym import OBS_SIZE, RL_STATE_WORDS
+    dev = learner.device
+    n = env.n_envs
+    nh = task.nh
+    env.reset(seeds=seeds)
+    obs = torch.zeros((n, OBS_SIZE), dtype=torch.float64, device=dev)
+    flags = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.zeros((n, RL_STATE_WORDS), dtype=torch.float64, device=dev)
+    act0 = torch.zeros((n, 3), dtype=torch.float64, device=dev)  # first step: no cached LOB, nothing placed
+    env.step_device(act0.data_ptr(), obs.data_ptr(), flags.data_ptr())
+    env.write_rl_state(st.data_ptr())
+    if record is not None:
+        record.append(act0.clone())
+    alive = ((flags & 2) != 0) & ((flags & 5) == 0)
+    lob_ok = (st[:, 7] == 3)
+    arrival = torch.where(lob_ok, (st[:, 3] + st[:, 4]) / 2, torch.ones_like(st[:, 3]))  # mid at start_time
+    rewards, actions = [], []
+    stored = 0
+    step_counter = 0
+    for _ in range(nh):
+        if not bool(alive.any().item()):
+            break
+        s = task.state(obs)
+        a = learner.choose_action(s)
+        act = task.actions(a, obs)
+        if record is not None:
+            record.append(act.clone())
+        prev = st.clone()
+        if timing is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        env.step_device(act.data_ptr(), obs.data_ptr(), flags.data_ptr())
+        if timing is not None:
+            e1.record()
+            timing.append((e0, e1))
+        env.write_rl_state(st.data_ptr())
+        ok = alive & ((flags & 2) != 0) & ((flags & 4) == 0)
+        r = task.reward(prev, st, arrival, task.q0)
+        s2 = task.state(obs)
+        if learner.mode == "train":
+            stored += learner.memory.add(s, a, s2, r, ok)
+            if step_counter % train_every == 0:
+                for _ in range(updates_per_train):
+                    learner.learn()
+        rewards.append(torch.where(ok, r, torch.zeros_like(r)))
+        actions.append(a)
+        step_counter += 1
+        alive = ok & ((flags & 1) == 0)
+    return {"rewards": torch.stack(rewards) if rewards else None,
+            "actions": torch.stack(actions) if actions else None,
+            "flags": flags, "arrival": arrival, "stored": stored, "steps": step_counter + 1}

@@ -19,6 +19,7 @@ from .tape import Tape, load_lobster
 
 OBS_SIZE = 9      # get_observation returns 9 values (the declared space says 10: dummy_rl:317-322)
 ACTION_SIZE = 3   # order_level 2 -> [total volume, level-1 share, level-2 share]
+RL_STATE_WORDS = 8  # mxa_write_rl_state row (include/mxa.h MXA_RL_STATE_WORDS)
 
 
 class VecABIDESEnv:
@@ -83,6 +84,11 @@ class VecABIDESEnv:
     def write_results(self, device_ptr):
         """Per-env (events, hash, status, current_time) int64 rows into device memory."""
         self._check(self.L.mxa_write_results(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_results")
+
+    def write_rl_state(self, device_ptr):
+        """Per-env execution-agent state [n][RL_STATE_WORDS] float64 (CASH, holdings, executed,
+        best bid, best ask, bid size, ask size, lob flags) into device memory, asynchronously."""
+        self._check(self.L.mxa_write_rl_state(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_rl_state")
 
     def summary(self):
         n = self.n_envs

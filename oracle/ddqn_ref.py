@@ -1,0 +1,75 @@
+"""TEST INFRASTRUCTURE ONLY (the checker, never the product path): a float64 numpy restatement
+of the reference DDQN learner's arithmetic, for the parity tests of mxabides.ddqn.
+
+Follows agent/execution/qlearning/ddqlearning_execution_agent.py and util/model/QNets.py; the
+Keras 2 (TensorFlow 2.1, requirements.txt:17) pieces are restated from their published
+algorithm because TensorFlow is not installed here: Dense = x @ W + b with W
+[in, out]; `mse` = mean over all elements; RMSprop optimizer_v2 with momentum 0, not centered:
+rms = rho*rms + (1-rho)*g^2, w -= lr * g / (sqrt(rms) + eps). Parity with Keras itself is
+therefore unpinned; what is pinned is the reference's own algorithm around it (the target of
+train_neural_nets, the action table, the state discretization)."""
+import numpy as np
+
+
+def action_table(size_allocation, size_scale):
+    """ddqlearning_execution_agent.py:27-37"""
+    alloc = list(size_allocation.keys())
+    alloc.append(0)
+    alloc.sort()
+    acts, k = {}, 0
+    for i in range(len(alloc)):
+        for j in range(len(size_scale)):
+            acts[k] = (alloc[i], size_scale[j])
+            k += 1
+    return acts
+
+
+def forward(layers, x):
+    """layers: [(W [in,out], b)], ReLU on all but the last (QNets.py:19-27, no dropout: predict)."""
+    acts = [x]
+    for i, (W, b) in enumerate(layers):
+        z = acts[-1] @ W + b
+        acts.append(z if i == len(layers) - 1 else np.maximum(z, 0.0))
+    return acts
+
+
+def q_target(eval_layers, target_layers, s, a, s2, r, gamma):
+    """train_neural_nets, ddqlearning_execution_agent.py:475-490"""
+    q_next = forward(target_layers, s2)[-1]
+    q_eval4next = forward(target_layers, s2)[-1]
+    q_eval = forward(eval_layers, s)[-1]
+    tgt = q_eval.copy()
+    bi = np.arange(len(s))
+    tgt[bi, a.astype(int)] = r + gamma * q_next[bi, np.argmax(q_eval4next, axis=1)]
+    return tgt
+
+
+def mse_grads(layers, x, tgt):
+    """loss = mean((f(x) - tgt)^2) and d loss / d (W, b) for every layer."""
+    acts = forward(layers, x)
+    out = acts[-1]
+    loss = np.mean((out - tgt) ** 2)
+    d = 2.0 * (out - tgt) / out.size
+    grads = [None] * len(layers)
+    for i in range(len(layers) - 1, -1, -1):
+        W, _ = layers[i]
+        grads[i] = (acts[i].T @ d, d.sum(0))
+        if i:
+            d = (d @ W.T) * (acts[i] > 0)
+    return loss, grads
+
+
+def rmsprop_step(layers, grads, rms, lr, rho=0.9, eps=1e-7):
+    """Keras optimizer_v2 RMSprop, momentum 0, not centered (TF 2.1 rmsprop.py)."""
+    new, new_rms = [], []
+    for (W, b), (gW, gb), (rW, rb) in zip(layers, grads, rms):
+        rW = rho * rW + (1 - rho) * gW * gW
+        rb = rho * rb + (1 - rho) * gb * gb
+        new.append((W - lr * gW / (np.sqrt(rW) + eps), b - lr * gb / (np.sqrt(rb) + eps)))
+        new_rms.append((rW, rb))
+    return new, new_rms
+
+
+def step_reward(fills, arrival, q0):
+    """compute_reward summed over fills [(qty, fill_price)] for a BUY (ddqlearning_execution_agent.py:425-432)"""
+    return sum((1 - ((f - arrival) / arrival)) * q / q0 * 10000 for q, f in fills)
