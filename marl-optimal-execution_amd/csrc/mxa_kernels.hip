@@ -2491,6 +2491,39 @@ struct Eng {
           atime_store(rcp, t);
           continue;
         }
+        if (type == MT_MESSAGE && m_kind(m) == MK_CANCELLED && rcp > 0 && rcp < ACK_LIMIT) {
+          // TradingAgent.orderCancelled (TradingAgent.py:464-480): del self.orders[id]. The
+          // open-order chunks are loaded with the record, not after it (one latency, not two)
+          rec_load(rcp);
+          OpenOrder my[OC];
+          {
+            const OpenOrder* oo = open_ptr(rcp);
+            for (int j = 0; j < OC; j++) {
+              my[j].oid = -1;
+              if (j * 64 + lane < PC.L.open_cap) my[j] = oo[j * 64 + lane];
+            }
+          }
+          cur = t;
+          const Rec rec = encode<PW == 8>(key, m);
+          hash = rec_hash(hash, rec);
+          if (trace && h.trace_len < trace_cap) {
+            if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
+            h.trace_len++;
+          }
+          pops++;
+          q_remove(slot);
+          const i32 u = rgi(AF_NUSED), oid = (i32)m.w[1];
+          for (int j = 0; j < OC; j++) {
+            const u64 hit = bal(j * 64 + lane < u && my[j].oid == oid);
+            if (hit) {
+              del_open(j * 64 + ffs64(hit));
+              break;
+            }
+          }
+          rs64(AF_ATIME, t);
+          rec_store();
+          continue;
+        }
       }
 #endif
       rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
