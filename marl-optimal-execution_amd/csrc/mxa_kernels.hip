@@ -2445,6 +2445,17 @@ struct Eng {
   }
 
   // ---------------- Kernel.runner event loop (Kernel.py:190-292)
+  // the per-pop bookkeeping of the fast paths: currentTime, parity trace + hash, ttl_messages
+  DEV void account_pop(i64 t, u64 key, const Msg& m) {
+    cur = t;
+    const Rec rec = encode<PW == 8>(key, m);
+    hash = rec_hash(hash, rec);
+    if (trace && h.trace_len < trace_cap) {
+      if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
+      h.trace_len++;
+    }
+    pops++;
+  }
   DEV void run(i64 max_pops) {
     for (i64 n = 0; n < max_pops && status == ST_RUNNING; n++) {
       if constexpr (GYM) {
@@ -2478,15 +2489,20 @@ struct Eng {
       int type = (int)(key & 3);
 #ifndef MXA_NO_ACK_FAST
       if constexpr (ACK_FAST) {
+        if (type == MT_MESSAGE && rcp == 0) {
+          // ExchangeAgent.receiveMessage reads nothing from its agent record but the
+          // computation delay, which is 0 here: no record round trip (half of all pops)
+          cur_agent = 0;
+          rlo = rhi = 0;
+          account_pop(t, key, m);
+          q_remove(slot);
+          ex_receive(m);
+          if (dirty) rng_maint();
+          atime_store(0, t);
+          continue;
+        }
         if (type == MT_MESSAGE && m_kind(m) == MK_ACCEPTED && rcp > 0 && rcp < ACK_LIMIT) {
-          cur = t;
-          const Rec rec = encode<PW == 8>(key, m);
-          hash = rec_hash(hash, rec);
-          if (trace && h.trace_len < trace_cap) {
-            if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
-            h.trace_len++;
-          }
-          pops++;
+          account_pop(t, key, m);
           q_remove(slot);
           atime_store(rcp, t);
           continue;
@@ -2503,14 +2519,7 @@ struct Eng {
               if (j * 64 + lane < PC.L.open_cap) my[j] = oo[j * 64 + lane];
             }
           }
-          cur = t;
-          const Rec rec = encode<PW == 8>(key, m);
-          hash = rec_hash(hash, rec);
-          if (trace && h.trace_len < trace_cap) {
-            if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
-            h.trace_len++;
-          }
-          pops++;
+          account_pop(t, key, m);
           q_remove(slot);
           const i32 u = rgi(AF_NUSED), oid = (i32)m.w[1];
           for (int j = 0; j < OC; j++) {
