@@ -152,10 +152,10 @@ extern "C" {
 
 #ifdef MXA_PROF
 // diagnostics build only (not in include/mxa.h): phase cycle totals, then cleared
-int mxa_prof_read(uint64_t* out32) {
-  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mxa::g_mxa_prof), 32 * 8) != hipSuccess) return MXA_EHIP;
-  static const uint64_t z[32] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(mxa::g_mxa_prof), z, 32 * 8) != hipSuccess) return MXA_EHIP;
+int mxa_prof_read(uint64_t* out48) {
+  if (hipMemcpyFromSymbol(out48, HIP_SYMBOL(mxa::g_mxa_prof), 48 * 8) != hipSuccess) return MXA_EHIP;
+  static const uint64_t z[48] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(mxa::g_mxa_prof), z, 48 * 8) != hipSuccess) return MXA_EHIP;
   return MXA_OK;
 }
 #endif

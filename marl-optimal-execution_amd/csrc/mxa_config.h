@@ -47,7 +47,7 @@ constexpr size_t lds_bytes(int cfg) {
   return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
 #ifdef MXA_PROF
-         + 256  // phase counters
+         + 384  // phase counters
 #endif
       ;
 }

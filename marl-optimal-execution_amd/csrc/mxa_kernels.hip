@@ -399,7 +399,7 @@ DEV i64 U(i64 v) {
 }
 #ifdef MXA_PROF
 // diagnostics build only: per-phase shader-cycle totals over all envs (tools/prof_phases.py)
-__device__ unsigned long long g_mxa_prof[32];
+__device__ unsigned long long g_mxa_prof[48];
 DEV u64 stamp() {
   u64 t;
   __builtin_amdgcn_sched_barrier(0);
@@ -482,7 +482,7 @@ struct Eng {
     trace_cap = tcap;
 #ifdef MXA_PROF
     prof = (LDSP u64*)(lds + LDS_Q + sizeof(EnvHdr));
-    if (lane < 32) prof[lane] = 0;
+    if (lane < 48) prof[lane] = 0;
 #endif
     trace = tcap ? (i64*)(env + PC.L.off_trace) : nullptr;
 #ifdef MXA_PROF
@@ -2448,7 +2448,7 @@ struct Eng {
   // the per-pop bookkeeping of the fast paths: currentTime, parity trace + hash, ttl_messages
   DEV void account_pop(i64 t, u64 key, const Msg& m) {
     cur = t;
-    const Rec rec = encode<PW == 8>(key, m);
+const Rec rec = encode<PW == 8>(key, m);
     hash = rec_hash(hash, rec);
     if (trace && h.trace_len < trace_cap) {
       if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
@@ -2494,17 +2494,29 @@ struct Eng {
           // computation delay, which is 0 here: no record round trip (half of all pops)
           cur_agent = 0;
           rlo = rhi = 0;
+          PROF_ADD(0, t0);
           account_pop(t, key, m);
+          PROF_ADD(32, t0);
           q_remove(slot);
+          PROF_ADD(33, t0);
           ex_receive(m);
+          PROF_ADD(2, t0);
+          PROF_CNT(16);
           if (dirty) rng_maint();
+          PROF_ADD(30, t0);
           atime_store(0, t);
+          PROF_ADD(31, t0);
           continue;
         }
         if (type == MT_MESSAGE && m_kind(m) == MK_ACCEPTED && rcp > 0 && rcp < ACK_LIMIT) {
+          PROF_ADD(0, t0);
           account_pop(t, key, m);
+          PROF_ADD(32, t0);
           q_remove(slot);
+          PROF_ADD(33, t0);
           atime_store(rcp, t);
+          PROF_ADD(14, t0);
+          PROF_CNT(28);
           continue;
         }
         if (type == MT_MESSAGE && m_kind(m) == MK_CANCELLED && rcp > 0 && rcp < ACK_LIMIT) {
@@ -2519,8 +2531,11 @@ struct Eng {
               if (j * 64 + lane < PC.L.open_cap) my[j] = oo[j * 64 + lane];
             }
           }
+          PROF_ADD(0, t0);
           account_pop(t, key, m);
+          PROF_ADD(32, t0);
           q_remove(slot);
+          PROF_ADD(33, t0);
           const i32 u = rgi(AF_NUSED), oid = (i32)m.w[1];
           for (int j = 0; j < OC; j++) {
             const u64 hit = bal(j * 64 + lane < u && my[j].oid == oid);
@@ -2531,10 +2546,13 @@ struct Eng {
           }
           rs64(AF_ATIME, t);
           rec_store();
+          PROF_ADD(15, t0);
+          PROF_CNT(29);
           continue;
         }
       }
 #endif
+      PROF_ADD(0, t0);
       rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
       cur = t;
       const Rec rec = encode<PW == 8>(key, m);
@@ -2544,6 +2562,7 @@ struct Eng {
         h.trace_len++;
       }
       pops++;
+      PROF_ADD(32, t0);
       add_delay = 0;
       if constexpr (GYM) {
         if (type == MT_CANCEL_ORDER) {  // GymKernel CANCEL_ORDER: no busy check, no delay
@@ -2560,7 +2579,9 @@ struct Eng {
         PROF_ADD(1, t0);
         continue;
       }
+      PROF_ADD(0, t0);
       q_remove(slot);
+      PROF_ADD(33, t0);
       rs64(AF_ATIME, t);
 #ifdef MXA_PROF
       int pb = 2 + 2 * (rgi(AF_TYPE) & 7) + (type == MT_WAKEUP);
@@ -2955,7 +2976,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
   g.run(max_pops);
   g.save();
 #ifdef MXA_PROF
-  if (g.lane < 32) atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
+  if (g.lane < 48) atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
 #endif
 }
 

@@ -13,7 +13,7 @@ from mxabides import _lib
 cfg = sys.argv[1] if len(sys.argv) > 1 else "rmsc03"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 m = mxabides.VecMarket(cfg, (123456789 + np.arange(n)) & 0xFFFFFFFF)
-buf = (ctypes.c_uint64 * 32)()
+buf = (ctypes.c_uint64 * 48)()
 lib = _lib.load()
 lib.mxa_prof_read(buf)  # clear
 m.reset()
@@ -22,7 +22,8 @@ lib.mxa_prof_read(buf)
 v = list(buf)
 ev = int(m.summary()["events"].sum())
 names = ["pop+hash+rec_load", "requeue"] + ["%s.%s" % (a, w) for a in ["EX", "ZI", "NOISE", "VALUE", "MM", "MOM"] for w in ["msg", "wake"]]
-tot = v[0] + v[1] + sum(v[2:14]) + v[30] + v[31]
+names += ["ACCEPTED fast", "CANCELLED fast"]  # phases 14, 15 (counts 28, 29)
+tot = v[0] + v[1] + sum(v[2:16]) + v[30] + v[31] + v[32] + v[33]
 print("events %d  total cycles/event (sum over waves) %.0f" % (ev, tot / ev))
 print("%-20s %8s %10s %12s" % ("phase", "share", "cyc/event", "cyc/call"))
 for i, nm in enumerate(names):
@@ -30,3 +31,5 @@ for i, nm in enumerate(names):
     print("%-20s %7.1f%% %10.0f %12s" % (nm, 100 * v[i] / tot, v[i] / ev, ("%.0f (%d calls)" % (v[i] / c, c)) if c else ""))
 print("%-20s %7.1f%% %10.0f" % ("rng_maint", 100 * v[30] / tot, v[30] / ev))
 print("%-20s %7.1f%% %10.0f" % ("tail+rec_store", 100 * v[31] / tot, v[31] / ev))
+print("%-20s %7.1f%% %10.0f" % ("encode+hash(+trace)", 100 * v[32] / tot, v[32] / ev))
+print("%-20s %7.1f%% %10.0f" % ("q_remove", 100 * v[33] / tot, v[33] / ev))
