@@ -46,6 +46,7 @@ constexpr Shape shape(int cfg) {
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
+         + 256                                                                                // batched-push scratch
 #ifdef MXA_PROF
          + 384  // phase counters
 #endif

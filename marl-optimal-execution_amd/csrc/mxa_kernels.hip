@@ -468,6 +468,7 @@ struct Eng {
   LDSP u64* prof;
 #endif
   LDSP u64* hotrec;  // [HOT][64]: the exchange's (and the market maker's) agent record
+  LDSP i32* scr;     // [64]: batched-push slot table (rank -> queue slot)
 
   static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 4 * PW : 0));
   DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
@@ -485,6 +486,7 @@ struct Eng {
     if (lane < 48) prof[lane] = 0;
 #endif
     trace = tcap ? (i64*)(env + PC.L.off_trace) : nullptr;
+    scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 256);
 #ifdef MXA_PROF
     hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 256);
 #else
@@ -677,6 +679,51 @@ struct Eng {
       if (lane < PW) qpl[slot * PW + lane] = msel(m, lane);
     }
     qcount++;
+    if (qcount > h.max_q) h.max_q = qcount;
+  }
+  // One q_push per active lane, in lane order (ranks 0..n-1, seqs seq..seq+n-1): the same
+  // (key, seq, message) set as n q_push calls, so the pop order is unchanged; only the slot
+  // placement differs, which the pop never sees. Free slots are ranked across lanes, the rank ->
+  // slot table goes through LDS, each message lane writes its own slot, and every lane rescans
+  // its slots once for the whole batch instead of a wave-serial push per message.
+  DEV void q_push_lanes(bool act, u64 key, const Msg& m) {
+    const u64 ab = bal(act);
+    const int n = __popcll(ab);
+    if (n == 0) return;
+    const int r = (int)__builtin_amdgcn_mbcnt_hi((u32)(ab >> 32), __builtin_amdgcn_mbcnt_lo((u32)ab, 0u));
+    const int c = __popcll(qfree);
+    int base = 0, total = 0;
+    for (int k = 0; k < SQ; k++) {
+      const u64 b = bal(c > k);
+      base += (int)__builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
+      total += __popcll(b);
+    }
+    if (total < n) {
+      fail(ERR_QUEUE_FULL);
+      return;
+    }
+    u64 f = qfree;
+    for (int t = 0; t < SQ; t++) {
+      if (f && base + t < n) {
+        const int j = ffs64(f);
+        f &= f - 1;
+        scr[base + t] = j * 64 + lane;
+        qfree &= ~(1ull << j);
+      }
+    }
+    __threadfence_block();
+    if (act) {
+      const int slot = scr[r];
+      qk[slot] = key;
+      qs[slot] = seq + (u32)r;
+      if constexpr (PL_LDS) pl_write(slot, m);
+      else
+        for (int i = 0; i < PW; i++) qpl[slot * PW + i] = m.w[i];
+    }
+    __threadfence_block();
+    q_rescan();
+    seq += (u32)n;
+    qcount += n;
     if (qcount > h.max_q) h.max_q = qcount;
   }
   // lexicographic wave-min of the per-lane cached (key, seq); returns winning slot or -1
@@ -1207,8 +1254,27 @@ struct Eng {
   // TradingAgent.orders (dict, insertion order) as an append-only list in HBM: deletions leave
   // a tombstone (oid -1), the list is compacted when its slots run out
   static constexpr int OC = (PC.L.open_cap + 63) / 64;
+  // zero latency, no noise draw, no replay dense ids: a message to the exchange is delivered at
+  // currentTime + computation delay, so a run of sends can be pushed as one batch
+  static constexpr bool BATCH = !RP && PC.lat_mode == 0 && PC.noise_len <= 1;
+  DEV u64 ex_key() { return ((u64)(cur + rg64(AF_COMP) + add_delay) << 13) | MT_MESSAGE; }
   // cancelOrder for every open order in dict (= list) order
   DEV void cancel_all() {
+    if constexpr (BATCH) {
+      const i32 u = rgi(AF_NUSED);
+      const OpenOrder* oo = open_ptr(cur_agent);
+      const u64 key = ex_key();
+      for (int j = 0; j < OC; j++) {
+        if (j * 64 >= u) break;
+        OpenOrder o;
+        o.oid = -1;
+        o.is_buy = o.qty = o.price = 0;
+        if (j * 64 + lane < u) o = oo[j * 64 + lane];
+        Msg cm = msg_order(MK_CANCEL, o.oid, cur_agent, o.is_buy, o.qty, o.price, 0);
+        q_push_lanes(o.oid != -1, key, cm);
+      }
+      return;
+    }
     const i32 u = rgi(AF_NUSED);
     OpenOrder* oo = open_ptr(cur_agent);
     OpenOrder my[OC];
@@ -1609,12 +1675,43 @@ struct Eng {
       i64 hb = mid - 1, la = mid + PC.mm_window;
       i64 lb = hb - PC.mm_ticks, ha = la + PC.mm_ticks;
       i64 sz = rgi(AF_ORDER_SIZE);
-      for (i64 p = lb; p <= hb; p++) place_limit(sz, 1, p);
-      for (i64 p = la; p <= ha; p++) place_limit(sz, 0, p);
+      constexpr int NL = 2 * (PC.mm_ticks + 1);
+      if (BATCH && NL <= 64 && sz > 0 && rgi(AF_NORD) + NL <= PC.L.open_cap) {
+        mm_place_ladder(sz, lb, la);
+      } else {
+        for (i64 p = lb; p <= hb; p++) place_limit(sz, 1, p);
+        for (i64 p = la; p <= ha; p++) place_limit(sz, 0, p);
+      }
       fl_set(FL_AW_SPREAD, true);
       fl_set(FL_AW_TV, true);
       wakeup_at(cur_agent, cur + PC.mm_wake);
     }
+  }
+
+  // the ladder's placeLimitOrder calls in one pass: lane i places bid lb+i (i < ticks+1) or ask
+  // la+i-(ticks+1); ids, open-order list entries and queue seqs in the same order as the loop
+  DEV void mm_place_ladder(i64 sz, i64 lb, i64 la) {
+    constexpr int NB = PC.mm_ticks + 1, NL = 2 * NB;
+    i32 u = rgi(AF_NUSED);
+    if (u + NL > PC.L.open_cap) u = open_compact();
+    const bool act = lane < NL;
+    const int buy = lane < NB;
+    const i32 price = (i32)(buy ? lb + lane : la + (lane - NB));
+    const i32 oid = (i32)(ocnt + lane);
+    ocnt += NL;
+    if (act) {
+      OpenOrder o;
+      o.oid = oid;
+      o.is_buy = buy;
+      o.qty = (i32)sz;
+      o.price = price;
+      open_ptr(cur_agent)[u + lane] = o;
+    }
+    rs(AF_NUSED, (u32)(u + NL));
+    rs(AF_NORD, (u32)(rgi(AF_NORD) + NL));
+    Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, (i32)sz, price, 0);
+    lm.w[0] = (lm.w[0] & 0xFFFFu) | ((u32)cur_agent << 16);
+    q_push_lanes(act, ex_key(), lm);
   }
 
   // ---------------- MomentumAgent (MomentumAgent.py:53-99)
