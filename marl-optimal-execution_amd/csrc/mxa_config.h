@@ -46,7 +46,11 @@ constexpr Shape shape(int cfg) {
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
-         + 256                                                                                // batched-push scratch
+#ifdef MXA_QREG
+         + 768  // batched-push scratch: slot table + staged keys
+#else
+         + 256  // batched-push scratch: slot table
+#endif
 #ifdef MXA_PROF
          + 384  // phase counters
 #endif

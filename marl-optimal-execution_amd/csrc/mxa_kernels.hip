@@ -447,6 +447,50 @@ struct Eng {
   // event queue: keys in LDS, payload in LDS (PL_LDS) or HBM; per-lane min cache
   LDSP u64* qk;
   LDSP u32* qs;
+#ifdef MXA_QREG
+  u64 rk[SQ];  // this lane's queue slots (j, lane) in VGPRs: keys and seqs
+  u32 rq[SQ];
+#endif
+  // this lane's slot j (every use of the key/seq arrays is the owning lane's own slot)
+  DEV u64 qkey(int j) {
+#ifdef MXA_QREG
+    u64 v = rk[0];
+    for (int jj = 1; jj < SQ; jj++) v = jj == j ? rk[jj] : v;
+    return v;
+#else
+    return qk[j * 64 + lane];
+#endif
+  }
+  DEV u32 qseq(int j) {
+#ifdef MXA_QREG
+    u32 v = rq[0];
+    for (int jj = 1; jj < SQ; jj++) v = jj == j ? rq[jj] : v;
+    return v;
+#else
+    return qs[j * 64 + lane];
+#endif
+  }
+  DEV void qset(int j, u64 k, u32 s, bool me) {
+#ifdef MXA_QREG
+    for (int jj = 0; jj < SQ; jj++) {
+      const bool w = me && jj == j;
+      rk[jj] = w ? k : rk[jj];
+      rq[jj] = w ? s : rq[jj];
+    }
+#else
+    if (me) {
+      qk[j * 64 + lane] = k;
+      qs[j * 64 + lane] = s;
+    }
+#endif
+  }
+  DEV void qsetk(int j, u64 k, bool me) {
+#ifdef MXA_QREG
+    for (int jj = 0; jj < SQ; jj++) rk[jj] = (me && jj == j) ? k : rk[jj];
+#else
+    if (me) qk[j * 64 + lane] = k;
+#endif
+  }
   PlPtr qpl;
   u64 mk;
   u32 ms;
@@ -468,7 +512,7 @@ struct Eng {
   LDSP u64* prof;
 #endif
   LDSP u64* hotrec;  // [HOT][64]: the exchange's (and the market maker's) agent record
-  LDSP i32* scr;     // [64]: batched-push slot table (rank -> queue slot)
+  LDSP i32* scr;     // [64] rank -> queue slot, then [64] u64 staged keys (MXA_QREG)
 
   static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 4 * PW : 0));
   DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
@@ -486,7 +530,11 @@ struct Eng {
     if (lane < 48) prof[lane] = 0;
 #endif
     trace = tcap ? (i64*)(env + PC.L.off_trace) : nullptr;
+    #ifdef MXA_QREG
+    scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 768);
+#else
     scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 256);
+#endif
 #ifdef MXA_PROF
     hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 256);
 #else
@@ -629,9 +677,14 @@ struct Eng {
     u32 bs = 0xFFFFFFFFu;
     i32 bj = -1;
     for (int j = 0; j < SQ; j++) {
+#ifdef MXA_QREG
+      u64 k = rk[j];
+      u32 s = rq[j];
+#else
       int slot = j * 64 + lane;
       u64 k = qk[slot];
       u32 s = qs[slot];
+#endif
       if (k < bk || (k == bk && s < bs)) {
         bk = k;
         bs = s;
@@ -664,9 +717,8 @@ struct Eng {
     u64 fm = rdl64(qfree, L);
     int j = ffs64(fm);
     int slot = j * 64 + L;
+    qset(j, key, seq, lane == L);
     if (lane == L) {
-      qk[slot] = key;
-      qs[slot] = seq;
       qfree &= ~(1ull << j);
       if (key < mk || (key == mk && seq < ms)) {
         mk = key;
@@ -703,24 +755,38 @@ struct Eng {
       return;
     }
     u64 f = qfree;
+    int tj[SQ];
     for (int t = 0; t < SQ; t++) {
+      tj[t] = -1;
       if (f && base + t < n) {
         const int j = ffs64(f);
         f &= f - 1;
         scr[base + t] = j * 64 + lane;
         qfree &= ~(1ull << j);
+        tj[t] = j;
       }
     }
     __threadfence_block();
     if (act) {
       const int slot = scr[r];
+#ifdef MXA_QREG
+      ((LDSP u64*)(scr + 64))[r] = key;  // staged for the slot's owner lane
+#else
       qk[slot] = key;
       qs[slot] = seq + (u32)r;
+#endif
       if constexpr (PL_LDS) pl_write(slot, m);
       else
         for (int i = 0; i < PW; i++) qpl[slot * PW + i] = m.w[i];
     }
     __threadfence_block();
+#ifdef MXA_QREG
+    for (int t = 0; t < SQ; t++) {
+      const bool mine = tj[t] >= 0;
+      const u64 k = mine ? ((LDSP u64*)(scr + 64))[base + t] : KEY_EMPTY;
+      qset(tj[t], k, seq + (u32)(base + t), mine);
+    }
+#endif
     q_rescan();
     seq += (u32)n;
     qcount += n;
@@ -781,10 +847,7 @@ struct Eng {
   }
 #else
   DEV void q_remove(int slot) {
-    if (lane == (slot & 63)) {
-      qk[slot] = KEY_EMPTY;
-      qs[slot] = 0xFFFFFFFFu;
-    }
+    qset(slot >> 6, KEY_EMPTY, 0xFFFFFFFFu, lane == (slot & 63));
     qfree |= (lane == (slot & 63)) ? (1ull << (slot >> 6)) : 0ull;
     u64 k0 = mk;
     u32 s0 = ms;
@@ -797,7 +860,7 @@ struct Eng {
     qcount--;
   }
   DEV void q_rekey(int slot, u64 key) {
-    if (lane == (slot & 63)) qk[slot] = key;
+    qsetk(slot >> 6, key, lane == (slot & 63));
     u64 k0 = mk;
     u32 s0 = ms;
     i32 j0 = mj;
@@ -2496,8 +2559,7 @@ struct Eng {
     for (int j = 0; j < SQ; j++) {
       int slot = j * 64 + lane;
       SavedEvent e = sq[slot];
-      qk[slot] = e.key;
-      qs[slot] = e.seq;
+      qset(j, e.key, e.seq, true);
       if (PL_LDS)
         for (int i = 0; i < PW; i++) qpl[slot * PW + i] = e.pl[i];
       if (e.key == KEY_EMPTY) qfree |= 1ull << j;
@@ -2519,8 +2581,8 @@ struct Eng {
     for (int j = 0; j < SQ; j++) {
       int slot = j * 64 + lane;
       SavedEvent e;
-      e.key = qk[slot];
-      e.seq = qs[slot];
+      e.key = qkey(j);
+      e.seq = qseq(j);
       e.pad = 0;
       for (int i = 0; i < 8; i++) e.pl[i] = (PL_LDS && i < PW) ? qpl[slot * PW + i] : 0u;
       sq[slot] = e;
@@ -2837,8 +2899,7 @@ struct Builder : Eng<CFG, true> {
     this->mj = -1;
     this->qfree = E::SQ >= 64 ? ~0ull : ((1ull << E::SQ) - 1ull);
     for (int j = 0; j < E::SQ; j++) {
-      this->qk[j * 64 + this->lane] = KEY_EMPTY;
-      this->qs[j * 64 + this->lane] = 0xFFFFFFFFu;
+      this->qset(j, KEY_EMPTY, 0xFFFFFFFFu, true);
     }
     for (int j = 0; j < E::SO; j++) this->bm[j] = -1;
     if constexpr (E::RP) {
