@@ -57,6 +57,7 @@ def replay_bench(args):
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     v.set_stream(stream.cuda_stream)
+    v.set_parity_hash(args.parity_hash)
     gen = torch.Generator(device="cuda")
     gen.manual_seed(1000 + rank)
     act = torch.empty((n_steps, n, ACTION_SIZE), dtype=torch.float64, device="cuda")
@@ -117,6 +118,7 @@ def replay_bench(args):
                           "envs_per_gpu": n, "global_envs": n * world, "tape_records": len(tp),
                           "gym_steps_per_s": n * world * n_steps * args.steps / el,
                           "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
+                          "parity_hash": bool(args.parity_hash),
                           "env_errors": nerr},
                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -165,6 +167,7 @@ def rl_bench(args):
     stream = torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
     torch.cuda.set_stream(stream)
     v.set_stream(stream.cuda_stream)
+    v.set_parity_hash(args.parity_hash)
     gen = torch.Generator(device="cuda")
     gen.manual_seed(1000 + rank)
     act = torch.empty((n_steps, n, ACTION_SIZE), dtype=torch.float64, device="cuda")
@@ -228,6 +231,7 @@ def rl_bench(args):
                           "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": v.n_agents,
                           "gym_steps_per_s": n * world * n_steps * args.steps / el,
                           "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
+                          "parity_hash": bool(args.parity_hash),
                           "env_errors": n_err, "all_done": bool(done_all.item())},
                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -274,6 +278,7 @@ def ddqn_bench(args):
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     v.set_stream(stream.cuda_stream)
+    v.set_parity_hash(args.parity_hash)
     learner = ddqn.DDQNLearner(device="cuda", seed=1000 + rank, batch_size=args.ddqn_batch)
     task = ddqn.ExecutionTask(device="cuda")
     res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
@@ -329,6 +334,7 @@ def ddqn_bench(args):
                           "learn_steps": learner.learn_step_counter - learns0,
                           "step_kernel_ms_total": sum(kms), "wall_ms_total": 1000.0 * el,
                           "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
+                          "parity_hash": bool(args.parity_hash),
                           "env_errors": int((s["status"] == 2).sum())},
                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -349,6 +355,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=1 << 22, help="max pops per env per kernel launch")
     ap.add_argument("--cpu-envs", type=int, default=2048, help="CPU-baseline sample size (envs)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--parity-hash", action="store_true",
+                    help="also compute the per-pop parity hash (test instrumentation, off by default: "
+                         "tests/test_gpu_hash_switch.py shows every market result is identical either way)")
     ap.add_argument("--ddqn-batch", type=int, default=32, help="rmsc03_ddqn: learner batch size (reference 32)")
     ap.add_argument("--tape", default=None, help="marketreplay tape under tests/golden (IBM_2003-01-14, GOOG_2012-06-21)")
     args = ap.parse_args()
@@ -374,6 +383,7 @@ def main():
     stream = torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
     torch.cuda.set_stream(stream)
     m.set_stream(stream.cuda_stream)
+    m.set_parity_hash(args.parity_hash)
     res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
 
     kernel_ms, launches = [0.0], [0]
@@ -432,6 +442,7 @@ def main():
                                    "the config's session), seeds %d+global_env" % (args.config, n, SEED0),
                        "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": m.n_agents,
                        "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
+                          "parity_hash": bool(args.parity_hash),
                        "env_errors": n_err, "device": torch.cuda.get_device_name(local),
                        "cus": torch.cuda.get_device_properties(local).multi_processor_count},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -136,6 +136,11 @@ int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32
  * best bid, best ask, best-bid size, best-ask size, lob flags: 1 bids, 2 asks) of
  * DummyRLExecutionAgent, the LOB being the newest ABIDESEnvMetrics entry (dummy_rl:294-315).
  * Asynchronous on the handle's stream; GymKernel handles only. */
+/* the per-pop parity hash (mxa_env_summary.hash: a rolling FNV-1a over every pop's trace
+ * record, the test harness's checksum; the reference computes nothing like it) is on by
+ * default.  Turning it off leaves every market result identical and the hash field frozen at
+ * its initial value; a handle with a trace ring keeps it on. */
+int mxa_set_parity_hash(mxa_handle* h, int32_t enabled);
 #define MXA_RL_STATE_WORDS 8
 int mxa_write_rl_state(mxa_handle* h, double* device_out);
 

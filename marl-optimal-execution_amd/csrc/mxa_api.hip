@@ -118,6 +118,8 @@ struct mxa_handle {
   char* d_tape = nullptr;
   double *d_act = nullptr, *d_obs = nullptr;
   int32_t* d_flags = nullptr;
+  bool parity_hash = true;  // per-pop trace hash (test instrumentation); off: kernel tcap -1
+  int32_t tcap_arg() const { return (parity_hash || P.L.trace_cap > 0) ? P.L.trace_cap : -1; }
   std::vector<char> tape_blob;  // host staging of the tape (uploaded by create_common)
   size_t tb_t, tb_oid, tb_dense, tb_price, tb_size, tb_buy, tb_tm, tb_tm0;
 };
@@ -356,7 +358,7 @@ int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32
   return MXA_EINVAL;
 #else
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  h->step(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap,
+  h->step(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(),
           (int64_t)1 << 40, (const RpCtx*)h->d_ctx, d_actions, d_obs, d_flags);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
@@ -381,7 +383,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
 
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
   if (!h || h->gym) return MXA_EINVAL;  // GymKernel handles advance by mxa_step
-  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, max_pops,
+  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
          h->d_ctx);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
@@ -401,7 +403,7 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   for (;;) {
     if (max_launches > 0 && launches >= max_launches) break;
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->P.L.trace_cap, chunk,
+    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), chunk,
            h->d_ctx);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
@@ -562,6 +564,12 @@ int mxa_write_results(mxa_handle* h, void* device_out) {
   hipLaunchKernelGGL(mxa_results_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env, h->P.L.env_stride,
                      n, (int64_t*)device_out);
   HIPCHK(h, hipGetLastError());
+  return MXA_OK;
+}
+
+int mxa_set_parity_hash(mxa_handle* h, int32_t enabled) {
+  if (!h) return MXA_EINVAL;
+  h->parity_hash = enabled != 0;
   return MXA_OK;
 }
 

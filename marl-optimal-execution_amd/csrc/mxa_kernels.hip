@@ -506,6 +506,7 @@ struct Eng {
   u32 dirty;  // RNG streams touched by this event: bits 0-3 G/O/K/L, bit 4 the agent's own
   i64* trace;
   i32 trace_cap;
+  bool hash_on;  // per-pop parity hash (kernel argument trace_cap < 0: off, and no trace ring)
   const RpCtx* rx;  // marketreplay: tape + runtime layout (nullptr otherwise)
   i32 end_step;     // GymKernel: the RL agent's spread reply ends a step
 #ifdef MXA_PROF
@@ -524,12 +525,13 @@ struct Eng {
     if constexpr (PL_LDS) qpl = (LDSP u32*)(lds + 12 * QCAP);
     else qpl = (u32*)(env + PC.L.off_q + sizeof(SavedEvent) * QCAP);  // [QCAP][PW] after the saved queue
     dirty = 0;
-    trace_cap = tcap;
+    hash_on = tcap >= 0;
+    trace_cap = tcap > 0 ? tcap : 0;
 #ifdef MXA_PROF
     prof = (LDSP u64*)(lds + LDS_Q + sizeof(EnvHdr));
     if (lane < 48) prof[lane] = 0;
 #endif
-    trace = tcap ? (i64*)(env + PC.L.off_trace) : nullptr;
+    trace = tcap > 0 ? (i64*)(env + PC.L.off_trace) : nullptr;
     #ifdef MXA_QREG
     scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 768);
 #else
@@ -2607,11 +2609,13 @@ struct Eng {
   // the per-pop bookkeeping of the fast paths: currentTime, parity trace + hash, ttl_messages
   DEV void account_pop(i64 t, u64 key, const Msg& m) {
     cur = t;
-const Rec rec = encode<PW == 8>(key, m);
-    hash = rec_hash(hash, rec);
-    if (trace && h.trace_len < trace_cap) {
-      if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
-      h.trace_len++;
+    if (hash_on || trace) {  // parity instrumentation (trace ring, per-pop hash)
+      const Rec rec = encode<PW == 8>(key, m);
+      if (hash_on) hash = rec_hash(hash, rec);
+      if (trace && h.trace_len < trace_cap) {
+        if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
+        h.trace_len++;
+      }
     }
     pops++;
   }
@@ -2714,11 +2718,13 @@ const Rec rec = encode<PW == 8>(key, m);
       PROF_ADD(0, t0);
       rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
       cur = t;
-      const Rec rec = encode<PW == 8>(key, m);
-      hash = rec_hash(hash, rec);
-      if (trace && h.trace_len < trace_cap) {
-        if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
-        h.trace_len++;
+      if (hash_on || trace) {
+        const Rec rec = encode<PW == 8>(key, m);
+        if (hash_on) hash = rec_hash(hash, rec);
+        if (trace && h.trace_len < trace_cap) {
+          if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
+          h.trace_len++;
+        }
       }
       pops++;
       PROF_ADD(32, t0);

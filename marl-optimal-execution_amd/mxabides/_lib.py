@@ -43,7 +43,7 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_read_book", "mxa_read_trace", "mxa_n_agents", "mxa_n_envs", "mxa_env_bytes", "mxa_set_stream",
            "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe",
            "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout", "mxa_create_replay", "mxa_step",
-           "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state"]
+           "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash"]
 
 _lib = None
 
@@ -85,6 +85,7 @@ def load():
     L.mxa_layout.argtypes = [P, P]
     L.mxa_write_results.argtypes = [P, P]
     L.mxa_write_rl_state.argtypes = [P, P]
+    L.mxa_set_parity_hash.argtypes = [P, I32]
     L.mxa_rng_probe.argtypes = [I32, U32, I32, D, D, I32, P]
     L.mxa_math_probe.argtypes = [I32, I32, P, P, P, I64]
     L.mxa_create_replay.argtypes = [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)]

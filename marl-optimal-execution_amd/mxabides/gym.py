@@ -76,6 +76,11 @@ class VecABIDESEnv:
         self._check(self.L.mxa_step_device(self._h, ctypes.c_void_p(d_actions), ctypes.c_void_p(d_obs),
                                            ctypes.c_void_p(d_flags)), "mxa_step_device")
 
+    def set_parity_hash(self, on):
+        """Per-pop parity hash (summary()["hash"]) on or off; market results are identical
+        either way (include/mxa.h mxa_set_parity_hash)."""
+        self._check(self.L.mxa_set_parity_hash(self._h, 1 if on else 0), "mxa_set_parity_hash")
+
     def set_stream(self, stream_ptr):
         """Step on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
         self._check(self.L.mxa_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None),

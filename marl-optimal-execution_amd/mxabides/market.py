@@ -50,6 +50,11 @@ class VecMarket:
         assert len(self.seeds) == self.n_envs
         self._check(self.L.mxa_set_seeds(self._h, self.seeds.ctypes.data), "mxa_set_seeds")
 
+    def set_parity_hash(self, on):
+        """Per-pop parity hash (summary()["hash"]) on or off; market results are identical
+        either way (include/mxa.h mxa_set_parity_hash)."""
+        self._check(self.L.mxa_set_parity_hash(self._h, 1 if on else 0), "mxa_set_parity_hash")
+
     def set_stream(self, stream_ptr):
         """Run on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
         self._check(self.L.mxa_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None),

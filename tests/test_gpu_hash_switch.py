@@ -1,0 +1,89 @@
+"""The per-pop parity hash is test instrumentation (the reference computes nothing like it).
+bench.py times the market step with it off, so these tests prove that switching it off changes
+nothing but the hash field: the whole HBM block of every env (agent records, open orders, RNG
+streams, queue, book, trade history) is byte-identical to the hash-on run except the 8-byte
+hash, for the bench workload's seeds, and the GymKernel composition steps to the same
+observations."""
+import numpy as np
+import pytest
+
+import mxabides
+from mxabides import shard
+from mxabides.gym import VecABIDESEnv
+
+pytestmark = pytest.mark.gpu
+HASH_OFF = 16  # EnvHdr.hash (include/mxa.h layout: cur, pops, hash, ...)
+
+
+SAVED_EVENT = 48  # include/mxa.h SavedEvent: u64 key, u32 seq, u32 pad, u32 payload[8]
+KEY_EMPTY = 0xFFFFFFFFFFFFFFFF
+
+
+def _blocks(m, envs):
+    """env blocks with the hash field and the payload words of EMPTY saved-queue slots zeroed:
+    a freed slot keeps the payload words of its last message, including words that message's
+    kind leaves unset (register contents at the push, never read), which is the only place
+    besides the hash where the two runs can differ."""
+    n = m.env_bytes
+    lay = m.layout()
+    q0, q1 = lay["q"], lay["book"]
+    out = []
+    for e in envs:
+        b = m.raw(int(e), 0, n)
+        b[HASH_OFF:HASH_OFF + 8] = 0
+        q = b[q0:q1].view(np.uint8)
+        nslot = (q1 - q0) // SAVED_EVENT
+        keys = q[:nslot * SAVED_EVENT].reshape(nslot, SAVED_EVENT)[:, :8].copy().view(np.uint64).ravel()
+        for sl in np.nonzero(keys == KEY_EMPTY)[0]:
+            b[q0 + sl * SAVED_EVENT + 16:q0 + (sl + 1) * SAVED_EVENT] = 0
+        out.append(b)
+    return out
+
+
+@pytest.mark.parametrize("config,n", [("rmsc03", 512), ("sparse_zi_100", 128), ("value_noise", 128)])
+def test_hash_off_leaves_every_env_block_identical(config, n):
+    seeds = shard.env_seeds(0, 0, 1, n)
+    on = mxabides.VecMarket(config, seeds)
+    on.run()
+    off = mxabides.VecMarket(config, seeds)
+    off.set_parity_hash(False)
+    off.run()
+    s_on, s_off = on.summary(), off.summary()
+    for k in ("events", "status", "current_time", "order_counter"):
+        assert (s_on[k] == s_off[k]).all(), k
+    assert (s_off["hash"] != s_on["hash"]).all()  # the hash really was not computed
+    envs = np.arange(n)
+    for e, a, b in zip(envs, _blocks(on, envs), _blocks(off, envs)):
+        assert np.array_equal(a, b), (config, e)
+
+
+def test_hash_off_bench_workload_summaries_identical():
+    seeds = shard.env_seeds(0, 0, 1, 4096)
+    on = mxabides.VecMarket("rmsc03", seeds)
+    on.run()
+    off = mxabides.VecMarket("rmsc03", seeds)
+    off.set_parity_hash(False)
+    off.run()
+    s_on, s_off = on.summary(), off.summary()
+    for k in ("events", "status", "current_time", "order_counter"):
+        assert (s_on[k] == s_off[k]).all(), k
+    for e in range(0, 4096, 97):
+        assert on.agents(e) == off.agents(e), e
+        assert on.book(e, 0) == off.book(e, 0) and on.book(e, 1) == off.book(e, 1), e
+
+
+def test_hash_off_gym_steps_identical():
+    seeds = [123456789, 2024, 7, 123, 99991, 31337]
+    a, b = VecABIDESEnv(seeds=seeds), VecABIDESEnv(seeds=seeds)
+    b.set_parity_hash(False)
+    rs = np.random.RandomState(5)
+    for _ in range(27):
+        act = rs.uniform(0, 1, (len(seeds), 3))
+        act[:, 0] *= 0.05
+        oa, da, va, ea = a.step(act)
+        ob, db, vb, eb = b.step(act)
+        assert np.array_equal(oa, ob) and (da == db).all() and (va == vb).all() and (ea == eb).all()
+    sa, sb = a.summary(), b.summary()
+    assert (sa["events"] == sb["events"]).all()
+    for e in range(len(seeds)):
+        assert a.agents(e) == b.agents(e) and a.book(e, 0) == b.book(e, 0)
