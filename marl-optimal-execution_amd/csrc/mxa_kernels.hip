@@ -423,6 +423,17 @@ struct Eng {
   static constexpr int SO = mxa_cfg::shape(CFG).so;
   static constexpr bool PL_LDS = mxa_cfg::shape(CFG).pl;
   static constexpr int PW = mxa_cfg::shape(CFG).pw;           // payload words queued
+  // grouped lane-min cache for deep queues (sparse_zi_1000: 48 slots per lane): a lane's slots
+  // in groups of QG, each group's min (key, seq, slot) kept in VGPRs, so a remove or requeue
+  // rescans one group of QG slots instead of all SQ
+#ifdef MXA_QREG
+  static constexpr bool QHIER = false;
+#else
+  static constexpr bool QHIER = SQ >= 16;
+#endif
+  static constexpr int QG = 8;
+  static constexpr int NG = QHIER ? SQ / QG : 1;
+  static_assert(!QHIER || SQ % QG == 0, "queue groups must tile the lane's slots");
   static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
   static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY;     // ABIDESEnv / replay composition
   static constexpr bool GYM = RP || CFG == MXA_CFG_RMSC03_RL;  // a GymKernel with a DummyRL agent
@@ -495,6 +506,9 @@ struct Eng {
   u64 mk;
   u32 ms;
   i32 mj;
+  u64 gk[NG];  // QHIER: per-group min of this lane's slots
+  u32 gs[NG];
+  i32 gj[NG];
   u64 qfree;
   // order book pool in VGPRs: slot (j, lane)
   i32 bp[SO], bq[SO], bo[SO], bm[SO], bh[SO];
@@ -674,7 +688,69 @@ struct Eng {
   }
 
   // ---------------- event queue
+  // min (key, seq, slot) over this lane's slots [j0, j0 + n)
+  DEV void q_scan(int j0, int n, u64& bk, u32& bs, i32& bj) {
+    bk = KEY_EMPTY;
+    bs = 0xFFFFFFFFu;
+    bj = -1;
+    for (int j = j0; j < j0 + n; j++) {
+      int slot = j * 64 + lane;
+      u64 k = qk[slot];
+      u32 s = qs[slot];
+      if (k < bk || (k == bk && s < bs)) {
+        bk = k;
+        bs = s;
+        bj = j;
+      }
+    }
+  }
+  DEV void q_lanemin() {  // QHIER: lane min from the group mins
+    u64 bk = gk[0];
+    u32 bs = gs[0];
+    i32 bj = gj[0];
+    for (int g = 1; g < NG; g++) {
+      if (gk[g] < bk || (gk[g] == bk && gs[g] < bs)) {
+        bk = gk[g];
+        bs = gs[g];
+        bj = gj[g];
+      }
+    }
+    mk = bk;
+    ms = bs;
+    mj = bj;
+  }
+  // QHIER: rescan group g (wave-uniform) in every lane, then the lane mins; lanes whose group g
+  // did not change recompute the same values
+  DEV void q_regroup(int g) {
+    u64 k;
+    u32 s;
+    i32 j;
+    q_scan(g * QG, QG, k, s, j);
+    for (int gg = 0; gg < NG; gg++) {
+      if (gg == g) {
+        gk[gg] = k;
+        gs[gg] = s;
+        gj[gg] = j;
+      }
+    }
+    q_lanemin();
+  }
+  DEV void q_gupd(int j, u64 k, u32 s) {  // QHIER: slot j of this lane now holds (k, s)
+    const int g = j / QG;
+    for (int gg = 0; gg < NG; gg++) {
+      if (gg == g && (k < gk[gg] || (k == gk[gg] && s < gs[gg]))) {
+        gk[gg] = k;
+        gs[gg] = s;
+        gj[gg] = j;
+      }
+    }
+  }
   DEV void q_rescan() {  // recompute this lane's min over its own slots
+    if constexpr (QHIER) {
+      for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
+      q_lanemin();
+      return;
+    }
     u64 bk = KEY_EMPTY;
     u32 bs = 0xFFFFFFFFu;
     i32 bj = -1;
@@ -727,6 +803,7 @@ struct Eng {
         ms = seq;
         mj = j;
       }
+      if constexpr (QHIER) q_gupd(j, key, seq);
       if (PL_LDS) pl_write(slot, m);
     }
     if (!PL_LDS) {
@@ -789,7 +866,16 @@ struct Eng {
       qset(tj[t], k, seq + (u32)(base + t), mine);
     }
 #endif
-    q_rescan();
+    if constexpr (QHIER) {  // only the new slots changed: fold them into the group mins
+      for (int t = 0; t < SQ; t++) {
+        if (tj[t] < 0) break;
+        const int slot = tj[t] * 64 + lane;
+        q_gupd(tj[t], qk[slot], qs[slot]);
+      }
+      q_lanemin();
+    } else {
+      q_rescan();
+    }
     seq += (u32)n;
     qcount += n;
     if (qcount > h.max_q) h.max_q = qcount;
@@ -851,6 +937,11 @@ struct Eng {
   DEV void q_remove(int slot) {
     qset(slot >> 6, KEY_EMPTY, 0xFFFFFFFFu, lane == (slot & 63));
     qfree |= (lane == (slot & 63)) ? (1ull << (slot >> 6)) : 0ull;
+    if constexpr (QHIER) {
+      q_regroup((slot >> 6) / QG);
+      qcount--;
+      return;
+    }
     u64 k0 = mk;
     u32 s0 = ms;
     i32 j0 = mj;
@@ -863,6 +954,10 @@ struct Eng {
   }
   DEV void q_rekey(int slot, u64 key) {
     qsetk(slot >> 6, key, lane == (slot & 63));
+    if constexpr (QHIER) {
+      q_regroup((slot >> 6) / QG);
+      return;
+    }
     u64 k0 = mk;
     u32 s0 = ms;
     i32 j0 = mj;
@@ -2907,6 +3002,7 @@ struct Builder : Eng<CFG, true> {
     for (int j = 0; j < E::SQ; j++) {
       this->qset(j, KEY_EMPTY, 0xFFFFFFFFu, true);
     }
+    if constexpr (E::QHIER) this->q_rescan();  // empty group mins
     for (int j = 0; j < E::SO; j++) this->bm[j] = -1;
     if constexpr (E::RP) {
       build_replay();
