@@ -426,12 +426,18 @@ struct Eng {
   // grouped lane-min cache for deep queues (sparse_zi_1000: 48 slots per lane): a lane's slots
   // in groups of QG, each group's min (key, seq, slot) kept in VGPRs, so a remove or requeue
   // rescans one group of QG slots instead of all SQ
+#ifndef MXA_QG
+#define MXA_QG 12  // group size at SQ >= 16 (measured, sparse_zi_1000: 4 -> 1194 ms, 6/8 -> 973, 12 -> 958)
+#endif
+#ifndef MXA_QHIER_MIN
+#define MXA_QHIER_MIN 6  // below 16 slots: two groups (sparse_zi_100, 8 slots: 149 -> 144 ms)
+#endif
+  static constexpr int QG = SQ >= 16 ? MXA_QG : SQ / 2;
 #ifdef MXA_QREG
   static constexpr bool QHIER = false;
 #else
-  static constexpr bool QHIER = SQ >= 16;
+  static constexpr bool QHIER = SQ >= MXA_QHIER_MIN && SQ % QG == 0 && SQ > QG;
 #endif
-  static constexpr int QG = 8;
   static constexpr int NG = QHIER ? SQ / QG : 1;
   static_assert(!QHIER || SQ % QG == 0, "queue groups must tile the lane's slots");
   static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
