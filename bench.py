@@ -427,12 +427,13 @@ def main():
         avg_launch_ms = kernel_ms[0] / max(1, launches[0])
         achieved = ALGO_BYTES_PER_EVENT * my_events_per_launch / (avg_launch_ms * 1e-3) / 1e9
         traffic = None
-        prof = os.path.join(ROOT, "profiles", "hbm_traffic_r01.json")
-        if os.path.exists(prof):
-            with open(prof) as f:
-                p = json.load(f)
-            if p.get("config") == args.config and p.get("envs") == n:
-                traffic = p.get("bytes_per_launch")
+        for name in ("hbm_traffic_%s.json" % args.config, "hbm_traffic_r01.json"):
+            prof = os.path.join(ROOT, "profiles", name)
+            if traffic is None and os.path.exists(prof):
+                with open(prof) as f:
+                    p = json.load(f)
+                if p.get("config") == args.config and p.get("envs") == n:
+                    traffic = p.get("bytes_per_launch")
         metric = METRIC if args.config == "rmsc03" else "env-steps/sec, %s x%d envs per GPU" % (args.config, n)
         out = {
             "metric": metric, "value": events / elapsed, "unit": "env-steps/s", "n_gpus": world,
