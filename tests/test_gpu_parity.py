@@ -122,6 +122,21 @@ def test_gpu_bench_workload_equals_oracle(mx):
     assert (s["hash"] == hs).all()
 
 
+@pytest.mark.parametrize("cfg,n", [("sparse_zi_1000", 1024), ("sparse_zi_100", 4096), ("value_noise", 4096)])
+def test_gpu_config_bench_workload_equals_oracle(mx, cfg, n):
+    """the exact `bench.py --config CFG --envs N` workloads (seeds 123456789 + env) are bit-exact
+    per env: sparse_zi_1000 x1024 is BASELINE configs[2] at full size"""
+    from mxabides import shard
+    seeds = shard.env_seeds(0, 0, 1, n)
+    m = mx.VecMarket(cfg, seeds)
+    m.run()
+    s = m.summary()
+    ev, hs, _ = pyoracle.run_batch(cfg, seeds, threads=min(16, os.cpu_count() or 1))
+    assert (s["status"] == 1).all()
+    assert (s["events"] == ev).all()
+    assert (s["hash"] == hs).all()
+
+
 @pytest.mark.parametrize("cfg,n", [("sparse_zi_1000", 8)])
 def test_gpu_wide_config_equals_oracle(mx, cfg, n):
     seeds = (np.arange(n, dtype=np.int64) * 104729 + 3) & 0xFFFFFFFF
