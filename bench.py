@@ -32,6 +32,33 @@ ALGO_BYTES_PER_EVENT = 256  # nominal algorithmic HBM bytes pe
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
+def traffic_record(config, envs, parity_hash):
+    """HBM bytes per run-kernel launch from the PMC record of THIS build (profiles/hbm_traffic_<config>.json,
+    written by tools/hbm_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
+    this same bench command).  A record is attached only when its build id (mxa_build_id(): a hash
+    of the kernel sources and flags), config, env count and parity-hash setting all match the
+    running bench; otherwise traffic is null and traffic_record says why."""
+    prof = os.path.join(ROOT, "profiles", "hbm_traffic_%s.json" % config)
+    if not os.path.exists(prof):
+        return None, {"file": None, "match": False, "why": "no PMC record for this config"}
+    with open(prof) as f:
+        p = json.load(f)
+    bid = mxabides.build_id()
+    src = {"file": os.path.relpath(prof, ROOT), "build_id": p.get("build_id"), "running_build_id": bid}
+    why = []
+    if p.get("build_id") != bid:
+        why.append("measured on another build")
+    if p.get("config") != config or p.get("envs") != envs:
+        why.append("other workload")
+    if bool(p.get("parity_hash")) != parity_hash:
+        why.append("parity hash setting differs")
+    src["match"] = not why
+    if why:
+        src["why"] = "; ".join(why)
+        return None, src
+    return p.get("bytes_per_launch"), src
+
+
 def replay_bench(args):
     """ABIDESEnv / market replay (BASELINE configs[4] shape): n envs stepping the reference's
     composition (Exchange + MarketReplayAgent + DummyRL) on a LOBSTER tape (IBM 2003-01-14 by
@@ -426,14 +453,7 @@ def main():
         my_events_per_launch = events / world / max(1, launches[0])
         avg_launch_ms = kernel_ms[0] / max(1, launches[0])
         achieved = ALGO_BYTES_PER_EVENT * my_events_per_launch / (avg_launch_ms * 1e-3) / 1e9
-        traffic = None
-        for name in ("hbm_traffic_%s.json" % args.config, "hbm_traffic_r01.json"):
-            prof = os.path.join(ROOT, "profiles", name)
-            if traffic is None and os.path.exists(prof):
-                with open(prof) as f:
-                    p = json.load(f)
-                if p.get("config") == args.config and p.get("envs") == n:
-                    traffic = p.get("bytes_per_launch")
+        traffic, traffic_src = traffic_record(args.config, n, bool(args.parity_hash))
         metric = METRIC if args.config == "rmsc03" else "env-steps/sec, %s x%d envs per GPU" % (args.config, n)
         out = {
             "metric": metric, "value": events / elapsed, "unit": "env-steps/s", "n_gpus": world,
@@ -447,7 +467,7 @@ def main():
                        "env_errors": n_err, "device": torch.cuda.get_device_name(local),
                        "cus": torch.cuda.get_device_properties(local).multi_processor_count},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_record": traffic_src,
                          "kernel": "mxa_run_kernel<%d> (%s)" % (mxabides.CONFIG_IDS[args.config], args.config), "avg_launch_ms": avg_launch_ms,
                          "launches": launches[0], "algo_bytes_per_event": ALGO_BYTES_PER_EVENT},
         }

@@ -130,19 +130,23 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
 int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags);
 /* the same on device arrays, asynchronous on the handle's stream */
 int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32_t* d_flags);
+/* the per-pop parity hash (mxa_env_summary.hash: a rolling FNV-1a over every pop's trace
+ * record, the test harness's checksum; the reference computes nothing like it) is on by
+ * default.  Turning it off leaves every market result identical and the hash field frozen at
+ * its initial value; a handle with a trace ring keeps it on. */
+int mxa_set_parity_hash(mxa_handle* h, int32_t enabled);
 /* the execution agent's state after the last step, for a learner on the device (the reward
  * inputs of DDQLearningExecutionAgent.compute_reward, ddqlearning_execution_agent.py:409-446):
  * DEVICE array [n_envs][MXA_RL_STATE_WORDS] float64 = (CASH, holdings, executed quantity,
  * best bid, best ask, best-bid size, best-ask size, lob flags: 1 bids, 2 asks) of
  * DummyRLExecutionAgent, the LOB being the newest ABIDESEnvMetrics entry (dummy_rl:294-315).
  * Asynchronous on the handle's stream; GymKernel handles only. */
-/* the per-pop parity hash (mxa_env_summary.hash: a rolling FNV-1a over every pop's trace
- * record, the test harness's checksum; the reference computes nothing like it) is on by
- * default.  Turning it off leaves every market result identical and the hash field frozen at
- * its initial value; a handle with a trace ring keeps it on. */
-int mxa_set_parity_hash(mxa_handle* h, int32_t enabled);
 #define MXA_RL_STATE_WORDS 8
 int mxa_write_rl_state(mxa_handle* h, double* device_out);
+/* identity of the kernel sources this library was built from (a hash of csrc/ and this header
+ * plus the compile flags): profile records (profiles/hbm_traffic_*.json) carry it, so a bench
+ * attaches measured HBM traffic only to the build it was measured on */
+const char* mxa_build_id(void);
 
 /* parity probes: device numpy-legacy RNG (mode 0 u32, 1 double, 2 randint(a,b),
  * 3 normal(a,b), 4 exponential(a), 5 uniform(a,b)) and device glibc math

@@ -610,6 +610,11 @@ int mxa_set_stream(mxa_handle* h, void* s) {
 double mxa_last_kernel_ms(const mxa_handle* h) { return h ? h->last_ms : 0; }
 const char* mxa_last_error(const mxa_handle* h) { return h ? h->err.c_str() : "null handle"; }
 
+#ifndef MXA_BUILD_ID
+#define MXA_BUILD_ID "unknown"
+#endif
+const char* mxa_build_id(void) { return MXA_BUILD_ID; }
+
 void mxa_destroy(mxa_handle* h) {
   if (!h) return;
   hipSetDevice(h->device);

@@ -436,10 +436,12 @@ struct Eng {
 #ifdef MXA_QREG
   static constexpr bool QHIER = false;
 #else
-  static constexpr bool QHIER = SQ >= MXA_QHIER_MIN && SQ % QG == 0 && SQ > QG;
+  static constexpr bool QHIER = SQ >= MXA_QHIER_MIN && SQ > QG;
+  // a group size that does not tile the deep queues is a build error, never a silent fall-back
+  // to the flat scan (a -DMXA_QG sweep must measure what it names)
+  static_assert(!QHIER || SQ % QG == 0, "queue groups must tile the lane's slots (MXA_QG)");
 #endif
   static constexpr int NG = QHIER ? SQ / QG : 1;
-  static_assert(!QHIER || SQ % QG == 0, "queue groups must tile the lane's slots");
   static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
   static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY;     // ABIDESEnv / replay composition
   static constexpr bool GYM = RP || CFG == MXA_CFG_RMSC03_RL;  // a GymKernel with a DummyRL agent

@@ -43,7 +43,8 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_read_book", "mxa_read_trace", "mxa_n_agents", "mxa_n_envs", "mxa_env_bytes", "mxa_set_stream",
            "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe",
            "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout", "mxa_create_replay", "mxa_step",
-           "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash"]
+           "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash",
+           "mxa_build_id"]
 
 _lib = None
 
@@ -93,5 +94,12 @@ def load():
     L.mxa_step_device.argtypes = [P, P, P, P]
     L.mxa_finalize.argtypes = [P]
     L.mxa_read_final.argtypes = [P, I32, P, I32]
+    L.mxa_build_id.argtypes = []
+    L.mxa_build_id.restype = ctypes.c_char_p
     _lib = L
     return L
+
+
+def build_id():
+    """the kernel-source hash libmxa was built with (build_lib.build_id)"""
+    return load().mxa_build_id().decode()

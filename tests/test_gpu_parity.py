@@ -148,14 +148,25 @@ def test_gpu_wide_config_equals_oracle(mx, cfg, n):
     assert (s["hash"] == hs).all()
 
 
-def test_gpu_chunked_launches_equal_single(mx):
-    seeds = [3, 5, 123456789, 1008]
-    a = mx.VecMarket("rmsc03", seeds)
+@pytest.mark.parametrize("cfg,seeds", [
+    ("rmsc03", [3, 5, 123456789, 1008]),            # flat queue (3 slots per lane)
+    ("sparse_zi_100", [3, 5, 123456789]),           # grouped queue: 2 groups of 4 slots
+    ("value_noise", [3, 5, 123456789]),             # grouped queue: 2 groups of 3 slots
+    ("sparse_zi_1000", [123456789, 5]),             # grouped queue: 4 groups of 12, payload in HBM
+])
+def test_gpu_chunked_launches_equal_single(mx, cfg, seeds):
+    """many save/restore cycles of the queue (LDS) and the book (VGPRs): the reload refills the
+    queue from the saved events and, in grouped mode, rebuilds the group minima from a
+    non-empty queue"""
+    a = mx.VecMarket(cfg, seeds)
     a.run(chunk=1 << 30)
-    b = mx.VecMarket("rmsc03", seeds)
-    b.run(chunk=977)  # many save/restore cycles of queue (LDS) and book (VGPRs)
+    b = mx.VecMarket(cfg, seeds)
+    b.run(chunk=977)
     sa, sb = a.summary(), b.summary()
+    assert (sa["status"] == 1).all() and (sb["status"] == 1).all()
     assert (sa["hash"] == sb["hash"]).all() and (sa["events"] == sb["events"]).all()
+    ev, hs, _ = pyoracle.run_batch(cfg, np.array(seeds, dtype=np.uint32), threads=4)
+    assert (sb["events"] == ev).all() and (sb["hash"] == hs).all()
 
 
 def test_gpu_reset_reproduces(mx):

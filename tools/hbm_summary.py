@@ -4,7 +4,13 @@ FETCH_SIZE / WRITE_SIZE are in KiB summed over the dispatch (rocprofv3).  Per
 MI355X_MICROARCH.md (HBM section) FETCH_SIZE on gfx950 reports half the bytes of coalesced
 reads, so reads are doubled; writes are taken as reported.  Our access widths (8-16 B per
 lane, scattered per env) are not the calibrated streaming case: the absolute figure is
-indicative, ratios between builds are exact."""
+indicative, ratios between builds are exact.
+
+    python tools/hbm_summary.py OUTDIR [--record CONFIG ENVS PARITY_HASH(0|1) SOURCE...]
+
+With --record, also writes profiles/hbm_traffic_<CONFIG>.json: the run kernel's bytes per
+launch stamped with the build id of the library that was profiled (mxa_build_id()), which is
+what bench.py matches before it reports the figure as roofline.traffic."""
 import csv
 import glob
 import json
@@ -12,6 +18,7 @@ import os
 import sys
 from collections import defaultdict
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = sys.argv[1]
 
 
@@ -43,3 +50,19 @@ print(json.dumps(res, indent=1))
 for f in stats:
     print(open(f).read())
 json.dump(res, open(os.path.join(out, "hbm_summary.json"), "w"), indent=1)
+
+if "--record" in sys.argv:
+    i = sys.argv.index("--record")
+    cfg, envs, ph = sys.argv[i + 1], int(sys.argv[i + 2]), sys.argv[i + 3] == "1"
+    source = " ".join(sys.argv[i + 4:])
+    sys.path.insert(0, os.path.join(ROOT, "marl-optimal-execution_amd"))
+    import mxabides
+    assert len(res) == 1, "expected exactly one run-kernel instantiation, got %s" % list(res)
+    (k, r), = res.items()
+    rec = {"config": cfg, "envs": envs, "kernel": k, "build_id": mxabides.build_id(), "parity_hash": ph}
+    rec.update({x: r[x] for x in ("bytes_per_launch", "read_bytes_corrected", "write_bytes", "fetch_size_kib",
+                                  "write_size_kib", "launches")})
+    rec["source"] = source
+    with open(os.path.join(out, "hbm_traffic_%s.json" % cfg), "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec, indent=1))
