@@ -531,6 +531,7 @@ struct Eng {
   bool hash_on;  // per-pop parity hash (kernel argument trace_cap < 0: off, and no trace ring)
   const RpCtx* rx;  // marketreplay: tape + runtime layout (nullptr otherwise)
   i32 end_step;     // GymKernel: the RL agent's spread reply ends a step
+  u32 run_skip;     // event runs: members below this seq are popped one by one (a LIMIT run that crosses)
 #ifdef MXA_PROF
   LDSP u64* prof;
 #endif
@@ -541,6 +542,8 @@ struct Eng {
   DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
     rx = ctx;
     end_step = 0;
+    add_delay = 0;
+    run_skip = 0;
     lane = laneid();
     qk = (LDSP u64*)lds;
     qs = (LDSP u32*)(lds + 8 * QCAP);
@@ -2722,6 +2725,219 @@ struct Eng {
     }
     pops++;
   }
+
+  // ---------------- event runs (zero-latency configurations: rmsc03, rmsc03 + DummyRL)
+  // A batched push (TradingAgent.cancelOrders, the POV market maker's 42-order ladder) and the
+  // exchange's replies to it leave n events with ONE key (t, recipient, MESSAGE) and
+  // consecutive seqs in the queue.  Once the first of them is the queue minimum, the other n-1
+  // are the next n-1 pops of Kernel.runner: every event pushed while they are handled takes a
+  // later seq, and none takes a smaller key (the exchange replies to recipients > 0 at
+  // t + pipeline delay; the acknowledgement handlers push nothing).  Such a run is handled in
+  // one pass, member i in lane i, with the per-pop effects of the reference applied in member
+  // order; ttl_messages (pops) and the parity hash count every member as its own pop.
+  // Handled: CANCEL_ORDER and non-crossing LIMIT_ORDER runs at the exchange, ORDER_ACCEPTED and
+  // ORDER_CANCELLED runs at a background TradingAgent.  About 95 % of rmsc03's pops are such
+  // members (the market maker's cancel / re-quote cycle every second).
+#if defined(MXA_NO_RUNS) || defined(MXA_QREG)
+  static constexpr bool RUNS = false;
+#else
+  static constexpr bool RUNS = ACK_FAST && BATCH && PL_LDS;
+#endif
+  // members of the run that starts at (key, s0): lane i gets member i's queue slot (-1 past
+  // the run); returns the run length (consecutive seqs from s0 that carry `key`)
+  DEV int run_collect(u64 key, u32 s0, int& mslot) {
+    scr[lane] = -1;
+    __threadfence_block();
+    for (int j = 0; j < SQ; j++) {
+      const int slot = j * 64 + lane;
+      const u32 d = qs[slot] - s0;
+      if (qk[slot] == key && d < 64u) scr[d] = slot;
+    }
+    __threadfence_block();
+    mslot = scr[lane];
+    const u64 b = bal(mslot >= 0);
+    return ~b == 0 ? 64 : ffs64(~b);
+  }
+  // the run's n slots leave the queue together (each lane rebuilds its free mask and minimum)
+  DEV void q_remove_run(int n, int mslot) {
+    if (lane < n) {
+      qk[mslot] = KEY_EMPTY;
+      qs[mslot] = 0xFFFFFFFFu;
+    }
+    __threadfence_block();
+    u64 fr = 0;
+    for (int j = 0; j < SQ; j++)
+      if (qk[j * 64 + lane] == KEY_EMPTY) fr |= 1ull << j;
+    qfree = fr;
+    q_rescan();
+    qcount -= n;
+  }
+  // per-pop accounting of the members, in member order
+  DEV void run_account(u64 key, i64 t, const Msg& mm, int n) {
+    if (hash_on || trace) {
+      for (int i = 0; i < n; i++) {
+        Msg m;
+        for (int w = 0; w < 8; w++) m.w[w] = w < PW ? rdl(mm.w[w], i) : 0u;
+        account_pop(t, key, m);
+      }
+    } else {
+      cur = t;
+      pops += n;
+    }
+  }
+  // OrderBook.cancelOrder for each member in order (OrderBook.py:284-339): the order is found
+  // by (side, price, id) and removed; ORDER_CANCELLED with the book's remaining quantity goes
+  // to the requester.  Members whose order is gone are silent no-ops.
+  DEV void run_ex_cancel(i64 t, const Msg& mm, int n) {
+    i32 nq = 0, nm = 0;
+    bool found = false;
+    for (int i = 0; i < n; i++) {
+      const u32 w0 = rdl(mm.w[0], i);
+      const int s = b_find((int)((w0 >> 6) & 1), (i32)rdl(mm.w[3], i), (i32)rdl(mm.w[1], i));
+      if (s >= 0) {
+        const i32 q = b_get(bq, s), mt = b_get(bm, s);
+        b_free(s);
+        const bool me = lane == i;
+        found = me || found;
+        nq = me ? q : nq;
+        nm = me ? mt : nm;
+      }
+    }
+    const Msg r = msg_order(MK_CANCELLED, (i32)mm.w[1], nm >> 1, nm & 1, nq, (i32)mm.w[3], 0);
+    const u64 rkey = ((u64)(t + PC.ex_pipeline) << 13) | ((u64)(u32)m_agent(mm) << 2) | MT_MESSAGE;
+    q_push_lanes(found, rkey, r);
+  }
+  // OrderBook.handleLimitOrder for a run of limit orders none of which can match: every buy is
+  // below the best ask and every sell above the best bid, counting the run's own earlier
+  // orders.  Each valid order (qty > 0) enters the book in member order (the same free slots,
+  // arrival stamps and history epoch as one-by-one entry) and gets ORDER_ACCEPTED.
+  // run_ex_limit_ok: no member can match and the book has room (else the run is popped one by
+  // one, and an overflow fails exactly where the reference's sequence would).
+  DEV bool run_ex_limit_ok(const Msg& mm, int n) {
+    const bool v = lane < n && (i32)mm.w[2] > 0;
+    const int buy = m_buy(mm);
+    const i32 price = (i32)mm.w[3];
+    const i32 bb = b_best(1), ba = b_best(0);
+    const i32 maxb = wmax_i32(v && buy ? price : INT32_MIN);
+    const i32 mins = wmin_i32(v && !buy ? price : INT32_MAX);
+    const int m = __popcll(bal(v));
+    int nfree = 0;
+    for (int j = 0; j < SO; j++) nfree += __popcll(bal(bm[j] < 0));
+    return maxb < ba && mins > bb && maxb < mins && nfree >= m;
+  }
+  DEV void run_ex_limit(i64 t, const Msg& mm, int n) {
+    const bool v = lane < n && (i32)mm.w[2] > 0;
+    const int buy = m_buy(mm);
+    const i32 price = (i32)mm.w[3];
+    const u64 vb = bal(v);
+    const int m = __popcll(vb);
+    if (m > 0) {
+      const int r = (int)__builtin_amdgcn_mbcnt_hi((u32)(vb >> 32), __builtin_amdgcn_mbcnt_lo((u32)vb, 0u));
+      if (v) scr[r] = lane;  // rank -> member lane
+      __threadfence_block();
+      const i32 agent = m_agent(mm), qty = (i32)mm.w[2], oid = (i32)mm.w[1];
+      const i32 meta = (agent << 1) | buy;
+      const i32 hep = h.epoch;
+      const u32 arr0 = h.arrival;
+      int base = 0;
+      for (int j = 0; j < SO; j++) {  // the k-th free slot in (j, lane) order takes rank k
+        const u64 fb = bal(bm[j] < 0);
+        const int fr = base + (int)__builtin_amdgcn_mbcnt_hi((u32)(fb >> 32), __builtin_amdgcn_mbcnt_lo((u32)fb, 0u));
+        const bool take = bm[j] < 0 && fr < m;
+        const int src = scr[take ? fr : 0];
+        const i32 sp = __shfl(price, src, 64), sq = __shfl(qty, src, 64), so = __shfl(oid, src, 64),
+                  sm = __shfl(meta, src, 64);
+        if (take) {
+          bp[j] = sp;
+          bq[j] = sq;
+          bo[j] = so;
+          bm[j] = sm;
+          ba[j] = arr0 + (u32)fr;
+          bh[j] = hep;
+        }
+        base += __popcll(fb);
+      }
+      h.arrival = arr0 + (u32)m;
+      h.b_count += m;
+      if (h.b_count > h.max_book) h.max_book = h.b_count;
+      LDSP i32* EP = ep_entries();
+      const i32 ne = EP[h.epoch & 15] + m;
+      if (lane == 0) EP[h.epoch & 15] = ne;
+      const Msg a = msg_order(MK_ACCEPTED, oid, agent, buy, qty, price, 0);
+      const u64 akey = ((u64)(t + PC.ex_pipeline) << 13) | ((u64)(u32)agent << 2) | MT_MESSAGE;
+      q_push_lanes(v, akey, a);
+    }
+  }
+  // TradingAgent.orderCancelled for each member (TradingAgent.py:464-480): del orders[id]
+  DEV void run_ta_cancelled(int rcp, i64 t, const Msg& mm, int n, OpenOrder* my) {
+    i32 u = rgi(AF_NUSED), nord = rgi(AF_NORD);
+    u32 dead = 0;
+    for (int i = 0; i < n; i++) {
+      const i32 oid = (i32)rdl(mm.w[1], i);
+      for (int j = 0; j < OC; j++) {
+        const u64 hit = bal(j * 64 + lane < u && my[j].oid == oid);
+        if (hit) {
+          const bool me = lane == ffs64(hit);
+          my[j].oid = me ? -1 : my[j].oid;
+          dead |= me ? (1u << j) : 0u;
+          nord--;
+          if (nord == 0) u = 0;
+          break;
+        }
+      }
+    }
+    OpenOrder* oo = open_ptr(rcp);
+    for (int j = 0; j < OC; j++)
+      if ((dead >> j) & 1) oo[j * 64 + lane].oid = -1;
+    rs(AF_NORD, (u32)nord);
+    rs(AF_NUSED, (u32)u);
+    rs64(AF_ATIME, t);
+    rec_store();
+  }
+  // one run starting at the popped event; returns the pops handled (0: pop it one by one)
+  DEV int run_event(u64 key, u32 s0, i64 t, int rcp, u32 kind, i64 budget) {
+    int mslot;
+    int n = run_collect(key, s0, mslot);
+    if (n < 2) return 0;
+    const Msg mm = pl_read(mslot >= 0 ? mslot : 0);
+    const u64 kb = bal(lane < n && m_kind(mm) == kind);  // same-kind prefix
+    n = ~kb == 0 ? 64 : ffs64(~kb);
+    if ((i64)n > budget) n = (int)budget;
+    if (n < 2) return 0;
+    if (rcp == 0) {
+      cur_agent = 0;
+      rlo = rhi = 0;
+      if (kind == MK_LIMIT) {
+        if (!run_ex_limit_ok(mm, n)) {
+          run_skip = s0 + (u32)n;
+          return 0;
+        }
+      }
+      run_account(key, t, mm, n);
+      q_remove_run(n, mslot);
+      if (kind == MK_CANCEL) run_ex_cancel(t, mm, n);
+      else run_ex_limit(t, mm, n);
+      atime_store(0, t);
+      return n;
+    }
+    if (kind == MK_CANCELLED) {
+      rec_load(rcp);
+      OpenOrder my[OC];
+      const OpenOrder* oo = open_ptr(rcp);
+      for (int j = 0; j < OC; j++) {
+        my[j].oid = -1;
+        if (j * 64 + lane < PC.L.open_cap) my[j] = oo[j * 64 + lane];
+      }
+      run_account(key, t, mm, n);
+      q_remove_run(n, mslot);
+      run_ta_cancelled(rcp, t, mm, n, my);
+      return n;
+    }
+    run_account(key, t, mm, n);  // ORDER_ACCEPTED: agentCurrentTimes only (see ACK_FAST)
+    q_remove_run(n, mslot);
+    atime_store(rcp, t);
+    return n;
+  }
   DEV void run(i64 max_pops) {
     for (i64 n = 0; n < max_pops && status == ST_RUNNING; n++) {
       if constexpr (GYM) {
@@ -2753,6 +2969,21 @@ struct Eng {
       i64 t = (i64)(key >> 13);
       int rcp = (int)((key >> 2) & 0x7FF);
       int type = (int)(key & 3);
+      if constexpr (RUNS) {
+        // a run past stopTime is not batched: the loop stops after its first member
+        if (type == MT_MESSAGE && t <= PC.stop && eseq >= run_skip) {
+          const u32 k = m_kind(m);
+          const bool exr = rcp == 0 && (k == MK_CANCEL || k == MK_LIMIT) && !(t > PC.mkt_close);
+          const bool ackr = rcp > 0 && rcp < ACK_LIMIT && (k == MK_ACCEPTED || k == MK_CANCELLED);
+          if (exr || ackr) {
+            const int nr = run_event(key, eseq, t, rcp, k, max_pops - n);
+            if (nr > 0) {
+              n += nr - 1;
+              continue;
+            }
+          }
+        }
+      }
 #ifndef MXA_NO_ACK_FAST
       if constexpr (ACK_FAST) {
         if (type == MT_MESSAGE && rcp == 0) {
