@@ -154,10 +154,10 @@ extern "C" {
 
 #ifdef MXA_PROF
 // diagnostics build only (not in include/mxa.h): phase cycle totals, then cleared
-int mxa_prof_read(uint64_t* out48) {
-  if (hipMemcpyFromSymbol(out48, HIP_SYMBOL(mxa::g_mxa_prof), 48 * 8) != hipSuccess) return MXA_EHIP;
-  static const uint64_t z[48] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(mxa::g_mxa_prof), z, 48 * 8) != hipSuccess) return MXA_EHIP;
+int mxa_prof_read(uint64_t* out64) {
+  if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(mxa::g_mxa_prof), 64 * 8) != hipSuccess) return MXA_EHIP;
+  static const uint64_t z[64] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(mxa::g_mxa_prof), z, 64 * 8) != hipSuccess) return MXA_EHIP;
   return MXA_OK;
 }
 #endif

@@ -52,7 +52,7 @@ constexpr size_t lds_bytes(int cfg) {
          + 256  // batched-push scratch: slot table
 #endif
 #ifdef MXA_PROF
-         + 384  // phase counters
+         + 512  // phase counters (64 x u64)
 #endif
       ;
 }

@@ -45,6 +45,7 @@ DEV i32 rdli(i32 v, int l) { return __builtin_amdgcn_readlane(v, l); }
 DEV u64 rdl64(u64 v, int l) {
   return ((u64)rdl((u32)(v >> 32), l) << 32) | rdl((u32)v, l);
 }
+DEV double rdl_d(double v, int l) { return __builtin_bit_cast(double, rdl64(__builtin_bit_cast(u64, v), l)); }
 DEV u64 bal(bool p) { return __ballot(p); }
 DEV int ffs64(u64 b) { return __ffsll((unsigned long long)b) - 1; }
 DEV int ffs32(u32 b) { return __ffs(b) - 1; }
@@ -399,7 +400,7 @@ DEV i64 U(i64 v) {
 }
 #ifdef MXA_PROF
 // diagnostics build only: per-phase shader-cycle totals over all envs (tools/prof_phases.py)
-__device__ unsigned long long g_mxa_prof[48];
+__device__ unsigned long long g_mxa_prof[64];
 DEV u64 stamp() {
   u64 t;
   __builtin_amdgcn_sched_barrier(0);
@@ -554,7 +555,7 @@ struct Eng {
     trace_cap = tcap > 0 ? tcap : 0;
 #ifdef MXA_PROF
     prof = (LDSP u64*)(lds + LDS_Q + sizeof(EnvHdr));
-    if (lane < 48) prof[lane] = 0;
+    prof[lane] = 0;
 #endif
     trace = tcap > 0 ? (i64*)(env + PC.L.off_trace) : nullptr;
     #ifdef MXA_QREG
@@ -563,7 +564,7 @@ struct Eng {
     scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 256);
 #endif
 #ifdef MXA_PROF
-    hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 256);
+    hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 512);
 #else
     hotrec = (LDSP u64*)(lds + LDS_Q + 512);
 #endif
@@ -1022,8 +1023,12 @@ struct Eng {
   DEV double o_compute(i64 ts, double v_adj, i64 pt, double pv) {
     i64 d = ts - pt;
     double mu = PC.o_rbar, gamma = PC.o_kappa, theta = PC.o_fundvol;
-    double loc = mu + (pv - mu) * gm_exp(-gamma * (double)d);
-    double scale = (gm_pow(theta, 2.0) / (2 * gamma)) * (1 - gm_exp(-2 * gamma * (double)d));
+    // the two exponentials are independent: lane 0 and lane 1 of ONE gm_exp evaluation.
+    // theta ** 2 (a constant of the config) was evaluated with the same glibc pow at build time
+    const double ex = gm_exp(lane == 0 ? -gamma * (double)d : -2 * gamma * (double)d);
+    double loc = mu + (pv - mu) * rdl_d(ex, 0);
+    double scale = (h.o_th2 / (2 * gamma)) * (1 - rdl_d(ex, 1));
+    (void)theta;
     RS O = grs(1);
     double v = rs_normal(O, loc, scale);
     grs_put(1, O);
@@ -1645,18 +1650,21 @@ struct Eng {
     }
     double delta = (double)(cur - rg64(AF_PREV_WAKE));
     double c = 1 - kappa;
+    double d2 = (double)(rg64(AF_MKT_CLOSE) - cur);
+    if (!(d2 > 0)) d2 = 0;
+    // the four powers of c are independent: lanes 0-3 of ONE gm_pow evaluation
+    const double pw = gm_pow(c, lane == 0 ? delta : lane == 1 ? 2 * delta : lane == 2 ? 2.0 : d2);
+    const double p_d = rdl_d(pw, 0), p_2d = rdl_d(pw, 1), p_2 = rdl_d(pw, 2), p_d2 = rdl_d(pw, 3);
     double r_t = rgd(AF_R_T), sigma_t = rgd(AF_SIGMA_T);
-    double r_tprime = (1 - gm_pow(c, delta)) * r_bar;
-    r_tprime += gm_pow(c, delta) * r_t;
-    double sigma_tprime = gm_pow(c, 2 * delta) * sigma_t;
-    sigma_tprime += ((1 - gm_pow(c, 2 * delta)) / (1 - gm_pow(c, 2.0))) * sigma_s;
+    double r_tprime = (1 - p_d) * r_bar;
+    r_tprime += p_d * r_t;
+    double sigma_tprime = p_2d * sigma_t;
+    sigma_tprime += ((1 - p_2d) / (1 - p_2)) * sigma_s;
     r_t = (sigma_n / (sigma_n + sigma_tprime)) * r_tprime;
     r_t += (sigma_tprime / (sigma_n + sigma_tprime)) * (double)obs;
     sigma_t = (sigma_n * sigma_t) / (sigma_n + sigma_t);
-    double d2 = (double)(rg64(AF_MKT_CLOSE) - cur);
-    if (!(d2 > 0)) d2 = 0;
-    double r_T = (1 - gm_pow(c, d2)) * r_bar;
-    r_T += gm_pow(c, d2) * r_t;
+    double r_T = (1 - p_d2) * r_bar;
+    r_T += p_d2 * r_t;
     rsd(AF_R_T, r_t);
     rsd(AF_SIGMA_T, sigma_t);
     rs64(AF_PREV_WAKE, cur);
@@ -2788,19 +2796,61 @@ struct Eng {
   // OrderBook.cancelOrder for each member in order (OrderBook.py:284-339): the order is found
   // by (side, price, id) and removed; ORDER_CANCELLED with the book's remaining quantity goes
   // to the requester.  Members whose order is gone are silent no-ops.
+  // Matching is one LDS bucket per member (order id mod 64): every book slot looks up its id's
+  // bucket and checks (id, price, side) against that member, so the cost does not grow with
+  // the run.  Ids are unique among live orders, so at most one live slot matches a member;
+  // members that share a bucket (ids 64 apart, or one id cancelled twice) take the serial path,
+  // which finds the orders member by member exactly as the reference's sequence does.
   DEV void run_ex_cancel(i64 t, const Msg& mm, int n) {
     i32 nq = 0, nm = 0;
     bool found = false;
-    for (int i = 0; i < n; i++) {
-      const u32 w0 = rdl(mm.w[0], i);
-      const int s = b_find((int)((w0 >> 6) & 1), (i32)rdl(mm.w[3], i), (i32)rdl(mm.w[1], i));
-      if (s >= 0) {
-        const i32 q = b_get(bq, s), mt = b_get(bm, s);
-        b_free(s);
-        const bool me = lane == i;
-        found = me || found;
-        nq = me ? q : nq;
-        nm = me ? mt : nm;
+    const bool mem = lane < n;
+    const i32 moid = (i32)mm.w[1], mprice = (i32)mm.w[3];
+    const i32 mside = m_buy(mm);
+    scr[lane] = -1;
+    __threadfence_block();
+    if (mem) scr[moid & 63] = lane;
+    __threadfence_block();
+    const bool coll = mem && scr[moid & 63] != lane;
+    if (!bal(coll)) {
+      int hit[SO];
+      int nfreed = 0;
+      for (int j = 0; j < SO; j++) {
+        const int c = scr[bo[j] & 63];
+        const int cs = c < 0 ? 0 : c;
+        const i32 co = __shfl(moid, cs, 64), cp = __shfl(mprice, cs, 64), csd = __shfl(mside, cs, 64);
+        hit[j] = (bm[j] >= 0 && c >= 0 && bo[j] == co && bp[j] == cp && (bm[j] & 1) == csd) ? c : -1;
+      }
+      __threadfence_block();
+      scr[lane] = -1;
+      __threadfence_block();
+      for (int j = 0; j < SO; j++) {
+        if (hit[j] >= 0) scr[hit[j]] = j * 64 + lane;  // member -> its book slot
+        nfreed += __popcll(bal(hit[j] >= 0));
+      }
+      __threadfence_block();
+      const int s = scr[lane];
+      const int sl = s < 0 ? 0 : (s & 63), sj = s < 0 ? 0 : (s >> 6);
+      for (int j = 0; j < SO; j++) {
+        const i32 q = __shfl(bq[j], sl, 64), mt = __shfl(bm[j], sl, 64);
+        nq = sj == j ? q : nq;
+        nm = sj == j ? mt : nm;
+      }
+      found = s >= 0;
+      for (int j = 0; j < SO; j++) bm[j] = hit[j] >= 0 ? -1 : bm[j];  // b_free
+      h.b_count -= nfreed;
+    } else {
+      for (int i = 0; i < n; i++) {
+        const u32 w0 = rdl(mm.w[0], i);
+        const int s = b_find((int)((w0 >> 6) & 1), (i32)rdl(mm.w[3], i), (i32)rdl(mm.w[1], i));
+        if (s >= 0) {
+          const i32 q = b_get(bq, s), mt = b_get(bm, s);
+          b_free(s);
+          const bool me = lane == i;
+          found = me || found;
+          nq = me ? q : nq;
+          nm = me ? mt : nm;
+        }
       }
     }
     const Msg r = msg_order(MK_CANCELLED, (i32)mm.w[1], nm >> 1, nm & 1, nq, (i32)mm.w[3], 0);
@@ -2869,9 +2919,31 @@ struct Eng {
     }
   }
   // TradingAgent.orderCancelled for each member (TradingAgent.py:464-480): del orders[id]
+  // (the same id buckets as run_ex_cancel: each live list entry looks up its id; a shared
+  // bucket takes the serial path)
   DEV void run_ta_cancelled(int rcp, i64 t, const Msg& mm, int n, OpenOrder* my) {
     i32 u = rgi(AF_NUSED), nord = rgi(AF_NORD);
     u32 dead = 0;
+    const i32 moid = (i32)mm.w[1];
+    scr[lane] = -1;
+    __threadfence_block();
+    if (lane < n) scr[moid & 63] = lane;
+    __threadfence_block();
+    const bool coll = lane < n && scr[moid & 63] != lane;
+    if (!bal(coll)) {
+      int nhit = 0;
+      for (int j = 0; j < OC; j++) {
+        const bool live = j * 64 + lane < u && my[j].oid != -1;
+        const int c = scr[my[j].oid & 63];
+        const i32 co = __shfl(moid, c < 0 ? 0 : c, 64);
+        const bool hit = live && c >= 0 && co == my[j].oid;
+        dead |= hit ? (1u << j) : 0u;
+        nhit += __popcll(bal(hit));
+      }
+      nord -= nhit;
+      if (nhit > 0 && nord == 0) u = 0;
+      n = 0;  // done
+    }
     for (int i = 0; i < n; i++) {
       const i32 oid = (i32)rdl(mm.w[1], i);
       for (int j = 0; j < OC; j++) {
@@ -2976,11 +3048,19 @@ struct Eng {
           const bool exr = rcp == 0 && (k == MK_CANCEL || k == MK_LIMIT) && !(t > PC.mkt_close);
           const bool ackr = rcp > 0 && rcp < ACK_LIMIT && (k == MK_ACCEPTED || k == MK_CANCELLED);
           if (exr || ackr) {
+            PROF_ADD(0, t0);
             const int nr = run_event(key, eseq, t, rcp, k, max_pops - n);
             if (nr > 0) {
+#ifdef MXA_PROF
+              const int kx = rcp == 0 ? (k == MK_CANCEL ? 0 : 1) : (k == MK_ACCEPTED ? 2 : 3);
+              PROF_ADD(34 + kx, t0);
+              PROF_CNT(38 + kx);
+              if (lane == 0) prof[42 + kx] += nr;
+#endif
               n += nr - 1;
               continue;
             }
+            PROF_ADD(46, t0);  // run detection that fell back to single pops
           }
         }
       }
@@ -2997,8 +3077,14 @@ struct Eng {
           q_remove(slot);
           PROF_ADD(33, t0);
           ex_receive(m);
-          PROF_ADD(2, t0);
-          PROF_CNT(16);
+#ifdef MXA_PROF
+          {  // by request kind: 48 SPREAD_REQ, 49 TV_REQ, 50 LIMIT, 51 CANCEL, 52 other (counts +8)
+            const u32 kk = m_kind(m);
+            const int eb = kk == MK_SPREAD_REQ ? 48 : kk == MK_TV_REQ ? 49 : kk == MK_LIMIT ? 50 : kk == MK_CANCEL ? 51 : 52;
+            PROF_ADD(eb, t0);
+            PROF_CNT(eb + 8);
+          }
+#endif
           if (dirty) rng_maint();
           PROF_ADD(30, t0);
           atime_store(0, t);
@@ -3083,11 +3169,14 @@ struct Eng {
       PROF_ADD(33, t0);
       rs64(AF_ATIME, t);
 #ifdef MXA_PROF
-      int pb = 2 + 2 * (rgi(AF_TYPE) & 7) + (type == MT_WAKEUP);
+      int pb = 2 + 2 * (rgi(AF_TYPE) & 7) + (type == MT_WAKEUP), pc = pb + 14;
+      if (type == MT_MESSAGE && m_kind(m) == MK_SPREAD && rgi(AF_TYPE) == AG_VALUE) pb = 53, pc = 61;
+      if (type == MT_MESSAGE && m_kind(m) == MK_SPREAD && rgi(AF_TYPE) == AG_POVMM) pb = 54, pc = 62;
+      if (type == MT_MESSAGE && m_kind(m) == MK_TV) pb = 55, pc = 63;
 #endif
       dispatch(rgi(AF_TYPE), type == MT_WAKEUP, m);
       PROF_ADD(pb, t0);
-      PROF_CNT(pb + 14);
+      PROF_CNT(pc);
       if (dirty) rng_maint();
       PROF_ADD(30, t0);
       rs64(AF_ATIME, t + rg64(AF_COMP) + add_delay);
@@ -3255,6 +3344,7 @@ struct Builder : Eng<CFG, true> {
       set_seed(1, g_seed(G));  // O
       h.o_pt = P.mkt_open;
       h.o_pv = P.o_rbar;
+      h.o_th2 = gm_pow(P.o_fundvol, 2.0);  // SMRO: theta ** 2 (SparseMeanRevertingOracle.py:105)
       h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
       tmp = g_seed(G);  // exchange
       set_seed(4 + 0, tmp);
@@ -3303,6 +3393,7 @@ struct Builder : Eng<CFG, true> {
       set_seed(2, g_seed(G));  // K
       h.o_pt = P.mkt_open;
       h.o_pv = P.o_rbar;
+      h.o_th2 = gm_pow(P.o_fundvol, 2.0);  // SMRO: theta ** 2 (SparseMeanRevertingOracle.py:105)
       h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
       set_seed(4 + 0, g_seed(G));  // exchange
       for (int a = P.first_noise; a < P.first_noise + P.n_noise; a++) {
@@ -3337,6 +3428,7 @@ struct Builder : Eng<CFG, true> {
       if (P.config == MXA_CFG_SPARSE_ZI_100) set_seed(3, g_seed(G));  // L
       h.o_pt = P.mkt_open;
       h.o_pv = P.o_rbar;
+      h.o_th2 = gm_pow(P.o_fundvol, 2.0);  // SMRO: theta ** 2 (SparseMeanRevertingOracle.py:105)
       h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
       set_seed(4 + 0, g_seed(G));  // exchange
       int a = P.first_zi;
@@ -3475,7 +3567,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
   g.run(max_pops);
   g.save();
 #ifdef MXA_PROF
-  if (g.lane < 48) atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
+  atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
 #endif
 }
 

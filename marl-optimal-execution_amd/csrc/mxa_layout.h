@@ -72,7 +72,7 @@ typedef struct {
   int64_t trace_len;
   int64_t ex_comp_delay;         // exchange's current computation delay
   int32_t max_q, max_book;       // capacity high-water marks (diagnostics)
-  int64_t pad1[1];
+  double o_th2;                  // oracle fund_vol ** 2 (glibc pow, evaluated at build)
 } EnvHdr;
 
 // one event slot as saved between launches (and payload as pushed)

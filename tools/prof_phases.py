@@ -13,7 +13,8 @@ from mxabides import _lib
 cfg = sys.argv[1] if len(sys.argv) > 1 else "rmsc03"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 m = mxabides.VecMarket(cfg, (123456789 + np.arange(n)) & 0xFFFFFFFF)
-buf = (ctypes.c_uint64 * 48)()
+m.set_parity_hash(os.environ.get("MXA_PROF_HASH", "0") == "1")  # off, as bench.py times it
+buf = (ctypes.c_uint64 * 64)()
 lib = _lib.load()
 lib.mxa_prof_read(buf)  # clear
 m.reset()
@@ -23,7 +24,7 @@ v = list(buf)
 ev = int(m.summary()["events"].sum())
 names = ["pop+hash+rec_load", "requeue"] + ["%s.%s" % (a, w) for a in ["EX", "ZI", "NOISE", "VALUE", "MM", "MOM"] for w in ["msg", "wake"]]
 names += ["ACCEPTED fast", "CANCELLED fast"]  # phases 14, 15 (counts 28, 29)
-tot = v[0] + v[1] + sum(v[2:16]) + v[30] + v[31] + v[32] + v[33]
+tot = v[0] + v[1] + sum(v[2:16]) + v[30] + v[31] + v[32] + v[33] + sum(v[34:38]) + v[46] + sum(v[48:56])
 print("events %d  total cycles/event (sum over waves) %.0f" % (ev, tot / ev))
 print("%-20s %8s %10s %12s" % ("phase", "share", "cyc/event", "cyc/call"))
 for i, nm in enumerate(names):
@@ -33,3 +34,14 @@ print("%-20s %7.1f%% %10.0f" % ("rng_maint", 100 * v[30] / tot, v[30] / ev))
 print("%-20s %7.1f%% %10.0f" % ("tail+rec_store", 100 * v[31] / tot, v[31] / ev))
 print("%-20s %7.1f%% %10.0f" % ("encode+hash(+trace)", 100 * v[32] / tot, v[32] / ev))
 print("%-20s %7.1f%% %10.0f" % ("q_remove", 100 * v[33] / tot, v[33] / ev))
+# event runs (phases 34-37, calls 38-41, member pops 42-45; 46 = detection that fell back)
+for i, nm in enumerate(["run EX.CANCEL", "run EX.LIMIT", "run ACCEPTED", "run CANCELLED"]):
+    c, mem = v[38 + i], v[42 + i]
+    print("%-20s %7.1f%% %10.0f %12s  members %d (%.1f%% of pops, %.1f per run)"
+          % (nm, 100 * v[34 + i] / tot, v[34 + i] / ev, ("%.0f (%d calls)" % (v[34 + i] / c, c)) if c else "",
+             mem, 100 * mem / ev, mem / c if c else 0))
+print("%-20s %7.1f%% %10.0f" % ("run fallback", 100 * v[46] / tot, v[46] / ev))
+for i, nm in enumerate(["EX SPREAD_REQ", "EX TV_REQ", "EX LIMIT (single)", "EX CANCEL (single)", "EX other",
+                        "VALUE SPREAD (place)", "MM SPREAD", "MM TV"]):
+    c = v[56 + i]
+    print("%-20s %7.1f%% %10.0f %12s" % (nm, 100 * v[48 + i] / tot, v[48 + i] / ev, ("%.0f (%d calls)" % (v[48 + i] / c, c)) if c else ""))
