@@ -292,6 +292,10 @@ DEV Msg msg_make(u32 kind, i32 agent) {
   return m;
 }
 #define MF_NOT_SAME (1u << 12)  // MODIFY_ORDER whose new order carries another id
+// queue-internal (never part of a message's content): another member of the same batched push
+// (q_push_lanes) follows this one with the same key and the next seq, so the pop of this event
+// starts an event run (Eng::run_event)
+#define MF_RUN (1u << 13)
 DEV Msg msg_order(u32 kind, i32 oid, i32 agent, int is_buy, i32 qty, i32 price, i32 fill) {
   Msg m = msg_make(kind, agent);
   m.w[0] |= (u32)is_buy << 6;
@@ -866,9 +870,11 @@ struct Eng {
       qk[slot] = key;
       qs[slot] = seq + (u32)r;
 #endif
-      if constexpr (PL_LDS) pl_write(slot, m);
+      Msg mw = m;
+      if (r < n - 1) mw.w[0] |= MF_RUN;
+      if constexpr (PL_LDS) pl_write(slot, mw);
       else
-        for (int i = 0; i < PW; i++) qpl[slot * PW + i] = m.w[i];
+        for (int i = 0; i < PW; i++) qpl[slot * PW + i] = mw.w[i];
     }
     __threadfence_block();
 #ifdef MXA_QREG
@@ -1194,6 +1200,57 @@ struct Eng {
     i64 start = cur - lookback;
     i64 vol = 0;
     int live_total = 0;
+#ifndef MXA_TV_FULLSCAN
+    // Newest records first, 64 per chunk (lane L = record lo + L, chronological).  Records are
+    // appended in time order, so once a chunk's oldest record is before `start` every older
+    // record is too, and the window is usually inside the newest chunk.  Whether ANY live
+    // record exists (pandas raising otherwise) is decided by the newest chunk: a maker logs its
+    // own entry epoch, which is never above the epoch its taker logs in the same match, and
+    // epochs never decrease, so the newest taker record (one of the two newest records) holds
+    // the largest epoch of the ring.  Duplicate (t, q) pairs sit in one contiguous equal-t
+    // block: lanes compare with their predecessors by shuffles, and only a block that crosses
+    // into the older chunk walks back through memory.
+    (void)live_total;
+    bool any = false;
+    for (int hi = n; hi > 0; hi -= 64) {
+      const int lo = hi > 64 ? hi - 64 : 0;
+      const int k = lo + lane;
+      const bool valid = k < hi;
+      TxRec r;
+      r.t = 0;
+      r.q = 0;
+      r.epoch = -1;
+      if (valid) r = R[(first + k) % cap];
+      const bool live = valid && r.epoch >= lo_ep;
+      const bool inwin = valid && r.t >= start;
+      if (hi == n) any = bal(live) != 0;
+      bool dup = false;
+      for (int d = 1; d < 64; d++) {
+        const int src = lane - d < 0 ? 0 : lane - d;
+        const i64 pt = (i64)(((u64)(u32)__shfl((i32)((u64)r.t >> 32), src, 64) << 32) |
+                             (u32)__shfl((i32)(u32)(u64)r.t, src, 64));
+        const i32 pq = __shfl(r.q, src, 64), pe = __shfl(r.epoch, src, 64);
+        const bool same = lane - d >= 0 && pt == r.t;
+        dup = dup || (same && pe >= lo_ep && pq == r.q);
+        if (!bal(same && live && inwin && !dup)) break;
+      }
+      if (lo > 0) {  // an equal-t block that started in the older chunk
+        const TxRec o = R[(first + lo - 1) % cap];
+        const i64 t0 = (i64)rdl64((u64)r.t, 0);
+        if (U(o.t) == t0) {
+          for (int j = lo - 1; live && inwin && !dup && r.t == o.t && j >= 0; j--) {
+            const TxRec p = R[(first + j) % cap];
+            if (p.t != r.t) break;
+            if (p.epoch >= lo_ep && p.q == r.q) dup = true;
+          }
+        }
+      }
+      vol += wsum_i64((live && !dup && inwin) ? (i64)r.q : 0);
+      if (!(bal(inwin) & 1ull)) break;  // the chunk's oldest record is before the window
+    }
+    if (!any) *perr = 1;  // pandas raises when no transaction records exist
+    return vol;
+#endif
     for (int b = 0; b < n; b += 64) {
       int k = b + lane;  // k-th record in chronological order
       bool live = false, dup = false, inwin = false;
@@ -3043,7 +3100,7 @@ struct Eng {
       int type = (int)(key & 3);
       if constexpr (RUNS) {
         // a run past stopTime is not batched: the loop stops after its first member
-        if (type == MT_MESSAGE && t <= PC.stop && eseq >= run_skip) {
+        if (type == MT_MESSAGE && (m.w[0] & MF_RUN) && t <= PC.stop && eseq >= run_skip) {
           const u32 k = m_kind(m);
           const bool exr = rcp == 0 && (k == MK_CANCEL || k == MK_LIMIT) && !(t > PC.mkt_close);
           const bool ackr = rcp > 0 && rcp < ACK_LIMIT && (k == MK_ACCEPTED || k == MK_CANCELLED);

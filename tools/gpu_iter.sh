@@ -15,3 +15,5 @@ if [ -f marl-optimal-execution_amd/lib/libmxa_prof.so ]; then
   MXA_LIB=$PWD/marl-optimal-execution_amd/lib/libmxa_prof.so timeout -k 10 300 python tools/prof_phases.py > $O/phases.txt 2>&1 || { echo "phases failed"; tail $O/phases.txt; exit 1; }
   cat $O/phases.txt
 fi
+timeout -k 10 200 python tools/host_timing.py > $O/host_timing.txt 2>&1 || { echo "host timing failed"; tail $O/host_timing.txt; exit 1; }
+cat $O/host_timing.txt
