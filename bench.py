@@ -109,8 +109,9 @@ def replay_bench(args):
         shard.gather_records(res, world)
         return res[:, 0].sum()
 
-    for _ in range(args.warmup):
-        episode(False)
+    evw = torch.zeros((), dtype=torch.int64, device="cuda")
+    for _ in range(args.warmup):  # the timed loop's exact ops
+        evw += episode(False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -219,8 +220,12 @@ def rl_bench(args):
         shard.gather_records(res, world)
         return res[:, 0].sum(), flags
 
-    for k in range(args.warmup):
-        episode(k, False)
+    evw = torch.zeros((), dtype=torch.int64, device="cuda")
+    dw = torch.ones((), dtype=torch.bool, device="cuda")
+    for k in range(args.warmup):  # the timed loop's exact ops (first launches of torch's kernels included)
+        e, f = episode(k, False)
+        evw += e
+        dw &= (((f & 1) != 0) | ((f & 4) != 0)).all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -318,8 +323,9 @@ def ddqn_bench(args):
         shard.gather_records(res, world)
         return res[:, 0].sum(), r["steps"]
 
-    for k in range(args.warmup):
-        episode(k, False)
+    evw = torch.zeros((), dtype=torch.int64, device="cuda")
+    for k in range(args.warmup):  # the timed loop's exact ops
+        evw += episode(k, False)[0]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

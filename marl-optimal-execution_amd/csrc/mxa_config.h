@@ -46,6 +46,7 @@ constexpr Shape shape(int cfg) {
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
+         + 1024                                                                               // RNG stream windows
 #ifdef MXA_QREG
          + 768  // batched-push scratch: slot table + staged keys
 #else

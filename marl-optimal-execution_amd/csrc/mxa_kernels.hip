@@ -127,6 +127,7 @@ DEV u64 as_u(double x) { return __builtin_bit_cast(u64, x); }
 // materialized at every event boundary (rs_maint, one code instance in the event loop), so
 // the draw sites inside the agent handlers never contain the twist; the build kernel
 // (BUILD = true) materializes blocks on demand instead.
+#define LDSP __attribute__((address_space(3)))
 template <bool BUILD>
 struct RSt {
   u32* key;
@@ -134,6 +135,11 @@ struct RSt {
   i32 m;      // highest materialized block
   i32 hasg;   // bit0: cached second gauss (legacy_gauss); bit1: look-ahead overrun
   double gauss;
+  // run kernel, global streams G/O/K/L: a 64-word window of the stream's outputs in LDS (words
+  // lw0 .. lw0 + lwn - 1, untempered), so a draw is an LDS read instead of an HBM round trip;
+  // lw == nullptr: draws read the MT block in HBM (agent streams, the build kernel)
+  LDSP u32* lw;
+  i32 lw0, lwn;
 };
 
 // materialize block b (>= 1) from block b-1, cooperatively over the wave in the four
@@ -176,8 +182,41 @@ DEV void mt_seed(u32* key, u32 s) {
   wfence();
 }
 
+// refill a stream window from position p: lane i loads output word p + i if its block is in
+// the double buffer (materialized and not yet overwritten); the window ends at the first word
+// that is not, and an empty window is the look-ahead overrun
+template <bool B>
+DEV void rs_fill(RSt<B>& r) {
+  const int lane = laneid();
+  const int q = r.p + lane, b = q / MXA_MT_N;
+  const bool ok = b <= r.m && b >= r.m - 1;
+  u32 v = 0;
+  if (ok) v = r.key[(b & 1) * MXA_MT_N + (q - b * MXA_MT_N)];
+  r.lw[lane] = v;
+  const u64 okb = __ballot(ok);
+  r.lwn = ~okb == 0 ? 64 : __ffsll((unsigned long long)~okb) - 1;
+  r.lw0 = r.p;
+  if (r.lwn == 0) r.hasg |= 2;
+  __threadfence_block();
+}
 template <bool B>
 DEV u32 rs_u32(RSt<B>& r) {
+  if constexpr (!B) {
+    if (r.lw) {
+      u32 off = (u32)(r.p - r.lw0);
+      if (off >= (u32)r.lwn) {
+        rs_fill(r);
+        off = 0;
+      }
+      u32 y = r.lw[off];
+      r.p++;
+      y ^= (y >> 11);
+      y ^= (y << 7) & 0x9d2c5680u;
+      y ^= (y << 15) & 0xefc60000u;
+      y ^= (y >> 18);
+      return y;
+    }
+  }
   int blk = r.p / MXA_MT_N;
   if (B) {
     while (r.m < blk) {
@@ -392,7 +431,6 @@ DEV u64 rec_hash(u64 h, const Rec& r) {
 // ------------------------------------------------------------------------------------
 // the engine: one instance per wave (= per env), lives in registers / LDS
 // ------------------------------------------------------------------------------------
-#define LDSP __attribute__((address_space(3)))
 // uniform view of a value the compiler cannot prove wave-uniform (loads of a wave-uniform
 // address): moves it to SGPRs so the arithmetic on it is scalar
 DEV i32 U(i32 v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -542,6 +580,7 @@ struct Eng {
 #endif
   LDSP u64* hotrec;  // [HOT][64]: the exchange's (and the market maker's) agent record
   LDSP i32* scr;     // [64] rank -> queue slot, then [64] u64 staged keys (MXA_QREG)
+  LDSP u32* rwin;    // [4][64] output windows of the global RNG streams (RSt::lw)
 
   static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 4 * PW : 0));
   DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
@@ -562,11 +601,12 @@ struct Eng {
     prof[lane] = 0;
 #endif
     trace = tcap > 0 ? (i64*)(env + PC.L.off_trace) : nullptr;
-    #ifdef MXA_QREG
+#ifdef MXA_QREG
     scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 768);
 #else
     scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 256);
 #endif
+    rwin = (LDSP u32*)((LDSP char*)scr - 1024);
 #ifdef MXA_PROF
     hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 512);
 #else
@@ -655,6 +695,8 @@ struct Eng {
   // agent RNG stream (Agent.random_state): key words in HBM, pos/gauss cache in the record
   DEV RS agent_rs() {
     RS r;
+    r.lw = nullptr;
+    r.lw0 = r.lwn = 0;
     r.key = rng_key(4 + cur_agent);
     r.p = rgi(AF_RS_POS);
     r.m = rgi(AF_RS_M);
@@ -677,6 +719,14 @@ struct Eng {
     r.m = h.rs_m[s];
     r.hasg = h.rs_has_gauss[s];
     r.gauss = h.rs_gauss[s];
+    if constexpr (BUILD) {
+      r.lw = nullptr;
+      r.lw0 = r.lwn = 0;
+    } else {
+      r.lw = rwin + s * 64;
+      r.lw0 = h.rs_w0[s];
+      r.lwn = h.rs_wn[s];
+    }
     return r;
   }
   DEV void grs_put(int s, const RS& r) {
@@ -684,6 +734,10 @@ struct Eng {
     h.rs_m[s] = r.m;
     h.rs_has_gauss[s] = r.hasg;
     h.rs_gauss[s] = r.gauss;
+    if constexpr (!BUILD) {
+      h.rs_w0[s] = r.lw0;
+      h.rs_wn[s] = r.lwn;
+    }
     dirty |= 1u << s;
   }
   // event boundary: keep one MT block of look-ahead for every stream this event drew from
@@ -2707,6 +2761,8 @@ struct Eng {
     status = h.status;
     err = h.err;
     qcount = h.q_count;
+    if (lane < 4) h.rs_wn[lane] = 0;  // the LDS stream windows did not survive the last launch
+    wfence();
   }
   DEV void hdr_to_global() {
     if (lane == 0) {

@@ -68,12 +68,17 @@ typedef struct {
   int32_t rs_pos[4], rs_has_gauss[4];
   double rs_gauss[4];
   int32_t rs_m[4];
+  int32_t rs_w0[4], rs_wn[4];    // run kernel: LDS output window of each stream (start, length)
   int32_t q_count, b_count;      // saved queue / book occupancy
   int64_t trace_len;
   int64_t ex_comp_delay;         // exchange's current computation delay
   int32_t max_q, max_book;       // capacity high-water marks (diagnostics)
   double o_th2;                  // oracle fund_vol ** 2 (glibc pow, evaluated at build)
 } EnvHdr;
+
+#ifdef __cplusplus
+static_assert(sizeof(EnvHdr) % 8 == 0 && sizeof(EnvHdr) <= 512, "EnvHdr: copied by 64 lanes x 8 B, 512 B of LDS");
+#endif
 
 // one event slot as saved between launches (and payload as pushed)
 typedef struct {

@@ -17,3 +17,7 @@ if [ -f marl-optimal-execution_amd/lib/libmxa_prof.so ]; then
 fi
 timeout -k 10 200 python tools/host_timing.py > $O/host_timing.txt 2>&1 || { echo "host timing failed"; tail $O/host_timing.txt; exit 1; }
 cat $O/host_timing.txt
+if [ -n "$RLT" ]; then
+  timeout -k 10 200 python tools/host_timing_rl.py > $O/host_timing_rl.txt 2>&1 || { echo "rl host timing failed"; tail $O/host_timing_rl.txt; exit 1; }
+  cat $O/host_timing_rl.txt
+fi
