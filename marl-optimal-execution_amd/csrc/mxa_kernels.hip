@@ -745,8 +745,11 @@ struct Eng {
 #pragma unroll 1
     for (int k = 0; k < 5; k++) {
       if (!((dirty >> k) & 1)) continue;
+      const i32 p = k < 4 ? h.rs_pos[k] : rgi(AF_RS_POS), m = k < 4 ? h.rs_m[k] : rgi(AF_RS_M);
+      const i32 hg = k < 4 ? h.rs_has_gauss[k] : rgi(AF_RS_HASG);
+      if (hg & 2) fail(ERR_RNG_OVERRUN);
+      if (m >= p / MXA_MT_N + 1) continue;  // the look-ahead block is there (almost always)
       RS r = k < 4 ? grs(k) : agent_rs();
-      if (r.hasg & 2) fail(ERR_RNG_OVERRUN);
       rs_maint(r);
       if (k < 4) {
         h.rs_m[k] = r.m;
