@@ -169,7 +169,7 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   static_assert((int)MXA_RMSC03 == (int)MXA_CFG_RMSC03 && (int)MXA_SPARSE_ZI_100 == (int)MXA_CFG_SPARSE_ZI_100 &&
                     (int)MXA_SPARSE_ZI_1000 == (int)MXA_CFG_SPARSE_ZI_1000 &&
                     (int)MXA_MARKETREPLAY == (int)MXA_CFG_MARKETREPLAY && (int)MXA_RMSC03_RL == (int)MXA_CFG_RMSC03_RL &&
-                    (int)MXA_VALUE_NOISE == (int)MXA_CFG_VALUE_NOISE,
+                    (int)MXA_VALUE_NOISE == (int)MXA_CFG_VALUE_NOISE && (int)MXA_RMSC01 == (int)MXA_CFG_RMSC01,
                 "config ids");
   if (config == MXA_RMSC03) bind<MXA_CFG_RMSC03>(h);
 #ifndef MXA_ONLY_RMSC03
@@ -177,6 +177,7 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   else if (config == MXA_SPARSE_ZI_1000) bind<MXA_CFG_SPARSE_ZI_1000>(h);
   else if (config == MXA_RMSC03_RL) bind<MXA_CFG_RMSC03_RL>(h);
   else if (config == MXA_VALUE_NOISE) bind<MXA_CFG_VALUE_NOISE>(h);
+  else if (config == MXA_RMSC01) bind<MXA_CFG_RMSC01>(h);
 #endif
   else {
     delete h;

@@ -38,6 +38,9 @@ constexpr Shape shape(int cfg) {
   // market-maker records in LDS
   return cfg == MXA_CFG_RMSC03 ? Shape{3, 2, true, MXA_RMSC03_WAVES, 6, 2 * MXA_HOT_RECORDS}
        : cfg == MXA_CFG_RMSC03_RL ? Shape{3, 2, true, 4, 8, 2 * MXA_HOT_RECORDS}  // wide spread replies (depth 500)
+       // rmsc01: oracle maxima over seeds 123456789 / 7: 140 pending events, 75 resting orders;
+       // wide replies for the market maker's depth-5 spread queries
+       : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, 4, 8, 0}
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, 2, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
@@ -211,6 +214,62 @@ constexpr void params_rmsc03_rl(MxaParams& P) {
   P.rl_depth = 500;
 }
 
+// config/rmsc01.py:49-263 (RMSC-1): 1 exchange, 1 MarketMakerAgent (500-1000 shares, 1 s, depth 5),
+// 50 ZI and 25 HBL agents (sigma_n 1e4, sigma_s = fund_vol 1e-4, kappa 1.67e-15, sigma_pv 5e4,
+// R 0-100, eta 1, lambda_a 1e-12, q_max 10; HBL L = 2), 24 momentum agents (1-10 shares, 60 s);
+// market 09:30-16:00, kernel 09:30-16:01, compute delay 0, zero latency
+#ifndef MXA_OH_CAP
+#define MXA_OH_CAP 16384  // order-history ring records (HBL streams reached 3,895 orders on seed 123456789)
+#endif
+#ifndef MXA_HBL_RANGE
+#define MXA_HBL_RANGE 16384  // HBL price-histogram bins (largest streamed range on seed 123456789: 4,399)
+#endif
+constexpr void params_rmsc01(MxaParams& P) {
+  base_params(P);
+  P.config = MXA_CFG_RMSC01;
+  P.mkt_close = 16 * HOUR;
+  P.start = P.mkt_open;
+  P.stop = 16 * HOUR + MIN;
+  P.default_comp_delay = 0;
+  P.lat_mode = 0;
+  P.noise_len = 1;
+  P.first_mk = 1;
+  P.n_mk = 1;
+  P.mk_min = 500;
+  P.mk_max = 1000;
+  P.mk_depth = 5;
+  P.mk_wake = NS;
+  P.mk_last_spread = 10;
+  P.zi_ngroups = 1;
+  P.zi_group_count[0] = 50;
+  P.zi_rmin[0] = 0;
+  P.zi_rmax[0] = 100;
+  P.zi_eta[0] = 1;
+  P.first_zi = 2;
+  P.n_zi = 50;
+  P.first_hbl = 52;
+  P.n_hbl = 25;
+  P.hbl_L = 2;
+  P.zi_sigma_n = 10000;
+  P.zi_rbar = 1e5;
+  P.zi_kappa = 1.67e-15;
+  P.zi_sigma_s = 1e-4;
+  P.zi_lambda = 1e-12;
+  P.zi_sigma_pv = 5e4;
+  P.zi_qmax = 10;
+  P.first_mom = 77;
+  P.n_mom = 24;
+  P.mom_min = 1;
+  P.mom_max = 10;
+  P.mom_wake = 60 * NS;
+  P.n_agents = 101;
+  P.L.open_cap = 64;
+  P.L.tx_cap = 256;
+  P.L.lat_len = 0;
+  P.L.oh_cap = MXA_OH_CAP;
+  P.L.hbl_range = MXA_HBL_RANGE;
+}
+
 constexpr uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 // per-env HBM block: header, agent records, open orders, RNG streams, latency row/col,
@@ -239,6 +298,10 @@ constexpr void layout(MxaParams& P, int cfg) {
   off = align_up(off + (uint64_t)L.ocap * sizeof(SavedOrder), 256);
   L.off_tx = (uint32_t)off;
   off = align_up(off + 64 + (uint64_t)L.tx_cap * sizeof(TxRec), 256);
+  L.off_oh = off;  // order-history ring (HBL configs; oh_cap = 0 otherwise)
+  off = align_up(off + (uint64_t)L.oh_cap * sizeof(OhRec), 256);
+  L.off_hh = off;  // HBL price histogram (zeroed between uses)
+  off = align_up(off + (uint64_t)L.hbl_range * 8, 256);
   L.off_trace = (uint32_t)off;
   L.env_stride = off;  // without trace; the handle adds trace_cap records
 }
@@ -282,6 +345,7 @@ constexpr MxaParams params(int cfg) {
   else if (cfg == MXA_CFG_RMSC03_RL) params_rmsc03_rl(P);
   else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);
   else if (cfg == MXA_CFG_VALUE_NOISE) params_value_noise(P);
+  else if (cfg == MXA_CFG_RMSC01) params_rmsc01(P);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;

@@ -91,6 +91,19 @@ DEV i64 wsum_i64(i64 x) {
   MXA_DPP_STEPS(op_add, 0u, hi)
   return (i64)(((u64)rdl(hi, 63) << 16) + rdl(lo, 63));
 }
+DEV u32 wsum_u32(u32 v) {
+  MXA_DPP_STEPS(op_add, 0u, v)
+  return rdl(v, 63);
+}
+// inclusive prefix sum over the lanes (lane l gets v_0 + ... + v_l)
+DEV u32 wscan_u32(u32 v) {
+  const int l = laneid();
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 o = (u32)__shfl_up((int)v, d, 64);
+    v += l >= d ? o : 0u;
+  }
+  return v;
+}
 // lexicographic (key64, seq32) min over the wave; returns in k/s (uniform)
 DEV void wmin_key(u64& k, u32& s) {
   u32 kh = (u32)(k >> 32), kl = (u32)k;
@@ -407,6 +420,14 @@ DEV Rec encode(u64 key, const Msg& m) {
     r.f0 = m_i64(m, 1);
     r.f5 = m_closed(m);
     break;
+  case MK_STREAM_REQ:
+    r.f0 = m_agent(m);
+    r.f1 = (i32)m.w[1];
+    break;
+  case MK_STREAM:
+    r.f0 = (i32)m.w[1];
+    r.f5 = m_closed(m);
+    break;
   case MK_LIMIT: case MK_ACCEPTED: case MK_CANCELLED: case MK_MODIFY: case MK_MODIFIED:
   case MK_CANCEL: case MK_EXECUTED:
     r.f0 = (i32)m.w[1];
@@ -564,6 +585,10 @@ struct Eng {
   // order book pool in VGPRs: slot (j, lane)
   i32 bp[SO], bq[SO], bo[SO], bm[SO], bh[SO];
   u32 ba[SO];
+  // HBL configurations: OrderBook.history restated as an order-history ring in HBM (one OhRec
+  // per handled limit order); a resting order keeps its record index to flag its transactions
+  static constexpr bool OH = PC.n_hbl > 0;
+  i32 bx[OH ? SO : 1];
   // current agent record (lane l holds dwords 2l, 2l+1)
   u32 rlo, rhi;
   i32 cur_agent;
@@ -1199,7 +1224,7 @@ struct Eng {
     }
     return n;
   }
-  DEV void b_enter(i32 oid, i32 agent, int is_buy, i32 qty, i32 price, i32 hep) {
+  DEV void b_enter(i32 oid, i32 agent, int is_buy, i32 qty, i32 price, i32 hep, i32 ridx = 0) {
     int s = b_free_slot();
     if (s < 0) {
       fail(ERR_BOOK_FULL);
@@ -1214,6 +1239,7 @@ struct Eng {
         bm[j] = (agent << 1) | is_buy;
         ba[j] = arr;
         bh[j] = hep;
+        if constexpr (OH) bx[j] = ridx;
       }
     h.b_count++;
     if (h.b_count > h.max_book) h.max_book = h.b_count;
@@ -1343,12 +1369,34 @@ struct Eng {
     i64 d = (k == MK_ACCEPTED || k == MK_CANCELLED || k == MK_EXECUTED) ? PC.ex_pipeline : 0;
     send(recipient, m, d);
   }
+  // ---------------- OrderBook.history as a ring of per-order records (HBL configurations)
+  DEV OhRec* ohr() { return (OhRec*)(env + PC.L.off_oh); }
+  // history[0][order_id] = {...} (OrderBook.py:52-60): one record per handled limit order
+  DEV i32 oh_append(i32 oid, i32 price, int is_buy) {
+    const i32 r = h.oh_head;
+    if (lane == 0) {
+      OhRec x;
+      x.oid = oid;
+      x.price = price;
+      x.meta = is_buy;
+      x.epoch = h.epoch;
+      ohr()[r % PC.L.oh_cap] = x;
+    }
+    h.oh_head = r + 1;
+    return r;
+  }
+  // an order's "transactions" list becomes non-empty (its record still in the ring)
+  DEV void oh_mark_tx(i32 r) {
+    if (h.oh_head - r <= PC.L.oh_cap && lane == 0) ohr()[r % PC.L.oh_cap].meta |= 2;
+  }
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
     if (qty <= 0) return;
     i32 hep = h.epoch;
     LDSP i32* EP = ep_entries();
     i32 ne = EP[h.epoch & 15] + 1;
     if (lane == 0) EP[h.epoch & 15] = ne;
+    i32 ridx = 0;
+    if constexpr (OH) ridx = oh_append(oid, price, is_buy);
     i64 ex_q = 0, ex_pq = 0;
     bool executed = false;
     for (;;) {
@@ -1370,6 +1418,11 @@ struct Eng {
         // history: taker logs its pre-match remaining qty; maker its matched qty if retained
         tx_add(cur, qty, h.epoch);
         if (hh >= h.epoch - PC.stream_history) tx_add(cur, mq, hh);
+        if constexpr (OH) {
+          const i32 mx = b_get(bx, s);
+          oh_mark_tx(ridx);
+          if (hh >= h.epoch - PC.stream_history) oh_mark_tx(mx);
+        }
         qty -= mq;
         Msg mt = msg_order(MK_EXECUTED, oid, agent, is_buy, mq, price, best);
         ex_notify(agent, mt);
@@ -1380,7 +1433,7 @@ struct Eng {
         executed = true;
         if (qty <= 0) break;
       } else {
-        b_enter(oid, agent, is_buy, qty, price, hep);
+        b_enter(oid, agent, is_buy, qty, price, hep, ridx);
         Msg ma = msg_order(MK_ACCEPTED, oid, agent, is_buy, qty, price, 0);
         ex_notify(agent, ma);
         break;
@@ -1414,7 +1467,7 @@ struct Eng {
       if (k == MK_LIMIT || k == MK_CANCEL || k == MK_MODIFY) {
         ex_notify(sender, msg_make(MK_MKT_CLOSED, 0));
         return;
-      } else if (k == MK_SPREAD_REQ || k == MK_LAST_REQ || k == MK_TV_REQ) {
+      } else if (k == MK_SPREAD_REQ || k == MK_LAST_REQ || k == MK_TV_REQ || k == MK_STREAM_REQ) {
       } else {
         ex_notify(sender, msg_make(MK_MKT_CLOSED, 0));
         return;
@@ -1484,6 +1537,20 @@ struct Eng {
       r.w[1] = (u32)(u64)vol;
       r.w[2] = (u32)((u64)vol >> 32);
       ex_notify(sender, r);
+      break;
+    }
+    case MK_STREAM_REQ: {  // QUERY_ORDER_STREAM (ExchangeAgent.py:251-279): history[1 : length + 1]
+      if constexpr (OH) {
+        const i32 avail = h.epoch < PC.stream_history ? h.epoch : PC.stream_history;  // len(history) - 1
+        const i32 len = (i32)m.w[1] < avail ? (i32)m.w[1] : avail;
+        const i64 hi = (i64)h.epoch - 1;  // absolute epoch of history[1]
+        Msg r = msg_make(MK_STREAM, 0);
+        r.w[0] |= (1u << 11) | ((u32)closed << 7);
+        r.w[1] = (u32)(len < 0 ? 0 : len);
+        r.w[2] = (u32)(u64)hi;
+        r.w[3] = (u32)((u64)hi >> 32);
+        ex_notify(sender, r);
+      }
       break;
     }
     case MK_LIMIT:
@@ -1648,6 +1715,7 @@ struct Eng {
   DEV i64 wake_frequency(int type) {
     if (type == AG_POVMM) return PC.mm_wake;
     if (type == AG_MOMENTUM) return PC.mom_wake;
+    if (type == AG_MKTMAKER) return PC.mk_wake;  // pd.Timedelta(wake_up_freq) (MarketMakerAgent.py:148-149)
     if constexpr (RP) {
       if (type == AG_REPLAY) return U(rx->tm[0]) - PC.mkt_open;  // MarketReplayAgent.py:94-96
     }
@@ -1737,6 +1805,14 @@ struct Eng {
       if (m_closed(m)) fl_set(FL_MKT_CLOSED, true);
       rs64(AF_TV, m_i64(m, 1));
       break;
+    case MK_STREAM:  // queryOrderStream (TradingAgent.py:240-246, 549-554)
+      if constexpr (OH) {
+        if (m_closed(m)) fl_set(FL_MKT_CLOSED, true);
+        fl_set(FL_HAS_STREAM, true);
+        rs(AF_STREAM_N, m.w[1]);
+        rs64(AF_STREAM_HI, m_i64(m, 2));
+      }
+      break;
     default:
       break;
     }
@@ -1786,7 +1862,9 @@ struct Eng {
   }
 
   // ---------------- ZeroIntelligenceAgent (ZI.py:125-309)
-  DEV void zi_wakeup() {
+  // ZeroIntelligenceAgent.wakeup; a subclass (HBL) does not query the spread but becomes ACTIVE
+  // (ZI.py:183-187)
+  DEV void zi_wakeup_as(bool is_zi) {
     ta_wakeup();
     rs(AF_STATE, AS_INACTIVE);
     if (!fl(FL_HAS_OPEN) || !fl(FL_HAS_CLOSE)) return;
@@ -1802,13 +1880,19 @@ struct Eng {
       return;
     }
     cancel_all();
-    get_spread(1);
-    rs(AF_STATE, AS_AWAITING_SPREAD);
+    if (is_zi) {
+      get_spread(1);
+      rs(AF_STATE, AS_AWAITING_SPREAD);
+    } else {
+      rs(AF_STATE, AS_ACTIVE);
+    }
   }
-  DEV void zi_place() {
+  DEV void zi_wakeup() { zi_wakeup_as(true); }
+  // updateEstimates (ZI.py:189-275): the total unit valuation v and the side; false where the
+  // reference raises (theta IndexError)
+  DEV bool zi_update_estimates(i64& v, int& buy) {
     i64 obs = o_observe(cur, PC.zi_sigma_n);
     i64 q = (i64)((double)rg64(AF_SHARES) / 100);
-    int buy;
     if (q >= PC.zi_qmax) buy = 0;
     else if (q <= -PC.zi_qmax) buy = 1;
     else {
@@ -1822,9 +1906,15 @@ struct Eng {
     if (idx < 0) idx += 2 * PC.zi_qmax;
     if (idx < 0 || idx >= 2 * PC.zi_qmax) {
       fail(ERR_THETA_INDEX);
-      return;
+      return false;
     }
-    i64 v = r_T + (i64)rgi(AF_THETA + (int)idx);
+    v = r_T + (i64)rgi(AF_THETA + (int)idx);
+    return true;
+  }
+  DEV void zi_place() {
+    i64 v;
+    int buy;
+    if (!zi_update_estimates(v, buy)) return;
     int g = rgi(AF_GROUP);
     RS A = agent_rs();
     i64 R = rs_randint(A, PC.zi_rmin[g], (i64)PC.zi_rmax[g] + 1);
@@ -2005,6 +2095,211 @@ struct Eng {
     Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, (i32)sz, price, 0);
     lm.w[0] = (lm.w[0] & 0xFFFFu) | ((u32)cur_agent << 16);
     q_push_lanes(act, ex_key(), lm);
+  }
+
+  // ---------------- MarketMakerAgent (agent/market_makers/MarketMakerAgent.py, polling mode)
+  DEV void mk_wakeup() {
+    if (ta_wakeup()) {  // MarketMakerAgent.py:69-79
+      cancel_all();
+      get_spread(PC.mk_depth);
+      rs(AF_STATE, AS_AWAITING_SPREAD);
+    }
+  }
+  DEV void mk_receive(const Msg& m) {
+    ta_receive(m, AG_MKTMAKER);  // MarketMakerAgent.py:81-107
+    if (!(rgi(AF_STATE) == AS_AWAITING_SPREAD && m_kind(m) == MK_SPREAD)) return;
+    cancel_all();
+    i64 mid = rg64(AF_LAST_TRADE), spread;
+    i32 bid, ask;
+    const bool hb = known_bid(bid), ha = known_ask(ask);  // getKnownBidAsk; `if bid and ask`
+    if (hb && ha) {
+      mid = (i64)((double)((i64)ask + bid) / 2);
+      spread = (i64)((double)(ask > bid ? (i64)ask - bid : (i64)bid - ask) / 2);
+    } else {
+      // mid = last_trade: while it is the exchange's opening price (a python float) the ladder's
+      // prices would travel as floats; not restated, so a loud error instead of a divergence
+      if (fl(FL_LAST_FLOAT)) {
+        fail(ERR_FLOAT_PRICE);
+        return;
+      }
+      spread = PC.mk_last_spread;
+    }
+    mk_place_ladder(mid, spread);
+    wakeup_at(cur_agent, cur + PC.mk_wake);
+    rs(AF_STATE, AS_AWAITING_WAKEUP);
+  }
+  // for i < num_levels (2 x depth): size = round(A.randint(min, max) / 2); a bid at mid - spread - i
+  // and an ask at mid + spread + i.  The sizes are drawn first (placeLimitOrder draws nothing), then
+  // the 4 x depth orders are placed in one pass: lane 2i the bid, lane 2i + 1 the ask, ids, list
+  // entries and queue seqs in the loop's order
+  DEV void mk_place_ladder(i64 mid, i64 spread) {
+    constexpr int NL = 4 * PC.mk_depth;
+    RS A = agent_rs();
+    i32 sz = 0;
+    i64 last = 0;
+    for (int i = 0; i < 2 * PC.mk_depth; i++) {
+      last = (i64)__builtin_rint((double)rs_randint(A, PC.mk_min, PC.mk_max) / 2);
+      sz = (lane >> 1) == i ? (i32)last : sz;
+    }
+    agent_rs_put(A);
+    rs(AF_SIZE, (u32)last);
+    if (BATCH && NL <= 64 && PC.mk_min >= 2 && rgi(AF_NORD) + NL <= PC.L.open_cap) {  // every size >= 1
+      i32 u = rgi(AF_NUSED);
+      if (u + NL > PC.L.open_cap) u = open_compact();
+      const bool act = lane < NL;
+      const int buy = !(lane & 1);
+      const i64 lvl = lane >> 1;
+      const i32 price = (i32)(buy ? mid - spread - lvl : mid + spread + lvl);
+      const i32 oid = (i32)(ocnt + lane);
+      ocnt += NL;
+      if (act) {
+        OpenOrder o;
+        o.oid = oid;
+        o.is_buy = buy;
+        o.qty = sz;
+        o.price = price;
+        open_ptr(cur_agent)[u + lane] = o;
+      }
+      rs(AF_NUSED, (u32)(u + NL));
+      rs(AF_NORD, (u32)(rgi(AF_NORD) + NL));
+      Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, sz, price, 0);
+      q_push_lanes(act, ex_key(), lm);
+    } else {
+      for (int i = 0; i < 2 * PC.mk_depth; i++) {
+        const i64 q = rdli(sz, 2 * i);
+        place_limit(q, 1, mid - spread - i);
+        place_limit(q, 0, mid + spread + i);
+      }
+    }
+  }
+
+  // ---------------- HeuristicBeliefLearningAgent (agent/HeuristicBeliefLearningAgent.py)
+  DEV void hbl_wakeup() {
+    zi_wakeup_as(false);  // HBL.py:61-73
+    if (rgi(AF_STATE) != AS_ACTIVE) return;
+    Msg m = msg_make(MK_STREAM_REQ, cur_agent);  // getOrderStream(symbol, length=L)
+    m.w[1] = (u32)PC.hbl_L;
+    send_ex(m);
+    rs(AF_STATE, AS_AWAITING_STREAM);
+  }
+  DEV void hbl_receive(const Msg& m) {
+    ta_receive(m, AG_HBL);
+    // ZeroIntelligenceAgent.receiveMessage (ZI.py:311-334) with HBL's placeOrder
+    if (rgi(AF_STATE) == AS_AWAITING_SPREAD && m_kind(m) == MK_SPREAD && !fl(FL_MKT_CLOSED)) {
+      hbl_place();
+      rs(AF_STATE, AS_AWAITING_WAKEUP);
+    }
+    // HBL.receiveMessage (HBL.py:197-217)
+    if (rgi(AF_STATE) == AS_AWAITING_STREAM && m_kind(m) == MK_STREAM && !fl(FL_MKT_CLOSED)) {
+      get_spread(1);
+      rs(AF_STATE, AS_AWAITING_SPREAD);
+    }
+  }
+  // HBL.placeOrder (HBL.py:75-195).  The streamed epochs are the exchange's live history dicts
+  // (the reply carried references), so their orders and "transactions" flags are read from the
+  // order-history ring as they are now.  The reference's dense arrays over [low_p, high_p] become a
+  // price histogram (4 categories in 16-bit fields of one u64 per price, in an HBM scratch that is
+  // zeroed again as it is scanned) and one 64-price-per-step scan: the cumulative sums, Pr = num /
+  // denom (0 for 0/0, np.nan_to_num) and the expected surplus in double, and numpy's first-maximum
+  // argmax.  Every count is an exact integer, so the doubles equal numpy's.
+  DEV void hbl_place() {
+    if (!fl(FL_HAS_STREAM) || rgi(AF_STREAM_N) < PC.hbl_L) {  // insufficient history: ZI.placeOrder
+      zi_place();
+      return;
+    }
+    i64 v;
+    int buy;
+    if (!zi_update_estimates(v, buy)) return;
+    const i32 n = rgi(AF_STREAM_N);
+    const i64 hi = rg64(AF_STREAM_HI), lo_e = hi - n + 1;
+    if (lo_e < 0 || (i64)h.epoch - lo_e > PC.stream_history) {
+      fail(ERR_HBL_WINDOW);  // a streamed epoch left the 11-epoch window (same-instant trade burst)
+      return;
+    }
+    // ring records of epochs lo_e..hi: [s0, s1), walking back from the current epoch's start
+    LDSP i32* EP = ep_entries();
+    i32 s1 = h.oh_head - EP[h.epoch & 15];
+    for (i64 e = (i64)h.epoch - 1; e > hi; e--) s1 -= EP[e & 15];
+    i32 s0 = s1;
+    for (i64 e = hi; e >= lo_e; e--) s0 -= EP[e & 15];
+    if (h.oh_head - s0 > PC.L.oh_cap) {
+      fail(ERR_HBL_WINDOW);  // overwritten in the device ring (MXA_OH_CAP)
+      return;
+    }
+    const OhRec* R = ohr();
+    constexpr i32 CAP = PC.L.oh_cap;
+    i32 lowp = INT32_MAX, highp = 0;  // low_p = sys.maxsize, high_p = 0 (HBL.py:100-110)
+    u32 t01 = 0, t23 = 0;             // category totals (sell-tx | buy-tx << 16, sell-none | buy-none << 16)
+    for (i32 b = s0; b < s1; b += 64) {
+      const i32 k = b + lane;
+      if (k < s1) {
+        const OhRec x = R[k % CAP];
+        lowp = x.price < lowp ? x.price : lowp;
+        highp = x.price > highp ? x.price : highp;
+      }
+    }
+    lowp = wmin_i32(lowp);
+    highp = wmax_i32(highp);
+    const i64 NB = (i64)highp - lowp + 1;
+    if (s1 <= s0 || NB <= 0 || NB > PC.L.hbl_range) {
+      fail(ERR_HBL_RANGE);
+      return;
+    }
+    u64* hist = (u64*)(env + PC.L.off_hh);
+    for (i32 b = s0; b < s1; b += 64) {
+      const i32 k = b + lane;
+      if (k < s1) {
+        const OhRec x = R[k % CAP];
+        const int tx = (x.meta >> 1) & 1, ib = x.meta & 1;
+        const int cat = ib ? (tx ? 1 : 3) : (tx ? 0 : 2);  // nd columns sa, sb, ua, ub
+        atomicAdd((unsigned long long*)&hist[x.price - lowp], 1ull << (16 * cat));
+        t01 += cat == 0 ? 1u : cat == 1 ? 0x10000u : 0u;
+        t23 += cat == 2 ? 1u : cat == 3 ? 0x10000u : 0u;
+      }
+    }
+    __threadfence();
+    t01 = wsum_u32(t01);
+    t23 = wsum_u32(t23);
+    const i64 T0 = t01 & 0xFFFF, T1 = t01 >> 16, T2 = t23 & 0xFFFF, T3 = t23 >> 16;
+    i64 run0 = 0, run1 = 0, run2 = 0, run3 = 0;  // cumulative counts below this step's prices
+    u64 best = 0;
+    i64 bestp = lowp;
+    for (i64 b = 0; b < NB; b += 64) {
+      const i64 i = b + lane;
+      u64 x = 0;
+      if (i < NB) {
+        x = hist[i];
+        hist[i] = 0;
+      }
+      const u32 c01 = (u32)(x & 0xFFFF) | ((u32)((x >> 16) & 0xFFFF) << 16);
+      const u32 c23 = (u32)((x >> 32) & 0xFFFF) | ((u32)(x >> 48) << 16);
+      const u32 s01 = wscan_u32(c01), s23 = wscan_u32(c23);  // inclusive, per 16-bit field
+      const i64 le0 = run0 + (s01 & 0xFFFF), le1 = run1 + (s01 >> 16);
+      const i64 le2 = run2 + (s23 & 0xFFFF), le3 = run3 + (s23 >> 16);
+      const i64 ge0 = T0 - (le0 - (c01 & 0xFFFF)), ge1 = T1 - (le1 - (c01 >> 16));
+      const i64 ge3 = T3 - (le3 - (c23 >> 16));
+      const i64 num = buy ? le0 + le1 + le2 : ge0 + ge1 + ge3;
+      const i64 den = buy ? num + ge3 : num + le2;
+      const double pr = den > 0 ? (double)num / (double)den : 0.0;
+      const i64 p = (i64)lowp + i;
+      double es = pr * (double)(buy ? v - p : p - v);
+      if (es == 0.0) es = 0.0;  // -0.0 ties +0.0 in numpy's argmax
+      const u64 bits = as_u(es);
+      const u64 key = i < NB ? ((bits >> 63) ? ~bits : (bits | (1ull << 63))) : 0ull;
+      const u32 kh = ~wmin_u32(~(u32)(key >> 32));
+      const u32 kl = ~wmin_u32((u32)(key >> 32) == kh ? ~(u32)key : 0xFFFFFFFFu);
+      const u64 kmax = ((u64)kh << 32) | kl;
+      if (b == 0 || kmax > best) {  // first maximum: a later step must be strictly greater
+        best = kmax;
+        bestp = (i64)lowp + b + ffs64(bal(key == kmax));
+      }
+      run0 += rdl(s01, 63) & 0xFFFF;
+      run1 += rdl(s01, 63) >> 16;
+      run2 += rdl(s23, 63) & 0xFFFF;
+      run3 += rdl(s23, 63) >> 16;
+    }
+    const double best_es = as_d((best >> 63) ? (best & ~(1ull << 63)) : ~best);
+    if (best_es > 0) place_limit(100, buy, bestp);
   }
 
   // ---------------- MomentumAgent (MomentumAgent.py:53-99)
@@ -2652,6 +2947,10 @@ struct Eng {
         if (type == AG_POVMM) return mm_wakeup();
       if constexpr (PC.n_mom > 0)
         if (type == AG_MOMENTUM) return mom_wakeup();
+      if constexpr (PC.n_mk > 0)
+        if (type == AG_MKTMAKER) return mk_wakeup();
+      if constexpr (PC.n_hbl > 0)
+        if (type == AG_HBL) return hbl_wakeup();
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_wakeup();
       }
@@ -2671,6 +2970,10 @@ struct Eng {
         if (type == AG_POVMM) return mm_receive(m);
       if constexpr (PC.n_mom > 0)
         if (type == AG_MOMENTUM) return mom_receive(m);
+      if constexpr (PC.n_mk > 0)
+        if (type == AG_MKTMAKER) return mk_receive(m);
+      if constexpr (PC.n_hbl > 0)
+        if (type == AG_HBL) return hbl_receive(m);
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_receive(m);
       }
@@ -2721,7 +3024,7 @@ struct Eng {
         } else {
           f.valuation = (double)(rg64(AF_LAST_TRADE) * H + cash - start) / (double)start;
         }
-      } else if (ty == AG_VALUE || ty == AG_ZI) {
+      } else if (ty == AG_VALUE || ty == AG_ZI || ty == AG_HBL) {  // HBL inherits ZI.kernelStopping
         const i64 rT = o_observe(rg64(AF_ATIME) - rg64(AF_COMP), 0.0);
         if (dirty) rng_maint();
         f.final_fundamental = rT;
@@ -2806,6 +3109,7 @@ struct Eng {
       bm[j] = o.meta;
       ba[j] = o.arrival;
       bh[j] = o.hepoch;
+      if constexpr (OH) bx[j] = o.pad[0];
     }
   }
   DEV void save() {
@@ -2828,7 +3132,8 @@ struct Eng {
       o.meta = bm[j];
       o.arrival = ba[j];
       o.hepoch = bh[j];
-      o.pad[0] = o.pad[1] = 0;
+      o.pad[0] = OH ? bx[OH ? j : 0] : 0;
+      o.pad[1] = 0;
       so[j * 64 + lane] = o;
     }
     for (int hs = 0; hs < HOT; hs++) agent_ptr(hot_agent(hs))[lane] = hotrec[hs * 64 + lane];
@@ -3005,6 +3310,19 @@ struct Eng {
       const i32 meta = (agent << 1) | buy;
       const i32 hep = h.epoch;
       const u32 arr0 = h.arrival;
+      i32 oh0 = 0;
+      if constexpr (OH) {  // history[0][id] for each member in order (records oh0 + rank)
+        oh0 = h.oh_head;
+        if (v) {
+          OhRec x;
+          x.oid = oid;
+          x.price = price;
+          x.meta = buy;
+          x.epoch = hep;
+          ohr()[(oh0 + r) % PC.L.oh_cap] = x;
+        }
+        h.oh_head = oh0 + m;
+      }
       int base = 0;
       for (int j = 0; j < SO; j++) {  // the k-th free slot in (j, lane) order takes rank k
         const u64 fb = bal(bm[j] < 0);
@@ -3020,6 +3338,7 @@ struct Eng {
           bm[j] = sm;
           ba[j] = arr0 + (u32)fr;
           bh[j] = hep;
+          if constexpr (OH) bx[j] = oh0 + fr;
         }
         base += __popcll(fb);
       }
@@ -3500,6 +3819,38 @@ struct Builder : Eng<CFG, true> {
         init_gym();
       }
       set_seed(2, g_seed(G));  // K
+    } else if (P.config == MXA_CFG_RMSC01) {
+      // config/rmsc01.py: the exchange's seed, the market maker's, the oracle symbol's, the
+      // oracle's first megashock time, per ZI and HBL agent its seed, per momentum agent its
+      // seed, the kernel's (each agent's own __init__ draws come after seed_streams)
+      set_seed(4 + 0, g_seed(G));  // exchange
+      for (int a = P.first_mk; a < P.first_mk + P.n_mk; a++) {
+        set_seed(4 + a, g_seed(G));
+        rec_init(a, AG_MKTMAKER);
+        this->rec_store();
+      }
+      set_seed(1, g_seed(G));  // O
+      h.o_pt = P.mkt_open;
+      h.o_pv = P.o_rbar;
+      h.o_th2 = gm_pow(P.o_fundvol, 2.0);  // SMRO: theta ** 2 (SparseMeanRevertingOracle.py:105)
+      h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
+      for (int a = P.first_zi; a < P.first_zi + P.n_zi + P.n_hbl; a++) {  // ZI, then HBL (ids follow)
+        set_seed(4 + a, g_seed(G));
+        rec_init(a, a < P.first_zi + P.n_zi ? AG_ZI : AG_HBL);
+        this->rs(AF_GROUP, 0u);
+        this->rsd(AF_R_T, P.zi_rbar);
+        this->rec_store();
+      }
+      for (int a = P.first_mom; a < P.first_mom + P.n_mom; a++) {
+        set_seed(4 + a, g_seed(G));
+        rec_init(a, AG_MOMENTUM);
+        this->rec_store();
+      }
+      set_seed(2, g_seed(G));  // K
+      if constexpr (E::OH) {  // the HBL price histogram starts (and stays) zeroed
+        u64* hist = (u64*)(this->env + P.L.off_hh);
+        for (int i = this->lane; i < P.L.hbl_range; i += 64) hist[i] = 0;
+      }
     } else if (P.config == MXA_CFG_VALUE_NOISE) {
       // config/value_noise.py: O and K seeds (the kernel is built before the oracle), the
       // oracle's first megashock time, the exchange; per noise agent its seed, its wakeup_time
@@ -3601,7 +3952,14 @@ struct Builder : Eng<CFG, true> {
       this->agent_rs_put(A);
       this->rec_store();
     }
-    for (int a = P.first_zi; a < P.first_zi + P.n_zi; a++) {
+    for (int a = P.first_mk; a < P.first_mk + P.n_mk; a++) {  // MarketMakerAgent.py:51
+      this->rec_load(a);
+      RS A = this->agent_rs();
+      this->rs(AF_SIZE, (u32)(i64)__builtin_rint((double)rs_randint(A, P.mk_min, P.mk_max) / 2));
+      this->agent_rs_put(A);
+      this->rec_store();
+    }
+    for (int a = P.first_zi; a < P.first_zi + P.n_zi + P.n_hbl; a++) {  // HBL agents are ZI subclasses
       this->rec_load(a);
       RS A = this->agent_rs();
       double th[20];
@@ -3779,6 +4137,7 @@ MXA_INST(MXA_CFG_SPARSE_ZI_1000)
 MXA_INST(MXA_CFG_MARKETREPLAY)
 MXA_INST(MXA_CFG_RMSC03_RL)
 MXA_INST(MXA_CFG_VALUE_NOISE)
+MXA_INST(MXA_CFG_RMSC01)
 #define MXA_INST_STEP(CFG) \
   template __global__ void mxa_step_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*, const double*, double*, int32_t*);
 MXA_INST_STEP(MXA_CFG_MARKETREPLAY)

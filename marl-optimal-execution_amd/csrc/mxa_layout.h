@@ -16,20 +16,22 @@
 #define MXA_RNG_WORDS 1280    // two 624-word MT blocks (double buffer) + pad (5120 B per stream)
 
 enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3,
-                     MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5 };
+                     MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
   MK_WAKEUP = 0, MK_WHEN_OPEN_REQ = 1, MK_WHEN_CLOSE_REQ = 2, MK_WHEN_OPEN = 3, MK_WHEN_CLOSE = 4,
   MK_SPREAD_REQ = 5, MK_SPREAD = 6, MK_LAST_REQ = 7, MK_LAST = 8, MK_TV_REQ = 9, MK_TV = 10,
   MK_LIMIT = 11, MK_CANCEL = 12, MK_MODIFY = 13, MK_ACCEPTED = 14, MK_EXECUTED = 15, MK_CANCELLED = 16,
-  MK_MKT_CLOSED = 17, MK_MODIFIED = 18, MK_KCANCEL = 19, MK_MARKET_DATA = 20
+  MK_MKT_CLOSED = 17, MK_MODIFIED = 18, MK_KCANCEL = 19, MK_MARKET_DATA = 20,
+  MK_STREAM_REQ = 21, MK_STREAM = 22  // QUERY_ORDER_STREAM request / reply
 };
 // kernel message types (message/Message.py:5-8)
 enum { MT_MESSAGE = 1, MT_WAKEUP = 2, MT_CANCEL_ORDER = 3 };
 
 // agent classes
-enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_MOMENTUM = 5, AG_REPLAY = 6, AG_DUMMYRL = 7 };
+enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_MOMENTUM = 5, AG_REPLAY = 6, AG_DUMMYRL = 7,
+       AG_MKTMAKER = 8, AG_HBL = 9 };
 
 // env status flags (EnvHdr::status)
 enum { ST_RUNNING = 0, ST_DONE = 1, ST_ERROR = 2 };
@@ -44,7 +46,11 @@ enum {
   ERR_RP_KEYERROR = 13,   // MarketReplayAgent: no tape group at the wake time
   ERR_RP_OBS = 14,        // get_observation / get_reward on missing or None data
   ERR_RP_STOPPING = 15,   // ExecutionAgent.kernelStopping with trade still on (arrival_price None)
-  ERR_RP_MODIFY = 16      // modify changing price or side (head-replace would re-key the level)
+  ERR_RP_MODIFY = 16,     // modify changing price or side (head-replace would re-key the level)
+  // HeuristicBeliefLearningAgent
+  ERR_HBL_WINDOW = 17,    // a streamed history epoch left the exchange's window / the device ring
+  ERR_HBL_RANGE = 18,     // streamed price range beyond the device scratch (MXA_HBL_RANGE)
+  ERR_FLOAT_PRICE = 19    // a limit price that the reference would carry as a python float (not restated)
 };
 
 // per-env scalar header (first bytes of the env block)
@@ -69,6 +75,7 @@ typedef struct {
   double rs_gauss[4];
   int32_t rs_m[4];
   int32_t rs_w0[4], rs_wn[4];    // run kernel: LDS output window of each stream (start, length)
+  int32_t oh_head, pad2;         // order-history ring: records written so far (HBL configs)
   int32_t q_count, b_count;      // saved queue / book occupancy
   int64_t trace_len;
   int64_t ex_comp_delay;         // exchange's current computation delay
@@ -100,6 +107,12 @@ typedef struct {  // transaction record of OrderBook.history (util/OrderBook.py:
   int64_t t;
   int32_t q, epoch;
 } TxRec;
+
+typedef struct {  // OrderBook.history entry of one limit order (util/OrderBook.py:52-60), HBL configs
+  int32_t oid, price;
+  int32_t meta;   // bit0 is_buy_order, bit1 "transactions" non-empty
+  int32_t epoch;  // absolute history epoch it was entered in
+} OhRec;
 
 typedef struct {  // TradingAgent.orders entry (agent's copy of an open order)
   int32_t oid, is_buy, qty, price;
@@ -159,6 +172,8 @@ typedef struct {
   uint64_t env_stride;
   uint32_t off_ag, off_open, off_rng, off_lat, off_q, off_book, off_tx, off_trace;
   int32_t n_agents, n_streams, qcap, ocap, open_cap, tx_cap, trace_cap, lat_len;
+  int32_t oh_cap, hbl_range;    // order-history ring records; HBL price-histogram bins (0: none)
+  uint64_t off_oh, off_hh;      // order-history ring; HBL histogram scratch (u64 bins)
 } Layout;
 
 // agent record: 128 dwords (512 B); lane i of the owning wave holds dwords 2i, 2i+1
@@ -171,6 +186,8 @@ enum {
   AF_ORDER_SIZE = 38, AF_NMID = 39, AF_N20 = 40, AF_N50 = 41, AF_AVG20 = 42, AF_AVG50 = 44,
   AF_THETA = 46,      // 20 x int32
   AF_MIDS = 66,       // 50 x int32 (2*mid ring), momentum
+  AF_STREAM_N = 66,   // HBL: epochs of the last QUERY_ORDER_STREAM reply (momentum's AF_MIDS area)
+  AF_STREAM_HI = 68,  // HBL: absolute history epoch of its first entry (history[1]), int64
   AF_RS_M = 116,      // highest materialized MT block of the agent's stream
   AF_NUSED = 117,     // open-order list slots used (live + tombstones); AF_NORD = live
   AF_ATIME = 120,     // Kernel.agentCurrentTimes[a]
@@ -181,9 +198,10 @@ enum {
 enum {
   FL_HAS_OPEN = 1, FL_HAS_CLOSE = 2, FL_MKT_CLOSED = 4, FL_FIRST_WAKE = 8, FL_DAILY_CLOSE = 16,
   FL_TRADING = 32, FL_HAS_KNOWN = 64, FL_NB = 128, FL_NA = 256, FL_HAS_LAST = 512,
-  FL_LAST_FLOAT = 1024, FL_PREV_WAKE = 2048, FL_AW_SPREAD = 4096, FL_AW_TV = 8192, FL_LAST_MID = 16384
+  FL_LAST_FLOAT = 1024, FL_PREV_WAKE = 2048, FL_AW_SPREAD = 4096, FL_AW_TV = 8192, FL_LAST_MID = 16384,
+  FL_HAS_STREAM = 32768
 };
-enum { AS_AWAITING_WAKEUP = 0, AS_INACTIVE = 1, AS_AWAITING_SPREAD = 2, AS_ACTIVE = 3 };
+enum { AS_AWAITING_WAKEUP = 0, AS_INACTIVE = 1, AS_AWAITING_SPREAD = 2, AS_ACTIVE = 3, AS_AWAITING_STREAM = 4 };
 
 typedef struct {
   int32_t config, n_envs, n_agents, n_streams;
@@ -218,6 +236,12 @@ typedef struct {
   int32_t first_replay, n_replay, first_rl, n_rl;
   int64_t rl_quantity, rl_h0, rl_hstep;   // DummyRL: BUY 1e5 over date_range(h0, ..., hstep)
   int32_t rl_nh, rl_depth, rl_ids, pad3;  // horizon length, spread depth, agent-id capacity
+  // MarketMakerAgent (agent/market_makers/MarketMakerAgent.py, polling mode)
+  int32_t first_mk, n_mk, mk_min, mk_max;
+  int32_t mk_depth, pad4;
+  int64_t mk_wake, mk_last_spread;
+  // HeuristicBeliefLearningAgent (ZI parameters of group 0, plus L)
+  int32_t first_hbl, n_hbl, hbl_L, pad5;
   Layout L;
 } MxaParams;
 

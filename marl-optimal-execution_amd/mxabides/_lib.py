@@ -10,8 +10,9 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MXA_LIB") or os.path.join(PKG_ROOT, "lib", "libmxa.so")
 
 MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000, MXA_MARKETREPLAY, MXA_RMSC03_RL, MXA_VALUE_NOISE = 0, 1, 2, 3, 4, 5
+MXA_RMSC01 = 6
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000,
-              "value_noise": MXA_VALUE_NOISE}
+              "value_noise": MXA_VALUE_NOISE, "rmsc01": MXA_RMSC01}
 ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
 ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",
              4: "transaction history capacity", 5: "get_transacted_volume without transactions (pandas error)",
@@ -19,7 +20,10 @@ ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: 
              9: "RNG look-ahead overrun", 10: "price outside the replay ladder", 11: "book entry pool capacity",
              12: "agent order-id capacity", 13: "MarketReplayAgent KeyError (no tape group at wake time)",
              14: "get_observation/get_reward on missing or None data", 15: "kernelStopping with trade on (TypeError)",
-             16: "modify changing price or side"}
+             16: "modify changing price or side",
+             17: "HBL order stream outside the history window / device ring (MXA_OH_CAP)",
+             18: "HBL streamed price range beyond the device histogram (MXA_HBL_RANGE)",
+             19: "limit price the reference would carry as a python float (not restated)"}
 
 
 class EnvSummary(ctypes.Structure):

@@ -1,7 +1,8 @@
 """Agent naming of the reference configs (used for the reference-format stdout report).
 
 config/rmsc03.py:95-197, config/sparse_zi_100.py:177-256, config/sparse_zi_1000.py,
-config/value_noise.py:98-161 (every ValueAgent gets its own type string "ValueAgent {id}").
+config/value_noise.py:98-161 (every ValueAgent gets its own type string "ValueAgent {id}"),
+config/rmsc01.py:75-211.
 """
 ZI_GROUPS = [(0, 250, "1"), (0, 500, "1"), (0, 1000, "0.8"), (0, 1000, "1"), (0, 2000, "0.8"), (250, 500, "0.8"),
              (250, 500, "1")]
@@ -13,6 +14,9 @@ def symbol_of(config):
 
 
 def agent_names(config):
+    if config == "rmsc01":
+        return (["EXCHANGE_AGENT", "MARKET_MAKER_AGENT_1"] + ["ZI_AGENT_%d" % j for j in range(2, 52)] +
+                ["HBL_AGENT_%d" % j for j in range(52, 77)] + ["MOMENTUM_AGENT_%d" % j for j in range(77, 101)])
     if config == "value_noise":
         return (["Exchange Agent 0"] + ["NoiseAgent %d" % j for j in range(1, 101)] +
                 ["Value Agent %d" % j for j in range(101, 151)])
@@ -30,6 +34,9 @@ def agent_names(config):
 
 
 def agent_type_names(config):
+    if config == "rmsc01":
+        return (["ExchangeAgent", "MarketMakerAgent"] + ["ZeroIntelligenceAgent"] * 50 +
+                ["HeuristicBeliefLearningAgent"] * 25 + ["MomentumAgent"] * 24)
     if config == "value_noise":
         return ["ExchangeAgent"] + ["NoiseAgent"] * 100 + ["ValueAgent %d" % j for j in range(101, 151)]
     if config == "rmsc03":

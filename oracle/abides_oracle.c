@@ -132,7 +132,8 @@ enum {
     K_WAKEUP = 0, K_WHEN_OPEN_REQ = 1, K_WHEN_CLOSE_REQ = 2, K_WHEN_OPEN = 3, K_WHEN_CLOSE = 4,
     K_SPREAD_REQ = 5, K_SPREAD = 6, K_LAST_REQ = 7, K_LAST = 8, K_TV_REQ = 9, K_TV = 10,
     K_LIMIT = 11, K_CANCEL = 12, K_MODIFY = 13, K_ACCEPTED = 14, K_EXECUTED = 15, K_CANCELLED = 16,
-    K_MKT_CLOSED = 17, K_MODIFIED = 18, K_KCANCEL = 19, K_MARKET_DATA = 20
+    K_MKT_CLOSED = 17, K_MODIFIED = 18, K_KCANCEL = 19, K_MARKET_DATA = 20,
+    K_STREAM_REQ = 21, K_STREAM = 22 /* QUERY_ORDER_STREAM request / reply */
 };
 enum { T_MESSAGE = 1, T_WAKEUP = 2, T_CANCEL_ORDER = 3 };
 
@@ -187,6 +188,8 @@ typedef struct {
 } txn_t;
 typedef struct {
     int64_t oid;
+    int64_t price; /* "limit_price" and "is_buy_order" of the history entry (HBL reads them) */
+    int is_buy;
     txn_t* tx;
     int ntx, captx;
 } hent_t;
@@ -198,8 +201,8 @@ typedef struct {
 /* ------------------------------------------------------------------------- */
 /* agents                                                                     */
 /* ------------------------------------------------------------------------- */
-enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL };
-enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE };
+enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL, AG_MKTMAKER, AG_HBL };
+enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE, ST_AWAITING_STREAM };
 
 typedef struct {
     int64_t id;
@@ -244,6 +247,13 @@ typedef struct {
     int64_t* mids2;
     int nmid, capmid, n20, n50;
     double avg20, avg50;
+    /* MarketMakerAgent (agent/market_makers/MarketMakerAgent.py) */
+    int64_t mk_min, mk_max, last_spread;
+    int spread_depth;
+    /* HeuristicBeliefLearningAgent: L, and the last order stream as absolute history epochs
+     * [stream_hi - stream_n + 1, stream_hi] (the reply holds live references to those dicts) */
+    int L, stream_n, has_stream;
+    int64_t stream_hi;
 } agent_t;
 
 struct ora_env {
@@ -258,6 +268,7 @@ struct ora_env {
     int last_trade_float;
     epoch_t hist[16];
     int nhist;
+    int64_t epoch_abs; /* absolute number of hist[0]: history shifts so far */
     /* SparseMeanRevertingOracle (one symbol) */
     ora_rs O;
     double o_rbar, o_kappa, o_fundvol, o_lambda, o_msmean, o_msvar;
@@ -522,6 +533,14 @@ static void encode(const ora_env* e, const ev_t* v, int64_t rec[10]) {
     case K_EXECUTED:
         f[0] = m->oid; f[1] = m->oagent; f[2] = m->is_buy; f[3] = m->qty; f[4] = m->price; f[5] = m->fill;
         break;
+    case K_STREAM_REQ:
+        f[0] = m->sender;
+        f[1] = m->depth;
+        break;
+    case K_STREAM:
+        f[0] = m->data;
+        f[5] = m->mkt_closed ? 1 : 0;
+        break;
     default:
         break;
     }
@@ -565,18 +584,20 @@ static hent_t* hist_find(epoch_t* ep, int64_t oid) {
         if (ep->e[i].oid == oid) return &ep->e[i];
     return NULL;
 }
-static void hist_add_order(ora_env* e, int64_t oid) {
+static void hist_add_order(ora_env* e, int64_t oid, int64_t price, int is_buy) {
     epoch_t* ep = &e->hist[0];
     hent_t* h = hist_find(ep, oid);
     if (h) { /* dict re-assignment keeps position, resets value */
         h->ntx = 0;
+        h->price = price;
+        h->is_buy = is_buy;
         return;
     }
     if (ep->n == ep->cap) {
         ep->cap = ep->cap ? 2 * ep->cap : 16;
         ep->e = (hent_t*)realloc(ep->e, sizeof(hent_t) * ep->cap);
     }
-    hent_t n0 = {oid, NULL, 0, 0};
+    hent_t n0 = {oid, price, is_buy, NULL, 0, 0};
     ep->e[ep->n++] = n0;
 }
 static void hent_add_tx(hent_t* h, int64_t t, int64_t q) {
@@ -603,6 +624,7 @@ static void hist_shift(ora_env* e) {
     memmove(e->hist + 1, e->hist, sizeof(epoch_t) * e->nhist);
     memset(&e->hist[0], 0, sizeof(epoch_t));
     e->nhist++;
+    e->epoch_abs++;
 }
 
 static void ex_send(ora_env* e, int recipient, msg_t* m) {
@@ -678,7 +700,7 @@ static void enter_order(ora_env* e, bord_t o) {
 /* handleLimitOrder (OrderBook.py:38-170) */
 static void handle_limit_order(ora_env* e, bord_t order) {
     if (order.qty <= 0) return;
-    hist_add_order(e, order.id);
+    hist_add_order(e, order.id, order.price, order.is_buy);
     int64_t ex_q = 0, ex_pq = 0;
     int executed = 0;
     for (;;) {
@@ -804,7 +826,7 @@ static void ex_receive(ora_env* e, const msg_t* m) {
             r.kind = K_MKT_CLOSED;
             ex_send(e, m->sender, &r);
             return;
-        } else if (m->kind == K_SPREAD_REQ || m->kind == K_LAST_REQ || m->kind == K_TV_REQ) {
+        } else if (m->kind == K_SPREAD_REQ || m->kind == K_LAST_REQ || m->kind == K_TV_REQ || m->kind == K_STREAM_REQ) {
         } else {
             r.kind = K_MKT_CLOSED;
             ex_send(e, m->sender, &r);
@@ -862,6 +884,17 @@ static void ex_receive(ora_env* e, const msg_t* m) {
         r.kind = K_TV;
         r.data = vol;
         r.has_data = 1;
+        r.mkt_closed = closed;
+        ex_send(e, m->sender, &r);
+        break;
+    }
+    case K_STREAM_REQ: {
+        /* QUERY_ORDER_STREAM (ExchangeAgent.py:251-279): history[1 : length + 1], live references */
+        int avail = e->nhist - 1;
+        r.kind = K_STREAM;
+        r.data = m->depth < avail ? m->depth : avail; /* number of epochs returned */
+        if (r.data < 0) r.data = 0;
+        r.lookback = e->epoch_abs - 1; /* absolute number of history[1] */
         r.mkt_closed = closed;
         ex_send(e, m->sender, &r);
         break;
@@ -1000,6 +1033,7 @@ static int64_t wake_frequency(agent_t* a) {
     switch (a->type) {
     case AG_POVMM: return a->wake_freq;
     case AG_MOMENTUM: return a->wake_freq;
+    case AG_MKTMAKER: return a->wake_freq; /* pd.Timedelta(wake_up_freq) (MarketMakerAgent.py:148-149) */
     case AG_REPLAY: return a->wake_freq;  /* first tape time - mkt_open (MarketReplayAgent.py:94-96) */
     case AG_DUMMYRL: return a->wake_freq; /* horizon[0] - mkt_open (execution_agent.py:129-130) */
     default: return rs_randint(&a->rs, 0, 100);
@@ -1056,6 +1090,12 @@ static void ta_receive(ora_env* e, agent_t* a, const msg_t* m) {
         if (m->mkt_closed) a->mkt_closed = 1;
         a->tv = m->data;
         break;
+    case K_STREAM: /* queryOrderStream (TradingAgent.py:240-246, 549-554) */
+        if (m->mkt_closed) a->mkt_closed = 1;
+        a->has_stream = 1;
+        a->stream_n = (int)m->data;
+        a->stream_hi = m->lookback;
+        break;
     default: break;
     }
     int have = a->has_open && a->has_close;
@@ -1089,7 +1129,9 @@ static int64_t bayes_r_T(ora_env* e, agent_t* a, int64_t obs_t) {
 }
 
 /* --------------------------- ZeroIntelligenceAgent -------------------------- */
-static void zi_wakeup(ora_env* e, agent_t* a) {
+/* ZeroIntelligenceAgent.wakeup (ZI.py:125-187).  A subclass (HBL) does not query the spread
+ * here: its state becomes ACTIVE (ZI.py:183-187). */
+static void zi_wakeup_as(ora_env* e, agent_t* a, int is_zi) {
     ta_wakeup(e, a);
     a->state = ST_INACTIVE;
     if (!a->has_open || !a->has_close) return;
@@ -1103,11 +1145,16 @@ static void zi_wakeup(ora_env* e, agent_t* a) {
         return;
     }
     cancel_all(e, a);
-    get_spread(e, a, 1);
-    a->state = ST_AWAITING_SPREAD;
+    if (is_zi) {
+        get_spread(e, a, 1);
+        a->state = ST_AWAITING_SPREAD;
+    } else {
+        a->state = ST_ACTIVE;
+    }
 }
-static void zi_place(ora_env* e, agent_t* a) {
-    /* updateEstimates (ZI.py:189-275) */
+static void zi_wakeup(ora_env* e, agent_t* a) { zi_wakeup_as(e, a, 1); }
+/* updateEstimates (ZI.py:189-275): total unit valuation v and side; 0 on the reference's IndexError */
+static int zi_update_estimates(ora_env* e, agent_t* a, int64_t* v_out, int* buy_out) {
     int64_t obs = o_observe(e, e->cur, a->sigma_n, &a->rs);
     int64_t q = (int64_t)((double)a->shares / 100); /* int(h / 100): truncation */
     int buy;
@@ -1120,10 +1167,16 @@ static void zi_place(ora_env* e, agent_t* a) {
     if (idx < 0) idx += 20; /* python negative index */
     if (idx < 0 || idx >= 20) {
         fail(e, -6, "ZeroIntelligenceAgent theta index out of range (IndexError)");
-        return;
+        return 0;
     }
-    int64_t theta = a->theta[idx];
-    int64_t v = r_T + theta;
+    *v_out = r_T + a->theta[idx];
+    *buy_out = buy;
+    return 1;
+}
+static void zi_place(ora_env* e, agent_t* a) {
+    int64_t v;
+    int buy;
+    if (!zi_update_estimates(e, a, &v, &buy)) return;
     /* placeOrder (ZI.py:277-309) */
     int64_t R = rs_randint(&a->rs, a->R_min, a->R_max + 1);
     int64_t p = buy ? v - R : v + R;
@@ -1300,6 +1353,139 @@ static void mom_receive(ora_env* e, agent_t* a, const msg_t* m) {
     }
 }
 
+
+/* --------------------------- MarketMakerAgent ------------------------------ */
+/* agent/market_makers/MarketMakerAgent.py, polling mode (subscribe=False) */
+static void mk_wakeup(ora_env* e, agent_t* a) {
+    int can_trade = ta_wakeup(e, a); /* MarketMakerAgent.py:69-79 */
+    if (can_trade) {
+        cancel_all(e, a);
+        get_spread(e, a, a->spread_depth);
+        a->state = ST_AWAITING_SPREAD;
+    }
+}
+static void mk_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m); /* MarketMakerAgent.py:81-107 */
+    if (!(a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD)) return;
+    cancel_all(e, a);
+    int64_t mid = a->last_trade, spread;
+    /* getKnownBidAsk: best levels or None; `if bid and ask` (0 is falsy too) */
+    if (a->nb && a->na && a->bid && a->ask) {
+        mid = (int64_t)((double)(a->ask + a->bid) / 2);
+        spread = (int64_t)((double)llabs(a->ask - a->bid) / 2);
+    } else {
+        if (a->last_trade_float) { /* mid = the opening price, a python float: float prices (not restated) */
+            fail(e, -13, "MarketMakerAgent: ladder priced from a float last trade (not restated)");
+            return;
+        }
+        spread = a->last_spread;
+    }
+    for (int i = 0; i < 2 * a->spread_depth; i++) {
+        a->size = (int64_t)rint((double)rs_randint(&a->rs, a->mk_min, a->mk_max) / 2); /* round(x / 2) */
+        place_limit(e, a, a->size, 1, mid - spread - i);
+        place_limit(e, a, a->size, 0, mid + spread + i);
+    }
+    k_wakeup(e, a->id, e->cur + a->wake_freq);
+    a->state = ST_AWAITING_WAKEUP;
+}
+
+/* ------------------------- HeuristicBeliefLearningAgent ----------------------- */
+/* agent/HeuristicBeliefLearningAgent.py */
+static void hbl_wakeup(ora_env* e, agent_t* a) {
+    zi_wakeup_as(e, a, 0); /* HBL.py:61-73 */
+    if (a->state != ST_ACTIVE) return;
+    msg_t m;
+    memset(&m, 0, sizeof m);
+    m.kind = K_STREAM_REQ; /* getOrderStream(symbol, length=L) (TradingAgent.py:285-289) */
+    m.depth = a->L;
+    ta_send_ex(e, a, &m);
+    a->state = ST_AWAITING_STREAM;
+}
+/* HBL.placeOrder (HBL.py:75-195): the orders of the streamed history epochs as they are NOW (the
+ * reply held references to the exchange's live dicts), dense over [low_p, high_p] as written */
+static void hbl_place(ora_env* e, agent_t* a) {
+    if (!a->has_stream || a->stream_n < a->L) { /* insufficient history: exactly ZI.placeOrder */
+        zi_place(e, a);
+        return;
+    }
+    int64_t v;
+    int buy;
+    if (!zi_update_estimates(e, a, &v, &buy)) return;
+    int64_t low_p = INT64_MAX, high_p = 0;
+    int nent = 0;
+    for (int k = 0; k < a->stream_n; k++) {
+        int64_t idx = e->epoch_abs - (a->stream_hi - k);
+        if (idx < 1 || idx >= e->nhist) {
+            fail(e, -11, "HBL: streamed history epoch left the exchange's window (not restated)");
+            return;
+        }
+        const epoch_t* ep = &e->hist[idx];
+        for (int j = 0; j < ep->n; j++) {
+            int64_t p = ep->e[j].price;
+            if (p < low_p) low_p = p;
+            if (p > high_p) high_p = p;
+            nent++;
+        }
+    }
+    if (nent == 0 || high_p - low_p + 1 <= 0) {
+        fail(e, -12, "HBL: empty order stream (numpy ValueError)");
+        return;
+    }
+    int64_t np_ = high_p - low_p + 1;
+    double* nd = (double*)calloc((size_t)np_ * 8, sizeof(double)); /* sa, sb, ua, ub, num, denom, Pr, Es */
+#define ND(i, c) nd[(size_t)(i) * 8 + (c)]
+    for (int k = 0; k < a->stream_n; k++) {
+        const epoch_t* ep = &e->hist[e->epoch_abs - (a->stream_hi - k)];
+        for (int j = 0; j < ep->n; j++) {
+            int64_t i = ep->e[j].price - low_p;
+            int tx = ep->e[j].ntx > 0;
+            if (ep->e[j].is_buy) ND(i, tx ? 1 : 3) += 1;
+            else ND(i, tx ? 0 : 2) += 1;
+        }
+    }
+    if (buy) {
+        for (int64_t i = 1; i < np_; i++)
+            for (int c = 0; c < 3; c++) ND(i, c) += ND(i - 1, c);
+        for (int64_t i = np_ - 2; i >= 0; i--) ND(i, 3) += ND(i + 1, 3);
+        for (int64_t i = 0; i < np_; i++) ND(i, 4) = ND(i, 0) + ND(i, 1) + ND(i, 2);
+    } else {
+        for (int64_t i = np_ - 2; i >= 0; i--) {
+            ND(i, 0) += ND(i + 1, 0);
+            ND(i, 1) += ND(i + 1, 1);
+            ND(i, 3) += ND(i + 1, 3);
+        }
+        for (int64_t i = 1; i < np_; i++) ND(i, 2) += ND(i - 1, 2);
+        for (int64_t i = 0; i < np_; i++) ND(i, 4) = ND(i, 0) + ND(i, 1) + ND(i, 3);
+    }
+    int64_t best = 0;
+    for (int64_t i = 0; i < np_; i++) {
+        ND(i, 5) = ND(i, 0) + ND(i, 1) + ND(i, 2) + ND(i, 3);
+        double pr = ND(i, 4) / ND(i, 5);
+        if (isnan(pr)) pr = 0.0; /* np.nan_to_num (inf cannot occur: num <= denom) */
+        ND(i, 6) = pr;
+        ND(i, 7) = pr * (double)(buy ? v - (low_p + i) : (low_p + i) - v);
+        if (ND(i, 7) > ND(best, 7)) best = i; /* np.argmax: first maximum */
+    }
+    double best_es = ND(best, 7);
+    free(nd);
+#undef ND
+    if (best_es > 0) place_limit(e, a, 100, buy, low_p + best);
+}
+static void hbl_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    /* ZeroIntelligenceAgent.receiveMessage (ZI.py:311-334), placeOrder dispatching to HBL's */
+    if (a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        if (a->mkt_closed) return;
+        hbl_place(e, a);
+        a->state = ST_AWAITING_WAKEUP;
+    }
+    /* HBL.receiveMessage (HBL.py:197-217) */
+    if (a->state == ST_AWAITING_STREAM && m->kind == K_STREAM) {
+        if (a->mkt_closed) return;
+        get_spread(e, a, 1);
+        a->state = ST_AWAITING_SPREAD;
+    }
+}
 
 /* ------------------------ marketreplay / ABIDESEnv -------------------------- */
 /* MarketReplayAgent.placeOrder (MarketReplayAgent.py:69-91) for one tape record.
@@ -1555,6 +1741,8 @@ static void dispatch_wakeup(ora_env* e, int id) {
     case AG_MOMENTUM: mom_wakeup(e, a); break;
     case AG_REPLAY: mr_wakeup(e, a); break;
     case AG_DUMMYRL: rl_wakeup(e, a); break;
+    case AG_MKTMAKER: mk_wakeup(e, a); break;
+    case AG_HBL: hbl_wakeup(e, a); break;
     }
 }
 static void dispatch_message(ora_env* e, int id, const msg_t* m) {
@@ -1562,6 +1750,8 @@ static void dispatch_message(ora_env* e, int id, const msg_t* m) {
     switch (a->type) {
     case AG_EXCHANGE: ex_receive(e, m); break;
     case AG_ZI: zi_receive(e, a, m); break;
+    case AG_HBL: hbl_receive(e, a, m); break;
+    case AG_MKTMAKER: mk_receive(e, a, m); break;
     case AG_NOISE: noise_receive(e, a, m); break;
     case AG_VALUE: value_receive(e, a, m); break;
     case AG_POVMM: mm_receive(e, a, m); break;
@@ -1699,7 +1889,7 @@ static void final_valuation(ora_env* e, agent_t* a) {
     } else if (a->type == AG_VALUE) {
         int64_t rT = o_observe(e, a->cur_time, 0, NULL);
         sum_add(e, a->id, 3, 1, 0, (double)(rT * H + a->cash - a->starting_cash) / (double)a->starting_cash);
-    } else if (a->type == AG_ZI) {
+    } else if (a->type == AG_ZI || a->type == AG_HBL) { /* HBL inherits ZI.kernelStopping */
         int64_t rT = o_observe(e, a->cur_time, 0, NULL);
         int64_t s = 0;
         int nq = 2 * a->q_max;
@@ -1977,6 +2167,93 @@ static int build_rmsc03(ora_env* e, uint32_t seed) {
     return 0;
 }
 
+/* config/rmsc01.py:49-263: 1 exchange, 1 MarketMakerAgent, 50 ZI, 25 HBL, 24 Momentum on JPM
+ * 2019-06-28, market 09:30-16:00, kernel 09:30-16:01, compute delay 0, latency zeros, noise [0.0].
+ * Global draw order: exchange seed, market maker seed (its __init__ draws its size from its
+ * own stream), the oracle symbol's seed, the oracle's megashock init, per ZI / HBL agent its
+ * seed (theta from its own stream), per momentum agent its seed (size from its own stream),
+ * the kernel's seed.  book_freq="M" only archives snapshots at the end (logging). */
+static void zi_params(agent_t* a, int64_t rmin, int64_t rmax, double sigma_n, double sigma_s, double sigma_pv) {
+    trading_init(a, 10000000);
+    a->sigma_n = sigma_n;
+    a->r_bar = 1e5;
+    a->kappa = 1.67e-15;
+    a->sigma_s = sigma_s;
+    a->q_max = 10;
+    a->R_min = rmin;
+    a->R_max = rmax;
+    a->eta = 1;
+    a->lambda_a = 1e-12;
+    a->r_t = 1e5;
+    a->sigma_t = 0;
+    double th[20];
+    for (int i = 0; i < 20; i++) th[i] = rint(rs_normal(&a->rs, 0, sqrt(sigma_pv)));
+    qsort(th, 20, sizeof(double), cmp_desc);
+    for (int i = 0; i < 20; i++) a->theta[i] = (int64_t)th[i];
+}
+static int build_rmsc01(ora_env* e, uint32_t seed) {
+    rs_seed(&e->G, seed);
+    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
+    agent_t* ex = add_agent(e, AG_EXCHANGE);
+    rs_seed(&ex->rs, seed_u32(&e->G));
+    snprintf(ex->name, 96, "EXCHANGE_AGENT");
+    snprintf(ex->tname, 96, "ExchangeAgent");
+    e->ex_open = open;
+    e->ex_close = close;
+    e->ex_pipeline = 0;
+    e->ex_comp = 0;
+    e->stream_history = 10;
+    {
+        agent_t* a = add_agent(e, AG_MKTMAKER);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        snprintf(a->name, 96, "MARKET_MAKER_AGENT_%d", a->id);
+        snprintf(a->tname, 96, "MarketMakerAgent");
+        trading_init(a, 10000000);
+        a->mk_min = 500;
+        a->mk_max = 1000;
+        a->size = (int64_t)rint((double)rs_randint(&a->rs, a->mk_min, a->mk_max) / 2);
+        a->wake_freq = NS_SEC;
+        a->spread_depth = 5;
+        a->last_spread = 10;
+    }
+    rs_seed(&e->O, seed_u32(&e->G));
+    oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+    for (int j = 0; j < 50; j++) {
+        agent_t* a = add_agent(e, AG_ZI);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        snprintf(a->name, 96, "ZI_AGENT_%d", a->id);
+        snprintf(a->tname, 96, "ZeroIntelligenceAgent");
+        zi_params(a, 0, 100, 10000, 1e-4, 5e4);
+    }
+    for (int j = 0; j < 25; j++) {
+        agent_t* a = add_agent(e, AG_HBL);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        snprintf(a->name, 96, "HBL_AGENT_%d", a->id);
+        snprintf(a->tname, 96, "HeuristicBeliefLearningAgent");
+        zi_params(a, 0, 100, 10000, 1e-4, 5e4);
+        a->L = 2;
+    }
+    for (int j = 0; j < 24; j++) {
+        agent_t* a = add_agent(e, AG_MOMENTUM);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        a->size = rs_randint(&a->rs, 1, 10);
+        snprintf(a->name, 96, "MOMENTUM_AGENT_%d", a->id);
+        snprintf(a->tname, 96, "MomentumAgent");
+        trading_init(a, 10000000);
+        a->wake_freq = 60 * NS_SEC;
+    }
+    rs_seed(&e->K, seed_u32(&e->G));
+    e->start = open;
+    e->stop = 16 * NS_HOUR + NS_MIN;
+    e->lat_mode = 0;
+    e->noise_len = 1;
+    int n = e->n;
+    e->agent_time = (int64_t*)calloc(n, sizeof(int64_t));
+    e->comp_delay = (int64_t*)calloc(n, sizeof(int64_t));
+    for (int i = 0; i < n; i++) e->agent_time[i] = e->start;
+    return 0;
+}
+
 /* config/value_noise.py:45-200 (argparse defaults: obs_noise 1e6): 1 exchange, 100 noise and
  * 50 value agents on JPM 2019-06-28, market 09:30-10:30, kernel midnight-17:00, compute delay
  * 1 s, latency matrix U(21000, 13e6) symmetrised (diagonal 20000), 6-way uniform noise.
@@ -2166,6 +2443,7 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     else if (!strcmp(config, "rmsc03")) rc = build_rmsc03(e, seed);
     else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
     else if (!strcmp(config, "value_noise")) rc = build_value_noise(e, seed);
+    else if (!strcmp(config, "rmsc01")) rc = build_rmsc01(e, seed);
     else rc = -1;
     if (rc) {
         free(e);
