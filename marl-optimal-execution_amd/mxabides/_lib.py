@@ -98,12 +98,14 @@ def load():
     L.mxa_step_device.argtypes = [P, P, P, P]
     L.mxa_finalize.argtypes = [P]
     L.mxa_read_final.argtypes = [P, I32, P, I32]
-    L.mxa_build_id.argtypes = []
-    L.mxa_build_id.restype = ctypes.c_char_p
+    if hasattr(L, "mxa_build_id"):  # (absent from libraries built before it existed: A/B runs)
+        L.mxa_build_id.argtypes = []
+        L.mxa_build_id.restype = ctypes.c_char_p
     _lib = L
     return L
 
 
 def build_id():
     """the kernel-source hash libmxa was built with (build_lib.build_id)"""
-    return load().mxa_build_id().decode()
+    L = load()
+    return L.mxa_build_id().decode() if hasattr(L, "mxa_build_id") else "unknown"

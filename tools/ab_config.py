@@ -1,0 +1,22 @@
+"""A/B of one configuration's run kernel between two libmxa builds (MXA_LIB selects the library):
+python tools/ab_config.py CONFIG N_ENVS [REPS]  ->  run-kernel ms per episode batch."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "marl-optimal-execution_amd")]
+import numpy as np
+import mxabides
+
+cfg, n = sys.argv[1], int(sys.argv[2])
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+m = mxabides.VecMarket(cfg, (123456789 + np.arange(n)) & 0xFFFFFFFF)
+m.set_parity_hash(False)
+ms = []
+for r in range(reps):
+    m.reset()
+    m.run(chunk=1 << 22)
+    ms.append(m.last_kernel_ms)
+ev = int(m.summary()["events"].sum())
+print("%s %s x%d: run kernel %s ms (best %.1f), %.1f M env-steps/s" % (
+    os.path.basename(os.environ.get("MXA_LIB", "libmxa.so")), cfg, n, ["%.1f" % x for x in ms], min(ms), ev / min(ms) / 1e3))
