@@ -149,6 +149,26 @@ int mxa_write_rl_state(mxa_handle* h, double* device_out);
  * attaches measured HBM traffic only to the build it was measured on */
 const char* mxa_build_id(void);
 
+/* book-update log, the input of the reference's order-book outputs: OrderBook.book_log rows
+ * (OrderBook.py:151-168, archived by ExchangeAgent.logOrderBookSnapshots, ExchangeAgent.py:389-469,
+ * as ORDERBOOK_<sym>_FULL) and the exchange's BEST_BID / BEST_ASK / LAST_TRADE events
+ * (OrderBook.py:112-141).  One record per handled limit order (price, qty > 0 for a buy, < 0
+ * for a sell) and per cancellation (-price, the cancelled quantity, > 0 on the bid side).  The
+ * host replays the price-level volumes (mxabides.booklog): matching at level granularity is
+ * exact, as a level gives min(remaining quantity, its volume) at its price. */
+typedef struct {
+  int64_t t;      /* Kernel.currentTime, ns since midnight */
+  int32_t price;  /* cents (limit orders), -cents (cancellations) */
+  int32_t qty;
+} mxa_book_rec;
+/* plain Kernel.runner configs: `cap` records per env (0 = off); resets every env's record
+ * count, so enable it after mxa_create / mxa_reset and before the first launch.  An env that
+ * fills its log stops with error ERR_BOOK_LOG_FULL (20).  The exchange's event runs (batched
+ * LIMIT/CANCEL handling) are off while logging. */
+int mxa_set_book_log(mxa_handle* h, int32_t cap);
+/* env's records: min(total, cap) are written to out, the total to *n */
+int mxa_read_book_log(mxa_handle* h, int32_t env, mxa_book_rec* out, int64_t cap, int64_t* n);
+
 /* parity probes: device numpy-legacy RNG (mode 0 u32, 1 double, 2 randint(a,b),
  * 3 normal(a,b), 4 exponential(a), 5 uniform(a,b)) and device glibc math
  * (mode 0 log, 1 exp, 2 pow) */

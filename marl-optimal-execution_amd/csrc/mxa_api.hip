@@ -18,7 +18,7 @@ namespace {
 
 typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*,
                          const RpCtx*);
-typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*);
+typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, BlRec*, int);
 typedef void (*stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, mxa_agent_final*);
 typedef void (*step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, const double*,
                         double*, int32_t*);
@@ -30,8 +30,8 @@ void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_
 }
 template <int CFG>
 void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
-                const RpCtx* ctx) {
-  hipLaunchKernelGGL((mxa_run_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx);
+                const RpCtx* ctx, BlRec* blog, int blog_cap) {
+  hipLaunchKernelGGL((mxa_run_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, blog, blog_cap);
 }
 
 template <int CFG>
@@ -107,6 +107,8 @@ struct mxa_handle {
   step_fn step = nullptr;  // GymKernel handles (replay, rmsc03_rl)
   stop_fn stop = nullptr;  // kernelStopping pass (plain Kernel.runner configs)
   mxa_agent_final* d_final = nullptr;
+  BlRec* d_blog = nullptr;  // book-update log [n_envs][blog_cap] (mxa_set_book_log)
+  int32_t blog_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0;
   std::string err;
@@ -385,7 +387,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
   if (!h || h->gym) return MXA_EINVAL;  // GymKernel handles advance by mxa_step
   h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
-         h->d_ctx);
+         h->d_ctx, h->d_blog, h->blog_cap);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
 }
@@ -405,7 +407,7 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
     if (max_launches > 0 && launches >= max_launches) break;
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), chunk,
-           h->d_ctx);
+           h->d_ctx, h->d_blog, h->blog_cap);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     launches++;
@@ -423,6 +425,43 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   }
   h->last_ms = total;
   if (launches_out) *launches_out = launches;
+  return MXA_OK;
+}
+
+// book-update log (OrderBook.book_log / the exchange's BEST_BID, BEST_ASK, LAST_TRADE events):
+// `cap` records per env in one device buffer; every env's record count restarts at 0
+int mxa_set_book_log(mxa_handle* h, int32_t cap) {
+  if (!h || h->gym || cap < 0) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->d_blog) HIPCHK(h, hipFree(h->d_blog));
+  h->d_blog = nullptr;
+  h->blog_cap = 0;
+  if (cap > 0) {
+    HIPCHK(h, hipMalloc(&h->d_blog, sizeof(BlRec) * (size_t)cap * h->P.n_envs));
+    h->blog_cap = cap;
+  }
+  HIPCHK(h, hipMemset2DAsync(h->d_env + offsetof(EnvHdr, blog_n), h->P.L.env_stride, 0, sizeof(int32_t), h->P.n_envs,
+                             h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_read_book_log(mxa_handle* h, int32_t env, mxa_book_rec* out, int64_t cap, int64_t* n) {
+  if (!h || env < 0 || env >= h->P.n_envs || !n || cap < 0 || (cap > 0 && !out)) return MXA_EINVAL;
+  static_assert(sizeof(mxa_book_rec) == sizeof(BlRec) && offsetof(mxa_book_rec, qty) == offsetof(BlRec, qty),
+                "mxa_book_rec mirrors BlRec");
+  int32_t cnt = 0;
+  HIPCHK(h, hipMemcpyAsync(&cnt, h->d_env + (size_t)env * h->P.L.env_stride + offsetof(EnvHdr, blog_n), sizeof(cnt),
+                           hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (!h->d_blog) cnt = 0;
+  *n = cnt;
+  const int64_t m = cnt < cap ? cnt : cap;
+  if (m > 0)
+    HIPCHK(h, hipMemcpyAsync(out, h->d_blog + (size_t)env * h->blog_cap, sizeof(BlRec) * m, hipMemcpyDeviceToHost,
+                             h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;
 }
 
@@ -629,6 +668,7 @@ void mxa_destroy(mxa_handle* h) {
   if (h->d_obs) hipFree(h->d_obs);
   if (h->d_flags) hipFree(h->d_flags);
   if (h->d_final) hipFree(h->d_final);
+  if (h->d_blog) hipFree(h->d_blog);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
   if (h->own) hipStreamDestroy(h->own);

@@ -600,6 +600,8 @@ struct Eng {
   const RpCtx* rx;  // marketreplay: tape + runtime layout (nullptr otherwise)
   i32 end_step;     // GymKernel: the RL agent's spread reply ends a step
   u32 run_skip;     // event runs: members below this seq are popped one by one (a LIMIT run that crosses)
+  BlRec* blog;      // book-update log of this env (nullptr: off)
+  i32 blog_cap;
 #ifdef MXA_PROF
   LDSP u64* prof;
 #endif
@@ -608,8 +610,11 @@ struct Eng {
   LDSP u32* rwin;    // [4][64] output windows of the global RNG streams (RSt::lw)
 
   static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 4 * PW : 0));
-  DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr) : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
+  DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr, BlRec* bl = nullptr, i32 bl_cap = 0)
+      : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
     rx = ctx;
+    blog = bl;
+    blog_cap = bl_cap;
     end_step = 0;
     add_delay = 0;
     run_skip = 0;
@@ -1389,8 +1394,27 @@ struct Eng {
   DEV void oh_mark_tx(i32 r) {
     if (h.oh_head - r <= PC.L.oh_cap && lane == 0) ohr()[r % PC.L.oh_cap].meta |= 2;
   }
+  // ---------------- book-update log (OrderBook.book_log rows, ExchangeAgent BEST_BID/ASK/LAST_TRADE)
+  // one record per handled limit order and per cancellation; the host replays the level
+  // volumes (matching at level granularity is exact: a level gives min(remaining, volume))
+  DEV void bl_put(i32 price, i32 qty) {
+    const i32 n = h.blog_n;
+    if (n >= blog_cap) {
+      fail(ERR_BOOK_LOG_FULL);
+      return;
+    }
+    if (lane == 0) {
+      BlRec r;
+      r.t = cur;
+      r.price = price;
+      r.qty = qty;
+      blog[n] = r;
+    }
+    h.blog_n = n + 1;
+  }
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
     if (qty <= 0) return;
+    if (blog) bl_put(price, is_buy ? qty : -qty);
     i32 hep = h.epoch;
     LDSP i32* EP = ep_entries();
     i32 ne = EP[h.epoch & 15] + 1;
@@ -1453,6 +1477,7 @@ struct Eng {
     if (s < 0) return;
     i32 q = b_get(bq, s), o = b_get(bo, s), mm = b_get(bm, s), p = b_get(bp, s);
     b_free(s);
+    if (blog) bl_put(-p, buy ? q : -q);
     Msg r = msg_order(MK_CANCELLED, o, mm >> 1, mm & 1, q, p, 0);
     ex_notify(m_agent(m), r);
   }
@@ -3480,7 +3505,7 @@ struct Eng {
         // a run past stopTime is not batched: the loop stops after its first member
         if (type == MT_MESSAGE && (m.w[0] & MF_RUN) && t <= PC.stop && eseq >= run_skip) {
           const u32 k = m_kind(m);
-          const bool exr = rcp == 0 && (k == MK_CANCEL || k == MK_LIMIT) && !(t > PC.mkt_close);
+          const bool exr = rcp == 0 && (k == MK_CANCEL || k == MK_LIMIT) && !(t > PC.mkt_close) && !blog;
           const bool ackr = rcp > 0 && rcp < ACK_LIMIT && (k == MK_ACCEPTED || k == MK_CANCELLED);
           if (exr || ackr) {
             PROF_ADD(0, t0);
@@ -4030,13 +4055,13 @@ __global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stri
 
 template <int CFG>
 __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops,
-                                                                              const RpCtx* ctx) {
+                                                                              const RpCtx* ctx, BlRec* blog, int blog_cap) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int env = blockIdx.x;
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
   if (((EnvHdr*)e)->status != ST_RUNNING) return;
-  mxa::Eng<CFG> g(e, lds, trace_cap, ctx);
+  mxa::Eng<CFG> g(e, lds, trace_cap, ctx, blog ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
   g.load();
   g.run(max_pops);
   g.save();
@@ -4128,7 +4153,7 @@ __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y
 // explicit instantiations per supported configuration
 #define MXA_INST(CFG)                                                                                      \
   template __global__ void mxa_build_kernel<CFG>(char*, uint64_t, int, const uint32_t*, const uint8_t*, const RpCtx*); \
-  template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*);               \
+  template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*, BlRec*, int);  \
   template __global__ void mxa_stop_kernel<CFG>(char*, uint64_t, int, mxa_agent_final*);
 MXA_INST(MXA_CFG_RMSC03)
 #ifndef MXA_ONLY_RMSC03

@@ -50,7 +50,8 @@ enum {
   // HeuristicBeliefLearningAgent
   ERR_HBL_WINDOW = 17,    // a streamed history epoch left the exchange's window / the device ring
   ERR_HBL_RANGE = 18,     // streamed price range beyond the device scratch (MXA_HBL_RANGE)
-  ERR_FLOAT_PRICE = 19    // a limit price that the reference would carry as a python float (not restated)
+  ERR_FLOAT_PRICE = 19,   // a limit price that the reference would carry as a python float (not restated)
+  ERR_BOOK_LOG_FULL = 20  // the book-update log of mxa_set_book_log ran out of records
 };
 
 // per-env scalar header (first bytes of the env block)
@@ -75,7 +76,8 @@ typedef struct {
   double rs_gauss[4];
   int32_t rs_m[4];
   int32_t rs_w0[4], rs_wn[4];    // run kernel: LDS output window of each stream (start, length)
-  int32_t oh_head, pad2;         // order-history ring: records written so far (HBL configs)
+  int32_t oh_head;               // order-history ring: records written so far (HBL configs)
+  int32_t blog_n;                // book-update log: records written (mxa_set_book_log)
   int32_t q_count, b_count;      // saved queue / book occupancy
   int64_t trace_len;
   int64_t ex_comp_delay;         // exchange's current computation delay
@@ -86,6 +88,16 @@ typedef struct {
 #ifdef __cplusplus
 static_assert(sizeof(EnvHdr) % 8 == 0 && sizeof(EnvHdr) <= 512, "EnvHdr: copied by 64 lanes x 8 B, 512 B of LDS");
 #endif
+
+// book-update log, the input of OrderBook.book_log and the exchange's BEST_BID / BEST_ASK /
+// LAST_TRADE events (OrderBook.py:112-168): one record per handled limit order (price, qty
+// positive for a buy, negative for a sell) and per cancellation (-price, the cancelled
+// quantity, positive on the bid side).  The host replays the level volumes.
+typedef struct {
+  int64_t t;       // Kernel.currentTime (ns since midnight)
+  int32_t price;
+  int32_t qty;
+} BlRec;
 
 // one event slot as saved between launches (and payload as pushed)
 typedef struct {

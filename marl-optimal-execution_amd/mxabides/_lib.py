@@ -23,7 +23,8 @@ ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: 
              16: "modify changing price or side",
              17: "HBL order stream outside the history window / device ring (MXA_OH_CAP)",
              18: "HBL streamed price range beyond the device histogram (MXA_HBL_RANGE)",
-             19: "limit price the reference would carry as a python float (not restated)"}
+             19: "limit price the reference would carry as a python float (not restated)",
+             20: "book-update log full (raise the book_log capacity)"}
 
 
 class EnvSummary(ctypes.Structure):
@@ -48,7 +49,7 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe",
            "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout", "mxa_create_replay", "mxa_step",
            "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash",
-           "mxa_build_id"]
+           "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log"]
 
 _lib = None
 
@@ -98,6 +99,9 @@ def load():
     L.mxa_step_device.argtypes = [P, P, P, P]
     L.mxa_finalize.argtypes = [P]
     L.mxa_read_final.argtypes = [P, I32, P, I32]
+    if hasattr(L, "mxa_set_book_log"):
+        L.mxa_set_book_log.argtypes = [P, I32]
+        L.mxa_read_book_log.argtypes = [P, I32, P, I64, ctypes.POINTER(I64)]
     if hasattr(L, "mxa_build_id"):  # (absent from libraries built before it existed: A/B runs)
         L.mxa_build_id.argtypes = []
         L.mxa_build_id.restype = ctypes.c_char_p

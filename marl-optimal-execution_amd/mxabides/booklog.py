@@ -1,0 +1,176 @@
+"""Order-book outputs of the reference's exchange, rebuilt from libmxa's book-update log.
+
+The device writes one 16-byte record per handled limit order and per cancellation
+(include/mxa.h mxa_book_rec).  This module replays the price-level volumes from them into what
+the reference produces at the end of OrderBook.handleLimitOrder (util/OrderBook.py:112-168):
+
+  * the OrderBook.book_log rows (one per handled limit order: every level, bids negative),
+    archived by ExchangeAgent.logOrderBookSnapshots (agent/ExchangeAgent.py:389-469) as
+    ORDERBOOK_<symbol>_FULL.bz2 with book_freq 0 (rmsc03's setting), narrow or wide_book;
+  * the exchange's BEST_BID / BEST_ASK / LAST_TRADE events (Agent.logEvent rows EventTime,
+    EventType, Event), the series cli/event_midpoint.py and cli/event_ticker.py read.
+
+Matching at level granularity is exact: executeOrder (OrderBook.py:172-240) fills an incoming
+order from the best opposite level while its price crosses, each level giving min(remaining,
+level volume) at the level's price, so the level volumes, the executed quantity and the
+LAST_TRADE average int(round(sum p*q / sum q)) follow from the records alone.
+
+Rows are kept in one flat int64 array, the format the CPU oracle writes too:
+    t, n, executed quantity, average trade price (0 without an execution),
+    then n (price, volume) pairs: bids best-first (negative volumes), then asks best-first.
+"""
+import bisect
+
+import numpy as np
+
+REC_DTYPE = np.dtype([("t", "<i8"), ("price", "<i4"), ("qty", "<i4")])
+SESSION_DATE = "2019-06-28"  # the plain configs' simulated date (abides.py -d / config defaults)
+# get_quote_range_iterator's excluded quotes (ExchangeAgent.py:399)
+FORBIDDEN_QUOTES = (0, 19999900)
+
+
+def rows_from_records(rec):
+    """Replay device records into flat book_log rows (format above)."""
+    rec = np.asarray(rec, dtype=REC_DTYPE)
+    vol = ({}, {})       # bids, asks: price -> resting volume
+    px = ([], [])        # their prices, ascending
+    out = []
+    for t, p, q in zip(rec["t"].tolist(), rec["price"].tolist(), rec["qty"].tolist()):
+        if p < 0:  # cancelOrder: the level loses the cancelled quantity
+            s = 0 if q > 0 else 1
+            p = -p
+            v = vol[s][p] - abs(q)
+            if v:
+                vol[s][p] = v
+            else:
+                del vol[s][p]
+                px[s].pop(bisect.bisect_left(px[s], p))
+            continue
+        own = 0 if q > 0 else 1  # the side the order rests on
+        opp = 1 - own
+        q = abs(q)
+        xq = tp = 0
+        ov, op = vol[opp], px[opp]
+        while q and op and (op[0] <= p if own == 0 else op[-1] >= p):
+            best = op[0] if own == 0 else op[-1]
+            v = ov[best]
+            c = v if q >= v else q
+            q -= c
+            xq += c
+            tp += best * c
+            if c == v:
+                del ov[best]
+                op.pop(0 if own == 0 else -1)
+            else:
+                ov[best] = v - c
+        if q:
+            if p in vol[own]:
+                vol[own][p] += q
+            else:
+                vol[own][p] = q
+                bisect.insort(px[own], p)
+        out += [t, len(px[0]) + len(px[1]), xq, int(round(tp / xq)) if xq else 0]
+        for b in reversed(px[0]):
+            out += [b, -vol[0][b]]
+        for a in px[1]:
+            out += [a, vol[1][a]]
+    return np.asarray(out, dtype=np.int64)
+
+
+def iter_rows(flat):
+    """(t, executed qty, average price, prices, volumes) per row."""
+    flat = np.asarray(flat, dtype=np.int64)
+    i, n = 0, len(flat)
+    while i < n:
+        t, m, xq, avg = (int(x) for x in flat[i:i + 4])
+        pv = flat[i + 4:i + 4 + 2 * m]
+        yield t, xq, avg, pv[0::2], pv[1::2]
+        i += 4 + 2 * m
+
+
+def strip_executions(flat):
+    """the rows without the executed-quantity / average-price words (t, n, pairs)"""
+    out = []
+    for t, _, _, p, v in iter_rows(flat):
+        out += [t, len(p)]
+        out += np.stack([p, v], axis=1).ravel().tolist()
+    return np.asarray(out, dtype=np.int64)
+
+
+def exchange_events(flat, symbol):
+    """The exchange log rows handleLimitOrder appends (OrderBook.py:114-141), in order:
+    (t, EventType, Event) with Event exactly the reference's strings."""
+    ev = []
+    for t, xq, avg, p, v in iter_rows(flat):
+        bid = np.flatnonzero(v < 0)
+        ask = np.flatnonzero(v > 0)
+        if len(bid):
+            ev.append((t, "BEST_BID", "%s,%d,%d" % (symbol, p[bid[0]], -v[bid[0]])))
+        if len(ask):
+            ev.append((t, "BEST_ASK", "%s,%d,%d" % (symbol, p[ask[0]], v[ask[0]])))
+        if xq:
+            ev.append((t, "LAST_TRADE", "{},${:0.4f}".format(xq, avg)))
+    return ev
+
+
+def exchange_events_frame(flat, symbol, date=SESSION_DATE):
+    """exchange_events as the exchange's log DataFrame (Agent.kernelTerminating,
+    Agent.py:92-95): index EventTime, columns EventType, Event."""
+    import pandas as pd
+    ev = exchange_events(flat, symbol)
+    base = pd.Timestamp(date)
+    df = pd.DataFrame({"EventTime": base + pd.to_timedelta([e[0] for e in ev], unit="ns"),
+                       "EventType": [e[1] for e in ev], "Event": [e[2] for e in ev]})
+    return df.set_index("EventTime")
+
+
+def book_log_frame(flat, date=SESSION_DATE):
+    """pd.DataFrame(book.book_log).set_index("QuoteTime") (ExchangeAgent.py:413-414): a column
+    per quote in first-appearance order; a row holds the quote's level volume, 0 once the quote
+    has been seen (OrderBook.quotes_seen) and NaN before; columns without a NaN stay int64."""
+    import pandas as pd
+    times, cols, first, cells = [], {}, [], []
+    for r, (t, _, _, p, v) in enumerate(iter_rows(flat)):
+        times.append(t)
+        for q, vol in zip(p.tolist(), v.tolist()):
+            j = cols.get(q)
+            if j is None:
+                j = cols[q] = len(first)
+                first.append(r)
+            cells.append((r, j, vol))
+    nr, nc = len(times), len(first)
+    m = np.where(np.arange(nr)[:, None] >= np.asarray(first, dtype=np.int64)[None, :], 0.0, np.nan)
+    if cells:
+        c = np.asarray(cells, dtype=np.int64)
+        m[c[:, 0], c[:, 1]] = c[:, 2]
+    index = pd.DatetimeIndex(pd.Timestamp(date) + pd.to_timedelta(np.asarray(times, dtype=np.int64), unit="ns"),
+                             name="QuoteTime")
+    data = {}
+    for q, j in cols.items():
+        col = m[:, j]
+        data[q] = col.astype(np.int64) if first[j] == 0 else col
+    return pd.DataFrame(data, index=index, columns=list(cols))
+
+
+def orderbook_full(flat, date=SESSION_DATE, wide_book=False):
+    """ExchangeAgent.logOrderBookSnapshots with book_freq 0 (ExchangeAgent.py:410-432, 457-464):
+    the last row per timestamp, sorted by time; narrow: a (time, quote) MultiIndex over every
+    time and every quote seen (except 0 and 19999900) with one column Volume; wide_book: the
+    quote columns sorted."""
+    import warnings
+
+    import pandas as pd
+    df = book_log_frame(flat, date)
+    df = df[~df.index.duplicated(keep="last")]
+    df = df.sort_index()
+    if wide_book:
+        return df.reindex(sorted(df.columns), axis=1)
+    quotes = sorted(q for q in df.columns.unique() if q not in FORBIDDEN_QUOTES)
+    filled = pd.MultiIndex.from_product([df.index, quotes], names=["time", "quote"])
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", FutureWarning)
+        s = df.stack()
+    s = s.reindex(filled)
+    out = pd.DataFrame(index=s.index)
+    out["Volume"] = s
+    return out

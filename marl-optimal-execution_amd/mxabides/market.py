@@ -16,7 +16,10 @@ CHUNK_DEFAULT = 1 << 20
 
 
 class VecMarket:
-    def __init__(self, config, seeds, device=0, trace_cap=0):
+    def __init__(self, config, seeds, device=0, trace_cap=0, book_log=0):
+        """book_log: records per env of the book-update log (0 off), the input of the exchange's
+        order-book outputs (orderbook_snapshots, exchange_events; include/mxa.h
+        mxa_set_book_log).  A limit order takes 2-4 records, a cancellation 1."""
         if config not in _lib.CONFIG_IDS:
             raise ValueError("unknown config %r (supported: %s)" % (config, sorted(_lib.CONFIG_IDS)))
         self.L = _lib.load()
@@ -30,6 +33,9 @@ class VecMarket:
                                ctypes.byref(self._h))
         self._check(rc, "mxa_create")
         self.n_agents = self.L.mxa_n_agents(self._h)
+        self.book_log_cap = int(book_log)
+        if book_log:
+            self._check(self.L.mxa_set_book_log(self._h, int(book_log)), "mxa_set_book_log")
 
     def _check(self, rc, what):
         if rc < 0:
@@ -44,6 +50,12 @@ class VecMarket:
         if mask is not None:
             m = np.ascontiguousarray(mask, dtype=np.uint8)
         self._check(self.L.mxa_reset(self._h, m.ctypes.data if m is not None else None), "mxa_reset")
+
+    def set_book_log(self, cap):
+        """(Re)size the book-update log to `cap` records per env (0 off); every env's log
+        restarts empty, so set it before the first launch of an episode."""
+        self._check(self.L.mxa_set_book_log(self._h, int(cap)), "mxa_set_book_log")
+        self.book_log_cap = int(cap)
 
     def set_seeds(self, seeds):
         self.seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
@@ -200,6 +212,42 @@ class VecMarket:
         os.makedirs(log_dir, exist_ok=True)
         path = os.path.join(log_dir, "summary_log.bz2")
         pd.DataFrame(self.summary_log(env)).to_pickle(path, compression="bz2")
+        return path
+
+    # ---- the exchange's order-book outputs (mxabides.booklog)
+    def book_log_records(self, env):
+        """env's raw book-update records (structured array t, price, qty; include/mxa.h)"""
+        if not self.book_log_cap:
+            raise ValueError("created with book_log=0")
+        from .booklog import REC_DTYPE
+        buf = np.zeros(self.book_log_cap, dtype=REC_DTYPE)
+        n = ctypes.c_int64()
+        self._check(self.L.mxa_read_book_log(self._h, env, buf.ctypes.data, self.book_log_cap, ctypes.byref(n)),
+                    "mxa_read_book_log")
+        return buf[:n.value]
+
+    def book_log_rows(self, env):
+        """OrderBook.book_log of env as flat rows (mxabides.booklog format: t, n, executed qty,
+        average price, n (price, volume) pairs)"""
+        from .booklog import rows_from_records
+        return rows_from_records(self.book_log_records(env))
+
+    def exchange_events(self, env):
+        """the exchange's BEST_BID / BEST_ASK / LAST_TRADE log rows (OrderBook.py:114-141) as a
+        DataFrame indexed by EventTime"""
+        from .booklog import exchange_events_frame
+        return exchange_events_frame(self.book_log_rows(env), symbol_of(self.config))
+
+    def orderbook_snapshots(self, env, wide_book=False):
+        """ExchangeAgent.logOrderBookSnapshots' DataFrame with book_freq 0 (ORDERBOOK_<sym>_FULL)"""
+        from .booklog import orderbook_full
+        return orderbook_full(self.book_log_rows(env), wide_book=wide_book)
+
+    def write_orderbook_log(self, env, log_dir, wide_book=False):
+        """log_dir/ORDERBOOK_<sym>_FULL.bz2 as Kernel.writeLog pickles it (Kernel.py:537-547)"""
+        os.makedirs(log_dir, exist_ok=True)
+        path = os.path.join(log_dir, "ORDERBOOK_%s_FULL.bz2" % symbol_of(self.config))
+        self.orderbook_snapshots(env, wide_book).to_pickle(path, compression="bz2")
         return path
 
     def close(self):

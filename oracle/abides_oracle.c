@@ -296,6 +296,12 @@ struct ora_env {
     uint64_t hash;
     int64_t* trace;
     int64_t trace_cap, trace_len;
+    /* OrderBook.book_log rows (ora_set_book_log): t, n levels, executed qty, average trade
+     * price, then n (price, volume) pairs, bids (negative volume) best-first, then asks */
+    int book_log;
+    int64_t *blg, nblg, capblg;
+    /* the device's record stream for the same run (mxa_book_rec: t, price, qty) */
+    int64_t *blr, nblr, capblr;
     int done, err;
     char errstr[160];
     int64_t order_counter;
@@ -697,9 +703,44 @@ static void enter_order(ora_env* e, bord_t o) {
     }
 }
 
+static void blr_push(ora_env* e, int64_t t, int64_t price, int64_t qty) {
+    if (e->nblr + 3 > e->capblr) {
+        e->capblr = e->capblr ? 2 * e->capblr : 4096;
+        e->blr = (int64_t*)realloc(e->blr, sizeof(int64_t) * e->capblr);
+    }
+    e->blr[e->nblr++] = t;
+    e->blr[e->nblr++] = price;
+    e->blr[e->nblr++] = qty;
+}
+static void blg_push(ora_env* e, int64_t w) {
+    if (e->nblg == e->capblg) {
+        e->capblg = e->capblg ? 2 * e->capblg : 4096;
+        e->blg = (int64_t*)realloc(e->blg, sizeof(int64_t) * e->capblg);
+    }
+    e->blg[e->nblg++] = w;
+}
+/* the tail of handleLimitOrder (OrderBook.py:112-168): BEST_BID / BEST_ASK / LAST_TRADE come
+ * from the first levels and the executed list; the book_log row holds every level
+ * (getInsideBids/getInsideAsks with the default depth), bids as negative volumes */
+static void book_log_row(ora_env* e, int64_t ex_q, int64_t avg) {
+    blg_push(e, e->cur);
+    blg_push(e, e->book[0].n + e->book[1].n);
+    blg_push(e, ex_q);
+    blg_push(e, avg);
+    for (int s = 0; s < 2; s++)
+        for (int i = 0; i < e->book[s].n; i++) {
+            const level_t* L = &e->book[s].lv[i];
+            int64_t v = 0;
+            for (int j = 0; j < L->n; j++) v += L->o[j].qty;
+            blg_push(e, L->o[0].price);
+            blg_push(e, s == 0 ? -v : v);
+        }
+}
+
 /* handleLimitOrder (OrderBook.py:38-170) */
 static void handle_limit_order(ora_env* e, bord_t order) {
     if (order.qty <= 0) return;
+    if (e->book_log) blr_push(e, e->cur, order.price, order.is_buy ? order.qty : -order.qty);
     hist_add_order(e, order.id, order.price, order.is_buy);
     int64_t ex_q = 0, ex_pq = 0;
     int executed = 0;
@@ -734,6 +775,7 @@ static void handle_limit_order(ora_env* e, bord_t order) {
         e->ex_has_last = 1;
         hist_shift(e);
     }
+    if (e->book_log) book_log_row(e, ex_q, executed ? e->last_trade : 0);
 }
 
 /* cancelOrder (OrderBook.py:284-339) */
@@ -745,6 +787,7 @@ static void cancel_order(ora_env* e, const msg_t* req) {
         for (int j = 0; j < L->n; j++) {
             if (L->o[j].id == req->oid) {
                 bord_t c = L->o[j];
+                if (e->book_log) blr_push(e, e->cur, -c.price, req->is_buy ? c.qty : -c.qty);
                 e->st_resting--;
                 level_remove(L, j);
                 if (L->n == 0) side_delete_level(book, i);
@@ -2474,6 +2517,8 @@ void ora_destroy(ora_env* e) {
         free(e->book[s].lv);
     }
     for (int i = 0; i < e->nhist; i++) epoch_free(&e->hist[i]);
+    free(e->blg);
+    free(e->blr);
     free(e->lat);
     free(e->agent_time);
     free(e->comp_delay);
@@ -2617,4 +2662,18 @@ int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads,
     free(th);
     pthread_mutex_destroy(&b.mu);
     return b.rc;
+}
+
+void ora_set_book_log(ora_env* e, int on) {
+    e->book_log = on;
+    e->nblg = 0;
+    e->nblr = 0;
+}
+int64_t ora_book_records(const ora_env* e, int64_t* buf, int64_t cap) {
+    if (buf) memcpy(buf, e->blr, sizeof(int64_t) * (size_t)(cap < e->nblr ? cap : e->nblr));
+    return e->nblr / 3;
+}
+int64_t ora_book_log(const ora_env* e, int64_t* buf, int64_t cap) {
+    if (buf) memcpy(buf, e->blg, sizeof(int64_t) * (size_t)(cap < e->nblg ? cap : e->nblg));
+    return e->nblg;
 }

@@ -54,6 +54,13 @@ int64_t ora_current_time(const ora_env* e);
 /* optional trace capture: records of 10 int64 (see DESIGN.md "trace record") */
 void ora_set_trace(ora_env* e, int64_t* buf, int64_t cap_records);
 int64_t ora_trace_len(const ora_env* e);
+/* OrderBook.book_log (OrderBook.py:151-168) as flat rows: t, n, executed qty, average trade price
+ * (0 without an execution), n x (price, volume; bids negative).  Returns the word count. */
+void ora_set_book_log(ora_env* e, int on);
+int64_t ora_book_log(const ora_env* e, int64_t* buf, int64_t cap);
+/* the same run as device book-update records (include/mxa.h mxa_book_rec) as int64 triples
+ * (t, price, qty); returns the record count */
+int64_t ora_book_records(const ora_env* e, int64_t* buf, int64_t cap);
 int ora_n_agents(const ora_env* e);
 /* per agent: cash, shares, number of open orders */
 int ora_agent_state(const ora_env* e, int id, int64_t* cash, int64_t* shares, int64_t* n_open);

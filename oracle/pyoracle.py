@@ -118,6 +118,33 @@ class OracleEnv:
         n = lib().ora_trace_len(self._h)
         return self.trace_buf[:n]
 
+    def set_book_log(self, on=True):
+        """keep OrderBook.book_log rows (ora_set_book_log); call before run()"""
+        L = lib()
+        L.ora_set_book_log.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.ora_set_book_log(self._h, 1 if on else 0)
+
+    def book_log(self):
+        """the rows as flat int64 (mxabides.booklog format: t, n, executed qty, average price,
+        n (price, volume) pairs, bids best-first then asks best-first)"""
+        L = lib()
+        L.ora_book_log.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        L.ora_book_log.restype = ctypes.c_int64
+        n = L.ora_book_log(self._h, None, 0)
+        buf = np.zeros(n, dtype=np.int64)
+        L.ora_book_log(self._h, buf.ctypes.data, n)
+        return buf
+
+    def book_records(self):
+        """the run as device book-update records: (t, price, qty) int64 rows"""
+        L = lib()
+        L.ora_book_records.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        L.ora_book_records.restype = ctypes.c_int64
+        n = L.ora_book_records(self._h, None, 0)
+        buf = np.zeros((n, 3), dtype=np.int64)
+        L.ora_book_records(self._h, buf.ctypes.data, 3 * n)
+        return buf
+
     def agents(self):
         L = lib()
         out = []

@@ -24,7 +24,8 @@ bz2 log writers are no-ops.  None of them touches the simulated arithmetic.
 
 Usage:  python tests/golden/gen_fixtures.py all          (writes tests/golden/*.npz/json)
         python tests/golden/gen_fixtures.py summaries    (only the *_summary.json summary logs)
-        python tests/golden/gen_fixtures.py run CFG SEED OUT [--full]
+        python tests/golden/gen_fixtures.py booklog      (*_booklog.npz: book snapshot outputs)
+        python tests/golden/gen_fixtures.py run CFG SEED OUT [--full] [--booklog]
 """
 import importlib
 import io
@@ -171,6 +172,24 @@ def encode(t_rel, recipient, mtype, msg):
 
 MIDNIGHT = 0
 TRACE = []
+BOOK_LOG = False  # book_freq 0 with a compact OrderBook.book_log (booklog fixtures only)
+BOOKLOG_FULL_ROWS = 300  # rows kept verbatim to run the reference's logOrderBookSnapshots on
+
+
+class CompactBookLog(list):
+    """OrderBook.book_log whose rows drop the quotes_seen zeros (a row holds every quote seen so
+    far, which for a whole session is gigabytes); the first BOOKLOG_FULL_ROWS rows are also kept
+    verbatim.  Row (t, [(price, volume) of the levels, bids negative])."""
+
+    def __init__(self):
+        super().__init__()
+        self.full = []
+
+    def append(self, row):
+        if len(self.full) < BOOKLOG_FULL_ROWS:
+            self.full.append(dict(row))
+        t = int(row["QuoteTime"].value)
+        super().append((t, [(int(q), int(v)) for q, v in row.items() if q != "QuoteTime" and v != 0]))
 SUMMARY_ONLY = False
 
 
@@ -211,7 +230,23 @@ def run_config(cfg, seed, out, full):
     K.Kernel.writeLog = lambda *a, **k: None
     K.Kernel.writeSummaryLog = lambda *a, **k: None
     from agent.ExchangeAgent import ExchangeAgent
+    orig_snapshots = ExchangeAgent.logOrderBookSnapshots
     ExchangeAgent.logOrderBookSnapshots = lambda *a, **k: None
+    # the book snapshot log (OrderBook.book_log, appended after every limit order whenever
+    # book_freq is not None) only feeds logOrderBookSnapshots at termination; rmsc01's
+    # book_freq="M" would hold every snapshot row of a 6.5 h session in memory (the config's own
+    # comment: "should be 0 but MemoryError").  It never touches the simulated arithmetic.
+    _ex_init = ExchangeAgent.__init__
+
+    def ex_init(self, *a, **k):
+        _ex_init(self, *a, **k)
+        if not BOOK_LOG:
+            self.book_freq = None
+        else:  # the full-depth snapshot log (rmsc03's own setting; -b 0 for the others)
+            self.book_freq = 0
+            for ob in self.order_books.values():
+                ob.book_log = CompactBookLog()
+    ExchangeAgent.__init__ = ex_init
     from agent.TradingAgent import TradingAgent
     TradingAgent.getTransactedVolume = TradingAgent.get_transacted_volume  # SURVEY.md key finding 3
 
@@ -288,6 +323,9 @@ def run_config(cfg, seed, out, full):
                for r in kern.summaryLog]
     with open(out + "_summary.json", "w") as f:
         json.dump(summary, f, indent=0)
+    if BOOK_LOG:
+        save_booklog(ex, ob, sym, orig_snapshots, out)
+        return
     if SUMMARY_ONLY:
         return
     with open(out + ".json", "w") as f:
@@ -297,6 +335,52 @@ def run_config(cfg, seed, out, full):
 
 
 CAPTURE = {}
+
+
+def save_booklog(ex, ob, sym, orig_snapshots, out):
+    """<out>_booklog.npz: every book_log row (flat int64: t - midnight, n, then n (price, volume)
+    pairs, bids best-first then asks best-first), the exchange's BEST_BID / BEST_ASK / LAST_TRADE
+    events (ExchangeAgent log: time, type 0/1/2, then the Event string), and
+    logOrderBookSnapshots' DataFrames (book_freq 0; wide_book False and True) over the first
+    BOOKLOG_FULL_ROWS rows, as the reference writes them."""
+    import pandas as pd
+    flat = []
+    for t, lv in ob.book_log:
+        bids = sorted((p, v) for p, v in lv if v < 0)[::-1]
+        asks = sorted((p, v) for p, v in lv if v > 0)
+        flat += [t - MIDNIGHT, len(bids) + len(asks)]
+        for p, v in bids + asks:
+            flat += [p, v]
+    types_ = {"BEST_BID": 0, "BEST_ASK": 1, "LAST_TRADE": 2}
+    ev = [(int(r["EventTime"].value) - MIDNIGHT, types_[r["EventType"]], r["Event"]) for r in ex.log
+          if r["EventType"] in types_]
+    frames = {}
+    full_rows = ob.book_log.full
+    for wide in (False, True):
+        got = {}
+        ob.book_log = list(full_rows)
+        ex.wide_book = wide
+        ex.writeLog = lambda df, filename=None: got.update(df=df, filename=filename)
+        orig_snapshots(ex, sym)
+        df = got["df"]
+        frames[wide] = df
+    narrow, wide = frames[False], frames[True]
+    np.savez_compressed(
+        out + "_booklog.npz",
+        rows=np.asarray(flat, dtype=np.int64),
+        ev_t=np.asarray([e[0] for e in ev], dtype=np.int64),
+        ev_type=np.asarray([e[1] for e in ev], dtype=np.int8),
+        ev_text=np.asarray([e[2] for e in ev]),
+        full_time=narrow.index.get_level_values(0).asi8 - MIDNIGHT,
+        full_quote=np.asarray(narrow.index.get_level_values(1), dtype=np.int64),
+        full_volume=narrow["Volume"].to_numpy(dtype=np.float64),
+        full_dtype=np.asarray(str(narrow["Volume"].dtype)),
+        full_filename=np.asarray(got["filename"]),
+        wide_time=wide.index.asi8 - MIDNIGHT,
+        wide_cols=np.asarray(wide.columns, dtype=np.int64),
+        wide_values=wide.to_numpy(dtype=np.float64),
+        wide_dtypes=np.asarray([str(d) for d in wide.dtypes]),
+        full_rows=np.asarray(BOOKLOG_FULL_ROWS))
 
 
 def rng_kats(path):
@@ -335,9 +419,22 @@ def rng_kats(path):
 
 def main():
     global SUMMARY_ONLY
+    global BOOK_LOG
     if sys.argv[1] == "run":
         SUMMARY_ONLY = "--summary-only" in sys.argv
+        BOOK_LOG = "--booklog" in sys.argv
         run_config(sys.argv[2], int(sys.argv[3]), sys.argv[4], "--full" in sys.argv)
+        return
+    if sys.argv[1] == "booklog":  # <cfg>_<seed>_booklog.npz: order-book snapshot outputs
+        jobs = [("rmsc03", 123456789), ("value_noise", 7)]
+        procs = []
+        for cfg, seed in jobs:
+            out = os.path.join(HERE, "%s_%d" % (cfg, seed))
+            cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out, "--booklog"]
+            procs.append(subprocess.Popen(cmd, cwd=tempfile.mkdtemp(prefix="gf_"),
+                                          env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1")))
+        for (cfg, seed), p in zip(jobs, procs):
+            print(cfg, seed, "rc", p.wait())
         return
     if sys.argv[1] == "summaries":  # only the summary logs (<cfg>_<seed>_summary.json)
         sys.argv[1] = "all"

@@ -1,0 +1,93 @@
+"""GPU parity of the book-update log (include/mxa.h mxa_set_book_log): the device's records,
+replayed on the host (mxabides.booklog), give exactly the oracle's OrderBook.book_log rows and
+the reference's own rows (tests/golden/*_booklog.npz); logging leaves the simulation itself
+(pop count, parity hash) unchanged although it turns the exchange's event runs off."""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from mxabides import booklog as bl
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CAP = 1 << 18
+
+
+@pytest.fixture(scope="module")
+def mx():
+    import mxabides
+    mxabides.load()
+    return mxabides
+
+
+def oracle(cfg, seed):
+    o = pyoracle.OracleEnv(cfg, seed)
+    o.set_book_log()
+    o.run()
+    return o
+
+
+@pytest.mark.parametrize("cfg,seeds", [("rmsc03", [123456789, 7, 1008]), ("value_noise", [7, 123456789]),
+                                       ("sparse_zi_100", [123456789]), ("rmsc01", [7])])
+def test_gpu_book_log_equals_oracle(mx, cfg, seeds):
+    m = mx.VecMarket(cfg, seeds, book_log=CAP * (16 if cfg == "rmsc01" else 1))
+    m.run()
+    s = m.summary()
+    for i, sd in enumerate(seeds):
+        o = oracle(cfg, sd)
+        assert s["status"][i] == 1, (s["status"][i], s["err"][i])
+        assert s["events"][i] == o.events and s["hash"][i] == o.hash
+        rows = m.book_log_rows(i)
+        ref = o.book_log()
+        assert len(rows) == len(ref)
+        assert np.array_equal(rows, ref)
+
+
+@pytest.mark.parametrize("cfg,seed", [("rmsc03", 123456789), ("value_noise", 7)])
+def test_gpu_book_log_equals_reference_fixture(mx, cfg, seed, tmp_path):
+    z = np.load(os.path.join(GOLDEN, "%s_%d_booklog.npz" % (cfg, seed)))
+    m = mx.VecMarket(cfg, [seed], book_log=CAP)
+    m.run()
+    rows = m.book_log_rows(0)
+    assert np.array_equal(bl.strip_executions(rows), z["rows"])
+    ev = m.exchange_events(0)
+    assert len(ev) == len(z["ev_t"]) and ev["Event"].tolist() == z["ev_text"].tolist()
+    import pandas as pd
+    path = m.write_orderbook_log(0, str(tmp_path))
+    assert os.path.basename(path) == "ORDERBOOK_%s_FULL.bz2" % ("ABM" if cfg == "rmsc03" else "JPM")
+    back = pd.read_pickle(path, compression="bz2")
+    assert list(back.columns) == ["Volume"] and back.index.names == ["time", "quote"]
+    times = {t for t, _, _, _, _ in bl.iter_rows(rows)}
+    assert back.index.get_level_values(0).nunique() == len(times)
+
+
+def test_gpu_book_log_chunked_launches(mx):
+    """records and their count survive launch boundaries"""
+    m = mx.VecMarket("rmsc03", [123456789, 7], book_log=CAP)
+    m.run(chunk=3001)
+    for i, sd in enumerate([123456789, 7]):
+        assert np.array_equal(m.book_log_rows(i), oracle("rmsc03", sd).book_log())
+
+
+def test_gpu_book_log_overflow_is_an_env_error(mx):
+    m = mx.VecMarket("rmsc03", [123456789, 7], book_log=1000)
+    m.run()
+    s = m.summary()
+    assert (s["status"] == 2).all() and (s["err"] == 20).all()
+    assert len(m.book_log_records(0)) == 1000
+
+
+def test_gpu_book_log_off_after_reset(mx):
+    """set_book_log(0) frees the log; the next episode runs with the event runs again"""
+    m = mx.VecMarket("value_noise", [7], book_log=CAP)
+    m.run()
+    m.set_book_log(0)
+    m.reset()
+    m.run()
+    o = oracle("value_noise", 7)
+    s = m.summary()
+    assert s["events"][0] == o.events and s["hash"][0] == o.hash
+    with pytest.raises(ValueError):
+        m.book_log_records(0)
