@@ -157,16 +157,21 @@ const char* mxa_build_id(void);
  * host replays the price-level volumes (mxabides.booklog): matching at level granularity is
  * exact, as a level gives min(remaining quantity, its volume) at its price. */
 typedef struct {
-  int64_t t;      /* Kernel.currentTime, ns since midnight */
-  int32_t price;  /* cents (limit orders), -cents (cancellations) */
+  int64_t t;      /* Kernel.currentTime, ns since midnight (FundamentalTime for f_log records) */
+  int32_t price;  /* cents (limit orders), -cents (cancellations), MXA_BL_FUNDAMENTAL */
   int32_t qty;
 } mxa_book_rec;
+/* the stream also carries SparseMeanRevertingOracle.f_log (SMRO:122): one record per computed
+ * fundamental value (price MXA_BL_FUNDAMENTAL, qty the value), including the oracle
+ * observations of the last mxa_finalize, the series written as fundamental_<sym>.bz2 */
+#define MXA_BL_FUNDAMENTAL (-2147483647 - 1)
 /* plain Kernel.runner configs: `cap` records per env (0 = off); resets every env's record
  * count, so enable it after mxa_create / mxa_reset and before the first launch.  An env that
  * fills its log stops with error ERR_BOOK_LOG_FULL (20).  The exchange's event runs (batched
  * LIMIT/CANCEL handling) are off while logging. */
 int mxa_set_book_log(mxa_handle* h, int32_t cap);
-/* env's records: min(total, cap) are written to out, the total to *n */
+/* env's records: min(total, cap, log capacity) are written to out, the total to *n (above the
+ * log capacity: the log overflowed) */
 int mxa_read_book_log(mxa_handle* h, int32_t env, mxa_book_rec* out, int64_t cap, int64_t* n);
 
 /* parity probes: device numpy-legacy RNG (mode 0 u32, 1 double, 2 randint(a,b),

@@ -19,7 +19,7 @@ namespace {
 typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*,
                          const RpCtx*);
 typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, BlRec*, int);
-typedef void (*stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, mxa_agent_final*);
+typedef void (*stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, mxa_agent_final*, BlRec*, int);
 typedef void (*step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, const double*,
                         double*, int32_t*);
 
@@ -35,8 +35,9 @@ void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t 
 }
 
 template <int CFG>
-void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, mxa_agent_final* out) {
-  hipLaunchKernelGGL((mxa_stop_kernel<CFG>), g, b, lds, s, base, stride, n, out);
+void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, mxa_agent_final* out,
+                 BlRec* blog, int blog_cap) {
+  hipLaunchKernelGGL((mxa_stop_kernel<CFG>), g, b, lds, s, base, stride, n, out, blog, blog_cap);
 }
 
 #ifndef MXA_ONLY_RMSC03
@@ -443,6 +444,8 @@ int mxa_set_book_log(mxa_handle* h, int32_t cap) {
   }
   HIPCHK(h, hipMemset2DAsync(h->d_env + offsetof(EnvHdr, blog_n), h->P.L.env_stride, 0, sizeof(int32_t), h->P.n_envs,
                              h->stream));
+  HIPCHK(h, hipMemset2DAsync(h->d_env + offsetof(EnvHdr, blog_fin), h->P.L.env_stride, 0, sizeof(int32_t),
+                             h->P.n_envs, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;
 }
@@ -451,12 +454,15 @@ int mxa_read_book_log(mxa_handle* h, int32_t env, mxa_book_rec* out, int64_t cap
   if (!h || env < 0 || env >= h->P.n_envs || !n || cap < 0 || (cap > 0 && !out)) return MXA_EINVAL;
   static_assert(sizeof(mxa_book_rec) == sizeof(BlRec) && offsetof(mxa_book_rec, qty) == offsetof(BlRec, qty),
                 "mxa_book_rec mirrors BlRec");
-  int32_t cnt = 0;
-  HIPCHK(h, hipMemcpyAsync(&cnt, h->d_env + (size_t)env * h->P.L.env_stride + offsetof(EnvHdr, blog_n), sizeof(cnt),
-                           hipMemcpyDeviceToHost, h->stream));
+  static_assert((int)MXA_BL_FUNDAMENTAL == (int)BL_FUNDAMENTAL, "f_log record tag");
+  EnvHdr hd;
+  HIPCHK(h, hipMemcpyAsync(&hd, h->d_env + (size_t)env * h->P.L.env_stride, sizeof(hd), hipMemcpyDeviceToHost,
+                           h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  if (!h->d_blog) cnt = 0;
-  *n = cnt;
+  // after a kernelStopping pass: its oracle observations follow the run's records
+  int64_t cnt = h->d_blog ? (hd.blog_fin > hd.blog_n ? hd.blog_fin : hd.blog_n) : 0;
+  *n = cnt;  // beyond the capacity: the log overflowed (the first `blog_cap` records are kept)
+  if (cnt > h->blog_cap) cnt = h->blog_cap;
   const int64_t m = cnt < cap ? cnt : cap;
   if (m > 0)
     HIPCHK(h, hipMemcpyAsync(out, h->d_blog + (size_t)env * h->blog_cap, sizeof(BlRec) * m, hipMemcpyDeviceToHost,
@@ -470,7 +476,8 @@ int mxa_finalize(mxa_handle* h) {
   HIPCHK(h, hipSetDevice(h->device));
   const size_t rows = (size_t)h->P.n_envs * h->P.n_agents;
   if (!h->d_final) HIPCHK(h, hipMalloc(&h->d_final, rows * sizeof(mxa_agent_final)));
-  h->stop(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_final);
+  h->stop(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_final,
+          h->d_blog, h->blog_cap);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;

@@ -1130,6 +1130,7 @@ struct Eng {
     i64 vi = py_round(v);
     h.o_pt = ts;
     h.o_pv = (double)vi;
+    if (blog) bl_put(ts, BL_FUNDAMENTAL, (i32)vi);  // f_log (SMRO:122)
     return (double)vi;
   }
   DEV double o_advance(i64 t) {
@@ -1397,24 +1398,23 @@ struct Eng {
   // ---------------- book-update log (OrderBook.book_log rows, ExchangeAgent BEST_BID/ASK/LAST_TRADE)
   // one record per handled limit order and per cancellation; the host replays the level
   // volumes (matching at level granularity is exact: a level gives min(remaining, volume))
-  DEV void bl_put(i32 price, i32 qty) {
+  // (past the capacity the count still advances, so the kernelStopping pass, which cannot
+  // fail an env, leaves an overflow the host sees)
+  DEV void bl_put(i64 t, i32 price, i32 qty) {
     const i32 n = h.blog_n;
-    if (n >= blog_cap) {
-      fail(ERR_BOOK_LOG_FULL);
-      return;
-    }
-    if (lane == 0) {
+    if (n < blog_cap && lane == 0) {
       BlRec r;
-      r.t = cur;
+      r.t = t;
       r.price = price;
       r.qty = qty;
       blog[n] = r;
     }
     h.blog_n = n + 1;
+    if (n >= blog_cap) fail(ERR_BOOK_LOG_FULL);
   }
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
     if (qty <= 0) return;
-    if (blog) bl_put(price, is_buy ? qty : -qty);
+    if (blog) bl_put(cur, price, is_buy ? qty : -qty);
     i32 hep = h.epoch;
     LDSP i32* EP = ep_entries();
     i32 ne = EP[h.epoch & 15] + 1;
@@ -1477,7 +1477,7 @@ struct Eng {
     if (s < 0) return;
     i32 q = b_get(bq, s), o = b_get(bo, s), mm = b_get(bm, s), p = b_get(bp, s);
     b_free(s);
-    if (blog) bl_put(-p, buy ? q : -q);
+    if (blog) bl_put(cur, -p, buy ? q : -q);
     Msg r = msg_order(MK_CANCELLED, o, mm >> 1, mm & 1, q, p, 0);
     ex_notify(m_agent(m), r);
   }
@@ -4071,13 +4071,18 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
 }
 
 template <int CFG>
-__global__ __launch_bounds__(64) void mxa_stop_kernel(char* base, uint64_t stride, int n_envs, mxa_agent_final* out) {
+__global__ __launch_bounds__(64) void mxa_stop_kernel(char* base, uint64_t stride, int n_envs, mxa_agent_final* out,
+                                                      BlRec* blog, int blog_cap) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int env = blockIdx.x;
   if (env >= n_envs) return;
-  mxa::Eng<CFG> g(base + (size_t)env * stride, lds, 0, nullptr);
+  char* e = base + (size_t)env * stride;
+  mxa::Eng<CFG> g(e, lds, 0, nullptr, blog ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
   g.load();
   g.stop(out + (size_t)env * mxa::Eng<CFG>::PC.n_agents);  // no save(): the pass is idempotent
+  // the oracle observations of the pass append to the log after the run's records; only
+  // their end is kept (a second pass rewrites the same records)
+  if (blog && g.lane == 0) ((EnvHdr*)e)->blog_fin = g.h.blog_n;
 }
 
 #ifndef MXA_ONLY_RMSC03
@@ -4154,7 +4159,7 @@ __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y
 #define MXA_INST(CFG)                                                                                      \
   template __global__ void mxa_build_kernel<CFG>(char*, uint64_t, int, const uint32_t*, const uint8_t*, const RpCtx*); \
   template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*, BlRec*, int);  \
-  template __global__ void mxa_stop_kernel<CFG>(char*, uint64_t, int, mxa_agent_final*);
+  template __global__ void mxa_stop_kernel<CFG>(char*, uint64_t, int, mxa_agent_final*, BlRec*, int);
 MXA_INST(MXA_CFG_RMSC03)
 #ifndef MXA_ONLY_RMSC03
 MXA_INST(MXA_CFG_SPARSE_ZI_100)

@@ -83,6 +83,7 @@ typedef struct {
   int64_t ex_comp_delay;         // exchange's current computation delay
   int32_t max_q, max_book;       // capacity high-water marks (diagnostics)
   double o_th2;                  // oracle fund_vol ** 2 (glibc pow, evaluated at build)
+  int32_t blog_fin, pad3;        // book-update log: records after the last kernelStopping pass
 } EnvHdr;
 
 #ifdef __cplusplus
@@ -92,12 +93,15 @@ static_assert(sizeof(EnvHdr) % 8 == 0 && sizeof(EnvHdr) <= 512, "EnvHdr: copied 
 // book-update log, the input of OrderBook.book_log and the exchange's BEST_BID / BEST_ASK /
 // LAST_TRADE events (OrderBook.py:112-168): one record per handled limit order (price, qty
 // positive for a buy, negative for a sell) and per cancellation (-price, the cancelled
-// quantity, positive on the bid side).  The host replays the level volumes.
+// quantity, positive on the bid side).  The host replays the level volumes.  The same stream
+// carries SparseMeanRevertingOracle.f_log (SMRO:122): price BL_FUNDAMENTAL, qty = the value,
+// t = FundamentalTime.
 typedef struct {
   int64_t t;       // Kernel.currentTime (ns since midnight)
   int32_t price;
   int32_t qty;
 } BlRec;
+enum { BL_FUNDAMENTAL = -2147483647 - 1 };
 
 // one event slot as saved between launches (and payload as pushed)
 typedef struct {

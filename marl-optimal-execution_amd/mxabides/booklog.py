@@ -15,6 +15,10 @@ order from the best opposite level while its price crosses, each level giving mi
 level volume) at the level's price, so the level volumes, the executed quantity and the
 LAST_TRADE average int(round(sum p*q / sum q)) follow from the records alone.
 
+The same stream carries SparseMeanRevertingOracle.f_log (util/oracle/SparseMeanRevertingOracle.py:
+63, 122): one record per fundamental value computed (price BL_FUNDAMENTAL, qty the value), the
+series ExchangeAgent.kernelTerminating writes as fundamental_<symbol>.bz2 (ExchangeAgent.py:111-117).
+
 Rows are kept in one flat int64 array, the format the CPU oracle writes too:
     t, n, executed quantity, average trade price (0 without an execution),
     then n (price, volume) pairs: bids best-first (negative volumes), then asks best-first.
@@ -24,6 +28,9 @@ import bisect
 import numpy as np
 
 REC_DTYPE = np.dtype([("t", "<i8"), ("price", "<i4"), ("qty", "<i4")])
+BL_FUNDAMENTAL = -(1 << 31)
+R_BAR = 100000.0           # SparseMeanRevertingOracle r_bar of every plain config (a float)
+MKT_OPEN_NS = (9 * 60 + 30) * 60 * 10**9
 SESSION_DATE = "2019-06-28"  # the plain configs' simulated date (abides.py -d / config defaults)
 # get_quote_range_iterator's excluded quotes (ExchangeAgent.py:399)
 FORBIDDEN_QUOTES = (0, 19999900)
@@ -32,6 +39,7 @@ FORBIDDEN_QUOTES = (0, 19999900)
 def rows_from_records(rec):
     """Replay device records into flat book_log rows (format above)."""
     rec = np.asarray(rec, dtype=REC_DTYPE)
+    rec = rec[rec["price"] != BL_FUNDAMENTAL]
     vol = ({}, {})       # bids, asks: price -> resting volume
     px = ([], [])        # their prices, ascending
     out = []
@@ -174,3 +182,22 @@ def orderbook_full(flat, date=SESSION_DATE, wide_book=False):
     out = pd.DataFrame(index=s.index)
     out["Volume"] = s
     return out
+
+
+def fundamental_log(rec, mkt_open=MKT_OPEN_NS, r_bar=R_BAR):
+    """SparseMeanRevertingOracle.f_log[symbol]: the opening entry (mkt_open, r_bar) and one
+    (FundamentalTime, FundamentalValue) per computed value, as (times ns, values) arrays"""
+    rec = np.asarray(rec, dtype=REC_DTYPE)
+    f = rec[rec["price"] == BL_FUNDAMENTAL]
+    t = np.concatenate([[mkt_open], f["t"]]).astype(np.int64)
+    v = np.concatenate([[r_bar], f["qty"].astype(np.float64)])
+    return t, v
+
+
+def fundamental_frame(rec, date=SESSION_DATE, mkt_open=MKT_OPEN_NS, r_bar=R_BAR):
+    """pd.DataFrame(f_log[symbol]).set_index("FundamentalTime") as ExchangeAgent.kernelTerminating
+    writes it (ExchangeAgent.py:111-117): FundamentalValue float64 (the opening r_bar is a float)"""
+    import pandas as pd
+    t, v = fundamental_log(rec, mkt_open, r_bar)
+    idx = pd.DatetimeIndex(pd.Timestamp(date) + pd.to_timedelta(t, unit="ns"), name="FundamentalTime")
+    return pd.DataFrame({"FundamentalValue": v}, index=idx)

@@ -215,8 +215,9 @@ class VecMarket:
         return path
 
     # ---- the exchange's order-book outputs (mxabides.booklog)
-    def book_log_records(self, env):
-        """env's raw book-update records (structured array t, price, qty; include/mxa.h)"""
+    def book_log_records(self, env, partial=False):
+        """env's raw book-update records (structured array t, price, qty; include/mxa.h); an
+        overflowed log raises unless partial (then its first book_log records)"""
         if not self.book_log_cap:
             raise ValueError("created with book_log=0")
         from .booklog import REC_DTYPE
@@ -224,7 +225,10 @@ class VecMarket:
         n = ctypes.c_int64()
         self._check(self.L.mxa_read_book_log(self._h, env, buf.ctypes.data, self.book_log_cap, ctypes.byref(n)),
                     "mxa_read_book_log")
-        return buf[:n.value]
+        if n.value > self.book_log_cap and not partial:
+            raise _lib.MxaError("env %d: book-update log overflow (%d records > book_log=%d)"
+                                % (env, n.value, self.book_log_cap))
+        return buf[:min(n.value, self.book_log_cap)]
 
     def book_log_rows(self, env):
         """OrderBook.book_log of env as flat rows (mxabides.booklog format: t, n, executed qty,
@@ -242,6 +246,27 @@ class VecMarket:
         """ExchangeAgent.logOrderBookSnapshots' DataFrame with book_freq 0 (ORDERBOOK_<sym>_FULL)"""
         from .booklog import orderbook_full
         return orderbook_full(self.book_log_rows(env), wide_book=wide_book)
+
+    def fundamental_log(self, env):
+        """SparseMeanRevertingOracle.f_log of env as the DataFrame fundamental_<sym>.bz2 holds,
+        after Kernel.runner's kernelStopping pass (whose oracle observations it includes)"""
+        from .booklog import fundamental_frame
+        if not getattr(self, "_finalized", False):
+            self.finalize()
+        return fundamental_frame(self.book_log_records(env))
+
+    def write_logs(self, env, log_dir, wide_book=False):
+        """env's run directory as the reference writes it at termination (Kernel.writeLog /
+        writeSummaryLog, Kernel.py:520-565): summary_log.bz2, fundamental_<sym>.bz2 and
+        ORDERBOOK_<sym>_FULL.bz2 (book_freq 0), each a bz2-pickled DataFrame.  Returns the paths."""
+        sym = symbol_of(self.config)
+        os.makedirs(log_dir, exist_ok=True)
+        paths = [self.write_summary_log(env, log_dir)]
+        p = os.path.join(log_dir, "fundamental_%s.bz2" % sym)
+        self.fundamental_log(env).to_pickle(p, compression="bz2")
+        paths.append(p)
+        paths.append(self.write_orderbook_log(env, log_dir, wide_book))
+        return paths
 
     def write_orderbook_log(self, env, log_dir, wide_book=False):
         """log_dir/ORDERBOOK_<sym>_FULL.bz2 as Kernel.writeLog pickles it (Kernel.py:537-547)"""

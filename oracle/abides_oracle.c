@@ -449,7 +449,9 @@ static void k_wakeup(ora_env* e, int sender, int64_t t) {
 static int64_t next_order_id(ora_env* e) { return e->order_counter++; }
 
 /* --------------------------- oracle (SMRO) -------------------------------- */
-/* compute_fundamental_at_timestamp (SMRO:88-125) */
+static void blr_push(ora_env* e, int64_t t, int64_t price, int64_t qty);
+#define BL_FUNDAMENTAL (-2147483647 - 1) /* f_log records in the book-record stream */
+/* compute_fundamental_at_timestamp (SMRO:88-125); f_log append at SMRO:122 */
 static double o_compute(ora_env* e, int64_t ts, double v_adj, int64_t pt, double pv) {
     int64_t d = ts - pt;
     double mu = e->o_rbar, gamma = e->o_kappa, theta = e->o_fundvol;
@@ -461,6 +463,7 @@ static double o_compute(ora_env* e, int64_t ts, double v_adj, int64_t pt, double
     int64_t vi = py_round(v);
     e->o_pt = ts;
     e->o_pv = (double)vi;
+    if (e->book_log) blr_push(e, ts, BL_FUNDAMENTAL, vi);
     return (double)vi;
 }
 /* advance_fundamental_value_series (SMRO:131-181) */

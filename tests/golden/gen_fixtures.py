@@ -380,6 +380,12 @@ def save_booklog(ex, ob, sym, orig_snapshots, out):
         wide_cols=np.asarray(wide.columns, dtype=np.int64),
         wide_values=wide.to_numpy(dtype=np.float64),
         wide_dtypes=np.asarray([str(d) for d in wide.dtypes]),
+        # SparseMeanRevertingOracle.f_log[sym] after kernelStopping, the frame ExchangeAgent.
+        # kernelTerminating writes as fundamental_<sym> (ExchangeAgent.py:111-117)
+        fund_time=np.asarray([int(r["FundamentalTime"].value) - MIDNIGHT for r in ex.oracle.f_log[sym]], dtype=np.int64),
+        fund_value=np.asarray([r["FundamentalValue"] for r in ex.oracle.f_log[sym]], dtype=np.float64),
+        fund_types=np.asarray([type(r["FundamentalValue"]).__name__ for r in ex.oracle.f_log[sym]]),
+        fund_dtype=np.asarray(str(pd.DataFrame(ex.oracle.f_log[sym]).set_index("FundamentalTime")["FundamentalValue"].dtype)),
         full_rows=np.asarray(BOOKLOG_FULL_ROWS))
 
 

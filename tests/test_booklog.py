@@ -98,6 +98,28 @@ def test_records_replay_into_oracle_rows(cfg, seed):
     assert np.array_equal(bl.rows_from_records(rec), o.book_log())
 
 
+@pytest.mark.parametrize("cfg,seed", BOOKLOG_FIXTURES)
+def test_oracle_fundamental_log_equals_reference(cfg, seed):
+    """SparseMeanRevertingOracle.f_log after the run and its kernelStopping pass, and the frame
+    written as fundamental_<sym>.bz2"""
+    z = fixture(cfg, seed)
+    o = pyoracle.OracleEnv(cfg, seed)
+    o.set_book_log()
+    o.run()
+    o.finish()
+    r = o.book_records()
+    rec = np.zeros(len(r), dtype=bl.REC_DTYPE)
+    rec["t"], rec["price"], rec["qty"] = r[:, 0], r[:, 1], r[:, 2]
+    t, v = bl.fundamental_log(rec)
+    assert np.array_equal(t, z["fund_time"]) and np.array_equal(v, z["fund_value"])
+    df = bl.fundamental_frame(rec)
+    assert df.index.name == "FundamentalTime" and list(df.columns) == ["FundamentalValue"]
+    assert str(df["FundamentalValue"].dtype) == str(z["fund_dtype"])
+    assert np.array_equal(df.index.asi8 - MIDNIGHT, z["fund_time"])
+    # the book rows ignore the f_log records
+    assert np.array_equal(bl.rows_from_records(rec), o.book_log())
+
+
 def test_records_replay_edge_cases():
     """the host replay of limit/cancel records: crossing sweeps, partial fills, resting
     remainders, cancellations (no row of their own), python rounding of the average price"""

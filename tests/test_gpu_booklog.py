@@ -76,7 +76,9 @@ def test_gpu_book_log_overflow_is_an_env_error(mx):
     m.run()
     s = m.summary()
     assert (s["status"] == 2).all() and (s["err"] == 20).all()
-    assert len(m.book_log_records(0)) == 1000
+    assert len(m.book_log_records(0, partial=True)) == 1000
+    with pytest.raises(mx.MxaError, match="overflow"):
+        m.book_log_records(0)
 
 
 def test_gpu_book_log_off_after_reset(mx):
@@ -91,3 +93,38 @@ def test_gpu_book_log_off_after_reset(mx):
     assert s["events"][0] == o.events and s["hash"][0] == o.hash
     with pytest.raises(ValueError):
         m.book_log_records(0)
+
+
+@pytest.mark.parametrize("cfg,seed", [("rmsc03", 123456789), ("value_noise", 7)])
+def test_gpu_fundamental_log_equals_reference(mx, cfg, seed, tmp_path):
+    """SparseMeanRevertingOracle.f_log from the device stream (run + kernelStopping pass) equals
+    the reference's; write_logs writes the run directory's frames"""
+    import pandas as pd
+    z = np.load(os.path.join(GOLDEN, "%s_%d_booklog.npz" % (cfg, seed)))
+    m = mx.VecMarket(cfg, [seed], book_log=CAP)
+    m.run()
+    df = m.fundamental_log(0)
+    assert np.array_equal(df.index.asi8 - pd.Timestamp(bl.SESSION_DATE).value, z["fund_time"])
+    assert np.array_equal(df["FundamentalValue"].to_numpy(), z["fund_value"])
+    m.finalize()  # idempotent: a second pass rewrites the same records
+    assert m.fundamental_log(0).equals(df)
+    paths = m.write_logs(0, str(tmp_path))
+    sym = "ABM" if cfg == "rmsc03" else "JPM"
+    assert sorted(os.path.basename(p) for p in paths) == sorted(
+        ["summary_log.bz2", "fundamental_%s.bz2" % sym, "ORDERBOOK_%s_FULL.bz2" % sym])
+    assert pd.read_pickle(os.path.join(str(tmp_path), "fundamental_%s.bz2" % sym), compression="bz2").equals(df)
+
+
+def test_gpu_fundamental_records_equal_oracle(mx):
+    seeds = [123456789, 7]
+    m = mx.VecMarket("rmsc03", seeds, book_log=CAP)
+    m.run()
+    m.finalize()
+    for i, sd in enumerate(seeds):
+        o = oracle("rmsc03", sd)
+        o.finish()
+        r = m.book_log_records(i)
+        ref = o.book_records()
+        assert len(r) == len(ref)
+        assert np.array_equal(r["t"], ref[:, 0]) and np.array_equal(r["price"], ref[:, 1])
+        assert np.array_equal(r["qty"], ref[:, 2])
