@@ -133,8 +133,10 @@ enum {
     K_SPREAD_REQ = 5, K_SPREAD = 6, K_LAST_REQ = 7, K_LAST = 8, K_TV_REQ = 9, K_TV = 10,
     K_LIMIT = 11, K_CANCEL = 12, K_MODIFY = 13, K_ACCEPTED = 14, K_EXECUTED = 15, K_CANCELLED = 16,
     K_MKT_CLOSED = 17, K_MODIFIED = 18, K_KCANCEL = 19, K_MARKET_DATA = 20,
-    K_STREAM_REQ = 21, K_STREAM = 22 /* QUERY_ORDER_STREAM request / reply */
+    K_STREAM_REQ = 21, K_STREAM = 22, /* QUERY_ORDER_STREAM request / reply */
+    K_MD_SUB_REQ = 23, K_MD_SUB_CANCEL = 24 /* MARKET_DATA_SUBSCRIPTION_REQUEST / _CANCELLATION */
 };
+#define MD_LEVELS 5 /* deepest market-data subscription restated (MarketMakerAgent's 5 levels) */
 enum { T_MESSAGE = 1, T_WAKEUP = 2, T_CANCEL_ORDER = 3 };
 
 typedef struct {
@@ -157,6 +159,9 @@ typedef struct {
     /* MODIFY_ORDER: the agent's current copy of the order (the new order is oid/qty/price) */
     int64_t ooid, oqty, oprice;
     int obuy, oagent2;
+    /* MARKET_DATA: level prices, best first (nb / na levels; bq / aq the best volumes) */
+    int64_t lvb[MD_LEVELS], lva[MD_LEVELS];
+    /* MARKET_DATA_SUBSCRIPTION_REQUEST: levels in depth, freq in lookback */
 } msg_t;
 
 typedef struct {
@@ -202,7 +207,7 @@ typedef struct {
 /* agents                                                                     */
 /* ------------------------------------------------------------------------- */
 enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL, AG_MKTMAKER, AG_HBL };
-enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE, ST_AWAITING_STREAM };
+enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE, ST_AWAITING_STREAM, ST_AWAITING_MARKET_DATA };
 
 typedef struct {
     int64_t id;
@@ -254,8 +259,13 @@ typedef struct {
      * [stream_hi - stream_n + 1, stream_hi] (the reply holds live references to those dicts) */
     int L, stream_n, has_stream;
     int64_t stream_hi;
+    /* market-data subscription (MarketMakerAgent / MomentumAgent subscribe=True) and the known
+     * level prices of the last MARKET_DATA (TradingAgent.known_bids / known_asks) */
+    int subscribe, sub_requested;
+    int64_t kb[MD_LEVELS], ka[MD_LEVELS];
 } agent_t;
 
+#define HIST_RETIRED 48
 struct ora_env {
     char config[32];
     int n;
@@ -266,8 +276,10 @@ struct ora_env {
     side_t book[2]; /* 0 bids, 1 asks */
     int64_t last_trade;
     int last_trade_float;
-    epoch_t hist[16];
-    int nhist;
+    /* OrderBook.history: hist[0, nhist) the window (history[0] newest), then nret epochs that
+     * left it, kept unchanged for QUERY_ORDER_STREAM replies still holding them */
+    epoch_t hist[16 + HIST_RETIRED];
+    int nhist, nret;
     int64_t epoch_abs; /* absolute number of hist[0]: history shifts so far */
     /* SparseMeanRevertingOracle (one symbol) */
     ora_rs O;
@@ -296,6 +308,14 @@ struct ora_env {
     uint64_t hash;
     int64_t* trace;
     int64_t trace_cap, trace_len;
+    /* ExchangeAgent.subscription_dict (ExchangeAgent.py:342-357) in insertion order, and
+     * OrderBook.last_update_ts (None until the first book change) */
+    int nsub;
+    int32_t sub_agent[128], sub_levels[128], sub_live[128];
+    double sub_freq[128];
+    int64_t sub_last[128];
+    int has_last_update;
+    int64_t last_update;
     /* OrderBook.book_log rows (ora_set_book_log): t, n levels, executed qty, average trade
      * price, then n (price, volume) pairs, bids (negative volume) best-first, then asks */
     int book_log;
@@ -550,6 +570,22 @@ static void encode(const ora_env* e, const ev_t* v, int64_t rec[10]) {
         f[0] = m->data;
         f[5] = m->mkt_closed ? 1 : 0;
         break;
+    case K_MARKET_DATA:
+        f[0] = m->nb ? m->bpx : -1;
+        f[1] = m->nb ? m->bq : 0;
+        f[2] = m->na ? m->apx : -1;
+        f[3] = m->na ? m->aq : 0;
+        f[4] = m->data_float ? m->data * 10000 : m->data;
+        f[5] = (int64_t)m->nb + ((int64_t)m->na << 8);
+        break;
+    case K_MD_SUB_REQ:
+        f[0] = m->sender;
+        f[1] = m->depth;
+        f[2] = m->lookback;
+        break;
+    case K_MD_SUB_CANCEL:
+        f[0] = m->sender;
+        break;
     default:
         break;
     }
@@ -626,11 +662,15 @@ static void epoch_free(epoch_t* ep) {
 static void hist_shift(ora_env* e) {
     /* history.insert(0, {}); history = history[:stream_history + 1] */
     int keep = e->stream_history + 1;
-    if (e->nhist >= keep) {
-        for (int i = keep - 1; i < e->nhist; i++) epoch_free(&e->hist[i]);
+    if (e->nhist >= keep) { /* the oldest window epochs retire (a stream reply may still read them) */
+        e->nret += e->nhist - (keep - 1);
         e->nhist = keep - 1;
     }
-    memmove(e->hist + 1, e->hist, sizeof(epoch_t) * e->nhist);
+    while (e->nhist + e->nret + 1 > 16 + HIST_RETIRED) {
+        epoch_free(&e->hist[e->nhist + e->nret - 1]);
+        e->nret--;
+    }
+    memmove(e->hist + 1, e->hist, sizeof(epoch_t) * (e->nhist + e->nret));
     memset(&e->hist[0], 0, sizeof(epoch_t));
     e->nhist++;
     e->epoch_abs++;
@@ -779,6 +819,8 @@ static void handle_limit_order(ora_env* e, bord_t order) {
         hist_shift(e);
     }
     if (e->book_log) book_log_row(e, ex_q, executed ? e->last_trade : 0);
+    e->last_update = e->cur; /* OrderBook.py:169 */
+    e->has_last_update = 1;
 }
 
 /* cancelOrder (OrderBook.py:284-339) */
@@ -797,6 +839,8 @@ static void cancel_order(ora_env* e, const msg_t* req) {
                 msg_t m;
                 order_msg(&m, K_CANCELLED, &c);
                 ex_send(e, req->oagent, &m);
+                e->last_update = e->cur; /* OrderBook.py:338 */
+                e->has_last_update = 1;
                 return;
             }
         }
@@ -809,6 +853,9 @@ static void cancel_order(ora_env* e, const msg_t* req) {
 static void modify_order(ora_env* e, const msg_t* req) {
     if (req->ooid != req->oid) return; /* isSameOrder(order, new_order) (OrderBook.py:343-344) */
     side_t* book = &e->book[req->obuy ? 0 : 1];
+    if (book->n == 0) return;
+    e->last_update = e->cur; /* OrderBook.py:372 (nothing below returns early) */
+    e->has_last_update = 1;
     bord_t nw = {req->oid, req->oagent, req->is_buy, req->qty, req->price};
     for (int i = 0; i < book->n; i++) {
         level_t* L = &book->lv[i];
@@ -861,6 +908,77 @@ static int64_t transacted_volume(ora_env* e, int64_t lookback, int* err) {
     return vol;
 }
 
+/* ExchangeAgent.publishOrderBookData (ExchangeAgent.py:359-387): after every LIMIT / CANCEL /
+ * MODIFY, each subscription in insertion order gets the top `levels` of both sides and the last
+ * trade when freq == 0 or the book changed at least freq ns after its last update */
+static void publish(ora_env* e) {
+    for (int i = 0; i < e->nsub; i++) {
+        if (!e->sub_live[i]) continue;
+        if (e->sub_freq[i] != 0) {
+            if (!e->has_last_update) { /* None > Timestamp */
+                fail(e, -14, "publishOrderBookData: book never updated (TypeError comparing None)");
+                return;
+            }
+            if (!(e->last_update > e->sub_last[i] && (double)(e->last_update - e->sub_last[i]) >= e->sub_freq[i]))
+                continue;
+        }
+        msg_t r;
+        memset(&r, 0, sizeof r);
+        r.kind = K_MARKET_DATA;
+        int lv = e->sub_levels[i];
+        const side_t* b = &e->book[0];
+        const side_t* a = &e->book[1];
+        r.nb = b->n < lv ? b->n : lv;
+        r.na = a->n < lv ? a->n : lv;
+        if (r.nb > MD_LEVELS || r.na > MD_LEVELS) {
+            fail(e, -15, "market-data subscription deeper than the restated levels");
+            return;
+        }
+        for (int k = 0; k < r.nb; k++) r.lvb[k] = b->lv[k].o[0].price;
+        for (int k = 0; k < r.na; k++) r.lva[k] = a->lv[k].o[0].price;
+        if (r.nb) {
+            r.bpx = r.lvb[0];
+            for (int j = 0; j < b->lv[0].n; j++) r.bq += b->lv[0].o[j].qty;
+        }
+        if (r.na) {
+            r.apx = r.lva[0];
+            for (int j = 0; j < a->lv[0].n; j++) r.aq += a->lv[0].o[j].qty;
+        }
+        r.data = e->last_trade;
+        r.data_float = e->last_trade_float;
+        r.has_data = 1;
+        ex_send(e, e->sub_agent[i], &r);
+        e->sub_last[i] = e->last_update;
+    }
+}
+
+/* ExchangeAgent.updateSubscriptionDict (ExchangeAgent.py:342-357): a request (re)sets the
+ * agent's entry, keeping its place in the dict; a cancellation empties it */
+static void update_subscription(ora_env* e, const msg_t* m) {
+    int i = 0;
+    while (i < e->nsub && e->sub_agent[i] != m->sender) i++;
+    if (m->kind == K_MD_SUB_CANCEL) {
+        if (i == e->nsub || !e->sub_live[i]) { /* del of a missing key */
+            fail(e, -16, "MARKET_DATA_SUBSCRIPTION_CANCELLATION without a subscription (KeyError)");
+            return;
+        }
+        e->sub_live[i] = 0;
+        return;
+    }
+    if (i == e->nsub) {
+        if (e->nsub == 128) {
+            fail(e, -15, "too many market-data subscriptions");
+            return;
+        }
+        e->nsub++;
+    }
+    e->sub_agent[i] = m->sender;
+    e->sub_levels[i] = m->depth;
+    e->sub_freq[i] = (double)m->lookback;
+    e->sub_last[i] = e->cur;
+    e->sub_live[i] = 1;
+}
+
 /* ExchangeAgent.receiveMessage (ExchangeAgent.py:129-340) */
 static void ex_receive(ora_env* e, const msg_t* m) {
     e->comp_delay[0] = e->ex_comp;
@@ -879,6 +997,7 @@ static void ex_receive(ora_env* e, const msg_t* m) {
             return;
         }
     }
+    if (m->kind == K_MD_SUB_REQ || m->kind == K_MD_SUB_CANCEL) update_subscription(e, m);
     switch (m->kind) {
     case K_WHEN_OPEN_REQ:
     case K_WHEN_CLOSE_REQ:
@@ -948,13 +1067,16 @@ static void ex_receive(ora_env* e, const msg_t* m) {
     case K_LIMIT: {
         bord_t o = {m->oid, m->oagent, m->is_buy, m->qty, m->price};
         handle_limit_order(e, o);
+        if (e->nsub) publish(e);
         break;
     }
     case K_CANCEL:
         cancel_order(e, m);
+        if (e->nsub) publish(e);
         break;
     case K_MODIFY:
         modify_order(e, m);
+        if (e->nsub) publish(e);
         break;
     default:
         break;
@@ -1135,6 +1257,20 @@ static void ta_receive(ora_env* e, agent_t* a, const msg_t* m) {
     case K_TV:
         if (m->mkt_closed) a->mkt_closed = 1;
         a->tv = m->data;
+        break;
+    case K_MARKET_DATA: /* handleMarketData (TradingAgent.py:539-546) */
+        a->has_known = 1;
+        a->nb = m->nb;
+        a->na = m->na;
+        a->bid = m->bpx;
+        a->bidq = m->bq;
+        a->ask = m->apx;
+        a->askq = m->aq;
+        memcpy(a->kb, m->lvb, sizeof a->kb);
+        memcpy(a->ka, m->lva, sizeof a->ka);
+        a->has_last_trade = 1;
+        a->last_trade = m->data;
+        a->last_trade_float = m->data_float;
         break;
     case K_STREAM: /* queryOrderStream (TradingAgent.py:240-246, 549-554) */
         if (m->mkt_closed) a->mkt_closed = 1;
@@ -1370,32 +1506,52 @@ static double mom_avg(agent_t* a, int n) {
     double x = ((double)s2 / 2.0) / (double)n;
     return rint(x * 100.0) / 100.0;
 }
+/* TradingAgent.requestDataSubscription (TradingAgent.py:160-172) */
+static void request_subscription(ora_env* e, agent_t* a, int levels, int64_t freq) {
+    msg_t m;
+    memset(&m, 0, sizeof m);
+    m.kind = K_MD_SUB_REQ;
+    m.depth = levels;
+    m.lookback = freq;
+    ta_send_ex(e, a, &m);
+    a->sub_requested = 1;
+}
+/* MomentumAgent.placeOrders (MomentumAgent.py:82-93) */
+static void mom_place(ora_env* e, agent_t* a, int64_t bid, int64_t ask) {
+    if (!(bid && ask)) return;
+    if (a->nmid == a->capmid) {
+        a->capmid = a->capmid ? 2 * a->capmid : 64;
+        a->mids2 = (int64_t*)realloc(a->mids2, sizeof(int64_t) * a->capmid);
+    }
+    a->mids2[a->nmid++] = bid + ask;
+    if (a->nmid > 20) { a->avg20 = mom_avg(a, 20); a->n20++; }
+    if (a->nmid > 50) { a->avg50 = mom_avg(a, 50); a->n50++; }
+    if (a->n20 > 0 && a->n50 > 0) {
+        if (a->avg20 >= a->avg50) place_limit(e, a, a->size, 1, ask);
+        else place_limit(e, a, a->size, 0, bid);
+    }
+}
+/* MomentumAgent.wakeup / receiveMessage (MomentumAgent.py:54-80); subscribe=True requests
+ * level-1 data every 10 s on the first wakeup and trades on each MARKET_DATA */
 static void mom_wakeup(ora_env* e, agent_t* a) {
     int can_trade = ta_wakeup(e, a);
-    if (can_trade) {
+    if (a->subscribe && !a->sub_requested) {
+        request_subscription(e, a, 1, 10000000000LL);
+        a->state = ST_AWAITING_MARKET_DATA;
+    } else if (can_trade && !a->subscribe) {
         get_spread(e, a, 1);
         a->state = ST_AWAITING_SPREAD;
     }
 }
 static void mom_receive(ora_env* e, agent_t* a, const msg_t* m) {
     ta_receive(e, a, m);
-    if (a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
-        int have_bid = a->nb && a->bid != 0, have_ask = a->na && a->ask != 0;
-        if (have_bid && have_ask) {
-            if (a->nmid == a->capmid) {
-                a->capmid = a->capmid ? 2 * a->capmid : 64;
-                a->mids2 = (int64_t*)realloc(a->mids2, sizeof(int64_t) * a->capmid);
-            }
-            a->mids2[a->nmid++] = a->bid + a->ask;
-            if (a->nmid > 20) { a->avg20 = mom_avg(a, 20); a->n20++; }
-            if (a->nmid > 50) { a->avg50 = mom_avg(a, 50); a->n50++; }
-            if (a->n20 > 0 && a->n50 > 0) {
-                if (a->avg20 >= a->avg50) place_limit(e, a, a->size, 1, a->ask);
-                else place_limit(e, a, a->size, 0, a->bid);
-            }
-        }
+    if (!a->subscribe && a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        /* getKnownBidAsk: the best levels or None */
+        mom_place(e, a, a->nb ? a->bid : 0, a->na ? a->ask : 0);
         k_wakeup(e, a->id, e->cur + a->wake_freq);
         a->state = ST_AWAITING_WAKEUP;
+    } else if (a->subscribe && a->state == ST_AWAITING_MARKET_DATA && m->kind == K_MARKET_DATA) {
+        if (a->nb && a->na) mom_place(e, a, a->kb[0], a->ka[0]); /* `if bids and asks` (lists) */
     }
 }
 
@@ -1404,14 +1560,49 @@ static void mom_receive(ora_env* e, agent_t* a, const msg_t* m) {
 /* agent/market_makers/MarketMakerAgent.py, polling mode (subscribe=False) */
 static void mk_wakeup(ora_env* e, agent_t* a) {
     int can_trade = ta_wakeup(e, a); /* MarketMakerAgent.py:69-79 */
-    if (can_trade) {
+    if (a->subscribe && !a->sub_requested) {
+        request_subscription(e, a, a->spread_depth, 10000000000LL); /* subscribe_freq 10e9 */
+        a->state = ST_AWAITING_MARKET_DATA;
+    } else if (can_trade && !a->subscribe) {
         cancel_all(e, a);
         get_spread(e, a, a->spread_depth);
         a->state = ST_AWAITING_SPREAD;
     }
 }
+/* DEFAULT_LEVELS_QUOTE_DICT (MarketMakerAgent.py:6-12) */
+static const double MK_SPLIT[6][5] = {{0}, {1, 0, 0, 0, 0}, {0.5, 0.5, 0, 0, 0}, {0.34, 0.33, 0.33, 0, 0},
+                                      {0.25, 0.25, 0.25, 0.25, 0}, {0.20, 0.20, 0.20, 0.20, 0.20}};
+/* MarketMakerAgent.receiveMessage subscribe branch + placeOrders (MarketMakerAgent.py:109-141):
+ * cancel every open order, 1-4 levels (randint(1, 5)), one size draw, then per side a dict
+ * price -> volume in first-insertion order, a missing level i quoting one cent beyond the last
+ * known level (repeated misses overwrite that one entry) */
+static void mk_market_data(ora_env* e, agent_t* a) {
+    cancel_all(e, a);
+    int nl = (int)rs_randint(&a->rs, 1, 5);
+    if (!(a->nb && a->na)) return;
+    a->size = (int64_t)rint((double)rs_randint(&a->rs, a->mk_min, a->mk_max) / 2);
+    for (int side = 1; side >= 0; side--) { /* buy quotes first, then sell */
+        const int64_t* lv = side ? a->kb : a->ka;
+        int n = side ? a->nb : a->na;
+        int64_t px[5], vol[5];
+        int k = 0;
+        for (int i = 0; i < nl; i++) {
+            int64_t v = (int64_t)rint(MK_SPLIT[nl][i] * (double)a->size);
+            int64_t p = i < n ? lv[i] : (side ? lv[n - 1] - 1 : lv[n - 1] + 1);
+            int j = 0;
+            while (j < k && px[j] != p) j++;
+            if (j == k) px[k++] = p;
+            vol[j] = v;
+        }
+        for (int j = 0; j < k; j++) place_limit(e, a, vol[j], side, px[j]);
+    }
+}
 static void mk_receive(ora_env* e, agent_t* a, const msg_t* m) {
     ta_receive(e, a, m); /* MarketMakerAgent.py:81-107 */
+    if (a->subscribe) {
+        if (a->state == ST_AWAITING_MARKET_DATA && m->kind == K_MARKET_DATA) mk_market_data(e, a);
+        return;
+    }
     if (!(a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD)) return;
     cancel_all(e, a);
     int64_t mid = a->last_trade, spread;
@@ -1461,8 +1652,8 @@ static void hbl_place(ora_env* e, agent_t* a) {
     int nent = 0;
     for (int k = 0; k < a->stream_n; k++) {
         int64_t idx = e->epoch_abs - (a->stream_hi - k);
-        if (idx < 1 || idx >= e->nhist) {
-            fail(e, -11, "HBL: streamed history epoch left the exchange's window (not restated)");
+        if (idx < 1 || idx >= e->nhist + e->nret) {
+            fail(e, -11, "HBL: streamed history epoch beyond the retained history");
             return;
         }
         const epoch_t* ep = &e->hist[idx];
@@ -2237,7 +2428,10 @@ static void zi_params(agent_t* a, int64_t rmin, int64_t rmax, double sigma_n, do
     qsort(th, 20, sizeof(double), cmp_desc);
     for (int i = 0; i < 20; i++) a->theta[i] = (int64_t)th[i];
 }
-static int build_rmsc01(ora_env* e, uint32_t seed) {
+/* config/rmsc02.py: rmsc01's agents with subscribe=True for the market maker (5 levels) and the
+ * momentum agents (1 level), both every 10 s; kernel midnight-17:00; latency
+ * U(21000, 13e6)[n][n] drawn after the kernel seed (not symmetrised) with 6-way noise */
+static int build_rmsc0x(ora_env* e, uint32_t seed, int v2) {
     rs_seed(&e->G, seed);
     int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
     agent_t* ex = add_agent(e, AG_EXCHANGE);
@@ -2261,6 +2455,7 @@ static int build_rmsc01(ora_env* e, uint32_t seed) {
         a->wake_freq = NS_SEC;
         a->spread_depth = 5;
         a->last_spread = 10;
+        a->subscribe = v2;
     }
     rs_seed(&e->O, seed_u32(&e->G));
     oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
@@ -2287,13 +2482,23 @@ static int build_rmsc01(ora_env* e, uint32_t seed) {
         snprintf(a->tname, 96, "MomentumAgent");
         trading_init(a, 10000000);
         a->wake_freq = 60 * NS_SEC;
+        a->subscribe = v2;
     }
     rs_seed(&e->K, seed_u32(&e->G));
-    e->start = open;
-    e->stop = 16 * NS_HOUR + NS_MIN;
-    e->lat_mode = 0;
-    e->noise_len = 1;
     int n = e->n;
+    if (v2) {
+        e->start = 0;
+        e->stop = 17 * NS_HOUR;
+        e->lat = (double*)malloc(sizeof(double) * (size_t)n * n);
+        for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, 21000, 13000000);
+        e->lat_mode = 1;
+        e->noise_len = 6;
+    } else {
+        e->start = open;
+        e->stop = 16 * NS_HOUR + NS_MIN;
+        e->lat_mode = 0;
+        e->noise_len = 1;
+    }
     e->agent_time = (int64_t*)calloc(n, sizeof(int64_t));
     e->comp_delay = (int64_t*)calloc(n, sizeof(int64_t));
     for (int i = 0; i < n; i++) e->agent_time[i] = e->start;
@@ -2489,7 +2694,8 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     else if (!strcmp(config, "rmsc03")) rc = build_rmsc03(e, seed);
     else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
     else if (!strcmp(config, "value_noise")) rc = build_value_noise(e, seed);
-    else if (!strcmp(config, "rmsc01")) rc = build_rmsc01(e, seed);
+    else if (!strcmp(config, "rmsc01")) rc = build_rmsc0x(e, seed, 0);
+    else if (!strcmp(config, "rmsc02")) rc = build_rmsc0x(e, seed, 1);
     else rc = -1;
     if (rc) {
         free(e);
@@ -2519,7 +2725,7 @@ void ora_destroy(ora_env* e) {
         for (int i = 0; i < e->book[s].n; i++) free(e->book[s].lv[i].o);
         free(e->book[s].lv);
     }
-    for (int i = 0; i < e->nhist; i++) epoch_free(&e->hist[i]);
+    for (int i = 0; i < e->nhist + e->nret; i++) epoch_free(&e->hist[i]);
     free(e->blg);
     free(e->blr);
     free(e->lat);

@@ -19,7 +19,8 @@ What is recorded per (config, seed):
 
 Third-party modules the reference imports but this image lacks are replaced by
 logging-only stubs: `jsons.dump` (used only to log orders),
-pandas 2 API renames (`pandas.io.json.json_normalize`, `SparseDataFrame`), and the
+pandas 2 API renames (`pandas.io.json.json_normalize`, `SparseDataFrame`, `Timedelta.delta` =
+the ns count of the pinned pandas 0.24, read by ExchangeAgent.publishOrderBookData), and the
 bz2 log writers are no-ops.  None of them touches the simulated arithmetic.
 
 Usage:  python tests/golden/gen_fixtures.py all          (writes tests/golden/*.npz/json)
@@ -55,6 +56,7 @@ KIND = {
     "MKT_CLOSED": 17, "ORDER_MODIFIED": 18, "KERNEL_CANCEL_ORDER": 19,
     "MARKET_DATA": 20,
     "QUERY_ORDER_STREAM_REQ": 21, "QUERY_ORDER_STREAM": 22,
+    "MARKET_DATA_SUBSCRIPTION_REQUEST": 23, "MARKET_DATA_SUBSCRIPTION_CANCELLATION": 24,
 }
 
 FNV_OFF = 0xCBF29CE484222325
@@ -154,7 +156,21 @@ def encode(t_rel, recipient, mtype, msg):
         # whose quantity can change before delivery; the replay agent ignores the message
         f[:5] = _order_fields(b["new_order"], with_qty=False)
     elif m == "MARKET_DATA":
+        # ExchangeAgent.publishOrderBookData: fresh level lists (not aliased)
         kind = KIND[m]
+        bids, asks = b["bids"], b["asks"]
+        f[0] = _price(bids[0][0]) if bids else -1
+        f[1] = int(bids[0][1]) if bids else 0
+        f[2] = _price(asks[0][0]) if asks else -1
+        f[3] = int(asks[0][1]) if asks else 0
+        f[4] = _price(b["last_transaction"])
+        f[5] = len(bids) + (len(asks) << 8)
+    elif m == "MARKET_DATA_SUBSCRIPTION_REQUEST":
+        kind = KIND[m]
+        f[0], f[1], f[2] = b["sender"], int(b["levels"]), int(b["freq"])
+    elif m == "MARKET_DATA_SUBSCRIPTION_CANCELLATION":
+        kind = KIND[m]
+        f[0] = b["sender"]
     elif m == "QUERY_ORDER_STREAM":
         if req:
             kind = KIND["QUERY_ORDER_STREAM_REQ"]
@@ -201,6 +217,8 @@ def install_stubs():
     import pandas.io.json
     pandas.io.json.json_normalize = pandas.json_normalize
     pandas.SparseDataFrame = pandas.DataFrame
+    if not hasattr(pandas.Timedelta, "delta"):  # pandas 0.24 (requirements.txt): ns as an int
+        pandas.Timedelta.delta = property(lambda self: self.value)
     sys.path.insert(0, REF)
 
 
@@ -251,7 +269,7 @@ def run_config(cfg, seed, out, full):
     TradingAgent.getTransactedVolume = TradingAgent.get_transacted_volume  # SURVEY.md key finding 3
 
     date = {"sparse_zi_100": "2019-06-28", "sparse_zi_1000": "2019-06-28", "rmsc03": "2019-06-28",
-            "value_noise": "2019-06-28", "rmsc01": "2019-06-28"}[cfg]
+            "value_noise": "2019-06-28", "rmsc01": "2019-06-28", "rmsc02": "2019-06-28"}[cfg]
     MIDNIGHT = int(pd.Timestamp(date).value)
     argv = ["abides.py", "-c", cfg, "-s", str(seed)]
     if cfg == "rmsc03":
@@ -455,7 +473,10 @@ def main():
             ("value_noise", 123456789, True), ("value_noise", 7, False),
             # rmsc01 (2M pops each; ~25 min of the reference): 123456789 ends in the reference's
             # IndexError in ZeroIntelligenceAgent.kernelStopping (recorded as stop_error)
-            ("rmsc01", 7, False), ("rmsc01", 99, False), ("rmsc01", 123456789, False)]
+            ("rmsc01", 7, False), ("rmsc01", 99, False), ("rmsc01", 123456789, False),
+            # rmsc02: rmsc01 with market-data subscriptions (market maker, momentum agents) and a
+            # latency matrix with noise, from midnight to 17:00
+            ("rmsc02", 7, False), ("rmsc02", 123456789, False)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2]]
     procs = []
