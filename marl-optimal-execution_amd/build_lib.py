@@ -1,14 +1,22 @@
-"""Build libmxa.so (HIP, gfx950) in-tree: marl-optimal-execution_amd/lib/libmxa.so."""
+"""Build libmxa.so (HIP, gfx950) in-tree: marl-optimal-execution_amd/lib/libmxa.so.
+
+The C-ABI (csrc/mxa_api.hip) and each configuration's engine (csrc/mxa_inst.hip with
+-DMXA_INST_CFG=<id>) are separate translation units compiled in parallel, then linked."""
 import hashlib
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "mxa_api.hip")
+INST = os.path.join(HERE, "csrc", "mxa_inst.hip")
 OUT = os.path.join(HERE, "lib", "libmxa.so")
-DEPS = ["mxa_api.hip", "mxa_kernels.hip", "mxa_layout.h", "mxa_config.h", "glibc_math.h", "glibc_math_tables.h"]
+OBJ = os.path.join(HERE, "build")
+N_CONFIGS = 8  # csrc/mxa_entry.h MXA_N_CONFIGS
+DEPS = ["mxa_api.hip", "mxa_inst.hip", "mxa_entry.h", "mxa_kernels.hip", "mxa_layout.h", "mxa_config.h", "glibc_math.h",
+        "glibc_math_tables.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
          "-Wno-unused-result", "-Wno-unused-value"]
@@ -36,15 +44,27 @@ def up_to_date():
     return all(os.path.getmtime(s) <= t for s in sources())
 
 
-def build(force=False, verbose=True):
+def build(force=False, verbose=True, jobs=None):
     if not force and up_to_date():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [HIPCC] + FLAGS + ['-DMXA_BUILD_ID="%s"' % build_id(), "-I" + os.path.join(HERE, "csrc"),
-                            "-I" + os.path.join(ROOT, "include"), SRC, "-o", OUT + ".tmp"]
+    os.makedirs(OBJ, exist_ok=True)
+    inc = ["-I" + os.path.join(HERE, "csrc"), "-I" + os.path.join(ROOT, "include")]
+    cflags = [f for f in FLAGS if f != "-shared"] + ["-c"]
+    units = [([HIPCC] + cflags + ['-DMXA_BUILD_ID="%s"' % build_id()] + inc + [SRC, "-o", os.path.join(OBJ, "mxa_api.o")])]
+    for c in range(N_CONFIGS):
+        units.append([HIPCC] + cflags + ["-DMXA_INST_CFG=%d" % c] + inc + [INST, "-o", os.path.join(OBJ, "mxa_inst_%d.o" % c)])
     if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd)
+        for u in units:
+            print(" ".join(u), flush=True)
+    jobs = jobs or min(len(units), max(1, min(16, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(subprocess.check_call, u) for u in units]:
+            f.result()
+    link = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared"] + [u[-1] for u in units] + ["-o", OUT + ".tmp"]
+    if verbose:
+        print(" ".join(link), flush=True)
+    subprocess.check_call(link)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

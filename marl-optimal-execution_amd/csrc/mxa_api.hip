@@ -1,8 +1,9 @@
 // mxa_api.hip — host side of libmxa: the C-ABI declared in include/mxa.h.
 //
 // Builds the per-configuration parameter block (the constants of the reference config
-// scripts), lays out one HBM block per env, and launches the kernels of
-// mxa_kernels.hip (included here so the templates are instantiated in one TU).
+// scripts), lays out one HBM block per env, and launches the kernels of mxa_kernels.hip.
+// Each configuration's engine is its own translation unit (mxa_inst.hip, mxa_entry.h); an
+// rmsc03-only variant build (-DMXA_ONLY_RMSC03) compiles everything in this one.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -12,41 +13,15 @@
 #include <vector>
 
 #include "../../include/mxa.h"
+#define MXA_API_TU
 #include "mxa_kernels.hip"
+#include "mxa_entry.h"
+#ifdef MXA_ONLY_RMSC03
+#define MXA_INST_CFG 0
+#include "mxa_inst.hip"
+#endif
 
 namespace {
-
-typedef void (*build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*,
-                         const RpCtx*);
-typedef void (*run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, BlRec*, int);
-typedef void (*stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, mxa_agent_final*, BlRec*, int);
-typedef void (*step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, const double*,
-                        double*, int32_t*);
-
-template <int CFG>
-void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, const uint32_t* seeds,
-                  const uint8_t* mask, const RpCtx* ctx) {
-  hipLaunchKernelGGL((mxa_build_kernel<CFG>), g, b, lds, s, base, stride, n, seeds, mask, ctx);
-}
-template <int CFG>
-void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
-                const RpCtx* ctx, BlRec* blog, int blog_cap) {
-  hipLaunchKernelGGL((mxa_run_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, blog, blog_cap);
-}
-
-template <int CFG>
-void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, mxa_agent_final* out,
-                 BlRec* blog, int blog_cap) {
-  hipLaunchKernelGGL((mxa_stop_kernel<CFG>), g, b, lds, s, base, stride, n, out, blog, blog_cap);
-}
-
-#ifndef MXA_ONLY_RMSC03
-template <int CFG>
-void launch_step(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
-                 const RpCtx* ctx, const double* act, double* obs, int32_t* flags) {
-  hipLaunchKernelGGL((mxa_step_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, act, obs, flags);
-}
-#endif
 
 __global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int n, int* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -103,10 +78,10 @@ struct mxa_handle {
   uint8_t* d_mask = nullptr;
   int* d_count = nullptr;
   size_t lds = 0;
-  build_fn build = nullptr;
-  run_fn run = nullptr;
-  step_fn step = nullptr;  // GymKernel handles (replay, rmsc03_rl)
-  stop_fn stop = nullptr;  // kernelStopping pass (plain Kernel.runner configs)
+  mxa_build_fn build = nullptr;
+  mxa_run_fn run = nullptr, run_log = nullptr;     // run_log: with the book-update log
+  mxa_step_fn step = nullptr;                      // GymKernel handles (replay, rmsc03_rl)
+  mxa_stop_fn stop = nullptr, stop_log = nullptr;  // kernelStopping pass (plain Kernel.runner configs)
   mxa_agent_final* d_final = nullptr;
   BlRec* d_blog = nullptr;  // book-update log [n_envs][blog_cap] (mxa_set_book_log)
   int32_t blog_cap = 0;
@@ -139,18 +114,31 @@ static int hip_fail(mxa_handle* h, hipError_t e, const char* what) {
 
 static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, int32_t device, mxa_handle** out);
 
-template <int CFG>
-static void bind(mxa_handle* h) {
-  h->build = launch_build<CFG>;
-  h->run = launch_run<CFG>;
-  h->stop = launch_stop<CFG>;
-  h->lds = mxa_cfg::lds_bytes(CFG);
+// the configuration's launchers (mxa_entry.h); false: not built into this library
+static bool bind(mxa_handle* h, int cfg) {
+  MxaEntry e{};
+  switch (cfg) {
+  case 0: e = mxa_entry_0(); break;
 #ifndef MXA_ONLY_RMSC03
-  if constexpr (CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL) {
-    h->step = launch_step<CFG>;
-    h->gym = true;
-  }
+  case 1: e = mxa_entry_1(); break;
+  case 2: e = mxa_entry_2(); break;
+  case 3: e = mxa_entry_3(); break;
+  case 4: e = mxa_entry_4(); break;
+  case 5: e = mxa_entry_5(); break;
+  case 6: e = mxa_entry_6(); break;
+  case 7: e = mxa_entry_7(); break;
 #endif
+  default: return false;
+  }
+  h->build = e.build;
+  h->run = e.run;
+  h->run_log = e.run_log;
+  h->stop = e.stop;
+  h->stop_log = e.stop_log;
+  h->step = e.step;
+  h->gym = e.step != nullptr;
+  h->lds = mxa_cfg::lds_bytes(cfg);
+  return true;
 }
 
 extern "C" {
@@ -172,17 +160,11 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
   static_assert((int)MXA_RMSC03 == (int)MXA_CFG_RMSC03 && (int)MXA_SPARSE_ZI_100 == (int)MXA_CFG_SPARSE_ZI_100 &&
                     (int)MXA_SPARSE_ZI_1000 == (int)MXA_CFG_SPARSE_ZI_1000 &&
                     (int)MXA_MARKETREPLAY == (int)MXA_CFG_MARKETREPLAY && (int)MXA_RMSC03_RL == (int)MXA_CFG_RMSC03_RL &&
-                    (int)MXA_VALUE_NOISE == (int)MXA_CFG_VALUE_NOISE && (int)MXA_RMSC01 == (int)MXA_CFG_RMSC01,
+                    (int)MXA_VALUE_NOISE == (int)MXA_CFG_VALUE_NOISE && (int)MXA_RMSC01 == (int)MXA_CFG_RMSC01 &&
+                    (int)MXA_RMSC02 == (int)MXA_CFG_RMSC02,
                 "config ids");
-  if (config == MXA_RMSC03) bind<MXA_CFG_RMSC03>(h);
-#ifndef MXA_ONLY_RMSC03
-  else if (config == MXA_SPARSE_ZI_100) bind<MXA_CFG_SPARSE_ZI_100>(h);
-  else if (config == MXA_SPARSE_ZI_1000) bind<MXA_CFG_SPARSE_ZI_1000>(h);
-  else if (config == MXA_RMSC03_RL) bind<MXA_CFG_RMSC03_RL>(h);
-  else if (config == MXA_VALUE_NOISE) bind<MXA_CFG_VALUE_NOISE>(h);
-  else if (config == MXA_RMSC01) bind<MXA_CFG_RMSC01>(h);
-#endif
-  else {
+  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_RMSC02 + 1, "one entry per configuration");
+  if (config == MXA_MARKETREPLAY || !bind(h, config)) {  // replay handles: mxa_create_replay
     delete h;
     return MXA_EINVAL;
   }
@@ -265,7 +247,10 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
   const int64_t auto_cap = (int64_t)P0.rl_ids + n_zero;
   if (min_id <= auto_cap) return MXA_EINVAL;
   mxa_handle* h = new mxa_handle();
-  bind<MXA_CFG_MARKETREPLAY>(h);
+  if (!bind(h, MXA_CFG_MARKETREPLAY)) {
+    delete h;
+    return MXA_EINVAL;
+  }
   h->replay = true;
   h->P = P0;
   h->P.n_envs = n_envs;
@@ -387,7 +372,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
 
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
   if (!h || h->gym) return MXA_EINVAL;  // GymKernel handles advance by mxa_step
-  h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
+  (h->d_blog ? h->run_log : h->run)(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
          h->d_ctx, h->d_blog, h->blog_cap);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
@@ -407,7 +392,7 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   for (;;) {
     if (max_launches > 0 && launches >= max_launches) break;
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    h->run(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), chunk,
+    (h->d_blog ? h->run_log : h->run)(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), chunk,
            h->d_ctx, h->d_blog, h->blog_cap);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
@@ -432,7 +417,7 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
 // book-update log (OrderBook.book_log / the exchange's BEST_BID, BEST_ASK, LAST_TRADE events):
 // `cap` records per env in one device buffer; every env's record count restarts at 0
 int mxa_set_book_log(mxa_handle* h, int32_t cap) {
-  if (!h || h->gym || cap < 0) return MXA_EINVAL;
+  if (!h || h->gym || !h->run_log || cap < 0) return MXA_EINVAL;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->d_blog) HIPCHK(h, hipFree(h->d_blog));
@@ -476,7 +461,7 @@ int mxa_finalize(mxa_handle* h) {
   HIPCHK(h, hipSetDevice(h->device));
   const size_t rows = (size_t)h->P.n_envs * h->P.n_agents;
   if (!h->d_final) HIPCHK(h, hipMalloc(&h->d_final, rows * sizeof(mxa_agent_final)));
-  h->stop(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_final,
+  (h->d_blog ? h->stop_log : h->stop)(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_final,
           h->d_blog, h->blog_cap);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));

@@ -41,6 +41,8 @@ constexpr Shape shape(int cfg) {
        // rmsc01: oracle maxima over seeds 123456789 / 7: 140 pending events, 75 resting orders;
        // wide replies for the market maker's depth-5 spread queries
        : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, 4, 8, 0}
+       // rmsc02: oracle maxima over 41 seeds: 225 pending events, 299 resting orders
+       : cfg == MXA_CFG_RMSC02 ? Shape{6, 5, true, 2, 8, 0}
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, 2, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
@@ -270,6 +272,27 @@ constexpr void params_rmsc01(MxaParams& P) {
   P.L.hbl_range = MXA_HBL_RANGE;
 }
 
+// config/rmsc02.py (RMSC-2): rmsc01's agents with subscribe=True for the market maker
+// (5 levels) and the momentum agents (1 level), both every 10e9 ns; kernel midnight-17:00;
+// latency G.uniform(21000, 13e6, (101, 101)) drawn after the kernel seed (not symmetrised:
+// row 0 and column 0 are read) with 6-way noise
+constexpr void params_rmsc02(MxaParams& P) {
+  params_rmsc01(P);
+  P.config = MXA_CFG_RMSC02;
+  P.start = 0;
+  P.stop = 17 * HOUR;
+  P.lat_mode = 1;
+  P.noise_len = 6;
+  P.lat_lo = 21000;
+  P.lat_hi = 13000000;
+  P.lat_asym = 1;
+  P.md_sub = 1;
+  P.md_mk_levels = 5;
+  P.md_mom_levels = 1;
+  P.md_freq = 10 * NS;
+  P.L.lat_len = 2 * P.n_agents;
+}
+
 constexpr uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 // per-env HBM block: header, agent records, open orders, RNG streams, latency row/col,
@@ -302,6 +325,10 @@ constexpr void layout(MxaParams& P, int cfg) {
   off = align_up(off + (uint64_t)L.oh_cap * sizeof(OhRec), 256);
   L.off_hh = off;  // HBL price histogram (zeroed between uses)
   off = align_up(off + (uint64_t)L.hbl_range * 8, 256);
+  L.off_sub = off;  // market-data subscriptions (md_sub configs)
+  off = align_up(off + (P.md_sub ? (uint64_t)MD_MAX_SUBS * sizeof(SubRec) : 0), 256);
+  L.off_md = off;
+  off = align_up(off + (P.md_sub ? (uint64_t)P.n_agents * MD_WORDS * 4 : 0), 256);
   L.off_trace = (uint32_t)off;
   L.env_stride = off;  // without trace; the handle adds trace_cap records
 }
@@ -346,6 +373,7 @@ constexpr MxaParams params(int cfg) {
   else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);
   else if (cfg == MXA_CFG_VALUE_NOISE) params_value_noise(P);
   else if (cfg == MXA_CFG_RMSC01) params_rmsc01(P);
+  else if (cfg == MXA_CFG_RMSC02) params_rmsc02(P);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;

@@ -1,0 +1,56 @@
+// mxa_inst.hip — one configuration's kernels: compiled once per configuration with
+// -DMXA_INST_CFG=<id> (mxa_layout.h mxa_config_id), exporting mxa_entry_<id>().
+#include "mxa_kernels.hip"
+#include "mxa_entry.h"
+
+#ifndef MXA_INST_CFG
+#error "mxa_inst.hip is compiled per configuration: -DMXA_INST_CFG=<id>"
+#endif
+
+namespace {
+
+template <int CFG>
+void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, const uint32_t* seeds,
+                  const uint8_t* mask, const RpCtx* ctx) {
+  hipLaunchKernelGGL((mxa_build_kernel<CFG>), g, b, lds, s, base, stride, n, seeds, mask, ctx);
+}
+template <int CFG, bool LOG>
+void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
+                const RpCtx* ctx, BlRec* blog, int blog_cap) {
+  hipLaunchKernelGGL((mxa_run_kernel<CFG, LOG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, blog, blog_cap);
+}
+template <int CFG, bool LOG>
+void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, mxa_agent_final* out,
+                 BlRec* blog, int blog_cap) {
+  hipLaunchKernelGGL((mxa_stop_kernel<CFG, LOG>), g, b, lds, s, base, stride, n, out, blog, blog_cap);
+}
+#ifndef MXA_ONLY_RMSC03
+template <int CFG>
+void launch_step(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
+                 const RpCtx* ctx, const double* act, double* obs, int32_t* flags) {
+  hipLaunchKernelGGL((mxa_step_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, act, obs, flags);
+}
+#endif
+
+template <int CFG>
+MxaEntry make_entry() {
+  MxaEntry e{};
+  e.build = launch_build<CFG>;
+  e.run = launch_run<CFG, false>;
+  e.stop = launch_stop<CFG, false>;
+  constexpr bool gym = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL;
+  if constexpr (!gym) {  // the book-update log: plain Kernel.runner configurations
+    e.run_log = launch_run<CFG, true>;
+    e.stop_log = launch_stop<CFG, true>;
+  }
+#ifndef MXA_ONLY_RMSC03
+  if constexpr (gym) e.step = launch_step<CFG>;
+#endif
+  return e;
+}
+
+}  // namespace
+
+#define MXA_ENTRY_CAT2(a, b) a##b
+#define MXA_ENTRY_CAT(a, b) MXA_ENTRY_CAT2(a, b)
+MxaEntry MXA_ENTRY_CAT(mxa_entry_, MXA_INST_CFG)() { return make_entry<MXA_INST_CFG>(); }

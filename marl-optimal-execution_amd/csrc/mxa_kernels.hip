@@ -19,8 +19,10 @@
 // Arithmetic follows the reference bit for bit: numpy-legacy MT19937 and distributions,
 // glibc log/exp/pow (glibc_math.h), Python round-half-even / truncation, pandas ns
 // truncation.  Compiled with -ffp-contract=off.
+#pragma once
 #include <hip/hip_runtime.h>
 
+#include "../../include/mxa.h"
 #include "glibc_math.h"
 #include "mxa_layout.h"
 #include "mxa_config.h"
@@ -370,7 +372,7 @@ struct Rec {  // named scalars, not an array: a private i64[10] is promoted to a
     }
   }
 };
-template <bool WIDE>
+template <bool WIDE, bool MDK>
 DEV Rec encode(u64 key, const Msg& m) {
   Rec r;
   r.t = (i64)(key >> 13);
@@ -440,6 +442,26 @@ DEV Rec encode(u64 key, const Msg& m) {
   default:
     break;
   }
+  // market-data kinds only where they exist: extra cases cost the other configurations' event
+  // loop registers (the hash path is compiled in even with the hash off)
+  if constexpr (MDK) {
+    if (k == MK_MARKET_DATA) {  // best levels, last transaction, level counts (w6 = nb | na << 8)
+      const int nb = (int)(m.w[6] & 0xFF), na = (int)((m.w[6] >> 8) & 0xFF);
+      const i64 d = (i32)m.w[5];
+      r.f0 = nb ? (i64)(i32)m.w[1] : -1;
+      r.f1 = nb ? (i64)(i32)m.w[2] : 0;
+      r.f2 = na ? (i64)(i32)m.w[3] : -1;
+      r.f3 = na ? (i64)(i32)m.w[4] : 0;
+      r.f4 = m_dfloat(m) ? d * 10000 : d;
+      r.f5 = (i64)nb + ((i64)na << 8);
+    } else if (k == MK_MD_SUB_REQ) {
+      r.f0 = m_agent(m);
+      r.f1 = (i32)m.w[1];
+      r.f2 = m_i64(m, 2);
+    } else if (k == MK_MD_SUB_CANCEL) {
+      r.f0 = m_agent(m);
+    }
+  }
   return r;
 }
 DEV u64 fnv(u64 h, i64 v) { return (h ^ (u64)v) * FNV_PRIME; }
@@ -479,7 +501,7 @@ DEV u64 stamp() {
 #define PROF_ADD(b, v)
 #define PROF_CNT(b)
 #endif
-template <int CFG, bool BUILD = false>
+template <int CFG, bool BUILD = false, bool LOG = false>
 struct Eng {
   // every configuration constant is an immediate (mxa_config.h)
   static constexpr MxaParams PC = mxa_cfg::params(CFG);
@@ -588,6 +610,9 @@ struct Eng {
   // HBL configurations: OrderBook.history restated as an order-history ring in HBM (one OhRec
   // per handled limit order); a resting order keeps its record index to flag its transactions
   static constexpr bool OH = PC.n_hbl > 0;
+  // market-data subscription configs (rmsc02): the exchange publishes after book changes
+  static constexpr bool MD = PC.md_sub != 0;
+  static_assert(!MD || PW == 8, "MARKET_DATA carries its level counts and slot tag in w6 / w7");
   i32 bx[OH ? SO : 1];
   // current agent record (lane l holds dwords 2l, 2l+1)
   u32 rlo, rhi;
@@ -600,7 +625,10 @@ struct Eng {
   const RpCtx* rx;  // marketreplay: tape + runtime layout (nullptr otherwise)
   i32 end_step;     // GymKernel: the RL agent's spread reply ends a step
   u32 run_skip;     // event runs: members below this seq are popped one by one (a LIMIT run that crosses)
-  BlRec* blog;      // book-update log of this env (nullptr: off)
+  // book-update log of this env: a kernel variant of its own (LOG), so the event loop of the
+  // plain kernels carries none of it
+  static constexpr bool BLOG = LOG;
+  BlRec* blog;
   i32 blog_cap;
 #ifdef MXA_PROF
   LDSP u64* prof;
@@ -650,6 +678,8 @@ struct Eng {
   DEV OpenOrder* open_ptr(int a) { return (OpenOrder*)(env + PC.L.off_open + (size_t)a * PC.L.open_cap * sizeof(OpenOrder)); }
   DEV u32* rng_key(int s) { return (u32*)(env + PC.L.off_rng + (size_t)s * MXA_RNG_WORDS * 4); }
   DEV double* lat() { return (double*)(env + PC.L.off_lat); }
+  DEV SubRec* subs() { return (SubRec*)(env + PC.L.off_sub); }
+  DEV u32* md_slot(int agent) { return (u32*)(env + PC.L.off_md) + (size_t)agent * MD_WORDS; }
   DEV LDSP i32* ep_entries() { return h.ep_n; }  // header field: LDS for the launch
   DEV TxRec* txr() { return (TxRec*)(env + PC.L.off_tx + 64); }
 
@@ -1088,7 +1118,7 @@ struct Eng {
       deliver = sent + (i64)l;
     } else {
       double l = 0.0;
-      if (PC.lat_mode == 1) l = lat()[cur_agent == 0 ? recipient : cur_agent];
+      if (PC.lat_mode == 1) l = lat()[cur_agent == 0 ? recipient : (PC.lat_asym ? PC.n_agents : 0) + cur_agent];
       i64 noise = 0;
       if (PC.noise_len > 1) {
         RS K = grs(2);
@@ -1130,7 +1160,7 @@ struct Eng {
     i64 vi = py_round(v);
     h.o_pt = ts;
     h.o_pv = (double)vi;
-    if (blog) bl_put(ts, BL_FUNDAMENTAL, (i32)vi);  // f_log (SMRO:122)
+    if constexpr (BLOG) bl_put(ts, BL_FUNDAMENTAL, (i32)vi);  // f_log (SMRO:122)
     return (double)vi;
   }
   DEV double o_advance(i64 t) {
@@ -1414,7 +1444,7 @@ struct Eng {
   }
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
     if (qty <= 0) return;
-    if (blog) bl_put(cur, price, is_buy ? qty : -qty);
+    if constexpr (BLOG) bl_put(cur, price, is_buy ? qty : -qty);
     i32 hep = h.epoch;
     LDSP i32* EP = ep_entries();
     i32 ne = EP[h.epoch & 15] + 1;
@@ -1470,6 +1500,10 @@ struct Eng {
       h.epoch++;
       if (lane == 0) EP[h.epoch & 15] = 0;
     }
+    if constexpr (MD) {  // OrderBook.py:169
+      h.ob_last_update = cur;
+      h.has_last_update = 1;
+    }
   }
   DEV void cancel_order(const Msg& m) {
     int buy = m_buy(m);
@@ -1477,9 +1511,118 @@ struct Eng {
     if (s < 0) return;
     i32 q = b_get(bq, s), o = b_get(bo, s), mm = b_get(bm, s), p = b_get(bp, s);
     b_free(s);
-    if (blog) bl_put(cur, -p, buy ? q : -q);
+    if constexpr (BLOG) bl_put(cur, -p, buy ? q : -q);
     Msg r = msg_order(MK_CANCELLED, o, mm >> 1, mm & 1, q, p, 0);
     ex_notify(m_agent(m), r);
+    if constexpr (MD) {  // OrderBook.py:338
+      h.ob_last_update = cur;
+      h.has_last_update = 1;
+    }
+  }
+
+  // ---------------- market-data subscriptions (ExchangeAgent.py:342-387)
+  // the first n prices of one side, best first (levels are distinct prices)
+  DEV i32 b_top_prices(int buy_side, i32 n, i32* out) {
+    i32 k = 0, p = buy_side ? INT32_MAX : INT32_MIN;
+    for (int i = 0; i < MD_LEVELS; i++) {
+      out[i] = 0;
+      if (i >= n) continue;
+      i32 v = buy_side ? INT32_MIN : INT32_MAX;
+      for (int j = 0; j < SO; j++) {
+        bool c = bm[j] >= 0 && (bm[j] & 1) == buy_side && (buy_side ? bp[j] < p : bp[j] > p);
+        if (c) v = buy_side ? (bp[j] > v ? bp[j] : v) : (bp[j] < v ? bp[j] : v);
+      }
+      v = buy_side ? wmax_i32(v) : wmin_i32(v);
+      if (v == (buy_side ? INT32_MIN : INT32_MAX)) break;
+      out[i] = v;
+      p = v;
+      k++;
+    }
+    return k;
+  }
+  // updateSubscriptionDict: a request (re)sets the sender's entry in place, a cancellation
+  // deletes its symbol (the entry stays, empty)
+  DEV void md_subscribe(const Msg& m) {
+    const i32 sender = m_agent(m);
+    SubRec* S = subs();
+    const i32 ns = h.nsub;
+    const bool mine = lane < ns && S[lane < MD_MAX_SUBS ? lane : 0].agent == sender;
+    const u64 hit = bal(mine);
+    const int i = hit ? ffs64(hit) : ns;
+    if (m_kind(m) == MK_MD_SUB_CANCEL) {
+      if (!hit || !U(S[i].live)) {
+        fail(ERR_MD_KEYERROR);
+        return;
+      }
+      if (lane == 0) S[i].live = 0;
+      return;
+    }
+    if (i >= MD_MAX_SUBS) {
+      fail(ERR_MD_SUBS);
+      return;
+    }
+    if (lane == 0) {
+      SubRec r;
+      r.agent = sender;
+      r.levels = (i32)m.w[1];
+      r.live = 1;
+      r.pad = 0;
+      r.freq = m_i64(m, 2);
+      r.last = cur;
+      S[i] = r;
+    }
+    if (!hit) h.nsub = ns + 1;
+  }
+  // publishOrderBookData: every subscription, in insertion order, whose freq is 0 or whose last
+  // update is at least freq ns before the book's gets the top `levels` of both sides and the last
+  // trade.  The best levels travel in the message; the deeper prices wait in the subscriber's slot
+  // (freq >= the latency keeps one MARKET_DATA in flight per subscriber; a second one fails)
+  DEV void md_publish() {
+    const i32 ns = h.nsub;
+    SubRec* S = subs();
+    SubRec r;
+    r.agent = r.levels = r.live = 0;
+    r.freq = r.last = 0;
+    if (lane < ns) r = S[lane];
+    const bool live = lane < ns && r.live;
+    const bool due = live && (r.freq == 0 || (h.has_last_update && h.ob_last_update > r.last &&
+                                              (double)(h.ob_last_update - r.last) >= (double)r.freq));
+    if (bal(live && r.freq != 0 && !h.has_last_update)) {
+      fail(ERR_MD_NO_UPDATE);
+      return;
+    }
+    u64 b = bal(due);
+    if (!b) return;
+    i32 kb[MD_LEVELS], ka[MD_LEVELS];
+    const i32 nb = b_top_prices(1, MD_LEVELS, kb), na = b_top_prices(0, MD_LEVELS, ka);
+    const i64 bq = nb ? b_level_qty(1, kb[0]) : 0, aq = na ? b_level_qty(0, ka[0]) : 0;
+    while (b) {
+      const int L = ffs64(b);
+      b &= b - 1;
+      const i32 ag = rdli(r.agent, L), lv = rdli(r.levels, L);
+      const i32 nbs = nb < lv ? nb : lv, nas = na < lv ? na : lv;
+      const u32 tag = ++h.md_seq;
+      u32* slot = md_slot(ag);
+      u32 w = 0;
+      w = lane == MD_TAG ? tag : w;
+      w = lane == MD_COUNTS ? ((u32)nbs | ((u32)nas << 8)) : w;
+      for (int k = 0; k < MD_LEVELS; k++) {
+        w = lane == MD_BIDS + k ? (u32)(k < nbs ? kb[k] : 0) : w;
+        w = lane == MD_ASKS + k ? (u32)(k < nas ? ka[k] : 0) : w;
+      }
+      if (lane < MD_WORDS) slot[lane] = w;
+      Msg md = msg_make(MK_MARKET_DATA, 0);
+      md.w[0] |= (1u << 11) | ((u32)h.last_trade_float << 8);
+      md.w[1] = nbs ? (u32)kb[0] : 0;
+      md.w[2] = nbs ? (u32)bq : 0;
+      md.w[3] = nas ? (u32)ka[0] : 0;
+      md.w[4] = nas ? (u32)aq : 0;
+      md.w[5] = (u32)h.last_trade;
+      md.w[6] = (u32)nbs | ((u32)nas << 8);
+      md.w[7] = tag;
+      ex_notify(ag, md);
+      if (lane == L) S[L].last = h.ob_last_update;
+    }
   }
 
   // ExchangeAgent.receiveMessage (ExchangeAgent.py:129-340)
@@ -1580,9 +1723,19 @@ struct Eng {
     }
     case MK_LIMIT:
       handle_limit((i32)m.w[1], sender, m_buy(m), (i32)m.w[2], (i32)m.w[3]);
+      if constexpr (MD) {
+        if (h.nsub && status != ST_ERROR) md_publish();
+      }
       break;
     case MK_CANCEL:
       cancel_order(m);
+      if constexpr (MD) {
+        if (h.nsub && status != ST_ERROR) md_publish();
+      }
+      break;
+    case MK_MD_SUB_REQ:
+    case MK_MD_SUB_CANCEL:
+      if constexpr (MD) md_subscribe(m);
       break;
     default:
       break;
@@ -1829,6 +1982,20 @@ struct Eng {
     case MK_TV:
       if (m_closed(m)) fl_set(FL_MKT_CLOSED, true);
       rs64(AF_TV, m_i64(m, 1));
+      break;
+    case MK_MARKET_DATA:  // handleMarketData (TradingAgent.py:539-546): known levels, last trade
+      if constexpr (MD) {
+        u32 f = flags() | FL_HAS_KNOWN | FL_HAS_LAST;
+        f = (m.w[6] & 0xFF) ? (f | FL_NB) : (f & ~FL_NB);
+        f = (m.w[6] & 0xFF00) ? (f | FL_NA) : (f & ~FL_NA);
+        f = m_dfloat(m) ? (f | FL_LAST_FLOAT) : (f & ~FL_LAST_FLOAT);
+        rs(AF_FLAGS, f);
+        rs(AF_BID, m.w[1]);
+        rs(AF_BIDQ, m.w[2]);
+        rs(AF_ASK, m.w[3]);
+        rs(AF_ASKQ, m.w[4]);
+        rs64(AF_LAST_TRADE, (i64)(i32)m.w[5]);
+      }
       break;
     case MK_STREAM:  // queryOrderStream (TradingAgent.py:240-246, 549-554)
       if constexpr (OH) {
@@ -2123,15 +2290,73 @@ struct Eng {
   }
 
   // ---------------- MarketMakerAgent (agent/market_makers/MarketMakerAgent.py, polling mode)
+  // TradingAgent.requestDataSubscription (TradingAgent.py:160-172)
+  DEV void request_subscription(i32 levels) {
+    Msg m = msg_make(MK_MD_SUB_REQ, cur_agent);
+    m.w[1] = (u32)levels;
+    m.w[2] = (u32)(u64)PC.md_freq;
+    m.w[3] = (u32)((u64)PC.md_freq >> 32);
+    send_ex(m);
+    fl_set(FL_SUB_REQ, true);
+    rs(AF_STATE, AS_AWAITING_MD);
+  }
   DEV void mk_wakeup() {
-    if (ta_wakeup()) {  // MarketMakerAgent.py:69-79
+    const bool can = ta_wakeup();  // MarketMakerAgent.py:69-79
+    if constexpr (MD) {            // subscribe=True: one request, later wakeups do nothing
+      if (!fl(FL_SUB_REQ)) request_subscription(PC.md_mk_levels);
+      return;
+    }
+    if (can) {
       cancel_all();
       get_spread(PC.mk_depth);
       rs(AF_STATE, AS_AWAITING_SPREAD);
     }
   }
+  // MarketMakerAgent.receiveMessage subscribe branch + placeOrders (MarketMakerAgent.py:109-141):
+  // cancel every open order; num_levels = randint(1, 5) (1-4); with both sides known one size
+  // draw, then per side a dict price -> round(split[i] * size) in first-insertion order, where a
+  // missing level i quotes one cent beyond the last known level (repeated misses overwrite that
+  // entry); bids placed first
+  DEV void mk_market_data(const Msg& m) {
+    cancel_all();
+    RS A = agent_rs();
+    const i32 nl = (i32)rs_randint(A, 1, 5);
+    const i32 nb = (i32)(m.w[6] & 0xFF), na = (i32)((m.w[6] >> 8) & 0xFF);
+    if (!(nb && na)) {
+      agent_rs_put(A);
+      return;
+    }
+    const i64 size = (i64)__builtin_rint((double)rs_randint(A, PC.mk_min, PC.mk_max) / 2);
+    agent_rs_put(A);
+    rs(AF_SIZE, (u32)size);
+    const u32* slot = md_slot(cur_agent);
+    if (U(slot[MD_TAG]) != m.w[7]) {
+      fail(ERR_MD_SLOT);
+      return;
+    }
+    for (int side = 1; side >= 0; side--) {
+      const i32 n = side ? nb : na;
+      const int base = side ? MD_BIDS : MD_ASKS;
+      i32 px[MD_LEVELS], vol[MD_LEVELS];
+      int k = 0;
+      for (int i = 0; i < nl; i++) {
+        const double split = nl == 1 ? 1.0 : nl == 2 ? 0.5 : nl == 3 ? (i == 0 ? 0.34 : 0.33) : 0.25;
+        const i32 v = (i32)__builtin_rint(split * (double)size);
+        const i32 p = i < n ? (i32)U(slot[base + i]) : (i32)U(slot[base + n - 1]) + (side ? -1 : 1);
+        int j = 0;
+        while (j < k && px[j] != p) j++;
+        if (j == k) px[k++] = p;
+        vol[j] = v;
+      }
+      for (int j = 0; j < k; j++) place_limit(vol[j], side, px[j]);
+    }
+  }
   DEV void mk_receive(const Msg& m) {
     ta_receive(m, AG_MKTMAKER);  // MarketMakerAgent.py:81-107
+    if constexpr (MD) {
+      if (rgi(AF_STATE) == AS_AWAITING_MD && m_kind(m) == MK_MARKET_DATA) mk_market_data(m);
+      return;
+    }
     if (!(rgi(AF_STATE) == AS_AWAITING_SPREAD && m_kind(m) == MK_SPREAD)) return;
     cancel_all();
     i64 mid = rg64(AF_LAST_TRADE), spread;
@@ -2237,16 +2462,38 @@ struct Eng {
     if (!zi_update_estimates(v, buy)) return;
     const i32 n = rgi(AF_STREAM_N);
     const i64 hi = rg64(AF_STREAM_HI), lo_e = hi - n + 1;
-    if (lo_e < 0 || (i64)h.epoch - lo_e > PC.stream_history) {
-      fail(ERR_HBL_WINDOW);  // a streamed epoch left the 11-epoch window (same-instant trade burst)
+    if (lo_e < 0) {
+      fail(ERR_HBL_WINDOW);
       return;
     }
-    // ring records of epochs lo_e..hi: [s0, s1), walking back from the current epoch's start
-    LDSP i32* EP = ep_entries();
-    i32 s1 = h.oh_head - EP[h.epoch & 15];
-    for (i64 e = (i64)h.epoch - 1; e > hi; e--) s1 -= EP[e & 15];
-    i32 s0 = s1;
-    for (i64 e = hi; e >= lo_e; e--) s0 -= EP[e & 15];
+    // ring records of epochs lo_e..hi: [s0, s1).  Epochs that left the exchange's 11-epoch window
+    // since the reply (with latency, trades keep coming) are the dicts the reply still holds:
+    // frozen, their records unchanged in the ring
+    i32 s0, s1;
+    if ((i64)h.epoch - lo_e <= 15) {  // within the 16-epoch entry-count ring: walk back from the current epoch
+      LDSP i32* EP = ep_entries();
+      s1 = h.oh_head - EP[h.epoch & 15];
+      for (i64 e = (i64)h.epoch - 1; e > hi; e--) s1 -= EP[e & 15];
+      s0 = s1;
+      for (i64 e = hi; e >= lo_e; e--) s0 -= EP[e & 15];
+    } else {  // older: count the ring's records by their epoch tags, newest chunk first
+      const OhRec* R0 = ohr();
+      i32 c0 = 0, c1 = 0;
+      for (i32 top = h.oh_head; top > 0; top -= 64) {
+        const i32 lo = top > 64 ? top - 64 : 0;
+        if (h.oh_head - lo > PC.L.oh_cap) {
+          fail(ERR_HBL_WINDOW);
+          return;
+        }
+        const i32 k = lo + lane;
+        const i64 ep = k < top ? (i64)R0[k % PC.L.oh_cap].epoch : (i64)INT32_MAX;
+        c1 += __popcll(bal(k < top && ep > hi));
+        c0 += __popcll(bal(k < top && ep >= lo_e));
+        if (bal(k < top && ep < lo_e)) break;
+      }
+      s1 = h.oh_head - c1;
+      s0 = h.oh_head - c0;
+    }
     if (h.oh_head - s0 > PC.L.oh_cap) {
       fail(ERR_HBL_WINDOW);  // overwritten in the device ring (MXA_OH_CAP)
       return;
@@ -2336,36 +2583,51 @@ struct Eng {
     return __builtin_rint(x * 100.0) / 100.0;
   }
   DEV void mom_wakeup() {
-    if (ta_wakeup()) {
+    const bool can = ta_wakeup();
+    if constexpr (MD) {  // subscribe=True (MomentumAgent.py:54-62): level-1 data every 10 s
+      if (!fl(FL_SUB_REQ)) request_subscription(PC.md_mom_levels);
+      return;
+    }
+    if (can) {
       get_spread(1);
       rs(AF_STATE, AS_AWAITING_SPREAD);
     }
   }
   DEV void mom_receive(const Msg& m) {
     ta_receive(m, AG_MOMENTUM);
+    if constexpr (MD) {  // MomentumAgent.py:71-75: `if bids and asks`, then placeOrders(best bid, best ask)
+      if (rgi(AF_STATE) == AS_AWAITING_MD && m_kind(m) == MK_MARKET_DATA) {
+        i32 bid, ask;
+        const bool hb = known_bid(bid), ha = known_ask(ask);
+        if (hb && ha) mom_place(bid, ask);
+      }
+      return;
+    }
     if (rgi(AF_STATE) == AS_AWAITING_SPREAD && m_kind(m) == MK_SPREAD) {
       i32 bid, ask;
       bool hb = known_bid(bid), ha = known_ask(ask);
-      if (hb && ha) {
-        i32 nm = rgi(AF_NMID);
-        rs(AF_MIDS + (nm % 50), (u32)(bid + ask));
-        nm++;
-        rs(AF_NMID, (u32)nm);
-        if (nm > 20) {
-          rsd(AF_AVG20, mom_avg(20));
-          rs(AF_N20, rg(AF_N20) + 1);
-        }
-        if (nm > 50) {
-          rsd(AF_AVG50, mom_avg(50));
-          rs(AF_N50, rg(AF_N50) + 1);
-        }
-        if (rgi(AF_N20) > 0 && rgi(AF_N50) > 0) {
-          if (rgd(AF_AVG20) >= rgd(AF_AVG50)) place_limit(rgi(AF_SIZE), 1, ask);
-          else place_limit(rgi(AF_SIZE), 0, bid);
-        }
-      }
+      if (hb && ha) mom_place(bid, ask);
       wakeup_at(cur_agent, cur + PC.mom_wake);
       rs(AF_STATE, AS_AWAITING_WAKEUP);
+    }
+  }
+  // MomentumAgent.placeOrders (MomentumAgent.py:82-93) with both prices known
+  DEV void mom_place(i32 bid, i32 ask) {
+    i32 nm = rgi(AF_NMID);
+    rs(AF_MIDS + (nm % 50), (u32)(bid + ask));
+    nm++;
+    rs(AF_NMID, (u32)nm);
+    if (nm > 20) {
+      rsd(AF_AVG20, mom_avg(20));
+      rs(AF_N20, rg(AF_N20) + 1);
+    }
+    if (nm > 50) {
+      rsd(AF_AVG50, mom_avg(50));
+      rs(AF_N50, rg(AF_N50) + 1);
+    }
+    if (rgi(AF_N20) > 0 && rgi(AF_N50) > 0) {
+      if (rgd(AF_AVG20) >= rgd(AF_AVG50)) place_limit(rgi(AF_SIZE), 1, ask);
+      else place_limit(rgi(AF_SIZE), 0, bid);
     }
   }
 
@@ -3170,7 +3432,7 @@ struct Eng {
   DEV void account_pop(i64 t, u64 key, const Msg& m) {
     cur = t;
     if (hash_on || trace) {  // parity instrumentation (trace ring, per-pop hash)
-      const Rec rec = encode<PW == 8>(key, m);
+      const Rec rec = encode<PW == 8, MD>(key, m);
       if (hash_on) hash = rec_hash(hash, rec);
       if (trace && h.trace_len < trace_cap) {
         if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
@@ -3505,7 +3767,7 @@ struct Eng {
         // a run past stopTime is not batched: the loop stops after its first member
         if (type == MT_MESSAGE && (m.w[0] & MF_RUN) && t <= PC.stop && eseq >= run_skip) {
           const u32 k = m_kind(m);
-          const bool exr = rcp == 0 && (k == MK_CANCEL || k == MK_LIMIT) && !(t > PC.mkt_close) && !blog;
+          const bool exr = rcp == 0 && (k == MK_CANCEL || k == MK_LIMIT) && !(t > PC.mkt_close) && !BLOG && !MD;
           const bool ackr = rcp > 0 && rcp < ACK_LIMIT && (k == MK_ACCEPTED || k == MK_CANCELLED);
           if (exr || ackr) {
             PROF_ADD(0, t0);
@@ -3599,7 +3861,7 @@ struct Eng {
       rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
       cur = t;
       if (hash_on || trace) {
-        const Rec rec = encode<PW == 8>(key, m);
+        const Rec rec = encode<PW == 8, MD>(key, m);
         if (hash_on) hash = rec_hash(hash, rec);
         if (trace && h.trace_len < trace_cap) {
           if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
@@ -3844,10 +4106,11 @@ struct Builder : Eng<CFG, true> {
         init_gym();
       }
       set_seed(2, g_seed(G));  // K
-    } else if (P.config == MXA_CFG_RMSC01) {
+    } else if (P.config == MXA_CFG_RMSC01 || P.config == MXA_CFG_RMSC02) {
       // config/rmsc01.py: the exchange's seed, the market maker's, the oracle symbol's, the
       // oracle's first megashock time, per ZI and HBL agent its seed, per momentum agent its
-      // seed, the kernel's (each agent's own __init__ draws come after seed_streams)
+      // seed, the kernel's (each agent's own __init__ draws come after seed_streams);
+      // config/rmsc02.py then draws the 101 x 101 latency matrix
       set_seed(4 + 0, g_seed(G));  // exchange
       for (int a = P.first_mk; a < P.first_mk + P.n_mk; a++) {
         set_seed(4 + a, g_seed(G));
@@ -3872,6 +4135,23 @@ struct Builder : Eng<CFG, true> {
         this->rec_store();
       }
       set_seed(2, g_seed(G));  // K
+      if (P.config == MXA_CFG_RMSC02) {  // G.uniform(lo, hi, (n, n)), C order: row 0, then column 0
+        double* lat = this->lat();
+        const i64 total = (i64)n * n;
+        i64 prev = -1;
+        for (i64 k = 0; k < 2 * (i64)n - 1; k++) {
+          const i64 d = k < n ? k : (k - n + 1) * (i64)n;
+          rs_skip_words(G, 2 * (d - prev - 1));
+          const double v = rs_uniform(G, P.lat_lo, P.lat_hi);
+          if (this->lane == 0) {
+            if (d < n) lat[d] = v;        // latency[0][d]: exchange -> agent d
+            if (d % n == 0) lat[n + d / n] = v;  // latency[d / n][0]: agent -> exchange
+          }
+          prev = d;
+        }
+        rs_skip_words(G, 2 * (total - prev - 1));
+        wfence();
+      }
       if constexpr (E::OH) {  // the HBL price histogram starts (and stays) zeroed
         u64* hist = (u64*)(this->env + P.L.off_hh);
         for (int i = this->lane; i < P.L.hbl_range; i += 64) hist[i] = 0;
@@ -4053,7 +4333,7 @@ __global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stri
   b.build(seeds[env]);
 }
 
-template <int CFG>
+template <int CFG, bool LOG>
 __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops,
                                                                               const RpCtx* ctx, BlRec* blog, int blog_cap) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -4061,7 +4341,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
   if (((EnvHdr*)e)->status != ST_RUNNING) return;
-  mxa::Eng<CFG> g(e, lds, trace_cap, ctx, blog ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
+  mxa::Eng<CFG, false, LOG> g(e, lds, trace_cap, ctx, LOG ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
   g.load();
   g.run(max_pops);
   g.save();
@@ -4070,19 +4350,19 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
 #endif
 }
 
-template <int CFG>
+template <int CFG, bool LOG>
 __global__ __launch_bounds__(64) void mxa_stop_kernel(char* base, uint64_t stride, int n_envs, mxa_agent_final* out,
                                                       BlRec* blog, int blog_cap) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int env = blockIdx.x;
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
-  mxa::Eng<CFG> g(e, lds, 0, nullptr, blog ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
+  mxa::Eng<CFG, false, LOG> g(e, lds, 0, nullptr, LOG ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
   g.load();
   g.stop(out + (size_t)env * mxa::Eng<CFG>::PC.n_agents);  // no save(): the pass is idempotent
   // the oracle observations of the pass append to the log after the run's records; only
   // their end is kept (a second pass rewrites the same records)
-  if (blog && g.lane == 0) ((EnvHdr*)e)->blog_fin = g.h.blog_n;
+  if (LOG && g.lane == 0) ((EnvHdr*)e)->blog_fin = g.h.blog_n;
 }
 
 #ifndef MXA_ONLY_RMSC03
@@ -4125,6 +4405,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
 }
 #endif
 
+#ifdef MXA_API_TU  // (compiled once, in the C-ABI translation unit)
 // parity helpers: numpy-legacy RNG draws and glibc math on the device (tests only call
 // these through the C-ABI; they exercise exactly the device functions the engine uses)
 __global__ __launch_bounds__(64) void mxa_rng_probe_kernel(uint32_t seed, int mode, double a, double b, int n, double* out, uint32_t* scratch) {
@@ -4154,22 +4435,4 @@ __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y
   if (i >= n) return;
   out[i] = mode == 0 ? gm_log(x[i]) : mode == 1 ? gm_exp(x[i]) : gm_pow(x[i], y[i]);
 }
-
-// explicit instantiations per supported configuration
-#define MXA_INST(CFG)                                                                                      \
-  template __global__ void mxa_build_kernel<CFG>(char*, uint64_t, int, const uint32_t*, const uint8_t*, const RpCtx*); \
-  template __global__ void mxa_run_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*, BlRec*, int);  \
-  template __global__ void mxa_stop_kernel<CFG>(char*, uint64_t, int, mxa_agent_final*, BlRec*, int);
-MXA_INST(MXA_CFG_RMSC03)
-#ifndef MXA_ONLY_RMSC03
-MXA_INST(MXA_CFG_SPARSE_ZI_100)
-MXA_INST(MXA_CFG_SPARSE_ZI_1000)
-MXA_INST(MXA_CFG_MARKETREPLAY)
-MXA_INST(MXA_CFG_RMSC03_RL)
-MXA_INST(MXA_CFG_VALUE_NOISE)
-MXA_INST(MXA_CFG_RMSC01)
-#define MXA_INST_STEP(CFG) \
-  template __global__ void mxa_step_kernel<CFG>(char*, uint64_t, int, int, int64_t, const RpCtx*, const double*, double*, int32_t*);
-MXA_INST_STEP(MXA_CFG_MARKETREPLAY)
-MXA_INST_STEP(MXA_CFG_RMSC03_RL)
 #endif

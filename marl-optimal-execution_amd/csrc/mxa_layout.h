@@ -16,7 +16,8 @@
 #define MXA_RNG_WORDS 1280    // two 624-word MT blocks (double buffer) + pad (5120 B per stream)
 
 enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3,
-                     MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6 };
+                     MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6,
+                     MXA_CFG_RMSC02 = 7 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -24,7 +25,8 @@ enum {
   MK_SPREAD_REQ = 5, MK_SPREAD = 6, MK_LAST_REQ = 7, MK_LAST = 8, MK_TV_REQ = 9, MK_TV = 10,
   MK_LIMIT = 11, MK_CANCEL = 12, MK_MODIFY = 13, MK_ACCEPTED = 14, MK_EXECUTED = 15, MK_CANCELLED = 16,
   MK_MKT_CLOSED = 17, MK_MODIFIED = 18, MK_KCANCEL = 19, MK_MARKET_DATA = 20,
-  MK_STREAM_REQ = 21, MK_STREAM = 22  // QUERY_ORDER_STREAM request / reply
+  MK_STREAM_REQ = 21, MK_STREAM = 22,  // QUERY_ORDER_STREAM request / reply
+  MK_MD_SUB_REQ = 23, MK_MD_SUB_CANCEL = 24  // MARKET_DATA_SUBSCRIPTION_REQUEST / _CANCELLATION
 };
 // kernel message types (message/Message.py:5-8)
 enum { MT_MESSAGE = 1, MT_WAKEUP = 2, MT_CANCEL_ORDER = 3 };
@@ -51,7 +53,12 @@ enum {
   ERR_HBL_WINDOW = 17,    // a streamed history epoch left the exchange's window / the device ring
   ERR_HBL_RANGE = 18,     // streamed price range beyond the device scratch (MXA_HBL_RANGE)
   ERR_FLOAT_PRICE = 19,   // a limit price that the reference would carry as a python float (not restated)
-  ERR_BOOK_LOG_FULL = 20  // the book-update log of mxa_set_book_log ran out of records
+  ERR_BOOK_LOG_FULL = 20, // the book-update log of mxa_set_book_log ran out of records
+  // market-data subscriptions (ExchangeAgent.publishOrderBookData)
+  ERR_MD_NO_UPDATE = 21,  // a publish before the book's first change: None > Timestamp (TypeError)
+  ERR_MD_SUBS = 22,       // more subscriptions than the device table (64)
+  ERR_MD_KEYERROR = 23,   // cancelling a subscription that does not exist (KeyError)
+  ERR_MD_SLOT = 24        // a second MARKET_DATA in flight to one agent (freq below the latency)
 };
 
 // per-env scalar header (first bytes of the env block)
@@ -84,6 +91,9 @@ typedef struct {
   int32_t max_q, max_book;       // capacity high-water marks (diagnostics)
   double o_th2;                  // oracle fund_vol ** 2 (glibc pow, evaluated at build)
   int32_t blog_fin, pad3;        // book-update log: records after the last kernelStopping pass
+  int64_t ob_last_update;        // OrderBook.last_update_ts (market-data configs)
+  int32_t nsub, has_last_update; // ExchangeAgent.subscription_dict entries; last_update_ts not None
+  uint32_t md_seq, pad4;         // MARKET_DATA messages sent (their snapshot-slot tags)
 } EnvHdr;
 
 #ifdef __cplusplus
@@ -129,6 +139,15 @@ typedef struct {  // OrderBook.history entry of one limit order (util/OrderBook.
   int32_t meta;   // bit0 is_buy_order, bit1 "transactions" non-empty
   int32_t epoch;  // absolute history epoch it was entered in
 } OhRec;
+
+typedef struct {  // ExchangeAgent.subscription_dict entry (agent -> [levels, freq, last update])
+  int32_t agent, levels;
+  int32_t live, pad;
+  int64_t freq, last;
+} SubRec;         // 32 B
+// MARKET_DATA snapshot slot of one subscriber (16 words): the message carries the best levels
+// and the last trade (and the slot tag); the deeper level prices wait here for the receipt
+enum { MD_TAG = 0, MD_COUNTS = 1, MD_BIDS = 4, MD_ASKS = 9, MD_WORDS = 16, MD_LEVELS = 5, MD_MAX_SUBS = 64 };
 
 typedef struct {  // TradingAgent.orders entry (agent's copy of an open order)
   int32_t oid, is_buy, qty, price;
@@ -190,6 +209,7 @@ typedef struct {
   int32_t n_agents, n_streams, qcap, ocap, open_cap, tx_cap, trace_cap, lat_len;
   int32_t oh_cap, hbl_range;    // order-history ring records; HBL price-histogram bins (0: none)
   uint64_t off_oh, off_hh;      // order-history ring; HBL histogram scratch (u64 bins)
+  uint64_t off_sub, off_md;     // subscription table [MD_MAX_SUBS]; per-agent MARKET_DATA slots
 } Layout;
 
 // agent record: 128 dwords (512 B); lane i of the owning wave holds dwords 2i, 2i+1
@@ -215,9 +235,10 @@ enum {
   FL_HAS_OPEN = 1, FL_HAS_CLOSE = 2, FL_MKT_CLOSED = 4, FL_FIRST_WAKE = 8, FL_DAILY_CLOSE = 16,
   FL_TRADING = 32, FL_HAS_KNOWN = 64, FL_NB = 128, FL_NA = 256, FL_HAS_LAST = 512,
   FL_LAST_FLOAT = 1024, FL_PREV_WAKE = 2048, FL_AW_SPREAD = 4096, FL_AW_TV = 8192, FL_LAST_MID = 16384,
-  FL_HAS_STREAM = 32768
+  FL_HAS_STREAM = 32768, FL_SUB_REQ = 65536
 };
-enum { AS_AWAITING_WAKEUP = 0, AS_INACTIVE = 1, AS_AWAITING_SPREAD = 2, AS_ACTIVE = 3, AS_AWAITING_STREAM = 4 };
+enum { AS_AWAITING_WAKEUP = 0, AS_INACTIVE = 1, AS_AWAITING_SPREAD = 2, AS_ACTIVE = 3, AS_AWAITING_STREAM = 4,
+       AS_AWAITING_MD = 5 };
 
 typedef struct {
   int32_t config, n_envs, n_agents, n_streams;
@@ -258,6 +279,9 @@ typedef struct {
   int64_t mk_wake, mk_last_spread;
   // HeuristicBeliefLearningAgent (ZI parameters of group 0, plus L)
   int32_t first_hbl, n_hbl, hbl_L, pad5;
+  // market-data subscriptions (rmsc02: MarketMakerAgent / MomentumAgent subscribe=True)
+  int32_t md_sub, md_mk_levels, md_mom_levels, lat_asym;  // lat_asym: latency row 0 + column 0
+  int64_t md_freq;
   Layout L;
 } MxaParams;
 

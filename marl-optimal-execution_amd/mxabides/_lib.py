@@ -11,8 +11,9 @@ LIB_PATH = os.environ.get("MXA_LIB") or os.path.join(PKG_ROOT, "lib", "libmxa.so
 
 MXA_RMSC03, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000, MXA_MARKETREPLAY, MXA_RMSC03_RL, MXA_VALUE_NOISE = 0, 1, 2, 3, 4, 5
 MXA_RMSC01 = 6
+MXA_RMSC02 = 7
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000,
-              "value_noise": MXA_VALUE_NOISE, "rmsc01": MXA_RMSC01}
+              "value_noise": MXA_VALUE_NOISE, "rmsc01": MXA_RMSC01, "rmsc02": MXA_RMSC02}
 ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
 ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",
              4: "transaction history capacity", 5: "get_transacted_volume without transactions (pandas error)",
@@ -24,7 +25,11 @@ ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: 
              17: "HBL order stream outside the history window / device ring (MXA_OH_CAP)",
              18: "HBL streamed price range beyond the device histogram (MXA_HBL_RANGE)",
              19: "limit price the reference would carry as a python float (not restated)",
-             20: "book-update log full (raise the book_log capacity)"}
+             20: "book-update log full (raise the book_log capacity)",
+             21: "market data published before the book's first change (the reference's TypeError)",
+             22: "more market-data subscriptions than the device table",
+             23: "cancelled a market-data subscription that does not exist (KeyError)",
+             24: "two MARKET_DATA messages in flight to one agent (subscription freq below the latency)"}
 
 
 class EnvSummary(ctypes.Structure):

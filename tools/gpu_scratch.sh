@@ -1,9 +1,10 @@
 set -o pipefail
-export TMPDIR=/tmp
-R=$PWD
-OUT=$R/gpurun_out/r2p5
-mkdir -p $OUT
-MXA_LIB=$R/marl-optimal-execution_amd/lib/libmxa_vexp.so timeout -k 10 300 python tools/prof_phases.py > $OUT/phases_vexp.txt 2>&1 || { echo "phases failed"; tail $OUT/phases_vexp.txt; exit 1; }
-cat $OUT/phases_vexp.txt
-cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_rl -o run -- python3 $R/bench.py --config rmsc03_rl --no-cpu --steps 2 --warmup 1 > $OUT/trace_rl.log 2>&1 || { echo "trace failed"; tail $OUT/trace_rl.log; exit 1; }
+O=gpurun_out/r02d
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for r in 1 2; do
+for lib in libmxa_nof.so libmxa.so; do
+  MXA_LIB=$PWD/marl-optimal-execution_amd/lib/$lib timeout -k 10 300 python tools/ab_config.py rmsc03 4096 3 || exit 1
+done
+done
