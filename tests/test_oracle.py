@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import pyoracle
-from golden_util import FIXTURES, first_mismatch, kat_lines, load
+from golden_util import FIXTURES, GOLDEN, first_mismatch, kat_lines, load
 
 
 @pytest.mark.parametrize("cfg,seed", FIXTURES)
@@ -88,3 +88,23 @@ def test_oracle_summary_log_matches_reference(cfg, seed):
     assert len(got) == len(ref)
     for a, b in zip(got, ref):
         assert a == b and type(a["Event"]) is type(b["Event"]), (a, b)
+
+
+def test_oracle_rmsc01_kernel_stopping_index_error():
+    """rmsc01 seed 123456789: the reference's own run ends in an IndexError inside
+    ZeroIntelligenceAgent.kernelStopping (agent 42's holdings index past its theta table); the
+    fixture holds the trace, the book and the stdout / summary rows written before the crash"""
+    d, ref = load("rmsc01", 123456789)
+    assert d["stop_error"].startswith("IndexError")
+    e = pyoracle.OracleEnv("rmsc01", 123456789, trace_cap=len(ref))
+    e.run()
+    assert e.error[0] == 0 and first_mismatch(e.trace(), ref) == -1
+    assert e.events == d["events"] and "%016x" % e.hash == d["hash"]
+    assert e.book(0) == d["bids"] and e.book(1) == d["asks"]
+    e.finish()
+    assert e.error[0] == -10
+    rep = [l for l in e.report() if l.startswith("Final holdings")]
+    assert rep[:len(d["final_holdings_lines"])] == d["final_holdings_lines"]
+    with open(os.path.join(GOLDEN, "rmsc01_123456789_summary.json")) as f:
+        summ = json.load(f)
+    assert e.summary_log()[:len(summ)] == summ
