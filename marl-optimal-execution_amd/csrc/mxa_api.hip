@@ -80,6 +80,7 @@ struct mxa_handle {
   size_t lds = 0;
   mxa_build_fn build = nullptr;
   mxa_run_fn run = nullptr, run_log = nullptr;     // run_log: with the book-update log
+  mxa_run_fn run_fast = nullptr;                   // hash off, no trace ring: instrumentation compiled out
   mxa_step_fn step = nullptr;                      // GymKernel handles (replay, rmsc03_rl)
   mxa_stop_fn stop = nullptr, stop_log = nullptr;  // kernelStopping pass (plain Kernel.runner configs)
   mxa_agent_final* d_final = nullptr;
@@ -98,6 +99,12 @@ struct mxa_handle {
   int32_t* d_flags = nullptr;
   bool parity_hash = true;  // per-pop trace hash (test instrumentation); off: kernel tcap -1
   int32_t tcap_arg() const { return (parity_hash || P.L.trace_cap > 0) ? P.L.trace_cap : -1; }
+  // the run kernel of the current settings: the log variant, the instrumented one, or (hash off,
+  // no trace ring) the one without the parity instrumentation
+  mxa_run_fn run_kernel() const {
+    if (d_blog) return run_log;
+    return (tcap_arg() < 0 && run_fast) ? run_fast : run;
+  }
   std::vector<char> tape_blob;  // host staging of the tape (uploaded by create_common)
   size_t tb_t, tb_oid, tb_dense, tb_price, tb_size, tb_buy, tb_tm, tb_tm0;
 };
@@ -133,6 +140,7 @@ static bool bind(mxa_handle* h, int cfg) {
   h->build = e.build;
   h->run = e.run;
   h->run_log = e.run_log;
+  h->run_fast = e.run_fast;
   h->stop = e.stop;
   h->stop_log = e.stop_log;
   h->step = e.step;
@@ -372,7 +380,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
 
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
   if (!h || h->gym) return MXA_EINVAL;  // GymKernel handles advance by mxa_step
-  (h->d_blog ? h->run_log : h->run)(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
+  h->run_kernel()(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
          h->d_ctx, h->d_blog, h->blog_cap);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
@@ -392,7 +400,7 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   for (;;) {
     if (max_launches > 0 && launches >= max_launches) break;
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    (h->d_blog ? h->run_log : h->run)(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), chunk,
+    h->run_kernel()(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), chunk,
            h->d_ctx, h->d_blog, h->blog_cap);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));

@@ -29,6 +29,9 @@ struct Shape {
 #ifndef MXA_RMSC03_WAVES
 #define MXA_RMSC03_WAVES 4
 #endif
+#ifndef MXA_RMSC01_WAVES
+#define MXA_RMSC01_WAVES 4
+#endif
 #ifndef MXA_HOT_RECORDS
 #define MXA_HOT_RECORDS 0  // measured (r01 s3i): exchange + MM records in LDS were 3 % slower than L1/L2-served loads
 #endif
@@ -40,7 +43,7 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_RMSC03_RL ? Shape{3, 2, true, 4, 8, 2 * MXA_HOT_RECORDS}  // wide spread replies (depth 500)
        // rmsc01: oracle maxima over seeds 123456789 / 7: 140 pending events, 75 resting orders;
        // wide replies for the market maker's depth-5 spread queries
-       : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, 4, 8, 0}
+       : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, MXA_RMSC01_WAVES, 8, 0}
        // rmsc02: oracle maxima over 41 seeds: 225 pending events, 299 resting orders
        : cfg == MXA_CFG_RMSC02 ? Shape{6, 5, true, 2, 8, 0}
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6, MXA_HOT_RECORDS}

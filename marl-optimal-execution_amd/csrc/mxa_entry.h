@@ -20,6 +20,7 @@ typedef void (*mxa_step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, in
 struct MxaEntry {
   mxa_build_fn build;
   mxa_run_fn run, run_log;     // run_log: the book-update-log variant (plain Kernel.runner configs)
+  mxa_run_fn run_fast;         // without the parity instrumentation (hash off, no trace ring)
   mxa_stop_fn stop, stop_log;
   mxa_step_fn step;            // GymKernel configurations
 };

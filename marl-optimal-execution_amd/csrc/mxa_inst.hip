@@ -14,10 +14,11 @@ void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_
                   const uint8_t* mask, const RpCtx* ctx) {
   hipLaunchKernelGGL((mxa_build_kernel<CFG>), g, b, lds, s, base, stride, n, seeds, mask, ctx);
 }
-template <int CFG, bool LOG>
+template <int CFG, bool LOG, bool INSTR>
 void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
                 const RpCtx* ctx, BlRec* blog, int blog_cap) {
-  hipLaunchKernelGGL((mxa_run_kernel<CFG, LOG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, blog, blog_cap);
+  hipLaunchKernelGGL((mxa_run_kernel<CFG, LOG, INSTR>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, blog,
+                     blog_cap);
 }
 template <int CFG, bool LOG>
 void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, mxa_agent_final* out,
@@ -36,11 +37,19 @@ template <int CFG>
 MxaEntry make_entry() {
   MxaEntry e{};
   e.build = launch_build<CFG>;
-  e.run = launch_run<CFG, false>;
+  e.run = launch_run<CFG, false, true>;
   e.stop = launch_stop<CFG, false>;
   constexpr bool gym = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL;
   if constexpr (!gym) {  // the book-update log: plain Kernel.runner configurations
-    e.run_log = launch_run<CFG, true>;
+    e.run_log = launch_run<CFG, true, true>;
+    // measured per configuration (one box, hash off, run kernel): without the instrumentation
+    // rmsc03 44.1 vs 44.6 ms, sparse_zi_100 132.5 vs 135.1, value_noise 22.1 vs 22.5, rmsc02
+    // 1190 vs 1245; but rmsc01 1201 vs 1147 and sparse_zi_1000 986 vs 976 (their register
+    // allocation comes out worse), so those two keep the instrumented kernel
+    constexpr bool fast = CFG != MXA_CFG_RMSC01 && CFG != MXA_CFG_SPARSE_ZI_1000;
+#ifndef MXA_NO_FAST
+    if constexpr (fast) e.run_fast = launch_run<CFG, false, false>;
+#endif
     e.stop_log = launch_stop<CFG, true>;
   }
 #ifndef MXA_ONLY_RMSC03

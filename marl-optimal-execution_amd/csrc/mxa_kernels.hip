@@ -501,7 +501,7 @@ DEV u64 stamp() {
 #define PROF_ADD(b, v)
 #define PROF_CNT(b)
 #endif
-template <int CFG, bool BUILD = false, bool LOG = false>
+template <int CFG, bool BUILD = false, bool LOG = false, bool INSTR = true>
 struct Eng {
   // every configuration constant is an immediate (mxa_config.h)
   static constexpr MxaParams PC = mxa_cfg::params(CFG);
@@ -3431,7 +3431,7 @@ struct Eng {
   // the per-pop bookkeeping of the fast paths: currentTime, parity trace + hash, ttl_messages
   DEV void account_pop(i64 t, u64 key, const Msg& m) {
     cur = t;
-    if (hash_on || trace) {  // parity instrumentation (trace ring, per-pop hash)
+    if (INSTR && (hash_on || trace)) {  // parity instrumentation (trace ring, per-pop hash)
       const Rec rec = encode<PW == 8, MD>(key, m);
       if (hash_on) hash = rec_hash(hash, rec);
       if (trace && h.trace_len < trace_cap) {
@@ -3490,7 +3490,7 @@ struct Eng {
   }
   // per-pop accounting of the members, in member order
   DEV void run_account(u64 key, i64 t, const Msg& mm, int n) {
-    if (hash_on || trace) {
+    if (INSTR && (hash_on || trace)) {
       for (int i = 0; i < n; i++) {
         Msg m;
         for (int w = 0; w < 8; w++) m.w[w] = w < PW ? rdl(mm.w[w], i) : 0u;
@@ -3860,7 +3860,7 @@ struct Eng {
       PROF_ADD(0, t0);
       rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
       cur = t;
-      if (hash_on || trace) {
+      if (INSTR && (hash_on || trace)) {
         const Rec rec = encode<PW == 8, MD>(key, m);
         if (hash_on) hash = rec_hash(hash, rec);
         if (trace && h.trace_len < trace_cap) {
@@ -4333,7 +4333,9 @@ __global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stri
   b.build(seeds[env]);
 }
 
-template <int CFG, bool LOG>
+// INSTR: the parity instrumentation (per-pop hash, trace ring) compiled in; the variant without
+// it is what a run with the hash off and no trace ring launches (same results, fewer registers)
+template <int CFG, bool LOG, bool INSTR>
 __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops,
                                                                               const RpCtx* ctx, BlRec* blog, int blog_cap) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -4341,7 +4343,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
   if (((EnvHdr*)e)->status != ST_RUNNING) return;
-  mxa::Eng<CFG, false, LOG> g(e, lds, trace_cap, ctx, LOG ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
+  mxa::Eng<CFG, false, LOG, INSTR> g(e, lds, trace_cap, ctx, LOG ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
   g.load();
   g.run(max_pops);
   g.save();
