@@ -136,7 +136,7 @@ enum {
     K_STREAM_REQ = 21, K_STREAM = 22, /* QUERY_ORDER_STREAM request / reply */
     K_MD_SUB_REQ = 23, K_MD_SUB_CANCEL = 24 /* MARKET_DATA_SUBSCRIPTION_REQUEST / _CANCELLATION */
 };
-#define MD_LEVELS 5 /* deepest market-data subscription restated (MarketMakerAgent's 5 levels) */
+#define MD_LEVELS 10 /* deepest market-data subscription restated (OrderBookImbalanceAgent's 10 levels) */
 enum { T_MESSAGE = 1, T_WAKEUP = 2, T_CANCEL_ORDER = 3 };
 
 typedef struct {
@@ -159,8 +159,8 @@ typedef struct {
     /* MODIFY_ORDER: the agent's current copy of the order (the new order is oid/qty/price) */
     int64_t ooid, oqty, oprice;
     int obuy, oagent2;
-    /* MARKET_DATA: level prices, best first (nb / na levels; bq / aq the best volumes) */
-    int64_t lvb[MD_LEVELS], lva[MD_LEVELS];
+    /* MARKET_DATA: level prices and volumes, best first (nb / na levels; bq / aq the best volumes) */
+    int64_t lvb[MD_LEVELS], lva[MD_LEVELS], lvbq[MD_LEVELS], lvaq[MD_LEVELS];
     /* MARKET_DATA_SUBSCRIPTION_REQUEST: levels in depth, freq in lookback */
 } msg_t;
 
@@ -206,7 +206,7 @@ typedef struct {
 /* ------------------------------------------------------------------------- */
 /* agents                                                                     */
 /* ------------------------------------------------------------------------- */
-enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL, AG_MKTMAKER, AG_HBL };
+enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL, AG_MKTMAKER, AG_HBL, AG_OBI };
 enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE, ST_AWAITING_STREAM, ST_AWAITING_MARKET_DATA };
 
 typedef struct {
@@ -263,6 +263,9 @@ typedef struct {
      * level prices of the last MARKET_DATA (TradingAgent.known_bids / known_asks) */
     int subscribe, sub_requested;
     int64_t kb[MD_LEVELS], ka[MD_LEVELS];
+    /* OrderBookImbalanceAgent: position state and trailing stop */
+    int obi_long, obi_short;
+    double obi_stop;
 } agent_t;
 
 #define HIST_RETIRED 48
@@ -934,15 +937,21 @@ static void publish(ora_env* e) {
             fail(e, -15, "market-data subscription deeper than the restated levels");
             return;
         }
-        for (int k = 0; k < r.nb; k++) r.lvb[k] = b->lv[k].o[0].price;
-        for (int k = 0; k < r.na; k++) r.lva[k] = a->lv[k].o[0].price;
+        for (int k = 0; k < r.nb; k++) {
+            r.lvb[k] = b->lv[k].o[0].price;
+            for (int j = 0; j < b->lv[k].n; j++) r.lvbq[k] += b->lv[k].o[j].qty;
+        }
+        for (int k = 0; k < r.na; k++) {
+            r.lva[k] = a->lv[k].o[0].price;
+            for (int j = 0; j < a->lv[k].n; j++) r.lvaq[k] += a->lv[k].o[j].qty;
+        }
         if (r.nb) {
             r.bpx = r.lvb[0];
-            for (int j = 0; j < b->lv[0].n; j++) r.bq += b->lv[0].o[j].qty;
+            r.bq = r.lvbq[0];
         }
         if (r.na) {
             r.apx = r.lva[0];
-            for (int j = 0; j < a->lv[0].n; j++) r.aq += a->lv[0].o[j].qty;
+            r.aq = r.lvaq[0];
         }
         r.data = e->last_trade;
         r.data_float = e->last_trade_float;
@@ -1202,6 +1211,7 @@ static int64_t wake_frequency(agent_t* a) {
     case AG_POVMM: return a->wake_freq;
     case AG_MOMENTUM: return a->wake_freq;
     case AG_MKTMAKER: return a->wake_freq; /* pd.Timedelta(wake_up_freq) (MarketMakerAgent.py:148-149) */
+    case AG_OBI: return NS_SEC;           /* pd.Timedelta("1s") (OrderBookImbalanceAgent.py:187-188) */
     case AG_REPLAY: return a->wake_freq;  /* first tape time - mkt_open (MarketReplayAgent.py:94-96) */
     case AG_DUMMYRL: return a->wake_freq; /* horizon[0] - mkt_open (execution_agent.py:129-130) */
     default: return rs_randint(&a->rs, 0, 100);
@@ -1626,6 +1636,66 @@ static void mk_receive(ora_env* e, agent_t* a, const msg_t* m) {
     a->state = ST_AWAITING_WAKEUP;
 }
 
+/* ------------------------- OrderBookImbalanceAgent ---------------------------- */
+/* agent/OrderBookImbalanceAgent.py: every wakeup (re)subscribes to 10 levels every hour and sets
+ * its computation delay to 1 ns (wakeup, :67-71); each MARKET_DATA cancels its orders and trades
+ * the bid share of the top-10 liquidity against entry / trailing-stop thresholds (:73-186) */
+static void obi_wakeup(ora_env* e, agent_t* a) {
+    ta_wakeup(e, a);
+    msg_t m;
+    memset(&m, 0, sizeof m);
+    m.kind = K_MD_SUB_REQ;
+    m.depth = 10;
+    m.lookback = 3600000000000LL;
+    ta_send_ex(e, a, &m);
+    e->comp_delay[a->id] = 1; /* setComputationDelay(1) */
+}
+static void obi_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    if (m->kind != K_MARKET_DATA) return;
+    cancel_all(e, a);
+    int64_t bl = 0, al = 0;
+    for (int k = 0; k < m->nb; k++) bl += m->lvbq[k];
+    for (int k = 0; k < m->na; k++) al += m->lvaq[k];
+    if (bl == 0 || al == 0) return; /* "zero bid or ask liquidity" */
+    const double entry = 0.17, trail = 0.085;
+    double bid_pct = (double)bl / (double)(bl + al);
+    int64_t target;
+    if (a->obi_short) {
+        if (bid_pct - trail > a->obi_stop) a->obi_stop = bid_pct - trail;
+        if (bid_pct < a->obi_stop) {
+            target = 0;
+            a->obi_short = 0;
+        } else {
+            target = -100;
+        }
+    } else if (a->obi_long) {
+        if (bid_pct + trail < a->obi_stop) a->obi_stop = bid_pct + trail;
+        if (bid_pct > a->obi_stop) {
+            target = 0;
+            a->obi_long = 0;
+        } else {
+            target = 100;
+        }
+    } else if (bid_pct < (0.5 - entry)) {
+        target = 100;
+        a->obi_long = 1;
+        a->obi_stop = bid_pct + trail;
+    } else if (bid_pct > (0.5 + entry)) {
+        target = -100;
+        a->obi_short = 1;
+        a->obi_stop = bid_pct - trail;
+    } else {
+        target = 0;
+    }
+    int64_t delta = target - a->shares;
+    int dir = delta > 0;
+    /* computeRequiredPrice (:190-206): the loop leaves p at the deepest level either way */
+    int n = dir ? m->na : m->nb;
+    int64_t price = dir ? m->lva[n - 1] : m->lvb[n - 1];
+    if (delta != 0) place_limit(e, a, delta > 0 ? delta : -delta, dir, price);
+}
+
 /* ------------------------- HeuristicBeliefLearningAgent ----------------------- */
 /* agent/HeuristicBeliefLearningAgent.py */
 static void hbl_wakeup(ora_env* e, agent_t* a) {
@@ -1980,6 +2050,7 @@ static void dispatch_wakeup(ora_env* e, int id) {
     case AG_DUMMYRL: rl_wakeup(e, a); break;
     case AG_MKTMAKER: mk_wakeup(e, a); break;
     case AG_HBL: hbl_wakeup(e, a); break;
+    case AG_OBI: obi_wakeup(e, a); break;
     }
 }
 static void dispatch_message(ora_env* e, int id, const msg_t* m) {
@@ -1989,6 +2060,7 @@ static void dispatch_message(ora_env* e, int id, const msg_t* m) {
     case AG_ZI: zi_receive(e, a, m); break;
     case AG_HBL: hbl_receive(e, a, m); break;
     case AG_MKTMAKER: mk_receive(e, a, m); break;
+    case AG_OBI: obi_receive(e, a, m); break;
     case AG_NOISE: noise_receive(e, a, m); break;
     case AG_VALUE: value_receive(e, a, m); break;
     case AG_POVMM: mm_receive(e, a, m); break;
@@ -2431,7 +2503,9 @@ static void zi_params(agent_t* a, int64_t rmin, int64_t rmax, double sigma_n, do
 /* config/rmsc02.py: rmsc01's agents with subscribe=True for the market maker (5 levels) and the
  * momentum agents (1 level), both every 10 s; kernel midnight-17:00; latency
  * U(21000, 13e6)[n][n] drawn after the kernel seed (not symmetrised) with 6-way noise */
-static int build_rmsc0x(ora_env* e, uint32_t seed, int v2) {
+/* config/obi_rmsc02.py: rmsc02's market with 89 ZI agents, 5 OrderBookImbalanceAgent (built
+ * after the ZI agents, each drawing only its seed) and 5 momentum agents; no HBL */
+static int build_rmsc0x(ora_env* e, uint32_t seed, int v2, int obi) {
     rs_seed(&e->G, seed);
     int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
     agent_t* ex = add_agent(e, AG_EXCHANGE);
@@ -2459,14 +2533,21 @@ static int build_rmsc0x(ora_env* e, uint32_t seed, int v2) {
     }
     rs_seed(&e->O, seed_u32(&e->G));
     oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
-    for (int j = 0; j < 50; j++) {
+    for (int j = 0; j < (obi ? 89 : 50); j++) {
         agent_t* a = add_agent(e, AG_ZI);
         rs_seed(&a->rs, seed_u32(&e->G));
         snprintf(a->name, 96, "ZI_AGENT_%d", a->id);
         snprintf(a->tname, 96, "ZeroIntelligenceAgent");
         zi_params(a, 0, 100, 10000, 1e-4, 5e4);
     }
-    for (int j = 0; j < 25; j++) {
+    for (int j = 0; j < (obi ? 5 : 0); j++) {
+        agent_t* a = add_agent(e, AG_OBI);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        snprintf(a->name, 96, "OBI_AGENT_%d", a->id);
+        snprintf(a->tname, 96, "OrderBookImbalanceAgent");
+        trading_init(a, 10000000);
+    }
+    for (int j = 0; j < (obi ? 0 : 25); j++) {
         agent_t* a = add_agent(e, AG_HBL);
         rs_seed(&a->rs, seed_u32(&e->G));
         snprintf(a->name, 96, "HBL_AGENT_%d", a->id);
@@ -2474,7 +2555,7 @@ static int build_rmsc0x(ora_env* e, uint32_t seed, int v2) {
         zi_params(a, 0, 100, 10000, 1e-4, 5e4);
         a->L = 2;
     }
-    for (int j = 0; j < 24; j++) {
+    for (int j = 0; j < (obi ? 5 : 24); j++) {
         agent_t* a = add_agent(e, AG_MOMENTUM);
         rs_seed(&a->rs, seed_u32(&e->G));
         a->size = rs_randint(&a->rs, 1, 10);
@@ -2694,8 +2775,9 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     else if (!strcmp(config, "rmsc03")) rc = build_rmsc03(e, seed);
     else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
     else if (!strcmp(config, "value_noise")) rc = build_value_noise(e, seed);
-    else if (!strcmp(config, "rmsc01")) rc = build_rmsc0x(e, seed, 0);
-    else if (!strcmp(config, "rmsc02")) rc = build_rmsc0x(e, seed, 1);
+    else if (!strcmp(config, "rmsc01")) rc = build_rmsc0x(e, seed, 0, 0);
+    else if (!strcmp(config, "rmsc02")) rc = build_rmsc0x(e, seed, 1, 0);
+    else if (!strcmp(config, "obi_rmsc02")) rc = build_rmsc0x(e, seed, 1, 1);
     else rc = -1;
     if (rc) {
         free(e);

@@ -269,7 +269,8 @@ def run_config(cfg, seed, out, full):
     TradingAgent.getTransactedVolume = TradingAgent.get_transacted_volume  # SURVEY.md key finding 3
 
     date = {"sparse_zi_100": "2019-06-28", "sparse_zi_1000": "2019-06-28", "rmsc03": "2019-06-28",
-            "value_noise": "2019-06-28", "rmsc01": "2019-06-28", "rmsc02": "2019-06-28"}[cfg]
+            "value_noise": "2019-06-28", "rmsc01": "2019-06-28", "rmsc02": "2019-06-28",
+            "obi_rmsc02": "2019-06-28"}[cfg]
     MIDNIGHT = int(pd.Timestamp(date).value)
     argv = ["abides.py", "-c", cfg, "-s", str(seed)]
     if cfg == "rmsc03":
@@ -476,7 +477,11 @@ def main():
             ("rmsc01", 7, False), ("rmsc01", 99, False), ("rmsc01", 123456789, False),
             # rmsc02: rmsc01 with market-data subscriptions (market maker, momentum agents) and a
             # latency matrix with noise, from midnight to 17:00
-            ("rmsc02", 7, False), ("rmsc02", 123456789, False)]
+            ("rmsc02", 7, False), ("rmsc02", 123456789, False),
+            # obi_rmsc02: rmsc02's market with 89 ZI, 5 OrderBookImbalanceAgent, 5 momentum agents
+            ("obi_rmsc02", 7, False), ("obi_rmsc02", 123456789, False),
+            # seeds on which the OBI agents trade (found with the oracle; 7 and 123456789 stay flat)
+            ("obi_rmsc02", 30, False), ("obi_rmsc02", 107, False)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2]]
     procs = []
