@@ -7,7 +7,7 @@
  * one HIP stream and is not thread-safe; multi-GPU runs use one process per GPU.
  *
  * Reference interfaces replaced (file:line in yutiansut/marl-optimal-execution):
- *   mxa_create ......... config/{rmsc01,rmsc02,rmsc03,sparse_zi_100,sparse_zi_1000,value_noise}.py module body
+ *   mxa_create ......... config/{rmsc01,rmsc02,obi_rmsc02,rmsc03,sparse_zi_100,sparse_zi_1000,value_noise}.py module body
  *                        (agent/oracle/kernel construction, global-RNG draw order) and
  *                        Kernel.__init__ (Kernel.py:13-46)
  *   mxa_reset .......... Kernel.runner kernelInitializing/kernelStarting (Kernel.py:143-177),
@@ -43,7 +43,8 @@ typedef struct mxa_handle mxa_handle;
 enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKETREPLAY = 3, MXA_RMSC03_RL = 4,
        MXA_VALUE_NOISE = 5 /* config/value_noise.py: 100 noise + 50 value agents, latency matrix */,
        MXA_RMSC01 = 6 /* config/rmsc01.py: market maker, 50 ZI, 25 HBL, 24 momentum agents */,
-       MXA_RMSC02 = 7 /* config/rmsc02.py: rmsc01 with market-data subscriptions and a latency matrix */ };
+       MXA_RMSC02 = 7 /* config/rmsc02.py: rmsc01 with market-data subscriptions and a latency matrix */,
+       MXA_OBI_RMSC02 = 8 /* config/obi_rmsc02.py: rmsc02's market with 89 ZI, 5 order-book-imbalance agents */ };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };

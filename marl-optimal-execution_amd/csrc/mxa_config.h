@@ -46,6 +46,8 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, MXA_RMSC01_WAVES, 8, 0}
        // rmsc02: oracle maxima over 41 seeds: 225 pending events, 299 resting orders
        : cfg == MXA_CFG_RMSC02 ? Shape{6, 5, true, 2, 8, 0}
+       // obi_rmsc02: oracle maxima over 61 seeds: 211 pending events, 96 resting orders
+       : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 2, true, 2, 8, 0}
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, 2, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
@@ -296,6 +298,29 @@ constexpr void params_rmsc02(MxaParams& P) {
   P.L.lat_len = 2 * P.n_agents;
 }
 
+// config/obi_rmsc02.py: rmsc02's market (subscribing market maker, latency matrix, midnight-17:00)
+// with 89 ZI agents, 5 OrderBookImbalanceAgent (10 levels every hour, entry 0.17, trail 0.085,
+// 1 s wake frequency, starting cash 1e7) and 5 subscribing momentum agents; no HBL
+constexpr void params_obi_rmsc02(MxaParams& P) {
+  params_rmsc02(P);
+  P.config = MXA_CFG_OBI_RMSC02;
+  P.zi_group_count[0] = 89;
+  P.n_zi = 89;
+  P.first_hbl = 0;
+  P.n_hbl = 0;
+  P.first_obi = 91;
+  P.n_obi = 5;
+  P.obi_levels = 10;
+  P.obi_freq = 3600 * NS;
+  P.obi_wake = NS;
+  P.obi_entry = 0.17;
+  P.obi_trail = 0.085;
+  P.first_mom = 96;
+  P.n_mom = 5;
+  P.L.oh_cap = 0;
+  P.L.hbl_range = 0;
+}
+
 constexpr uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 // per-env HBM block: header, agent records, open orders, RNG streams, latency row/col,
@@ -377,6 +402,7 @@ constexpr MxaParams params(int cfg) {
   else if (cfg == MXA_CFG_VALUE_NOISE) params_value_noise(P);
   else if (cfg == MXA_CFG_RMSC01) params_rmsc01(P);
   else if (cfg == MXA_CFG_RMSC02) params_rmsc02(P);
+  else if (cfg == MXA_CFG_OBI_RMSC02) params_obi_rmsc02(P);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;

@@ -33,4 +33,5 @@ MxaEntry mxa_entry_4();
 MxaEntry mxa_entry_5();
 MxaEntry mxa_entry_6();
 MxaEntry mxa_entry_7();
-#define MXA_N_CONFIGS 8
+MxaEntry mxa_entry_8();
+#define MXA_N_CONFIGS 9

@@ -536,7 +536,8 @@ struct Eng {
   // POV-MM's both-replies-in test cannot fire on it). With every computation delay 0 the busy
   // check cannot requeue it, so its whole effect is Kernel.agentCurrentTimes[a] = t: one 8-byte
   // store, no record round trip (rmsc03: a quarter of all pops).
-  static constexpr bool ACK_FAST = !BUILD && !RP && PC.default_comp_delay == 0 && PC.ex_comp == 0;
+  static constexpr bool ACK_FAST = !BUILD && !RP && PC.default_comp_delay == 0 && PC.ex_comp == 0 &&
+                                   PC.n_obi == 0;  // OrderBookImbalanceAgent sets a 1 ns delay at runtime
   static constexpr int ACK_LIMIT = GYM ? PC.first_rl : PC.n_agents;  // background agents 1..ACK_LIMIT-1
   typedef RSt<BUILD> RS;
   typedef typename std::conditional<PL_LDS, LDSP u32*, u32*>::type PlPtr;
@@ -1521,25 +1522,6 @@ struct Eng {
   }
 
   // ---------------- market-data subscriptions (ExchangeAgent.py:342-387)
-  // the first n prices of one side, best first (levels are distinct prices)
-  DEV i32 b_top_prices(int buy_side, i32 n, i32* out) {
-    i32 k = 0, p = buy_side ? INT32_MAX : INT32_MIN;
-    for (int i = 0; i < MD_LEVELS; i++) {
-      out[i] = 0;
-      if (i >= n) continue;
-      i32 v = buy_side ? INT32_MIN : INT32_MAX;
-      for (int j = 0; j < SO; j++) {
-        bool c = bm[j] >= 0 && (bm[j] & 1) == buy_side && (buy_side ? bp[j] < p : bp[j] > p);
-        if (c) v = buy_side ? (bp[j] > v ? bp[j] : v) : (bp[j] < v ? bp[j] : v);
-      }
-      v = buy_side ? wmax_i32(v) : wmin_i32(v);
-      if (v == (buy_side ? INT32_MIN : INT32_MAX)) break;
-      out[i] = v;
-      p = v;
-      k++;
-    }
-    return k;
-  }
   // updateSubscriptionDict: a request (re)sets the sender's entry in place, a cancellation
   // deletes its symbol (the entry stays, empty)
   DEV void md_subscribe(const Msg& m) {
@@ -1593,9 +1575,35 @@ struct Eng {
     }
     u64 b = bal(due);
     if (!b) return;
-    i32 kb[MD_LEVELS], ka[MD_LEVELS];
-    const i32 nb = b_top_prices(1, MD_LEVELS, kb), na = b_top_prices(0, MD_LEVELS, ka);
-    const i64 bq = nb ? b_level_qty(1, kb[0]) : 0, aq = na ? b_level_qty(0, ka[0]) : 0;
+    if (bal(due && (r.levels < 0 || r.levels > MD_LEVELS))) {
+      fail(ERR_MD_SUBS);
+      return;
+    }
+    // the book's top levels once (as deep as the deepest due subscription), lane-distributed in
+    // the slot layout: lane MD_BIDS + k the k-th bid price, MD_BIDQ + k its volume, asks alike
+    const i32 maxlv = wmax_i32(due ? r.levels : 0);
+    u32 snap = 0;
+    i32 nb = 0, na = 0;
+    for (int side = 1; side >= 0; side--) {
+      i32 p = side ? INT32_MAX : INT32_MIN;
+      i32 c = 0;
+      for (int k = 0; k < maxlv; k++) {
+        i32 v = side ? INT32_MIN : INT32_MAX;
+        for (int j = 0; j < SO; j++) {
+          const bool in = bm[j] >= 0 && (bm[j] & 1) == side && (side ? bp[j] < p : bp[j] > p);
+          if (in) v = side ? (bp[j] > v ? bp[j] : v) : (bp[j] < v ? bp[j] : v);
+        }
+        v = side ? wmax_i32(v) : wmin_i32(v);
+        if (v == (side ? INT32_MIN : INT32_MAX)) break;
+        const i64 q = b_level_qty(side, v);
+        snap = lane == (side ? MD_BIDS : MD_ASKS) + k ? (u32)v : snap;
+        snap = lane == (side ? MD_BIDQ : MD_ASKQ) + k ? (u32)q : snap;
+        p = v;
+        c++;
+      }
+      if (side) nb = c;
+      else na = c;
+    }
     while (b) {
       const int L = ffs64(b);
       b &= b - 1;
@@ -1603,20 +1611,17 @@ struct Eng {
       const i32 nbs = nb < lv ? nb : lv, nas = na < lv ? na : lv;
       const u32 tag = ++h.md_seq;
       u32* slot = md_slot(ag);
-      u32 w = 0;
-      w = lane == MD_TAG ? tag : w;
-      w = lane == MD_COUNTS ? ((u32)nbs | ((u32)nas << 8)) : w;
-      for (int k = 0; k < MD_LEVELS; k++) {
-        w = lane == MD_BIDS + k ? (u32)(k < nbs ? kb[k] : 0) : w;
-        w = lane == MD_ASKS + k ? (u32)(k < nas ? ka[k] : 0) : w;
-      }
+      const int j = lane;
+      const bool keep = (j >= MD_BIDS && j < MD_BIDS + nbs) || (j >= MD_ASKS && j < MD_ASKS + nas) ||
+                        (j >= MD_BIDQ && j < MD_BIDQ + nbs) || (j >= MD_ASKQ && j < MD_ASKQ + nas);
+      const u32 w = j == MD_TAG ? tag : j == MD_COUNTS ? ((u32)nbs | ((u32)nas << 8)) : keep ? snap : 0u;
       if (lane < MD_WORDS) slot[lane] = w;
       Msg md = msg_make(MK_MARKET_DATA, 0);
       md.w[0] |= (1u << 11) | ((u32)h.last_trade_float << 8);
-      md.w[1] = nbs ? (u32)kb[0] : 0;
-      md.w[2] = nbs ? (u32)bq : 0;
-      md.w[3] = nas ? (u32)ka[0] : 0;
-      md.w[4] = nas ? (u32)aq : 0;
+      md.w[1] = nbs ? rdl(snap, MD_BIDS) : 0;
+      md.w[2] = nbs ? rdl(snap, MD_BIDQ) : 0;
+      md.w[3] = nas ? rdl(snap, MD_ASKS) : 0;
+      md.w[4] = nas ? rdl(snap, MD_ASKQ) : 0;
       md.w[5] = (u32)h.last_trade;
       md.w[6] = (u32)nbs | ((u32)nas << 8);
       md.w[7] = tag;
@@ -1894,6 +1899,7 @@ struct Eng {
     if (type == AG_POVMM) return PC.mm_wake;
     if (type == AG_MOMENTUM) return PC.mom_wake;
     if (type == AG_MKTMAKER) return PC.mk_wake;  // pd.Timedelta(wake_up_freq) (MarketMakerAgent.py:148-149)
+    if (type == AG_OBI) return PC.obi_wake;      // pd.Timedelta("1s") (OrderBookImbalanceAgent.py:187-188)
     if constexpr (RP) {
       if (type == AG_REPLAY) return U(rx->tm[0]) - PC.mkt_open;  // MarketReplayAgent.py:94-96
     }
@@ -2421,6 +2427,73 @@ struct Eng {
         place_limit(q, 0, mid + spread + i);
       }
     }
+  }
+
+  // ---------------- OrderBookImbalanceAgent (agent/OrderBookImbalanceAgent.py)
+  // wakeup (:67-71): TradingAgent.wakeup, a (re)subscription to 10 levels every hour, then a
+  // computation delay of 1 ns for every later event of the agent
+  DEV void obi_wakeup() {
+    ta_wakeup();
+    Msg m = msg_make(MK_MD_SUB_REQ, cur_agent);
+    m.w[1] = (u32)PC.obi_levels;
+    m.w[2] = (u32)(u64)PC.obi_freq;
+    m.w[3] = (u32)((u64)PC.obi_freq >> 32);
+    send_ex(m);
+    rs64(AF_COMP, 1);
+  }
+  // receiveMessage (:73-186): on MARKET_DATA cancel every open order; with liquidity on both sides
+  // trade the bid share of the received levels against the entry threshold and the trailing stop;
+  // computeRequiredPrice (:190-206) always ends on the deepest received level's price
+  DEV void obi_receive(const Msg& m) {
+    ta_receive(m, AG_OBI);
+    if (m_kind(m) != MK_MARKET_DATA) return;
+    cancel_all();
+    const u32* slot = md_slot(cur_agent);
+    const u32 x = lane < MD_WORDS ? slot[lane] : 0u;
+    if (rdl(x, MD_TAG) != m.w[7]) {
+      fail(ERR_MD_SLOT);
+      return;
+    }
+    const i32 nb = (i32)(m.w[6] & 0xFF), na = (i32)((m.w[6] >> 8) & 0xFF);
+    const i64 bl = wsum_i64(lane >= MD_BIDQ && lane < MD_BIDQ + nb ? (i64)x : 0);
+    const i64 al = wsum_i64(lane >= MD_ASKQ && lane < MD_ASKQ + na ? (i64)x : 0);
+    if (bl == 0 || al == 0) return;  // "zero bid or ask liquidity"
+    const double bid_pct = (double)bl / (double)(bl + al);
+    const double trail = PC.obi_trail;
+    double stop = rgd(AF_OBI_STOP);
+    i64 target;
+    if (fl(FL_OBI_SHORT)) {
+      if (bid_pct - trail > stop) stop = bid_pct - trail;
+      if (bid_pct < stop) {
+        target = 0;
+        fl_set(FL_OBI_SHORT, false);
+      } else {
+        target = -100;
+      }
+    } else if (fl(FL_OBI_LONG)) {
+      if (bid_pct + trail < stop) stop = bid_pct + trail;
+      if (bid_pct > stop) {
+        target = 0;
+        fl_set(FL_OBI_LONG, false);
+      } else {
+        target = 100;
+      }
+    } else if (bid_pct < (0.5 - PC.obi_entry)) {
+      target = 100;
+      fl_set(FL_OBI_LONG, true);
+      stop = bid_pct + trail;
+    } else if (bid_pct > (0.5 + PC.obi_entry)) {
+      target = -100;
+      fl_set(FL_OBI_SHORT, true);
+      stop = bid_pct - trail;
+    } else {
+      target = 0;
+    }
+    rsd(AF_OBI_STOP, stop);
+    const i64 delta = target - rg64(AF_SHARES);
+    const int dir = delta > 0;
+    const i32 price = (i32)rdl(x, dir ? MD_ASKS + na - 1 : MD_BIDS + nb - 1);
+    if (delta != 0) place_limit(delta > 0 ? delta : -delta, dir, price);
   }
 
   // ---------------- HeuristicBeliefLearningAgent (agent/HeuristicBeliefLearningAgent.py)
@@ -3238,6 +3311,8 @@ struct Eng {
         if (type == AG_MKTMAKER) return mk_wakeup();
       if constexpr (PC.n_hbl > 0)
         if (type == AG_HBL) return hbl_wakeup();
+      if constexpr (PC.n_obi > 0)
+        if (type == AG_OBI) return obi_wakeup();
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_wakeup();
       }
@@ -3261,6 +3336,8 @@ struct Eng {
         if (type == AG_MKTMAKER) return mk_receive(m);
       if constexpr (PC.n_hbl > 0)
         if (type == AG_HBL) return hbl_receive(m);
+      if constexpr (PC.n_obi > 0)
+        if (type == AG_OBI) return obi_receive(m);
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_receive(m);
       }
@@ -4106,7 +4183,7 @@ struct Builder : Eng<CFG, true> {
         init_gym();
       }
       set_seed(2, g_seed(G));  // K
-    } else if (P.config == MXA_CFG_RMSC01 || P.config == MXA_CFG_RMSC02) {
+    } else if (P.config == MXA_CFG_RMSC01 || P.config == MXA_CFG_RMSC02 || P.config == MXA_CFG_OBI_RMSC02) {
       // config/rmsc01.py: the exchange's seed, the market maker's, the oracle symbol's, the
       // oracle's first megashock time, per ZI and HBL agent its seed, per momentum agent its
       // seed, the kernel's (each agent's own __init__ draws come after seed_streams);
@@ -4129,13 +4206,19 @@ struct Builder : Eng<CFG, true> {
         this->rsd(AF_R_T, P.zi_rbar);
         this->rec_store();
       }
+      for (int a = P.first_obi; a < P.first_obi + P.n_obi; a++) {  // obi_rmsc02: after the ZI agents
+        set_seed(4 + a, g_seed(G));
+        rec_init(a, AG_OBI);
+        this->rsd(AF_OBI_STOP, 0.0);
+        this->rec_store();
+      }
       for (int a = P.first_mom; a < P.first_mom + P.n_mom; a++) {
         set_seed(4 + a, g_seed(G));
         rec_init(a, AG_MOMENTUM);
         this->rec_store();
       }
       set_seed(2, g_seed(G));  // K
-      if (P.config == MXA_CFG_RMSC02) {  // G.uniform(lo, hi, (n, n)), C order: row 0, then column 0
+      if (P.config == MXA_CFG_RMSC02 || P.config == MXA_CFG_OBI_RMSC02) {  // G.uniform(lo, hi, (n, n)), C order: row 0, then column 0
         double* lat = this->lat();
         const i64 total = (i64)n * n;
         i64 prev = -1;

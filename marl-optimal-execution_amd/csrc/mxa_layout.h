@@ -17,7 +17,7 @@
 
 enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3,
                      MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6,
-                     MXA_CFG_RMSC02 = 7 };
+                     MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -33,7 +33,7 @@ enum { MT_MESSAGE = 1, MT_WAKEUP = 2, MT_CANCEL_ORDER = 3 };
 
 // agent classes
 enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_MOMENTUM = 5, AG_REPLAY = 6, AG_DUMMYRL = 7,
-       AG_MKTMAKER = 8, AG_HBL = 9 };
+       AG_MKTMAKER = 8, AG_HBL = 9, AG_OBI = 10 };
 
 // env status flags (EnvHdr::status)
 enum { ST_RUNNING = 0, ST_DONE = 1, ST_ERROR = 2 };
@@ -145,9 +145,10 @@ typedef struct {  // ExchangeAgent.subscription_dict entry (agent -> [levels, fr
   int32_t live, pad;
   int64_t freq, last;
 } SubRec;         // 32 B
-// MARKET_DATA snapshot slot of one subscriber (16 words): the message carries the best levels
-// and the last trade (and the slot tag); the deeper level prices wait here for the receipt
-enum { MD_TAG = 0, MD_COUNTS = 1, MD_BIDS = 4, MD_ASKS = 9, MD_WORDS = 16, MD_LEVELS = 5, MD_MAX_SUBS = 64 };
+// MARKET_DATA snapshot slot of one subscriber (64 words): the message carries the best levels
+// and the last trade (and the slot tag); the level prices and volumes wait here for the receipt
+enum { MD_LEVELS = 10, MD_TAG = 0, MD_COUNTS = 1, MD_BIDS = 2, MD_ASKS = 12, MD_BIDQ = 22, MD_ASKQ = 32, MD_WORDS = 64,
+       MD_MAX_SUBS = 64 };
 
 typedef struct {  // TradingAgent.orders entry (agent's copy of an open order)
   int32_t oid, is_buy, qty, price;
@@ -235,8 +236,10 @@ enum {
   FL_HAS_OPEN = 1, FL_HAS_CLOSE = 2, FL_MKT_CLOSED = 4, FL_FIRST_WAKE = 8, FL_DAILY_CLOSE = 16,
   FL_TRADING = 32, FL_HAS_KNOWN = 64, FL_NB = 128, FL_NA = 256, FL_HAS_LAST = 512,
   FL_LAST_FLOAT = 1024, FL_PREV_WAKE = 2048, FL_AW_SPREAD = 4096, FL_AW_TV = 8192, FL_LAST_MID = 16384,
-  FL_HAS_STREAM = 32768, FL_SUB_REQ = 65536
+  FL_HAS_STREAM = 32768, FL_SUB_REQ = 65536,
+  FL_OBI_LONG = 131072, FL_OBI_SHORT = 262144  // OrderBookImbalanceAgent.is_long / is_short
 };
+enum { AF_OBI_STOP = AF_R_T };  // OrderBookImbalanceAgent.trailing_stop (double; OBI has no r_t)
 enum { AS_AWAITING_WAKEUP = 0, AS_INACTIVE = 1, AS_AWAITING_SPREAD = 2, AS_ACTIVE = 3, AS_AWAITING_STREAM = 4,
        AS_AWAITING_MD = 5 };
 
@@ -282,6 +285,10 @@ typedef struct {
   // market-data subscriptions (rmsc02: MarketMakerAgent / MomentumAgent subscribe=True)
   int32_t md_sub, md_mk_levels, md_mom_levels, lat_asym;  // lat_asym: latency row 0 + column 0
   int64_t md_freq;
+  // OrderBookImbalanceAgent (agent/OrderBookImbalanceAgent.py defaults)
+  int32_t first_obi, n_obi, obi_levels, pad6;
+  int64_t obi_freq, obi_wake;
+  double obi_entry, obi_trail;
   Layout L;
 } MxaParams;
 

@@ -2,7 +2,7 @@
 
 config/rmsc03.py:95-197, config/sparse_zi_100.py:177-256, config/sparse_zi_1000.py,
 config/value_noise.py:98-161 (every ValueAgent gets its own type string "ValueAgent {id}"),
-config/rmsc01.py:75-211 and config/rmsc02.py (the same agents).
+config/rmsc01.py:75-211 and config/rmsc02.py (the same agents), config/obi_rmsc02.py.
 """
 ZI_GROUPS = [(0, 250, "1"), (0, 500, "1"), (0, 1000, "0.8"), (0, 1000, "1"), (0, 2000, "0.8"), (250, 500, "0.8"),
              (250, 500, "1")]
@@ -14,6 +14,9 @@ def symbol_of(config):
 
 
 def agent_names(config):
+    if config == "obi_rmsc02":
+        return (["EXCHANGE_AGENT", "MARKET_MAKER_AGENT_1"] + ["ZI_AGENT_%d" % j for j in range(2, 91)] +
+                ["OBI_AGENT_%d" % j for j in range(91, 96)] + ["MOMENTUM_AGENT_%d" % j for j in range(96, 101)])
     if config in ("rmsc01", "rmsc02"):
         return (["EXCHANGE_AGENT", "MARKET_MAKER_AGENT_1"] + ["ZI_AGENT_%d" % j for j in range(2, 52)] +
                 ["HBL_AGENT_%d" % j for j in range(52, 77)] + ["MOMENTUM_AGENT_%d" % j for j in range(77, 101)])
@@ -34,6 +37,9 @@ def agent_names(config):
 
 
 def agent_type_names(config):
+    if config == "obi_rmsc02":
+        return (["ExchangeAgent", "MarketMakerAgent"] + ["ZeroIntelligenceAgent"] * 89 +
+                ["OrderBookImbalanceAgent"] * 5 + ["MomentumAgent"] * 5)
     if config in ("rmsc01", "rmsc02"):
         return (["ExchangeAgent", "MarketMakerAgent"] + ["ZeroIntelligenceAgent"] * 50 +
                 ["HeuristicBeliefLearningAgent"] * 25 + ["MomentumAgent"] * 24)

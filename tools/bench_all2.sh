@@ -17,3 +17,4 @@ run sparse_zi_100_4096 --config sparse_zi_100 --envs 4096 --steps 2 --warmup 1
 run value_noise_4096 --config value_noise --envs 4096 --steps 3 --warmup 1
 run rmsc01_4096 --config rmsc01 --envs 4096 --steps 2 --warmup 1
 run rmsc02_4096 --config rmsc02 --envs 4096 --steps 2 --warmup 1
+run obi_rmsc02_4096 --config obi_rmsc02 --envs 4096 --steps 2 --warmup 1
