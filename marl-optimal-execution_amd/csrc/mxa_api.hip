@@ -17,7 +17,10 @@
 #include "mxa_kernels.hip"
 #include "mxa_entry.h"
 #ifdef MXA_ONLY_RMSC03
-#define MXA_INST_CFG 0
+#ifndef MXA_ONLY_CFG  // single-configuration variant builds (profiling): that one configuration
+#define MXA_ONLY_CFG 0
+#endif
+#define MXA_INST_CFG MXA_ONLY_CFG
 #include "mxa_inst.hip"
 #endif
 
@@ -125,8 +128,10 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
 static bool bind(mxa_handle* h, int cfg) {
   MxaEntry e{};
   switch (cfg) {
+#ifdef MXA_ONLY_RMSC03
+  case MXA_ONLY_CFG: e = MXA_ENTRY_CAT(mxa_entry_, MXA_ONLY_CFG)(); break;
+#else
   case 0: e = mxa_entry_0(); break;
-#ifndef MXA_ONLY_RMSC03
   case 1: e = mxa_entry_1(); break;
   case 2: e = mxa_entry_2(); break;
   case 3: e = mxa_entry_3(); break;

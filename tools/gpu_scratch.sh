@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/obi1
+O=gpurun_out/ph4
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_obi.py tests/test_gpu_rmsc02.py tests/test_gpu_booklog.py tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -k "obi or rmsc02 or book_log or fundamental" > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
-tail -3 $O/pytest.log
+MXA_LIB=$PWD/marl-optimal-execution_amd/lib/libmxa_prof2.so timeout -k 10 300 python tools/prof_phases.py sparse_zi_1000 1024 > $O/phases_z1k.txt 2>&1 || { tail $O/phases_z1k.txt; exit 1; }
+cat $O/phases_z1k.txt
