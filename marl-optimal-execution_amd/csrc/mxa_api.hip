@@ -84,7 +84,7 @@ struct mxa_handle {
   mxa_build_fn build = nullptr;
   mxa_run_fn run = nullptr, run_log = nullptr;     // run_log: with the book-update log
   mxa_run_fn run_fast = nullptr;                   // hash off, no trace ring: instrumentation compiled out
-  mxa_step_fn step = nullptr;                      // GymKernel handles (replay, rmsc03_rl)
+  mxa_step_fn step = nullptr, step_fast = nullptr;  // GymKernel handles (replay, rmsc03_rl)
   mxa_stop_fn stop = nullptr, stop_log = nullptr;  // kernelStopping pass (plain Kernel.runner configs)
   mxa_agent_final* d_final = nullptr;
   BlRec* d_blog = nullptr;  // book-update log [n_envs][blog_cap] (mxa_set_book_log)
@@ -150,6 +150,7 @@ static bool bind(mxa_handle* h, int cfg) {
   h->stop = e.stop;
   h->stop_log = e.stop_log;
   h->step = e.step;
+  h->step_fast = e.step_fast;
   h->gym = e.step != nullptr;
   h->lds = mxa_cfg::lds_bytes(cfg);
   return true;
@@ -361,7 +362,8 @@ int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32
   return MXA_EINVAL;
 #else
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  h->step(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(),
+  (h->tcap_arg() < 0 && h->step_fast ? h->step_fast : h->step)(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env,
+                                                                 h->P.L.env_stride, h->P.n_envs, h->tcap_arg(),
           (int64_t)1 << 40, (const RpCtx*)h->d_ctx, d_actions, d_obs, d_flags);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));

@@ -22,7 +22,7 @@ struct MxaEntry {
   mxa_run_fn run, run_log;     // run_log: the book-update-log variant (plain Kernel.runner configs)
   mxa_run_fn run_fast;         // without the parity instrumentation (hash off, no trace ring)
   mxa_stop_fn stop, stop_log;
-  mxa_step_fn step;            // GymKernel configurations
+  mxa_step_fn step, step_fast; // GymKernel configurations (step_fast: without the instrumentation)
 };
 
 MxaEntry mxa_entry_0();

@@ -26,10 +26,10 @@ void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t
   hipLaunchKernelGGL((mxa_stop_kernel<CFG, LOG>), g, b, lds, s, base, stride, n, out, blog, blog_cap);
 }
 #ifndef MXA_ONLY_RMSC03
-template <int CFG>
+template <int CFG, bool INSTR>
 void launch_step(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
                  const RpCtx* ctx, const double* act, double* obs, int32_t* flags) {
-  hipLaunchKernelGGL((mxa_step_kernel<CFG>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, act, obs, flags);
+  hipLaunchKernelGGL((mxa_step_kernel<CFG, INSTR>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, act, obs, flags);
 }
 #endif
 
@@ -53,7 +53,12 @@ MxaEntry make_entry() {
     e.stop_log = launch_stop<CFG, true>;
   }
 #ifndef MXA_ONLY_RMSC03
-  if constexpr (gym) e.step = launch_step<CFG>;
+  if constexpr (gym) {
+    e.step = launch_step<CFG, true>;
+#ifndef MXA_NO_FAST
+    e.step_fast = launch_step<CFG, false>;
+#endif
+  }
 #endif
   return e;
 }

@@ -4453,8 +4453,8 @@ __global__ __launch_bounds__(64) void mxa_stop_kernel(char* base, uint64_t strid
 #ifndef MXA_ONLY_RMSC03
 // ABIDESEnv.step for every env: DummyRL.place_orders(action), then the GymKernel loop until
 // the RL agent's spread reply (end of step) or the end of the episode.  obs [n][9] float64;
-// flags [n]: bit0 done, bit1 observation valid, bit2 env error.
-template <int CFG>
+// flags [n]: bit0 done, bit1 observation valid, bit2 env error.  INSTR as for the run kernel.
+template <int CFG, bool INSTR>
 __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel(
     char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops, const RpCtx* ctx, const double* actions,
     double* obs, int32_t* flags) {
@@ -4462,7 +4462,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
   int env = blockIdx.x;
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
-  mxa::Eng<CFG> g(e, lds, trace_cap, ctx);
+  mxa::Eng<CFG, false, false, INSTR> g(e, lds, trace_cap, ctx);
   g.load();
   if (g.status == ST_RUNNING) {
     double a[3];

@@ -1,5 +1,6 @@
 set -o pipefail
-O=gpurun_out/ph4
+O=gpurun_out/st1
 mkdir -p $O
-MXA_LIB=$PWD/marl-optimal-execution_amd/lib/libmxa_prof2.so timeout -k 10 300 python tools/prof_phases.py sparse_zi_1000 1024 > $O/phases_z1k.txt 2>&1 || { tail $O/phases_z1k.txt; exit 1; }
-cat $O/phases_z1k.txt
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+bash tools/bench_all2.sh st1 2>&1 | head -4
