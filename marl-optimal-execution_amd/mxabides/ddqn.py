@@ -107,30 +107,56 @@ class QNet(nn.Module):
 
 class ReplayRing:
     """Device-resident experience (s, a, s', r) of every env (the reference keeps one
-    OrderedDict per agent, :115-116). Valid rows are compacted with a prefix sum, no host loop."""
+    OrderedDict per agent, :115-116). Valid rows are compacted with a prefix sum, no host loop.
+
+    The row count lives on the device (`n_dev`); the host keeps bounds on it (`n_lb`, `n_ub`) and
+    reads it only when a size test cannot be decided from them, so the per-step loop does not
+    wait for the GPU (in practice one read per training run)."""
 
     def __init__(self, capacity, n_state, device):
         self.cap = int(capacity)
-        self.s = torch.zeros((self.cap, n_state), dtype=torch.float32, device=device)
+        # one extra row: masked-out rows of a batched append are written there
+        self.s = torch.zeros((self.cap + 1, n_state), dtype=torch.float32, device=device)
         self.s2 = torch.zeros_like(self.s)
-        self.a = torch.zeros(self.cap, dtype=torch.int64, device=device)
-        self.r = torch.zeros(self.cap, dtype=torch.float32, device=device)
-        self.n = 0  # rows written so far (host)
+        self.a = torch.zeros(self.cap + 1, dtype=torch.int64, device=device)
+        self.r = torch.zeros(self.cap + 1, dtype=torch.float32, device=device)
+        self.n_dev = torch.zeros((), dtype=torch.int64, device=device)  # rows written so far
+        self.n_lb = 0  # host bounds on n_dev
+        self.n_ub = 0
+
+    def add_device(self, s, a, s2, r, mask):
+        """append rows where mask without a host read; returns the count as a device scalar"""
+        m = mask.to(torch.int64)
+        c = torch.cumsum(m, 0)
+        pos = torch.where(mask, (self.n_dev + c - 1) % self.cap, torch.full_like(c, self.cap))
+        self.s[pos] = s.float()
+        self.s2[pos] = s2.float()
+        self.a[pos] = a
+        self.r[pos] = r.float()
+        k = c[-1] if len(c) else torch.zeros((), dtype=torch.int64, device=m.device)
+        self.n_dev += k
+        self.n_ub += len(mask)
+        return k
 
     def add(self, s, a, s2, r, mask):
         """append rows where mask; returns the number appended (one host read)."""
-        m = mask.to(torch.int64)
-        k = int(m.sum().item())
-        if k:
-            pos = (self.n + torch.cumsum(m, 0) - 1) % self.cap
-            sel = mask.nonzero(as_tuple=True)[0]
-            p = pos[sel]
-            self.s[p] = s[sel].float()
-            self.s2[p] = s2[sel].float()
-            self.a[p] = a[sel]
-            self.r[p] = r[sel].float()
-            self.n += k
+        k = int(self.add_device(s, a, s2, r, mask).item())
+        self.n_lb = int(self.n_dev.item())
         return k
+
+    @property
+    def n(self):
+        return int(self.n_dev.item())
+
+    def more_than(self, x):
+        """len(self) > x, reading the device count only when the host bounds cannot decide"""
+        if min(self.n_lb, self.cap) > x:
+            return True
+        if min(self.n_ub, self.cap) <= x:
+            return False
+        self.n_lb = int(self.n_dev.item())
+        self.n_ub = max(self.n_ub, self.n_lb)
+        return min(self.n_lb, self.cap) > x
 
     def __len__(self):
         return min(self.n, self.cap)
@@ -178,7 +204,7 @@ class DDQNLearner:
             return greedy
         u = torch.rand(n, generator=self.gen, device=self.device, dtype=torch.float64)
         rnd = torch.randint(0, self.n_actions, (n,), generator=self.gen, device=self.device)
-        exploit = (u < self.epsilon) & (len(self.memory) + 1 > self.batch_size)
+        exploit = (u < self.epsilon) & self.memory.more_than(self.batch_size - 1)  # len + 1 > batch_size
         return torch.where(exploit, greedy, rnd)
 
     # ---- learning (train_neural_nets, :448-515)
@@ -212,11 +238,12 @@ class DDQNLearner:
 
     def learn(self):
         """sample a batch with replacement (np.random.choice(current_size, batch)) and update."""
-        n = len(self.memory)
-        if n <= self.batch_size:
-            return None
-        idx = torch.randint(0, n, (self.batch_size,), generator=self.gen, device=self.device)
         m = self.memory
+        if not m.more_than(self.batch_size):
+            return None
+        size = torch.clamp(m.n_dev, max=m.cap).to(torch.float64)  # the current size, on the device
+        u = torch.rand(self.batch_size, generator=self.gen, device=self.device, dtype=torch.float64)
+        idx = torch.clamp((u * size).to(torch.int64), max=m.cap - 1)
         cost = self.learn_on(m.s[idx], m.a[idx], m.s2[idx], m.r[idx])
         self.cost_hist.append(cost)
         return cost
@@ -292,11 +319,11 @@ def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train
     lob_ok = (st[:, 7] == 3)
     arrival = torch.where(lob_ok, (st[:, 3] + st[:, 4]) / 2, torch.ones_like(st[:, 3]))  # mid at start_time
     rewards, actions = [], []
-    stored = 0
+    stored = torch.zeros((), dtype=torch.int64, device=dev)
     step_counter = 0
+    # every horizon step is enqueued without waiting for the GPU (no host read of `alive`): envs
+    # that are done stay done in the step kernel, and their rows are masked out below
     for _ in range(nh):
-        if not bool(alive.any().item()):
-            break
         s = task.state(obs)
         a = learner.choose_action(s)
         act = task.actions(a, obs)
@@ -315,7 +342,7 @@ def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train
         r = task.reward(prev, st, arrival, task.q0)
         s2 = task.state(obs)
         if learner.mode == "train":
-            stored += learner.memory.add(s, a, s2, r, ok)
+            stored += learner.memory.add_device(s, a, s2, r, ok)
             if step_counter % train_every == 0:
                 for _ in range(updates_per_train):
                     learner.learn()

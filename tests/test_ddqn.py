@@ -148,7 +148,7 @@ def test_replay_ring_compacts_and_wraps():
     assert R.a[:5].tolist() == [0, 2, 3, 5, 6] and R.r[:5].tolist() == [0, 20, 30, 50, 60]
     assert R.add(s, a, s, r, m) == 5 and R.add(s, a + 100, s, r, m) == 5
     assert len(R) == 10 and R.n == 15
-    assert R.a.tolist() == [100, 102, 103, 105, 106, 0, 2, 3, 5, 6]
+    assert R.a[:10].tolist() == [100, 102, 103, 105, 106, 0, 2, 3, 5, 6]  # (row 10: masked-out rows)
 
 
 def test_actions_and_reward_mapping():
