@@ -241,7 +241,7 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
                       const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
                       mxa_handle** out) {
   if (!out || !t || !oid || !price || !size || !buy || n_rec <= 0 || n_envs <= 0 || trace_cap < 0) return MXA_EINVAL;
-#ifdef MXA_ONLY_RMSC03
+#ifdef MXA_NO_GYM
   return MXA_EINVAL;
 #else
   int64_t pmin = INT64_MAX, pmax = INT64_MIN, min_id = INT64_MAX;
@@ -337,7 +337,7 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
 // ABIDESEnv.step for every env: actions [n][3] -> obs [n][9], flags [n] (all host arrays)
 int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags) {
   if (!h || !h->gym || !actions || !obs || !flags) return MXA_EINVAL;
-#ifdef MXA_ONLY_RMSC03
+#ifdef MXA_NO_GYM
   return MXA_EINVAL;
 #else
   HIPCHK(h, hipSetDevice(h->device));
@@ -358,7 +358,7 @@ int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags) 
 // the same with device arrays (e.g. torch tensors), asynchronous on the handle's stream
 int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32_t* d_flags) {
   if (!h || !h->gym) return MXA_EINVAL;
-#ifdef MXA_ONLY_RMSC03
+#ifdef MXA_NO_GYM
   return MXA_EINVAL;
 #else
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));

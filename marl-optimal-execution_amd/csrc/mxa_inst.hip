@@ -25,7 +25,7 @@ void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t
                  BlRec* blog, int blog_cap) {
   hipLaunchKernelGGL((mxa_stop_kernel<CFG, LOG>), g, b, lds, s, base, stride, n, out, blog, blog_cap);
 }
-#ifndef MXA_ONLY_RMSC03
+#ifndef MXA_NO_GYM
 template <int CFG, bool INSTR>
 void launch_step(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
                  const RpCtx* ctx, const double* act, double* obs, int32_t* flags) {
@@ -52,7 +52,7 @@ MxaEntry make_entry() {
 #endif
     e.stop_log = launch_stop<CFG, true>;
   }
-#ifndef MXA_ONLY_RMSC03
+#ifndef MXA_NO_GYM
   if constexpr (gym) {
     e.step = launch_step<CFG, true>;
 #ifndef MXA_NO_FAST

@@ -21,6 +21,11 @@
 // truncation.  Compiled with -ffp-contract=off.
 #pragma once
 #include <hip/hip_runtime.h>
+// single-configuration variant builds (-DMXA_ONLY_RMSC03 [-DMXA_ONLY_CFG=<id>]) carry the
+// GymKernel step kernel only for the GymKernel configurations
+#if defined(MXA_ONLY_RMSC03) && !(defined(MXA_ONLY_CFG) && (MXA_ONLY_CFG == 3 || MXA_ONLY_CFG == 4))
+#define MXA_NO_GYM
+#endif
 
 #include "../../include/mxa.h"
 #include "glibc_math.h"
@@ -3069,9 +3074,15 @@ struct Eng {
     i32 wi = U(R->mr_wi);
     const i32 ntm = U(rx->L.ntm);
     if (wi >= ntm) return;  // IndexError: every order submitted (the last group never is)
-    wakeup_at(cur_agent, U(rx->tm[wi]));
+    const i64 tn = U(rx->tm[wi]);
+    wakeup_at(cur_agent, tn);
     R->mr_wi = wi + 1;
+    // orders[currentTime]: tm is strictly increasing (sorted tape), so the match is unique. A
+    // wakeup on time is at the group just scheduled before (wi - 1) or at wi itself (the first
+    // one); anything else (a delayed wakeup) takes the binary search
     i32 lo = 0, hi = ntm - 1, g = -1;
+    if (tn == cur) g = wi, lo = hi + 1;
+    else if (wi > 0 && U(rx->tm[wi - 1]) == cur) g = wi - 1, lo = hi + 1;
     while (lo <= hi) {
       i32 mid = (lo + hi) >> 1;
       i64 tv = U(rx->tm[mid]);
@@ -4450,7 +4461,7 @@ __global__ __launch_bounds__(64) void mxa_stop_kernel(char* base, uint64_t strid
   if (LOG && g.lane == 0) ((EnvHdr*)e)->blog_fin = g.h.blog_n;
 }
 
-#ifndef MXA_ONLY_RMSC03
+#ifndef MXA_NO_GYM
 // ABIDESEnv.step for every env: DummyRL.place_orders(action), then the GymKernel loop until
 // the RL agent's spread reply (end of step) or the end of the episode.  obs [n][9] float64;
 // flags [n]: bit0 done, bit1 observation valid, bit2 env error.  INSTR as for the run kernel.
@@ -4487,6 +4498,9 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
   const int done = !(pending && g.cur <= mxa::Eng<CFG>::PC.stop) || g.status != ST_RUNNING;
   const int hobs = mxa::U(R->has_obs);
   if (g.lane == 0) flags[env] = done | (hobs ? 2 : 0) | (g.status == ST_ERROR ? 4 : 0);
+#ifdef MXA_PROF
+  atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
+#endif
 }
 #endif
 
