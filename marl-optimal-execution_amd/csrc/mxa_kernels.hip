@@ -543,6 +543,10 @@ struct Eng {
   // store, no record round trip (rmsc03: a quarter of all pops).
   static constexpr bool ACK_FAST = !BUILD && !RP && PC.default_comp_delay == 0 && PC.ex_comp == 0 &&
                                    PC.n_obi == 0;  // OrderBookImbalanceAgent sets a 1 ns delay at runtime
+  // ABIDESEnv replay: the exchange and ORDER_ACCEPTED shortcuts hold as well (MarketReplayAgent
+  // ignores ORDER_ACCEPTED too, every delay is 0); ORDER_CANCELLED updates its orders table, so
+  // the CANCELLED shortcut (open-order list) stays off
+  static constexpr bool RP_FAST = !BUILD && RP && PC.default_comp_delay == 0 && PC.ex_comp == 0;
   static constexpr int ACK_LIMIT = GYM ? PC.first_rl : PC.n_agents;  // background agents 1..ACK_LIMIT-1
   typedef RSt<BUILD> RS;
   typedef typename std::conditional<PL_LDS, LDSP u32*, u32*>::type PlPtr;
@@ -3875,7 +3879,7 @@ struct Eng {
         }
       }
 #ifndef MXA_NO_ACK_FAST
-      if constexpr (ACK_FAST) {
+      if constexpr (ACK_FAST || RP_FAST) {
         if (type == MT_MESSAGE && rcp == 0) {
           // ExchangeAgent.receiveMessage reads nothing from its agent record but the
           // computation delay, which is 0 here: no record round trip (half of all pops)
@@ -3912,7 +3916,7 @@ struct Eng {
           PROF_CNT(28);
           continue;
         }
-        if (type == MT_MESSAGE && m_kind(m) == MK_CANCELLED && rcp > 0 && rcp < ACK_LIMIT) {
+        if (ACK_FAST && type == MT_MESSAGE && m_kind(m) == MK_CANCELLED && rcp > 0 && rcp < ACK_LIMIT) {
           // TradingAgent.orderCancelled (TradingAgent.py:464-480): del self.orders[id]. The
           // open-order chunks are loaded with the record, not after it (one latency, not two)
           rec_load(rcp);
