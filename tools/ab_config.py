@@ -1,5 +1,6 @@
 """A/B of one configuration's run kernel between two libmxa builds (MXA_LIB selects the library):
 python tools/ab_config.py CONFIG N_ENVS [REPS]  ->  run-kernel ms per episode batch."""
+import hashlib
 import os
 import sys
 
@@ -18,5 +19,11 @@ for r in range(reps):
     m.run(chunk=1 << 22)
     ms.append(m.last_kernel_ms)
 ev = int(m.summary()["events"].sum())
-print("%s %s x%d: run kernel %s ms (best %.1f), %.1f M env-steps/s" % (
-    os.path.basename(os.environ.get("MXA_LIB", "libmxa.so")), cfg, n, ["%.1f" % x for x in ms], min(ms), ev / min(ms) / 1e3))
+# one more episode with the parity hash on: a digest over every env's (events, hash) for A/B parity
+m.set_parity_hash(True)
+m.reset()
+m.run(chunk=1 << 22)
+s = m.summary()
+dig = hashlib.sha1(np.ascontiguousarray(s["events"]).tobytes() + np.ascontiguousarray(s["hash"]).tobytes()).hexdigest()[:16]
+print("%s %s x%d: run kernel %s ms (best %.1f), %.1f M env-steps/s, digest %s" % (
+    os.path.basename(os.environ.get("MXA_LIB", "libmxa.so")), cfg, n, ["%.1f" % x for x in ms], min(ms), ev / min(ms) / 1e3, dig))
