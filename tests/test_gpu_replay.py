@@ -18,7 +18,7 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 TAPE = os.path.join(GOLD, "tape_IBM_2003-01-14.npz")
 # (ticker, date): IBM 2003-01-14 has explicit ids only; GOOG 2012-06-21 has 3,913 ORDER_ID 0
 # records (hidden executions) that take auto ids interleaved with DummyRL's
-EPISODES = [("IBM", "2003-01-14"), ("GOOG", "2012-06-21")]
+EPISODES = [("IBM", "2003-01-14"), ("GOOG", "2012-06-21"), ("IBM", "2003-01-13"), ("YHOO", "2003-01-14")]
 OBS_RTOL = 1e-9
 
 

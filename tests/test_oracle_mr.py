@@ -1,8 +1,8 @@
 """C oracle vs the reference ABIDESEnv (Exchange + MarketReplayAgent + DummyRL on a LOBSTER
 tape): every step's observation, done flag and event count, the event trace head, the
-whole-episode hash, the final book and holdings.  Two episodes: IBM 2003-01-14 (explicit
+whole-episode hash, the final book and holdings.  Four episodes: IBM 2003-01-14 (explicit
 order ids only) and GOOG 2012-06-21 (3,913 ORDER_ID 0 records, which take auto ids from the
-counter DummyRL also uses).  Fixtures produced by tests/golden/gen_mr_fixtures.py from the
+counter DummyRL also uses), plus IBM 2003-01-13 and YHOO 2003-01-14 (round 2).  Fixtures produced by tests/golden/gen_mr_fixtures.py from the
 reference itself (LOBSTER CSV path; the reference's processed pickles are never loaded)."""
 import json
 import os
@@ -16,7 +16,7 @@ from mxabides import tape
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 TAPE = os.path.join(GOLD, "tape_IBM_2003-01-14.npz")
 LOB = "/root/reference/data/lobster/LOBSTER_SampleFile_%s_1/%s_%s_34200000_57600000_message_1.csv"
-EPISODES = [("IBM", "2003-01-14"), ("GOOG", "2012-06-21")]
+EPISODES = [("IBM", "2003-01-14"), ("GOOG", "2012-06-21"), ("IBM", "2003-01-13"), ("YHOO", "2003-01-14")]
 OBS_RTOL = 1e-9  # observations are float64 (numpy log/tanh/std vs glibc): north_star tolerance
 
 
