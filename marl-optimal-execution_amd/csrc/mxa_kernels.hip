@@ -2657,10 +2657,20 @@ struct Eng {
   }
 
   // ---------------- MomentumAgent (MomentumAgent.py:53-99)
+  // the mean of the last n mids (n <= 50 < AF_NMID): the ring entries (nm - n .. nm - 1) % 50
+  // summed across the record's lanes at once (an exact integer sum, any order)
   DEV double mom_avg(int n) {
-    i32 nm = rgi(AF_NMID);
-    i64 s2 = 0;
-    for (int i = nm - n; i < nm; i++) s2 += rgi(AF_MIDS + (i % 50));
+    static_assert(AF_MIDS % 2 == 0, "the mid ring starts on a lane's low dword");
+    const i32 nm = rgi(AF_NMID);
+    const i32 newest = (nm - 1) % 50;
+    i64 part = 0;
+    for (int hw = 0; hw < 2; hw++) {
+      const int k = 2 * lane + hw - AF_MIDS;  // this dword's ring index
+      i32 back = newest - k;                   // how many entries older than the newest
+      if (back < 0) back += 50;
+      if (k >= 0 && k < 50 && back < n) part += (i64)(i32)(hw ? rhi : rlo);
+    }
+    const i64 s2 = wsum_i64(part);
     double x = ((double)s2 / 2.0) / (double)n;
     return __builtin_rint(x * 100.0) / 100.0;
   }
