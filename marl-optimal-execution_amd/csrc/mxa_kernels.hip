@@ -89,6 +89,11 @@ DEV u32 wmin_u32(u32 v) {
   MXA_DPP_STEPS(op_minu, 0xffffffffu, v)
   return rdl(v, 63);
 }
+DEV u64 wmin_u64(u64 v) {  // two 32-bit wave-mins (high word, then the low word among its ties)
+  const u32 hi = wmin_u32((u32)(v >> 32));
+  const u32 lo = wmin_u32((u32)(v >> 32) == hi ? (u32)v : 0xFFFFFFFFu);
+  return ((u64)hi << 32) | lo;
+}
 // 64-bit sum: reduce the two 32-bit halves separately (each fits: |parts| < 2^32 * 64)
 DEV i64 wsum_i64(i64 x) {
   // values summed here are non-negative quantities < 2^31; sum the low and high 32 bits as
@@ -1534,6 +1539,7 @@ struct Eng {
   // updateSubscriptionDict: a request (re)sets the sender's entry in place, a cancellation
   // deletes its symbol (the entry stays, empty)
   DEV void md_subscribe(const Msg& m) {
+    h.md_next_due = 0;  // the due-time cache is rebuilt by the next publish
     const i32 sender = m_agent(m);
     SubRec* S = subs();
     const i32 ns = h.nsub;
@@ -1569,6 +1575,8 @@ struct Eng {
   // trade.  The best levels travel in the message; the deeper prices wait in the subscriber's slot
   // (freq >= the latency keeps one MARKET_DATA in flight per subscriber; a second one fails)
   DEV void md_publish() {
+    // nothing comes due before h.md_next_due (kept by the previous publish): no table read
+    if (!h.md_any0 && h.has_last_update && h.ob_last_update < h.md_next_due) return;
     const i32 ns = h.nsub;
     SubRec* S = subs();
     SubRec r;
@@ -1581,6 +1589,11 @@ struct Eng {
     if (bal(live && r.freq != 0 && !h.has_last_update)) {
       fail(ERR_MD_NO_UPDATE);
       return;
+    }
+    {  // the earliest update time at which a freq > 0 subscription comes due, after this publish
+      const i64 nl = due ? h.ob_last_update : r.last;
+      h.md_next_due = (i64)wmin_u64(live && r.freq > 0 ? (u64)(nl + r.freq) : ~0ull);
+      h.md_any0 = bal(live && r.freq <= 0) != 0;
     }
     u64 b = bal(due);
     if (!b) return;

@@ -93,7 +93,9 @@ typedef struct {
   int32_t blog_fin, pad3;        // book-update log: records after the last kernelStopping pass
   int64_t ob_last_update;        // OrderBook.last_update_ts (market-data configs)
   int32_t nsub, has_last_update; // ExchangeAgent.subscription_dict entries; last_update_ts not None
-  uint32_t md_seq, pad4;         // MARKET_DATA messages sent (their snapshot-slot tags)
+  uint32_t md_seq;               // MARKET_DATA messages sent (their snapshot-slot tags)
+  int32_t md_any0;               // a live subscription with freq <= 0 (due at every update)
+  int64_t md_next_due;           // no freq > 0 subscription is due before this update time (0: unknown)
 } EnvHdr;
 
 #ifdef __cplusplus
