@@ -51,6 +51,9 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, 2, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
+       // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
+       // maximum over 1024 seeds is 5,120 events), payload in HBM; 320 book slots (max 259)
+       : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, 1, 6, 0}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr size_t lds_bytes(int cfg) {
@@ -122,6 +125,30 @@ constexpr void params_rmsc03(MxaParams& P) {
   P.L.open_cap = 128;
   P.L.tx_cap = 256;
   P.L.lat_len = 0;
+}
+
+// config/random_fund_value.py:59-180: rmsc03's agent classes at 5,100 agents over a whole day:
+// 5000 noise agents (wakeup_time in 09:30-16:00), 100 value agents (sigma_n 1e4, lambda_a 1e-12),
+// no market maker or momentum agents; market 09:30-16:00, kernel 09:30-16:01, zero latency
+constexpr void params_random_fund_value(MxaParams& P) {
+  params_rmsc03(P);
+  P.config = MXA_CFG_RANDOM_FUND_VALUE;
+  P.mkt_close = 16 * HOUR;
+  P.start = P.mkt_open;
+  P.stop = P.mkt_close + MIN;
+  P.n_noise = 5000;
+  P.first_value = 5001;
+  P.n_value = 100;
+  P.first_mm = 0;
+  P.n_mm = 0;
+  P.first_mom = 0;
+  P.n_mom = 0;
+  P.n_agents = 5101;
+  P.v_lambda = 1e-12;
+  P.noise_open = P.mkt_open;
+  P.noise_close = 16 * HOUR;
+  P.L.open_cap = 8;
+  P.L.tx_cap = 64;
 }
 
 // config/sparse_zi_100.py:73-334 and config/sparse_zi_1000.py
@@ -403,6 +430,7 @@ constexpr MxaParams params(int cfg) {
   else if (cfg == MXA_CFG_RMSC01) params_rmsc01(P);
   else if (cfg == MXA_CFG_RMSC02) params_rmsc02(P);
   else if (cfg == MXA_CFG_OBI_RMSC02) params_obi_rmsc02(P);
+  else if (cfg == MXA_CFG_RANDOM_FUND_VALUE) params_random_fund_value(P);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;

@@ -34,4 +34,5 @@ MxaEntry mxa_entry_5();
 MxaEntry mxa_entry_6();
 MxaEntry mxa_entry_7();
 MxaEntry mxa_entry_8();
-#define MXA_N_CONFIGS 9
+MxaEntry mxa_entry_9();
+#define MXA_N_CONFIGS 10

@@ -385,8 +385,8 @@ struct Rec {  // named scalars, not an array: a private i64[10] is promoted to a
 template <bool WIDE, bool MDK>
 DEV Rec encode(u64 key, const Msg& m) {
   Rec r;
-  r.t = (i64)(key >> 13);
-  r.rcp = (i64)((key >> 2) & 0x7FF);
+  r.t = (i64)(key >> MXA_KEY_SHIFT);
+  r.rcp = (i64)((key >> 2) & MXA_KEY_RCP);
   i32 type = (i32)(key & 3);
   r.type = type;
   r.f0 = r.f1 = r.f2 = r.f3 = r.f4 = r.f5 = 0;
@@ -618,7 +618,28 @@ struct Eng {
   u64 gk[NG];  // QHIER: per-group min of this lane's slots
   u32 gs[NG];
   i32 gj[NG];
-  u64 qfree;
+  // free-slot mask of this lane, bit j = slot j (128 bits above 64 slots per lane: the wide
+  // random_fund_value queue)
+  static_assert(SQ <= 128, "at most 128 queue slots per lane");
+  typedef typename std::conditional<(SQ > 64), unsigned __int128, u64>::type QM;
+  static DEV QM qm_bit(int j) { return (QM)1 << j; }
+  static DEV int qm_ffs(QM m) {
+    if constexpr (SQ > 64) {
+      const u64 lo = (u64)m;
+      return lo ? ffs64(lo) : 64 + ffs64((u64)(m >> 64));
+    } else {
+      return ffs64(m);
+    }
+  }
+  static DEV int qm_pop(QM m) {
+    if constexpr (SQ > 64) return __popcll((u64)m) + __popcll((u64)(m >> 64));
+    else return __popcll(m);
+  }
+  static DEV QM qm_rdl(QM m, int L) {
+    if constexpr (SQ > 64) return (QM)rdl64((u64)m, L) | ((QM)rdl64((u64)(m >> 64), L) << 64);
+    else return rdl64(m, L);
+  }
+  QM qfree;
   // order book pool in VGPRs: slot (j, lane)
   i32 bp[SO], bq[SO], bo[SO], bm[SO], bh[SO];
   u32 ba[SO];
@@ -940,12 +961,12 @@ struct Eng {
     int r = (int)(seq & 63u);
     u64 rot = r ? ((b >> r) | (b << (64 - r))) : b;
     int L = (ffs64(rot) + r) & 63;
-    u64 fm = rdl64(qfree, L);
-    int j = ffs64(fm);
+    QM fm = qm_rdl(qfree, L);
+    int j = qm_ffs(fm);
     int slot = j * 64 + L;
     qset(j, key, seq, lane == L);
     if (lane == L) {
-      qfree &= ~(1ull << j);
+      qfree &= ~qm_bit(j);
       if (key < mk || (key == mk && seq < ms)) {
         mk = key;
         ms = seq;
@@ -970,7 +991,7 @@ struct Eng {
     const int n = __popcll(ab);
     if (n == 0) return;
     const int r = (int)__builtin_amdgcn_mbcnt_hi((u32)(ab >> 32), __builtin_amdgcn_mbcnt_lo((u32)ab, 0u));
-    const int c = __popcll(qfree);
+    const int c = qm_pop(qfree);
     int base = 0, total = 0;
     for (int k = 0; k < SQ; k++) {
       const u64 b = bal(c > k);
@@ -981,15 +1002,15 @@ struct Eng {
       fail(ERR_QUEUE_FULL);
       return;
     }
-    u64 f = qfree;
+    QM f = qfree;
     int tj[SQ];
     for (int t = 0; t < SQ; t++) {
       tj[t] = -1;
       if (f && base + t < n) {
-        const int j = ffs64(f);
+        const int j = qm_ffs(f);
         f &= f - 1;
         scr[base + t] = j * 64 + lane;
-        qfree &= ~(1ull << j);
+        qfree &= ~qm_bit(j);
         tj[t] = j;
       }
     }
@@ -1072,7 +1093,7 @@ struct Eng {
     if (lane == (slot & 63)) {
       qk[slot] = KEY_EMPTY;
       qs[slot] = 0xFFFFFFFFu;
-      qfree |= 1ull << (slot >> 6);
+      qfree |= qm_bit(slot >> 6);
       q_rescan();
     }
     qcount--;
@@ -1086,7 +1107,7 @@ struct Eng {
 #else
   DEV void q_remove(int slot) {
     qset(slot >> 6, KEY_EMPTY, 0xFFFFFFFFu, lane == (slot & 63));
-    qfree |= (lane == (slot & 63)) ? (1ull << (slot >> 6)) : 0ull;
+    qfree |= (lane == (slot & 63)) ? qm_bit(slot >> 6) : (QM)0;
     if constexpr (QHIER) {
       q_regroup((slot >> 6) / QG);
       qcount--;
@@ -1142,7 +1163,7 @@ struct Eng {
       }
       deliver = sent + (i64)(l + (double)noise);
     }
-    u64 key = ((u64)deliver << 13) | ((u64)recipient << 2) | MT_MESSAGE;
+    u64 key = ((u64)deliver << MXA_KEY_SHIFT) | ((u64)recipient << 2) | MT_MESSAGE;
     q_push(key, seq++, m);
   }
   // Kernel.setWakeup (Kernel.py:435-462)
@@ -1152,7 +1173,7 @@ struct Eng {
       return;
     }
     Msg m = msg_make(MK_WAKEUP, 0);
-    u64 key = ((u64)t << 13) | ((u64)agent << 2) | MT_WAKEUP;
+    u64 key = ((u64)t << MXA_KEY_SHIFT) | ((u64)agent << 2) | MT_WAKEUP;
     q_push(key, seq++, m);
   }
   DEV i64 next_order_id() { return ocnt++; }
@@ -1819,7 +1840,7 @@ struct Eng {
   // zero latency, no noise draw, no replay dense ids: a message to the exchange is delivered at
   // currentTime + computation delay, so a run of sends can be pushed as one batch
   static constexpr bool BATCH = !RP && PC.lat_mode == 0 && PC.noise_len <= 1;
-  DEV u64 ex_key() { return ((u64)(cur + rg64(AF_COMP) + add_delay) << 13) | MT_MESSAGE; }
+  DEV u64 ex_key() { return ((u64)(cur + rg64(AF_COMP) + add_delay) << MXA_KEY_SHIFT) | MT_MESSAGE; }
   // cancelOrder for every open order in dict (= list) order
   DEV void cancel_all() {
     if constexpr (BATCH) {
@@ -3136,7 +3157,7 @@ struct Eng {
       return;
     }
     Msg m = msg_make(MK_KCANCEL, 0);
-    u64 key = ((u64)t << 13) | ((u64)cur_agent << 2) | MT_CANCEL_ORDER;
+    u64 key = ((u64)t << MXA_KEY_SHIFT) | ((u64)cur_agent << 2) | MT_CANCEL_ORDER;
     q_push(key, seq++, m);
   }
   DEV void rl_wakeup() {
@@ -3499,7 +3520,7 @@ struct Eng {
       qset(j, e.key, e.seq, true);
       if (PL_LDS)
         for (int i = 0; i < PW; i++) qpl[slot * PW + i] = e.pl[i];
-      if (e.key == KEY_EMPTY) qfree |= 1ull << j;
+      if (e.key == KEY_EMPTY) qfree |= qm_bit(j);
     }
     q_rescan();
     SavedOrder* so = (SavedOrder*)(env + PC.L.off_book);
@@ -3596,9 +3617,9 @@ struct Eng {
       qs[mslot] = 0xFFFFFFFFu;
     }
     __threadfence_block();
-    u64 fr = 0;
+    QM fr = 0;
     for (int j = 0; j < SQ; j++)
-      if (qk[j * 64 + lane] == KEY_EMPTY) fr |= 1ull << j;
+      if (qk[j * 64 + lane] == KEY_EMPTY) fr |= qm_bit(j);
     qfree = fr;
     q_rescan();
     qcount -= n;
@@ -3677,7 +3698,7 @@ struct Eng {
       }
     }
     const Msg r = msg_order(MK_CANCELLED, (i32)mm.w[1], nm >> 1, nm & 1, nq, (i32)mm.w[3], 0);
-    const u64 rkey = ((u64)(t + PC.ex_pipeline) << 13) | ((u64)(u32)m_agent(mm) << 2) | MT_MESSAGE;
+    const u64 rkey = ((u64)(t + PC.ex_pipeline) << MXA_KEY_SHIFT) | ((u64)(u32)m_agent(mm) << 2) | MT_MESSAGE;
     q_push_lanes(found, rkey, r);
   }
   // OrderBook.handleLimitOrder for a run of limit orders none of which can match: every buy is
@@ -3751,7 +3772,7 @@ struct Eng {
       const i32 ne = EP[h.epoch & 15] + m;
       if (lane == 0) EP[h.epoch & 15] = ne;
       const Msg a = msg_order(MK_ACCEPTED, oid, agent, buy, qty, price, 0);
-      const u64 akey = ((u64)(t + PC.ex_pipeline) << 13) | ((u64)(u32)agent << 2) | MT_MESSAGE;
+      const u64 akey = ((u64)(t + PC.ex_pipeline) << MXA_KEY_SHIFT) | ((u64)(u32)agent << 2) | MT_MESSAGE;
       q_push_lanes(v, akey, a);
     }
   }
@@ -3875,8 +3896,8 @@ struct Eng {
         break;
       }
       Msg m = pl_read(slot);
-      i64 t = (i64)(key >> 13);
-      int rcp = (int)((key >> 2) & 0x7FF);
+      i64 t = (i64)(key >> MXA_KEY_SHIFT);
+      int rcp = (int)((key >> 2) & MXA_KEY_RCP);
       int type = (int)(key & 3);
       if constexpr (RUNS) {
         // a run past stopTime is not batched: the loop stops after its first member
@@ -3997,7 +4018,7 @@ struct Eng {
       i64 at = rg64(AF_ATIME);
       PROF_ADD(0, t0);
       if (at > t) {  // agent in the future: requeue unchanged (same uniq)
-        q_rekey(slot, ((u64)at << 13) | (key & 0x1FFF));
+        q_rekey(slot, ((u64)at << MXA_KEY_SHIFT) | (key & ((1ull << MXA_KEY_SHIFT) - 1)));
         PROF_ADD(1, t0);
         continue;
       }
@@ -4163,7 +4184,8 @@ struct Builder : Eng<CFG, true> {
     this->mk = KEY_EMPTY;
     this->ms = 0xFFFFFFFFu;
     this->mj = -1;
-    this->qfree = E::SQ >= 64 ? ~0ull : ((1ull << E::SQ) - 1ull);
+    typedef typename E::QM QM;
+    this->qfree = E::SQ >= (int)(8 * sizeof(QM)) ? ~(QM)0 : (((QM)1 << E::SQ) - 1);
     for (int j = 0; j < E::SQ; j++) {
       this->qset(j, KEY_EMPTY, 0xFFFFFFFFu, true);
     }
@@ -4177,7 +4199,8 @@ struct Builder : Eng<CFG, true> {
     RS G = this->grs(0);
     int n = P.n_agents;
     u32 tmp;
-    if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_RL) {
+    if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_RL || P.config == MXA_CFG_RANDOM_FUND_VALUE) {
+      // config/rmsc03.py and config/random_fund_value.py: the same global-draw order
       set_seed(1, g_seed(G));  // O
       h.o_pt = P.mkt_open;
       h.o_pv = P.o_rbar;

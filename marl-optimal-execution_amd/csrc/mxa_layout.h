@@ -10,14 +10,16 @@
 #pragma once
 #include <stdint.h>
 
-#define MXA_MAX_AGENTS 2047  // 11-bit recipient field in the event key
+#define MXA_MAX_AGENTS 8191  // 13-bit recipient field in the event key
+#define MXA_KEY_SHIFT 15     // key = t << 15 | recipient << 2 | type (t < 2^48 ns: 78 h after midnight)
+#define MXA_KEY_RCP 0x1FFF
 #define MXA_MT_N 624
 #define MXA_MT_M 397
 #define MXA_RNG_WORDS 1280    // two 624-word MT blocks (double buffer) + pad (5120 B per stream)
 
 enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3,
                      MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6,
-                     MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8 };
+                     MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8, MXA_CFG_RANDOM_FUND_VALUE = 9 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -117,7 +119,7 @@ enum { BL_FUNDAMENTAL = -2147483647 - 1 };
 
 // one event slot as saved between launches (and payload as pushed)
 typedef struct {
-  uint64_t key;   // t << 13 | recipient << 2 | type
+  uint64_t key;   // t << MXA_KEY_SHIFT | recipient << 2 | type
   uint32_t seq;
   uint32_t pad;
   uint32_t pl[8]; // payload (6 words used except by the marketreplay config)

@@ -2224,7 +2224,7 @@ static void final_valuation(ora_env* e, agent_t* a) {
 /* TradingAgent.kernelStopping (TradingAgent.py:112-138) + Kernel mean print (Kernel.py:337-341) */
 int ora_finish(ora_env* e) {
     char line[512];
-    const char* sym = strncmp(e->config, "rmsc03", 6) == 0 ? "ABM" : "JPM";
+    const char* sym = strncmp(e->config, "rmsc03", 6) == 0 || strcmp(e->config, "random_fund_value") == 0 ? "ABM" : "JPM";
     /* one entry per distinct agent type string (value_noise names every ValueAgent's type apart) */
     char (*tnames)[96] = (char (*)[96])malloc(sizeof(char[96]) * (size_t)e->n);
     long long* gains = (long long*)malloc(sizeof(long long) * (size_t)e->n);
@@ -2400,10 +2400,14 @@ static int build_sparse_zi(ora_env* e, uint32_t seed, int big) {
     return 0;
 }
 
-static int build_rmsc03(ora_env* e, uint32_t seed) {
-    /* config/rmsc03.py:55-235 */
+/* config/rmsc03.py:55-235 (rfv = 0) and config/random_fund_value.py:59-180 (rfv = 1): the same
+ * global-draw order (oracle symbol seed, first megashock, exchange seed, per noise agent its
+ * wakeup_time then seed then size, per value agent seed then size, [market maker, momentum],
+ * kernel seed); random_fund_value has 5000 noise agents waking in 09:30-16:00, 100 value agents
+ * (lambda_a 1e-12), no market maker or momentum agents, market 09:30-16:00, kernel 09:30-16:01 */
+static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv) {
     rs_seed(&e->G, seed);
-    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 9 * NS_HOUR + 45 * NS_MIN;
+    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = rfv ? 16 * NS_HOUR : 9 * NS_HOUR + 45 * NS_MIN;
     rs_seed(&e->O, seed_u32(&e->G));
     oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
     agent_t* ex = add_agent(e, AG_EXCHANGE);
@@ -2415,8 +2419,8 @@ static int build_rmsc03(ora_env* e, uint32_t seed) {
     e->ex_pipeline = 0;
     e->ex_comp = 0;
     e->stream_history = 10;
-    int64_t nopen = 9 * NS_HOUR, nclose = 16 * NS_HOUR;
-    for (int j = 0; j < 50; j++) {
+    int64_t nopen = rfv ? open : 9 * NS_HOUR, nclose = 16 * NS_HOUR;
+    for (int j = 0; j < (rfv ? 5000 : 50); j++) {
         int64_t wt = get_wake_time(e, nopen, nclose);
         agent_t* a = add_agent(e, AG_NOISE);
         a->wakeup_time = wt;
@@ -2426,7 +2430,7 @@ static int build_rmsc03(ora_env* e, uint32_t seed) {
         snprintf(a->tname, 96, "NoiseAgent");
         trading_init(a, 10000000);
     }
-    for (int j = 0; j < 10; j++) {
+    for (int j = 0; j < (rfv ? 100 : 10); j++) {
         agent_t* a = add_agent(e, AG_VALUE);
         rs_seed(&a->rs, seed_u32(&e->G));
         a->size = rs_randint(&e->G, 20, 50);
@@ -2437,11 +2441,11 @@ static int build_rmsc03(ora_env* e, uint32_t seed) {
         a->r_bar = 1e5;
         a->kappa = 1.67e-15;
         a->sigma_s = 100000;
-        a->lambda_a = 7e-11;
+        a->lambda_a = rfv ? 1e-12 : 7e-11;
         a->r_t = 1e5;
         a->sigma_t = 0;
     }
-    {
+    for (int j = 0; j < (rfv ? 0 : 1); j++) {
         agent_t* a = add_agent(e, AG_POVMM);
         rs_seed(&a->rs, seed_u32(&e->G));
         snprintf(a->name, 96, "POV_MARKET_MAKER_AGENT_%d", a->id);
@@ -2455,7 +2459,7 @@ static int build_rmsc03(ora_env* e, uint32_t seed) {
         a->order_size = 20;
         a->aw_spread = a->aw_tv = 1;
     }
-    for (int j = 0; j < 2; j++) {
+    for (int j = 0; j < (rfv ? 0 : 2); j++) {
         agent_t* a = add_agent(e, AG_MOMENTUM);
         rs_seed(&a->rs, seed_u32(&e->G));
         a->size = rs_randint(&a->rs, 1, 10);
@@ -2659,7 +2663,7 @@ static int build_value_noise(ora_env* e, uint32_t seed) {
  * pd.date_range(09:31, 09:44, "30S"), run by a GymKernel with rmsc03's start/stop, latency
  * zeros(65, 65), noise [0.0] and compute delay 0.  The DummyRL draws nothing. */
 static int build_rmsc03_rl(ora_env* e, uint32_t seed) {
-    int rc = build_rmsc03(e, seed);
+    int rc = build_rmsc03_like(e, seed, 0);
     if (rc) return rc;
     agent_t* r = add_agent(e, AG_DUMMYRL);
     trading_init(r, 0);
@@ -2772,7 +2776,8 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     int rc;
     if (!strcmp(config, "sparse_zi_100")) rc = build_sparse_zi(e, seed, 0);
     else if (!strcmp(config, "sparse_zi_1000")) rc = build_sparse_zi(e, seed, 1);
-    else if (!strcmp(config, "rmsc03")) rc = build_rmsc03(e, seed);
+    else if (!strcmp(config, "rmsc03")) rc = build_rmsc03_like(e, seed, 0);
+    else if (!strcmp(config, "random_fund_value")) rc = build_rmsc03_like(e, seed, 1);
     else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
     else if (!strcmp(config, "value_noise")) rc = build_value_noise(e, seed);
     else if (!strcmp(config, "rmsc01")) rc = build_rmsc0x(e, seed, 0, 0);
