@@ -25,12 +25,17 @@ struct Shape {
   int waves;
   int pw;  // message payload words kept in the queue
   int hot;  // agent records kept in LDS for a launch: the exchange, then the market maker
+  int sql = 0;  // queue slots per lane in LDS (0: all sq); the rest are an HBM tier (far events)
 };
+constexpr int sq_lds(int cfg);
 #ifndef MXA_RMSC03_WAVES
 #define MXA_RMSC03_WAVES 4
 #endif
 #ifndef MXA_RMSC01_WAVES
 #define MXA_RMSC01_WAVES 4
+#endif
+#ifndef MXA_RFV_SQL
+#define MXA_RFV_SQL 12  // random_fund_value: LDS-resident queue slots per lane (96 = no HBM tier)
 #endif
 #ifndef MXA_HOT_RECORDS
 #define MXA_HOT_RECORDS 0  // measured (r01 s3i): exchange + MM records in LDS were 3 % slower than L1/L2-served loads
@@ -53,11 +58,14 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
        // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
        // maximum over 1024 seeds is 5,120 events), payload in HBM; 320 book slots (max 259)
-       : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, 1, 6, 0}
+       // the first 12 slots per lane (768) in LDS for events due within a second, the other 84 per
+       // lane an HBM tier for the far wakeups (the two-tier queue, mxa_kernels.hip q_push)
+       : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, 1, 6, 0, MXA_RFV_SQL}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
+constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
 constexpr size_t lds_bytes(int cfg) {
-  return (size_t)shape(cfg).sq * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
+  return (size_t)sq_lds(cfg) * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
          + 1024                                                                               // RNG stream windows
 #ifdef MXA_QREG
@@ -371,7 +379,9 @@ constexpr void layout(MxaParams& P, int cfg) {
   L.off_lat = (uint32_t)off;
   off = align_up(off + (uint64_t)L.lat_len * 8, 256);
   L.off_q = (uint32_t)off;
-  off = align_up(off + (uint64_t)L.qcap * sizeof(SavedEvent) + (S.pl ? 0 : (uint64_t)L.qcap * 4 * S.pw), 256);
+  off = align_up(off + (uint64_t)L.qcap * sizeof(SavedEvent) + (S.pl ? 0 : (uint64_t)L.qcap * 4 * S.pw) +
+                     (uint64_t)(S.sq - sq_lds(cfg)) * 64 * 12,  // HBM queue tier: keys, then sequence numbers
+                 256);
   L.off_book = (uint32_t)off;
   off = align_up(off + (uint64_t)L.ocap * sizeof(SavedOrder), 256);
   L.off_tx = (uint32_t)off;

@@ -153,6 +153,7 @@ DEV u64 as_u(double x) { return __builtin_bit_cast(u64, x); }
 // the draw sites inside the agent handlers never contain the twist; the build kernel
 // (BUILD = true) materializes blocks on demand instead.
 #define LDSP __attribute__((address_space(3)))
+#define GLBP __attribute__((address_space(1)))
 template <bool BUILD>
 struct RSt {
   u32* key;
@@ -382,10 +383,10 @@ struct Rec {  // named scalars, not an array: a private i64[10] is promoted to a
     }
   }
 };
-template <bool WIDE, bool MDK>
+template <bool WIDE, bool MDK, int KSH>
 DEV Rec encode(u64 key, const Msg& m) {
   Rec r;
-  r.t = (i64)(key >> MXA_KEY_SHIFT);
+  r.t = (i64)(key >> KSH);
   r.rcp = (i64)((key >> 2) & MXA_KEY_RCP);
   i32 type = (i32)(key & 3);
   r.type = type;
@@ -522,6 +523,9 @@ struct Eng {
   // grouped lane-min cache for deep queues (sparse_zi_1000: 48 slots per lane): a lane's slots
   // in groups of QG, each group's min (key, seq, slot) kept in VGPRs, so a remove or requeue
   // rescans one group of QG slots instead of all SQ
+#ifndef MXA_TIER_NEAR_NS
+#define MXA_TIER_NEAR_NS 1000000000LL  // two-tier queue: events due within this many ns take LDS slots
+#endif
 #ifndef MXA_QG
 #define MXA_QG 12  // group size at SQ >= 16 (measured, sparse_zi_1000: 4 -> 1194 ms, 6/8 -> 973, 12 -> 958)
 #endif
@@ -556,7 +560,21 @@ struct Eng {
   typedef RSt<BUILD> RS;
   typedef typename std::conditional<PL_LDS, LDSP u32*, u32*>::type PlPtr;
   static constexpr int QCAP = SQ * 64;
-  char* env;
+  // event key t << KSH | recipient << 2 | type (13 recipient bits: random_fund_value's 5,101 agents)
+  static constexpr int KSH = MXA_KEY_SHIFT;
+  static constexpr u64 KRCP = MXA_KEY_RCP;
+  static_assert(PC.n_agents <= (int)KRCP, "recipient field of the event key");
+  // two-tier queue (random_fund_value): slots j < SQL of every lane in LDS, the rest in HBM; an
+  // event is placed by its due time (far wakeups in the HBM tier), which the pop never sees
+  static constexpr int SQL = mxa_cfg::sq_lds(CFG);
+  static constexpr bool TIER = SQL < SQ;
+  static constexpr int QCL = SQL * 64;
+  static_assert(!TIER || (!PL_LDS && SQL % 12 == 0 && SQ >= 16), "HBM queue tier: payloads in HBM, whole groups per tier");
+  // the env block.  The two-tier queue configuration spells out the global address space (its
+  // generic env-derived pointers otherwise became flat accesses); the others keep the generic
+  // pointer their measured code generation was tuned with (rmsc01 1116 -> 1250 ms with it)
+  typedef typename std::conditional<TIER, GLBP char*, char*>::type EnvPtr;
+  EnvPtr env;
   int lane;
   LDSP EnvHdr& h;  // cold header fields live in LDS for the duration of a launch
   // hot header fields in SGPRs
@@ -567,6 +585,42 @@ struct Eng {
   // event queue: keys in LDS, payload in LDS (PL_LDS) or HBM; per-lane min cache
   LDSP u64* qk;
   LDSP u32* qs;
+  // HBM tier (TIER): keys and sequence numbers of slots QCL .. QCAP - 1.  Global address space
+  // spelled out: a generic pointer next to the LDS arrays let the optimizer merge the two tiers
+  // into flat accesses (273 flat loads, 1,949 scratch reloads, 2x slower)
+  static constexpr size_t OFF_HQ = PC.L.off_q + sizeof(SavedEvent) * QCAP + (PL_LDS ? 0 : (size_t)QCAP * 4 * PW);
+  DEV GLBP u64* hqk() { return (GLBP u64*)(env + OFF_HQ); }
+  DEV GLBP u32* hqs() { return (GLBP u32*)(env + OFF_HQ + (size_t)(QCAP - QCL) * 8); }
+  DEV u64 qk_get(int slot) {
+    if constexpr (TIER) {
+      if (slot >= QCL) return hqk()[slot - QCL];
+    }
+    return qk[slot];
+  }
+  DEV u32 qs_get(int slot) {
+    if constexpr (TIER) {
+      if (slot >= QCL) return hqs()[slot - QCL];
+    }
+    return qs[slot];
+  }
+  DEV void qk_put(int slot, u64 v) {
+    if constexpr (TIER) {
+      if (slot >= QCL) {
+        hqk()[slot - QCL] = v;
+        return;
+      }
+    }
+    qk[slot] = v;
+  }
+  DEV void qs_put(int slot, u32 v) {
+    if constexpr (TIER) {
+      if (slot >= QCL) {
+        hqs()[slot - QCL] = v;
+        return;
+      }
+    }
+    qs[slot] = v;
+  }
 #ifdef MXA_QREG
   u64 rk[SQ];  // this lane's queue slots (j, lane) in VGPRs: keys and seqs
   u32 rq[SQ];
@@ -578,7 +632,8 @@ struct Eng {
     for (int jj = 1; jj < SQ; jj++) v = jj == j ? rk[jj] : v;
     return v;
 #else
-    return qk[j * 64 + lane];
+    if constexpr (TIER) return qk_get(j * 64 + lane);
+    else return qk[j * 64 + lane];
 #endif
   }
   DEV u32 qseq(int j) {
@@ -587,7 +642,8 @@ struct Eng {
     for (int jj = 1; jj < SQ; jj++) v = jj == j ? rq[jj] : v;
     return v;
 #else
-    return qs[j * 64 + lane];
+    if constexpr (TIER) return qs_get(j * 64 + lane);
+    else return qs[j * 64 + lane];
 #endif
   }
   DEV void qset(int j, u64 k, u32 s, bool me) {
@@ -599,8 +655,13 @@ struct Eng {
     }
 #else
     if (me) {
-      qk[j * 64 + lane] = k;
-      qs[j * 64 + lane] = s;
+      if constexpr (TIER) {
+        qk_put(j * 64 + lane, k);
+        qs_put(j * 64 + lane, s);
+      } else {
+        qk[j * 64 + lane] = k;
+        qs[j * 64 + lane] = s;
+      }
     }
 #endif
   }
@@ -608,7 +669,10 @@ struct Eng {
 #ifdef MXA_QREG
     for (int jj = 0; jj < SQ; jj++) rk[jj] = (me && jj == j) ? k : rk[jj];
 #else
-    if (me) qk[j * 64 + lane] = k;
+    if (me) {
+      if constexpr (TIER) qk_put(j * 64 + lane, k);
+      else qk[j * 64 + lane] = k;
+    }
 #endif
   }
   PlPtr qpl;
@@ -673,9 +737,9 @@ struct Eng {
   LDSP i32* scr;     // [64] rank -> queue slot, then [64] u64 staged keys (MXA_QREG)
   LDSP u32* rwin;    // [4][64] output windows of the global RNG streams (RSt::lw)
 
-  static constexpr size_t LDS_Q = (size_t)QCAP * (12 + (PL_LDS ? 4 * PW : 0));
+  static constexpr size_t LDS_Q = (size_t)QCL * (12 + (PL_LDS ? 4 * PW : 0));
   DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr, BlRec* bl = nullptr, i32 bl_cap = 0)
-      : env(e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
+      : env((EnvPtr)e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
     rx = ctx;
     blog = bl;
     blog_cap = bl_cap;
@@ -684,8 +748,8 @@ struct Eng {
     run_skip = 0;
     lane = laneid();
     qk = (LDSP u64*)lds;
-    qs = (LDSP u32*)(lds + 8 * QCAP);
-    if constexpr (PL_LDS) qpl = (LDSP u32*)(lds + 12 * QCAP);
+    qs = (LDSP u32*)(lds + 8 * QCL);
+    if constexpr (PL_LDS) qpl = (LDSP u32*)(lds + 12 * QCL);
     else qpl = (u32*)(env + PC.L.off_q + sizeof(SavedEvent) * QCAP);  // [QCAP][PW] after the saved queue
     dirty = 0;
     hash_on = tcap >= 0;
@@ -862,6 +926,22 @@ struct Eng {
     bk = KEY_EMPTY;
     bs = 0xFFFFFFFFu;
     bj = -1;
+    if constexpr (TIER) {
+      if (j0 >= SQL) {  // a whole group of the HBM tier (groups never straddle the tiers)
+        const GLBP u64* K = hqk() + (j0 - SQL) * 64 + lane;
+        const GLBP u32* S = hqs() + (j0 - SQL) * 64 + lane;
+        for (int j = 0; j < n; j++) {
+          const u64 k = K[j * 64];
+          const u32 s = S[j * 64];
+          if (k < bk || (k == bk && s < bs)) {
+            bk = k;
+            bs = s;
+            bj = j0 + j;
+          }
+        }
+        return;
+      }
+    }
     for (int j = j0; j < j0 + n; j++) {
       int slot = j * 64 + lane;
       u64 k = qk[slot];
@@ -916,7 +996,12 @@ struct Eng {
   }
   DEV void q_rescan() {  // recompute this lane's min over its own slots
     if constexpr (QHIER) {
-      for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
+      if constexpr (TIER) {  // unrolled: a rolled loop indexes gk/gs/gj dynamically (scratch)
+#pragma unroll
+        for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
+      } else {
+        for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
+      }
       q_lanemin();
       return;
     }
@@ -953,7 +1038,14 @@ struct Eng {
     return m;
   }
   DEV void q_push(u64 key, u32 seq, const Msg& m) {
-    u64 b = bal(qfree != 0);
+    QM use = qfree;
+    if constexpr (TIER) {  // due within a second: an LDS slot; later: an HBM slot (either if full)
+      const QM lm = ((QM)1 << SQL) - 1;
+      const bool far = (i64)(key >> KSH) - cur > MXA_TIER_NEAR_NS;
+      use = far ? (qfree & ~lm) : (qfree & lm);
+      if (bal(use != 0) == 0) use = qfree;
+    }
+    u64 b = bal(use != 0);
     if (b == 0) {
       fail(ERR_QUEUE_FULL);
       return;
@@ -961,7 +1053,7 @@ struct Eng {
     int r = (int)(seq & 63u);
     u64 rot = r ? ((b >> r) | (b << (64 - r))) : b;
     int L = (ffs64(rot) + r) & 63;
-    QM fm = qm_rdl(qfree, L);
+    QM fm = qm_rdl(use, L);
     int j = qm_ffs(fm);
     int slot = j * 64 + L;
     qset(j, key, seq, lane == L);
@@ -1020,8 +1112,13 @@ struct Eng {
 #ifdef MXA_QREG
       ((LDSP u64*)(scr + 64))[r] = key;  // staged for the slot's owner lane
 #else
-      qk[slot] = key;
-      qs[slot] = seq + (u32)r;
+      if constexpr (TIER) {
+        qk_put(slot, key);
+        qs_put(slot, seq + (u32)r);
+      } else {
+        qk[slot] = key;
+        qs[slot] = seq + (u32)r;
+      }
 #endif
       Msg mw = m;
       if (r < n - 1) mw.w[0] |= MF_RUN;
@@ -1041,7 +1138,8 @@ struct Eng {
       for (int t = 0; t < SQ; t++) {
         if (tj[t] < 0) break;
         const int slot = tj[t] * 64 + lane;
-        q_gupd(tj[t], qk[slot], qs[slot]);
+        if constexpr (TIER) q_gupd(tj[t], qk_get(slot), qs_get(slot));
+        else q_gupd(tj[t], qk[slot], qs[slot]);
       }
       q_lanemin();
     } else {
@@ -1091,8 +1189,8 @@ struct Eng {
 #ifdef MXA_DIVERGENT_Q
   DEV void q_remove(int slot) {
     if (lane == (slot & 63)) {
-      qk[slot] = KEY_EMPTY;
-      qs[slot] = 0xFFFFFFFFu;
+      qk_put(slot, KEY_EMPTY);
+      qs_put(slot, 0xFFFFFFFFu);
       qfree |= qm_bit(slot >> 6);
       q_rescan();
     }
@@ -1100,7 +1198,7 @@ struct Eng {
   }
   DEV void q_rekey(int slot, u64 key) {
     if (lane == (slot & 63)) {
-      qk[slot] = key;
+      qk_put(slot, key);
       q_rescan();
     }
   }
@@ -1163,7 +1261,7 @@ struct Eng {
       }
       deliver = sent + (i64)(l + (double)noise);
     }
-    u64 key = ((u64)deliver << MXA_KEY_SHIFT) | ((u64)recipient << 2) | MT_MESSAGE;
+    u64 key = ((u64)deliver << KSH) | ((u64)recipient << 2) | MT_MESSAGE;
     q_push(key, seq++, m);
   }
   // Kernel.setWakeup (Kernel.py:435-462)
@@ -1173,7 +1271,7 @@ struct Eng {
       return;
     }
     Msg m = msg_make(MK_WAKEUP, 0);
-    u64 key = ((u64)t << MXA_KEY_SHIFT) | ((u64)agent << 2) | MT_WAKEUP;
+    u64 key = ((u64)t << KSH) | ((u64)agent << 2) | MT_WAKEUP;
     q_push(key, seq++, m);
   }
   DEV i64 next_order_id() { return ocnt++; }
@@ -1840,7 +1938,7 @@ struct Eng {
   // zero latency, no noise draw, no replay dense ids: a message to the exchange is delivered at
   // currentTime + computation delay, so a run of sends can be pushed as one batch
   static constexpr bool BATCH = !RP && PC.lat_mode == 0 && PC.noise_len <= 1;
-  DEV u64 ex_key() { return ((u64)(cur + rg64(AF_COMP) + add_delay) << MXA_KEY_SHIFT) | MT_MESSAGE; }
+  DEV u64 ex_key() { return ((u64)(cur + rg64(AF_COMP) + add_delay) << KSH) | MT_MESSAGE; }
   // cancelOrder for every open order in dict (= list) order
   DEV void cancel_all() {
     if constexpr (BATCH) {
@@ -3157,7 +3255,7 @@ struct Eng {
       return;
     }
     Msg m = msg_make(MK_KCANCEL, 0);
-    u64 key = ((u64)t << MXA_KEY_SHIFT) | ((u64)cur_agent << 2) | MT_CANCEL_ORDER;
+    u64 key = ((u64)t << KSH) | ((u64)cur_agent << 2) | MT_CANCEL_ORDER;
     q_push(key, seq++, m);
   }
   DEV void rl_wakeup() {
@@ -3568,7 +3666,7 @@ struct Eng {
   DEV void account_pop(i64 t, u64 key, const Msg& m) {
     cur = t;
     if (INSTR && (hash_on || trace)) {  // parity instrumentation (trace ring, per-pop hash)
-      const Rec rec = encode<PW == 8, MD>(key, m);
+      const Rec rec = encode<PW == 8, MD, KSH>(key, m);
       if (hash_on) hash = rec_hash(hash, rec);
       if (trace && h.trace_len < trace_cap) {
         if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
@@ -3602,8 +3700,8 @@ struct Eng {
     __threadfence_block();
     for (int j = 0; j < SQ; j++) {
       const int slot = j * 64 + lane;
-      const u32 d = qs[slot] - s0;
-      if (qk[slot] == key && d < 64u) scr[d] = slot;
+      const u32 d = qs_get(slot) - s0;
+      if (qk_get(slot) == key && d < 64u) scr[d] = slot;
     }
     __threadfence_block();
     mslot = scr[lane];
@@ -3613,13 +3711,13 @@ struct Eng {
   // the run's n slots leave the queue together (each lane rebuilds its free mask and minimum)
   DEV void q_remove_run(int n, int mslot) {
     if (lane < n) {
-      qk[mslot] = KEY_EMPTY;
-      qs[mslot] = 0xFFFFFFFFu;
+      qk_put(mslot, KEY_EMPTY);
+      qs_put(mslot, 0xFFFFFFFFu);
     }
     __threadfence_block();
     QM fr = 0;
     for (int j = 0; j < SQ; j++)
-      if (qk[j * 64 + lane] == KEY_EMPTY) fr |= qm_bit(j);
+      if (qk_get(j * 64 + lane) == KEY_EMPTY) fr |= qm_bit(j);
     qfree = fr;
     q_rescan();
     qcount -= n;
@@ -3698,7 +3796,7 @@ struct Eng {
       }
     }
     const Msg r = msg_order(MK_CANCELLED, (i32)mm.w[1], nm >> 1, nm & 1, nq, (i32)mm.w[3], 0);
-    const u64 rkey = ((u64)(t + PC.ex_pipeline) << MXA_KEY_SHIFT) | ((u64)(u32)m_agent(mm) << 2) | MT_MESSAGE;
+    const u64 rkey = ((u64)(t + PC.ex_pipeline) << KSH) | ((u64)(u32)m_agent(mm) << 2) | MT_MESSAGE;
     q_push_lanes(found, rkey, r);
   }
   // OrderBook.handleLimitOrder for a run of limit orders none of which can match: every buy is
@@ -3772,7 +3870,7 @@ struct Eng {
       const i32 ne = EP[h.epoch & 15] + m;
       if (lane == 0) EP[h.epoch & 15] = ne;
       const Msg a = msg_order(MK_ACCEPTED, oid, agent, buy, qty, price, 0);
-      const u64 akey = ((u64)(t + PC.ex_pipeline) << MXA_KEY_SHIFT) | ((u64)(u32)agent << 2) | MT_MESSAGE;
+      const u64 akey = ((u64)(t + PC.ex_pipeline) << KSH) | ((u64)(u32)agent << 2) | MT_MESSAGE;
       q_push_lanes(v, akey, a);
     }
   }
@@ -3880,7 +3978,7 @@ struct Eng {
         u32 plo = (u32)__builtin_amdgcn_readfirstlane((int)(u32)pv);
         u32 phi = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(pv >> 32));
         asm volatile("" : "+s"(plo), "+s"(phi));
-        env = (char*)(__attribute__((address_space(1))) char*)(((u64)phi << 32) | plo);
+        env = (EnvPtr)(GLBP char*)(((u64)phi << 32) | plo);
 #ifndef MXA_NO_LAUNDER_LANE
         // lane-derived masks (lane == field/2 ...) are rebuilt per use, not hoisted
         asm volatile("" : "+v"(lane));
@@ -3896,8 +3994,8 @@ struct Eng {
         break;
       }
       Msg m = pl_read(slot);
-      i64 t = (i64)(key >> MXA_KEY_SHIFT);
-      int rcp = (int)((key >> 2) & MXA_KEY_RCP);
+      i64 t = (i64)(key >> KSH);
+      int rcp = (int)((key >> 2) & KRCP);
       int type = (int)(key & 3);
       if constexpr (RUNS) {
         // a run past stopTime is not batched: the loop stops after its first member
@@ -3997,7 +4095,7 @@ struct Eng {
       rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
       cur = t;
       if (INSTR && (hash_on || trace)) {
-        const Rec rec = encode<PW == 8, MD>(key, m);
+        const Rec rec = encode<PW == 8, MD, KSH>(key, m);
         if (hash_on) hash = rec_hash(hash, rec);
         if (trace && h.trace_len < trace_cap) {
           if (lane < 10) trace[h.trace_len * 10 + lane] = rec.at(lane);
@@ -4018,7 +4116,7 @@ struct Eng {
       i64 at = rg64(AF_ATIME);
       PROF_ADD(0, t0);
       if (at > t) {  // agent in the future: requeue unchanged (same uniq)
-        q_rekey(slot, ((u64)at << MXA_KEY_SHIFT) | (key & ((1ull << MXA_KEY_SHIFT) - 1)));
+        q_rekey(slot, ((u64)at << KSH) | (key & ((1ull << KSH) - 1)));
         PROF_ADD(1, t0);
         continue;
       }

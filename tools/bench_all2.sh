@@ -18,3 +18,4 @@ run value_noise_4096 --config value_noise --envs 4096 --steps 3 --warmup 1
 run rmsc01_4096 --config rmsc01 --envs 4096 --steps 2 --warmup 1
 run rmsc02_4096 --config rmsc02 --envs 4096 --steps 2 --warmup 1
 run obi_rmsc02_4096 --config obi_rmsc02 --envs 4096 --steps 2 --warmup 1
+run random_fund_value_2048 --config random_fund_value --envs 2048 --steps 2 --warmup 1
