@@ -45,7 +45,8 @@ enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKET
        MXA_RMSC01 = 6 /* config/rmsc01.py: market maker, 50 ZI, 25 HBL, 24 momentum agents */,
        MXA_RMSC02 = 7 /* config/rmsc02.py: rmsc01 with market-data subscriptions and a latency matrix */,
        MXA_OBI_RMSC02 = 8 /* config/obi_rmsc02.py: rmsc02's market with 89 ZI, 5 order-book-imbalance agents */,
-       MXA_RANDOM_FUND_VALUE = 9 /* config/random_fund_value.py: 5000 noise + 100 value agents, 09:30-16:00 */ };
+       MXA_RANDOM_FUND_VALUE = 9 /* config/random_fund_value.py: 5000 noise + 100 value agents, 09:30-16:00 */,
+       MXA_RANDOM_FUND_DIVERSE = 10 /* config/random_fund_diverse.py: random_fund_value + market maker + 25 momentum */ };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };

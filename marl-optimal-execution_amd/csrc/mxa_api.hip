@@ -141,6 +141,7 @@ static bool bind(mxa_handle* h, int cfg) {
   case 7: e = mxa_entry_7(); break;
   case 8: e = mxa_entry_8(); break;
   case 9: e = mxa_entry_9(); break;
+  case 10: e = mxa_entry_10(); break;
 #endif
   default: return false;
   }
@@ -178,9 +179,10 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
                     (int)MXA_MARKETREPLAY == (int)MXA_CFG_MARKETREPLAY && (int)MXA_RMSC03_RL == (int)MXA_CFG_RMSC03_RL &&
                     (int)MXA_VALUE_NOISE == (int)MXA_CFG_VALUE_NOISE && (int)MXA_RMSC01 == (int)MXA_CFG_RMSC01 &&
                     (int)MXA_RMSC02 == (int)MXA_CFG_RMSC02 && (int)MXA_OBI_RMSC02 == (int)MXA_CFG_OBI_RMSC02 &&
-                    (int)MXA_RANDOM_FUND_VALUE == (int)MXA_CFG_RANDOM_FUND_VALUE,
+                    (int)MXA_RANDOM_FUND_VALUE == (int)MXA_CFG_RANDOM_FUND_VALUE &&
+                    (int)MXA_RANDOM_FUND_DIVERSE == (int)MXA_CFG_RANDOM_FUND_DIVERSE,
                 "config ids");
-  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_RANDOM_FUND_VALUE + 1, "one entry per configuration");
+  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_RANDOM_FUND_DIVERSE + 1, "one entry per configuration");
   if (config == MXA_MARKETREPLAY || !bind(h, config)) {  // replay handles: mxa_create_replay
     delete h;
     return MXA_EINVAL;

@@ -61,6 +61,9 @@ constexpr Shape shape(int cfg) {
        // the first 12 slots per lane (768) in LDS for events due within a second, the other 84 per
        // lane an HBM tier for the far wakeups (the two-tier queue, mxa_kernels.hip q_push)
        : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, 1, 6, 0, MXA_RFV_SQL}
+       // random_fund_diverse: the same queue; 448 book slots (oracle max 341 over 256 seeds) and
+       // wide replies for the market maker's depth-5 spread queries
+       : cfg == MXA_CFG_RANDOM_FUND_DIVERSE ? Shape{96, 7, false, 1, 8, 0, MXA_RFV_SQL}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
@@ -157,6 +160,27 @@ constexpr void params_random_fund_value(MxaParams& P) {
   P.noise_close = 16 * HOUR;
   P.L.open_cap = 8;
   P.L.tx_cap = 64;
+}
+
+// config/random_fund_diverse.py:157-198: random_fund_value plus a MarketMakerAgent (polling,
+// 100-101 shares, depth-5 spread queries, "1min") and 25 momentum agents (1-10 shares, 60 s)
+constexpr void params_random_fund_diverse(MxaParams& P) {
+  params_random_fund_value(P);
+  P.config = MXA_CFG_RANDOM_FUND_DIVERSE;
+  P.first_mk = 5101;
+  P.n_mk = 1;
+  P.mk_min = 100;
+  P.mk_max = 101;
+  P.mk_depth = 5;
+  P.mk_wake = MIN;
+  P.mk_last_spread = 10;
+  P.first_mom = 5102;
+  P.n_mom = 25;
+  P.mom_min = 1;
+  P.mom_max = 10;
+  P.mom_wake = MIN;
+  P.n_agents = 5127;
+  P.L.open_cap = 64;  // the market maker's ladder (oracle max 59 open orders)
 }
 
 // config/sparse_zi_100.py:73-334 and config/sparse_zi_1000.py
@@ -441,6 +465,7 @@ constexpr MxaParams params(int cfg) {
   else if (cfg == MXA_CFG_RMSC02) params_rmsc02(P);
   else if (cfg == MXA_CFG_OBI_RMSC02) params_obi_rmsc02(P);
   else if (cfg == MXA_CFG_RANDOM_FUND_VALUE) params_random_fund_value(P);
+  else if (cfg == MXA_CFG_RANDOM_FUND_DIVERSE) params_random_fund_diverse(P);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;

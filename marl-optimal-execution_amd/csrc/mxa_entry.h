@@ -35,4 +35,5 @@ MxaEntry mxa_entry_6();
 MxaEntry mxa_entry_7();
 MxaEntry mxa_entry_8();
 MxaEntry mxa_entry_9();
-#define MXA_N_CONFIGS 10
+MxaEntry mxa_entry_10();
+#define MXA_N_CONFIGS 11

@@ -4297,8 +4297,10 @@ struct Builder : Eng<CFG, true> {
     RS G = this->grs(0);
     int n = P.n_agents;
     u32 tmp;
-    if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_RL || P.config == MXA_CFG_RANDOM_FUND_VALUE) {
-      // config/rmsc03.py and config/random_fund_value.py: the same global-draw order
+    if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_RL || P.config == MXA_CFG_RANDOM_FUND_VALUE ||
+        P.config == MXA_CFG_RANDOM_FUND_DIVERSE) {
+      // config/rmsc03.py, config/random_fund_value.py and config/random_fund_diverse.py: the same
+      // global-draw order (random_fund_diverse's MarketMakerAgent seed after the value agents)
       set_seed(1, g_seed(G));  // O
       h.o_pt = P.mkt_open;
       h.o_pv = P.o_rbar;
@@ -4327,6 +4329,11 @@ struct Builder : Eng<CFG, true> {
         set_seed(4 + a, g_seed(G));
         rec_init(a, AG_POVMM);
         this->rs(AF_ORDER_SIZE, (u32)P.mm_min_size);
+        this->rec_store();
+      }
+      for (int a = P.first_mk; a < P.first_mk + P.n_mk; a++) {  // random_fund_diverse
+        set_seed(4 + a, g_seed(G));
+        rec_init(a, AG_MKTMAKER);
         this->rec_store();
       }
       for (int a = P.first_mom; a < P.first_mom + P.n_mom; a++) {

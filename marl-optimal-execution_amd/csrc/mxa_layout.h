@@ -19,7 +19,8 @@
 
 enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3,
                      MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6,
-                     MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8, MXA_CFG_RANDOM_FUND_VALUE = 9 };
+                     MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8, MXA_CFG_RANDOM_FUND_VALUE = 9,
+                     MXA_CFG_RANDOM_FUND_DIVERSE = 10 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {

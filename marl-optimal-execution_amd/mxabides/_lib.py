@@ -14,9 +14,11 @@ MXA_RMSC01 = 6
 MXA_RMSC02 = 7
 MXA_OBI_RMSC02 = 8
 MXA_RANDOM_FUND_VALUE = 9
+MXA_RANDOM_FUND_DIVERSE = 10
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000,
               "value_noise": MXA_VALUE_NOISE, "rmsc01": MXA_RMSC01, "rmsc02": MXA_RMSC02,
-              "obi_rmsc02": MXA_OBI_RMSC02, "random_fund_value": MXA_RANDOM_FUND_VALUE}
+              "obi_rmsc02": MXA_OBI_RMSC02, "random_fund_value": MXA_RANDOM_FUND_VALUE,
+              "random_fund_diverse": MXA_RANDOM_FUND_DIVERSE}
 ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
 ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",
              4: "transaction history capacity", 5: "get_transacted_volume without transactions (pandas error)",

@@ -3,7 +3,7 @@
 config/rmsc03.py:95-197, config/sparse_zi_100.py:177-256, config/sparse_zi_1000.py,
 config/value_noise.py:98-161 (every ValueAgent gets its own type string "ValueAgent {id}"),
 config/rmsc01.py:75-211 and config/rmsc02.py (the same agents), config/obi_rmsc02.py,
-config/random_fund_value.py:113-153.
+config/random_fund_value.py:113-153, config/random_fund_diverse.py:116-198.
 """
 ZI_GROUPS = [(0, 250, "1"), (0, 500, "1"), (0, 1000, "0.8"), (0, 1000, "1"), (0, 2000, "0.8"), (250, 500, "0.8"),
              (250, 500, "1")]
@@ -11,7 +11,7 @@ ZI_COUNTS = {"sparse_zi_100": [15, 15, 14, 14, 14, 14, 14], "sparse_zi_1000": [1
 
 
 def symbol_of(config):
-    return "ABM" if config in ("rmsc03", "random_fund_value") else "JPM"
+    return "ABM" if config in ("rmsc03", "random_fund_value", "random_fund_diverse") else "JPM"
 
 
 def agent_names(config):
@@ -24,9 +24,10 @@ def agent_names(config):
     if config == "value_noise":
         return (["Exchange Agent 0"] + ["NoiseAgent %d" % j for j in range(1, 101)] +
                 ["Value Agent %d" % j for j in range(101, 151)])
-    if config == "random_fund_value":
+    if config in ("random_fund_value", "random_fund_diverse"):
+        extra = ["MARKET_MAKER_AGENT_5101"] + ["MOMENTUM_AGENT_%d" % j for j in range(5102, 5127)]
         return (["EXCHANGE_AGENT"] + ["NoiseAgent %d" % j for j in range(1, 5001)] +
-                ["Value Agent %d" % j for j in range(5001, 5101)])
+                ["Value Agent %d" % j for j in range(5001, 5101)] + (extra if config == "random_fund_diverse" else []))
     if config == "rmsc03":
         return (["EXCHANGE_AGENT"] + ["NoiseAgent %d" % j for j in range(1, 51)] +
                 ["Value Agent %d" % j for j in range(51, 61)] + ["POV_MARKET_MAKER_AGENT_61"] +
@@ -49,8 +50,9 @@ def agent_type_names(config):
                 ["HeuristicBeliefLearningAgent"] * 25 + ["MomentumAgent"] * 24)
     if config == "value_noise":
         return ["ExchangeAgent"] + ["NoiseAgent"] * 100 + ["ValueAgent %d" % j for j in range(101, 151)]
-    if config == "random_fund_value":
-        return ["ExchangeAgent"] + ["NoiseAgent"] * 5000 + ["ValueAgent"] * 100
+    if config in ("random_fund_value", "random_fund_diverse"):
+        extra = ["MarketMakerAgent"] + ["MomentumAgent"] * 25 if config == "random_fund_diverse" else []
+        return ["ExchangeAgent"] + ["NoiseAgent"] * 5000 + ["ValueAgent"] * 100 + extra
     if config == "rmsc03":
         return ["ExchangeAgent"] + ["NoiseAgent"] * 50 + ["ValueAgent"] * 10 + ["POVMarketMakerAgent"] + ["MomentumAgent"] * 2
     out = ["ExchangeAgent"]

@@ -2224,7 +2224,7 @@ static void final_valuation(ora_env* e, agent_t* a) {
 /* TradingAgent.kernelStopping (TradingAgent.py:112-138) + Kernel mean print (Kernel.py:337-341) */
 int ora_finish(ora_env* e) {
     char line[512];
-    const char* sym = strncmp(e->config, "rmsc03", 6) == 0 || strcmp(e->config, "random_fund_value") == 0 ? "ABM" : "JPM";
+    const char* sym = strncmp(e->config, "rmsc03", 6) == 0 || strncmp(e->config, "random_fund_", 12) == 0 ? "ABM" : "JPM";
     /* one entry per distinct agent type string (value_noise names every ValueAgent's type apart) */
     char (*tnames)[96] = (char (*)[96])malloc(sizeof(char[96]) * (size_t)e->n);
     long long* gains = (long long*)malloc(sizeof(long long) * (size_t)e->n);
@@ -2467,6 +2467,31 @@ static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv) {
         snprintf(a->tname, 96, "MomentumAgent");
         trading_init(a, 10000000);
         a->wake_freq = 20 * NS_SEC;
+    }
+    if (rfv == 2) { /* config/random_fund_diverse.py:157-198: a MarketMakerAgent (100-101 shares, 1 min,
+                       polling) and 25 momentum agents (1-10 shares, the default 60 s) */
+        agent_t* a = add_agent(e, AG_MKTMAKER);
+        rs_seed(&a->rs, seed_u32(&e->G));
+        snprintf(a->name, 96, "MARKET_MAKER_AGENT_%d", a->id);
+        snprintf(a->tname, 96, "MarketMakerAgent");
+        trading_init(a, 10000000);
+        a->mk_min = 100;
+        a->mk_max = 101;
+        a->size = (int64_t)rint((double)rs_randint(&a->rs, a->mk_min, a->mk_max) / 2);
+        a->wake_freq = 60 * NS_SEC;
+        a->spread_depth = 5;
+        a->last_spread = 10;
+        a->subscribe = 0;
+        for (int j = 0; j < 25; j++) {
+            agent_t* m = add_agent(e, AG_MOMENTUM);
+            rs_seed(&m->rs, seed_u32(&e->G));
+            m->size = rs_randint(&m->rs, 1, 10);
+            snprintf(m->name, 96, "MOMENTUM_AGENT_%d", m->id);
+            snprintf(m->tname, 96, "MomentumAgent");
+            trading_init(m, 10000000);
+            m->wake_freq = 60 * NS_SEC;
+            m->subscribe = 0;
+        }
     }
     rs_seed(&e->K, seed_u32(&e->G));
     e->start = open;
@@ -2778,6 +2803,7 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     else if (!strcmp(config, "sparse_zi_1000")) rc = build_sparse_zi(e, seed, 1);
     else if (!strcmp(config, "rmsc03")) rc = build_rmsc03_like(e, seed, 0);
     else if (!strcmp(config, "random_fund_value")) rc = build_rmsc03_like(e, seed, 1);
+    else if (!strcmp(config, "random_fund_diverse")) rc = build_rmsc03_like(e, seed, 2);
     else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
     else if (!strcmp(config, "value_noise")) rc = build_value_noise(e, seed);
     else if (!strcmp(config, "rmsc01")) rc = build_rmsc0x(e, seed, 0, 0);

@@ -270,10 +270,11 @@ def run_config(cfg, seed, out, full):
 
     date = {"sparse_zi_100": "2019-06-28", "sparse_zi_1000": "2019-06-28", "rmsc03": "2019-06-28",
             "value_noise": "2019-06-28", "rmsc01": "2019-06-28", "rmsc02": "2019-06-28",
-            "obi_rmsc02": "2019-06-28", "random_fund_value": "2019-06-28"}[cfg]
+            "obi_rmsc02": "2019-06-28", "random_fund_value": "2019-06-28",
+            "random_fund_diverse": "2019-06-28"}[cfg]
     MIDNIGHT = int(pd.Timestamp(date).value)
     argv = ["abides.py", "-c", cfg, "-s", str(seed)]
-    if cfg in ("rmsc03", "random_fund_value"):
+    if cfg in ("rmsc03", "random_fund_value", "random_fund_diverse"):
         argv += ["-t", "ABM", "-d", "20190628"]
     sys.argv = argv
     buf = io.StringIO()
@@ -484,7 +485,9 @@ def main():
             ("obi_rmsc02", 30, False), ("obi_rmsc02", 107, False),
             # random_fund_value: rmsc03's agent classes at 5,100 agents (5000 noise, 100 value) over
             # the whole 09:30-16:00 session; ~5,100 pending events in the queue
-            ("random_fund_value", 7, False), ("random_fund_value", 123456789, False)]
+            ("random_fund_value", 7, False), ("random_fund_value", 123456789, False),
+            # random_fund_diverse: random_fund_value plus a MarketMakerAgent and 25 momentum agents
+            ("random_fund_diverse", 7, False), ("random_fund_diverse", 123456789, False)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2]]
     procs = []

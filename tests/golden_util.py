@@ -9,7 +9,8 @@ FIXTURES = [("sparse_zi_100", 123456789), ("rmsc03", 123456789), ("rmsc03", 1008
             ("sparse_zi_1000", 123456789), ("value_noise", 123456789), ("value_noise", 7),
             ("rmsc02", 7), ("rmsc02", 123456789), ("rmsc01", 7), ("rmsc01", 99),
             ("obi_rmsc02", 7), ("obi_rmsc02", 123456789), ("obi_rmsc02", 30), ("obi_rmsc02", 107),
-            ("random_fund_value", 7), ("random_fund_value", 123456789)]
+            ("random_fund_value", 7), ("random_fund_value", 123456789),
+            ("random_fund_diverse", 7), ("random_fund_diverse", 123456789)]
 
 
 def load(cfg, seed):

@@ -1,9 +1,11 @@
 """GPU parity of config/random_fund_value.py (rmsc03's agent classes at 5,101 agents: 5000 noise
 agents waking once in 09:30-16:00, 100 value agents, the sparse mean-reverting oracle, a whole
-09:30-16:00 session) against the CPU oracle: pop counts and per-pop trace hashes, the book,
-holdings and the summary log.  Every agent keeps a wakeup pending, so the event queue holds
-~5,100 events (96 slots per lane, 13-bit recipient field in the event key); the reference
-fixtures (seeds 7, 123456789) run through test_gpu_parity.py (golden_util.FIXTURES)."""
+09:30-16:00 session) and config/random_fund_diverse.py (the same plus a MarketMakerAgent and 25
+momentum agents) against the CPU oracle: pop counts and per-pop trace hashes, the book, holdings
+and the summary log.  Every agent keeps a wakeup pending, so the event queue holds ~5,100 events
+(96 slots per lane: one group per lane in LDS, seven in HBM; 13-bit recipient field in the event
+key); the reference fixtures (seeds 7, 123456789) run through test_gpu_parity.py
+(golden_util.FIXTURES)."""
 import numpy as np
 import pytest
 
@@ -19,35 +21,41 @@ def mx():
     return mxabides
 
 
-def test_gpu_random_fund_value_batch_equals_oracle(mx):
+CONFIGS = ["random_fund_value", "random_fund_diverse"]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_gpu_random_fund_batch_equals_oracle(mx, cfg):
     seeds = (np.arange(64, dtype=np.int64) * 7919 + 11) & 0xFFFFFFFF
-    m = mx.VecMarket("random_fund_value", seeds)
+    m = mx.VecMarket(cfg, seeds)
     m.run()
     s = m.summary()
-    ev, hs, _ = pyoracle.run_batch("random_fund_value", seeds.astype(np.uint32), threads=8)
+    ev, hs, _ = pyoracle.run_batch(cfg, seeds.astype(np.uint32), threads=8)
     assert (s["status"] == 1).all(), (s["status"], s["err"])
     assert (s["events"] == ev).all()
     assert (s["hash"] == hs).all()
 
 
-def test_gpu_random_fund_value_chunked_launches_equal_oracle(mx):
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_gpu_random_fund_chunked_launches_equal_oracle(mx, cfg):
     """997-pop launches: the 6,144-slot queue (payloads in HBM) and the 128-bit free-slot masks
-    are saved and rebuilt ~100 times per env"""
+    are saved and rebuilt ~100-200 times per env"""
     seeds = [123456789, 7, 42]
-    m = mx.VecMarket("random_fund_value", seeds)
+    m = mx.VecMarket(cfg, seeds)
     m.run(chunk=997)
     s = m.summary()
-    ev, hs, _ = pyoracle.run_batch("random_fund_value", np.array(seeds, dtype=np.uint32), threads=3)
+    ev, hs, _ = pyoracle.run_batch(cfg, np.array(seeds, dtype=np.uint32), threads=3)
     assert (s["status"] == 1).all(), (s["status"], s["err"])
     assert (s["events"] == ev).all() and (s["hash"] == hs).all()
 
 
-def test_gpu_random_fund_value_state_and_summary_equal_oracle(mx):
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_gpu_random_fund_state_and_summary_equal_oracle(mx, cfg):
     seeds = [7, 1008]
-    m = mx.VecMarket("random_fund_value", seeds)
+    m = mx.VecMarket(cfg, seeds)
     m.run()
     for i, sd in enumerate(seeds):
-        o = pyoracle.OracleEnv("random_fund_value", sd)
+        o = pyoracle.OracleEnv(cfg, sd)
         o.run()
         assert m.book(i, 0) == o.book(0) and m.book(i, 1) == o.book(1)
         o.finish()
