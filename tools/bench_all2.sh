@@ -19,3 +19,4 @@ run rmsc01_4096 --config rmsc01 --envs 4096 --steps 2 --warmup 1
 run rmsc02_4096 --config rmsc02 --envs 4096 --steps 2 --warmup 1
 run obi_rmsc02_4096 --config obi_rmsc02 --envs 4096 --steps 2 --warmup 1
 run random_fund_value_2048 --config random_fund_value --envs 2048 --steps 2 --warmup 1
+run random_fund_diverse_2048 --config random_fund_diverse --envs 2048 --steps 2 --warmup 1
