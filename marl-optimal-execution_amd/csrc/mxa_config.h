@@ -34,6 +34,9 @@ constexpr int sq_lds(int cfg);
 #ifndef MXA_RMSC01_WAVES
 #define MXA_RMSC01_WAVES 4
 #endif
+#ifndef MXA_RFV_WAVES
+#define MXA_RFV_WAVES 2  // random_fund_value / _diverse waves per SIMD (rfv x4096 run kernel: 1 wave/SIMD at x2048 1412 ms, 2 -> 2446, 3 -> 4014, 4 -> 4378)
+#endif
 #ifndef MXA_RFV_SQL
 #define MXA_RFV_SQL 12  // random_fund_value: LDS-resident queue slots per lane (96 = no HBM tier)
 #endif
@@ -60,10 +63,10 @@ constexpr Shape shape(int cfg) {
        // maximum over 1024 seeds is 5,120 events), payload in HBM; 320 book slots (max 259)
        // the first 12 slots per lane (768) in LDS for events due within a second, the other 84 per
        // lane an HBM tier for the far wakeups (the two-tier queue, mxa_kernels.hip q_push)
-       : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, 1, 6, 0, MXA_RFV_SQL}
+       : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, MXA_RFV_WAVES, 6, 0, MXA_RFV_SQL}
        // random_fund_diverse: the same queue; 448 book slots (oracle max 341 over 256 seeds) and
        // wide replies for the market maker's depth-5 spread queries
-       : cfg == MXA_CFG_RANDOM_FUND_DIVERSE ? Shape{96, 7, false, 1, 8, 0, MXA_RFV_SQL}
+       : cfg == MXA_CFG_RANDOM_FUND_DIVERSE ? Shape{96, 7, false, MXA_RFV_WAVES, 8, 0, MXA_RFV_SQL}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
