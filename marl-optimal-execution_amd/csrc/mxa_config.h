@@ -34,8 +34,21 @@ constexpr int sq_lds(int cfg);
 #ifndef MXA_RMSC01_WAVES
 #define MXA_RMSC01_WAVES 4
 #endif
+// run-kernel waves per SIMD the register budget targets (-D overrides for A/B builds)
+#ifndef MXA_W_RMSC02
+#define MXA_W_RMSC02 2
+#endif
+#ifndef MXA_W_OBI
+#define MXA_W_OBI 2
+#endif
+#ifndef MXA_W_Z1
+#define MXA_W_Z1 2
+#endif
+#ifndef MXA_W_VN
+#define MXA_W_VN 2
+#endif
 #ifndef MXA_RFV_WAVES
-#define MXA_RFV_WAVES 2  // random_fund_value / _diverse waves per SIMD (rfv x4096 run kernel: 1 wave/SIMD at x2048 1412 ms, 2 -> 2446, 3 -> 4014, 4 -> 4378)
+#define MXA_RFV_WAVES 2  // random_fund_value / _diverse waves per SIMD (rfv run kernel x2048: 1 wave 1412 ms, 2 waves 1230; x4096: 2 waves 2446, 3 4014, 4 4378)
 #endif
 #ifndef MXA_RFV_SQL
 #define MXA_RFV_SQL 12  // random_fund_value: LDS-resident queue slots per lane (96 = no HBM tier)
@@ -53,11 +66,11 @@ constexpr Shape shape(int cfg) {
        // wide replies for the market maker's depth-5 spread queries
        : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, MXA_RMSC01_WAVES, 8, 0}
        // rmsc02: oracle maxima over 41 seeds: 225 pending events, 299 resting orders
-       : cfg == MXA_CFG_RMSC02 ? Shape{6, 5, true, 2, 8, 0}
+       : cfg == MXA_CFG_RMSC02 ? Shape{6, 5, true, MXA_W_RMSC02, 8, 0}
        // obi_rmsc02: oracle maxima over 61 seeds: 211 pending events, 96 resting orders
-       : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 2, true, 2, 8, 0}
-       : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, 2, 6, MXA_HOT_RECORDS}
-       : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, 2, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
+       : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 2, true, MXA_W_OBI, 8, 0}
+       : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, MXA_W_Z1, 6, MXA_HOT_RECORDS}
+       : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, MXA_W_VN, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
        // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
        // maximum over 1024 seeds is 5,120 events), payload in HBM; 320 book slots (max 259)
