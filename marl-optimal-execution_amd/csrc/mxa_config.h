@@ -51,7 +51,7 @@ constexpr int sq_lds(int cfg);
 #define MXA_RFV_WAVES 2  // random_fund_value / _diverse waves per SIMD (rfv run kernel x2048: 1 wave 1412 ms, 2 waves 1230; x4096: 2 waves 2446, 3 4014, 4 4378)
 #endif
 #ifndef MXA_RFV_SQL
-#define MXA_RFV_SQL 12  // random_fund_value: LDS-resident queue slots per lane (96 = no HBM tier)
+#define MXA_RFV_SQL 24  // LDS-resident queue slots per lane (96 = no HBM tier); rfv x2048 run kernel: 12 -> 1220 ms, 24 -> 840, 36 -> 1237 (fewer waves fit)
 #endif
 #ifndef MXA_HOT_RECORDS
 #define MXA_HOT_RECORDS 0  // measured (r01 s3i): exchange + MM records in LDS were 3 % slower than L1/L2-served loads
@@ -74,8 +74,8 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
        // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
        // maximum over 1024 seeds is 5,120 events), payload in HBM; 320 book slots (max 259)
-       // the first 12 slots per lane (768) in LDS for events due within a second, the other 84 per
-       // lane an HBM tier for the far wakeups (the two-tier queue, mxa_kernels.hip q_push)
+       // the first MXA_RFV_SQL slots per lane (24: 1,536) in LDS for events due within a second,
+       // the other 72 per lane an HBM tier for the far wakeups (the two-tier queue, q_push)
        : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, MXA_RFV_WAVES, 6, 0, MXA_RFV_SQL}
        // random_fund_diverse: the same queue; 448 book slots (oracle max 341 over 256 seeds) and
        // wide replies for the market maker's depth-5 spread queries
