@@ -153,7 +153,7 @@ def test_gpu_wide_config_equals_oracle(mx, cfg, n):
     ("sparse_zi_100", [3, 5, 123456789]),           # grouped queue: 2 groups of 4 slots
     ("value_noise", [3, 5, 123456789]),             # grouped queue: 2 groups of 3 slots
     ("sparse_zi_1000", [123456789, 5]),             # grouped queue: 4 groups of 12, payload in HBM
-    ("random_fund_value", [123456789, 5]),          # two-tier queue: 1 LDS group + 7 HBM groups of 12
+    ("random_fund_value", [123456789, 5]),          # two-tier queue: 2 LDS groups + 6 HBM groups of 12
 ])
 def test_gpu_chunked_launches_equal_single(mx, cfg, seeds):
     """many save/restore cycles of the queue (LDS) and the book (VGPRs): the reload refills the

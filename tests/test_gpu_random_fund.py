@@ -3,7 +3,7 @@ agents waking once in 09:30-16:00, 100 value agents, the sparse mean-reverting o
 09:30-16:00 session) and config/random_fund_diverse.py (the same plus a MarketMakerAgent and 25
 momentum agents) against the CPU oracle: pop counts and per-pop trace hashes, the book, holdings
 and the summary log.  Every agent keeps a wakeup pending, so the event queue holds ~5,100 events
-(96 slots per lane: one group per lane in LDS, seven in HBM; 13-bit recipient field in the event
+(96 slots per lane: two groups per lane in LDS, six in HBM; 13-bit recipient field in the event
 key); the reference fixtures (seeds 7, 123456789) run through test_gpu_parity.py
 (golden_util.FIXTURES)."""
 import numpy as np
