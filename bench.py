@@ -2,42 +2,390 @@
 """Benchmark: env-steps/sec of the rmsc03 market step on MI355X (BASELINE.json metric).
 
 One env-step = one Kernel event pop in one env (the reference's ttl_messages,
-Kernel.py:211, 321-326).  One bench "step" = one full rmsc03 episode (config build from
-seeds + the whole 15-minute session + stop-time tail) of every env on every GPU; the
-per-env episode records are all-gathered over RCCL (the only collective: envs are
-independent, so the batch shards with no data-path exchange — weak scaling, 4096 envs
-per GPU).  Rank 0 prints one JSON line.
+Kernel.py:211, 321-326).  One bench "step" = one full episode (config build from seeds + the
+whole session + stop-time tail, or a whole GymKernel episode) of every env on every GPU; the
+per-env episode records (include/mxa.h mxa_write_records) are all-gathered over RCCL, the only
+collective: envs are independent, so the batch shards with no data-path exchange (weak scaling,
+`--envs` per GPU).  Rank 0 prints one JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--config rmsc03]
+
+`--gpus N` without a launcher starts N rank processes itself (one per GPU, before anything
+touches a GPU) with the same RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* environment that
+`torch.distributed.run --nproc-per-node N` gives them; under such a launcher the world size
+comes from WORLD_SIZE.  This replaces config/parallel.py:15-25 (one OS process per simulation).
+`--stub` runs the same launcher, timing and all-gather on CPU (gloo) with a synthetic engine:
+the harness self-test of tests/test_bench_launcher.py, never a bench number.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "marl-optimal-execution_amd"), os.path.join(ROOT, "oracle")]
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
-import mxabides
-from mxabides import shard
-
 METRIC = "env-steps/sec (whole node), rmsc03 100-agent market ×4096 envs, 1/2/4/8 GPUs"
-SEED0 = shard.SEED0
-ALGO_BYTES_PER_EVENT = 256  # SURVEY.md §8(d): nominal algorithmic HBM bytes per event (DESIGN.md §Roofline)
-HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+NOMINAL_BYTES_PER_EVENT = 256  # SURVEY.md §8(d) nominal figure (shown next to the counted one)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's bench size)")
+    ap.add_argument("--config", default="rmsc03")
+    ap.add_argument("--chunk", type=int, default=1 << 22, help="max pops per env per kernel launch")
+    ap.add_argument("--cpu-envs", type=int, default=None, help="CPU-baseline sample size (envs)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU-baseline threads (default: the cores this process may run on, capped by OMP_NUM_THREADS)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--parity-hash", action="store_true",
+                    help="also compute the per-pop parity hash (test instrumentation, off by default: "
+                         "tests/test_gpu_hash_switch.py shows every market result is identical either way)")
+    ap.add_argument("--ddqn-batch", type=int, default=32, help="rmsc03_ddqn: learner batch size (reference 32)")
+    ap.add_argument("--tape", default=None, help="marketreplay tape under tests/golden (IBM_2003-01-14, GOOG_2012-06-21)")
+    ap.add_argument("--stub", action="store_true", help="launcher self-test on CPU/gloo with a synthetic engine")
+    return ap.parse_args()
+
+
+DEFAULT_ENVS = {"marketreplay": 512, "sparse_zi_1000": 1024, "random_fund_value": 2048, "random_fund_diverse": 2048}
+
+
+# ----------------------------------------------------------------------------------------------
+# rank processes
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """Start n rank processes of this same command (rank r on GPU r), wait for all, return the
+    worst exit status.  Runs before this process touches any GPU; a rank that fails ends the
+    others (their exact PIDs), so no rank waits forever in a collective."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0:
+                rc = rc or c
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+class Ctx:
+    """this rank's place in the job (env of torch.distributed.run, or of spawn_ranks)"""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if args.gpus > 1 and self.world != args.gpus:
+            raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, self.world))
+        self.stub = args.stub
+        if self.stub:
+            self.device = torch.device("cpu")
+            backend = "gloo"
+        else:
+            torch.cuda.set_device(self.local)
+            self.device = torch.device("cuda", self.local)
+            backend = "nccl"  # RCCL over xGMI on ROCm
+        if self.world > 1:
+            kw = {} if self.stub else {"device_id": self.device}
+            dist.init_process_group(backend, **kw)
+
+    def sync(self):
+        if not self.stub:
+            self.torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------------
+# engines: one full episode of this rank's envs per step, records written and all-gathered
+class Engine:
+    kernel = "?"
+    launches = 0
+    kernel_ms = 0.0
+
+    def __init__(self, args, ctx):
+        import torch
+        from mxabides import shard
+        self.args, self.ctx, self.torch, self.shard = args, ctx, torch, shard
+        self.n = args.envs
+        self.records = torch.zeros((self.n, shard.RECORD_WORDS), dtype=torch.int64, device=ctx.device)
+        self.gathered = None
+        self.last_batch = None
+
+    def seeds(self, k):
+        return self.shard.env_seeds(k, self.ctx.rank, self.ctx.world, self.n)
+
+    def gather(self, k):
+        self.last_batch = k
+        self.gathered = self.shard.gather_records(self.records, self.ctx.world)
+        return self.records[:, self.shard.R_EVENTS].sum()
+
+    def check_gathered(self):
+        """rank 0: the gathered rows are in global env order (seed column) and hold this rank's
+        own rows where they belong"""
+        sh, g, n = self.shard, self.gathered, self.n
+        own = bool((g[self.ctx.rank * n:(self.ctx.rank + 1) * n] == self.records).all())
+        if not self.has_seeds:
+            return {"own_rows_in_place": own}
+        import numpy as np
+        want = np.concatenate([sh.env_seeds(self.last_batch, r, self.ctx.world, n) for r in range(self.ctx.world)])
+        got = g[:, sh.R_SEED].cpu().numpy().astype(np.uint32)
+        return {"own_rows_in_place": own, "global_env_order": bool((got == want).all())}
+
+    def env_errors(self):
+        g = self.gathered
+        return int((g[:, self.shard.R_STATUS] == 2).sum())
+
+    has_seeds = True
+
+
+class StubEngine(Engine):
+    """launcher self-test: records from the seeds, no market (CPU, gloo)"""
+    kernel = "stub"
+
+    def step(self, k, timed):
+        torch, sh = self.torch, self.shard
+        s = torch.from_numpy(self.seeds(k).astype("int64"))
+        r = self.records
+        r.zero_()
+        r[:, sh.R_EVENTS] = 1000 + s % 997
+        r[:, sh.R_HASH] = s * 31
+        r[:, sh.R_STATUS] = 1
+        r[:, sh.R_SEED] = s
+        self.launches += 1
+        return self.gather(k)
+
+    def describe(self):
+        return {"metric": "launcher self-test (stub engine, no market)", "dtype": "int64", "data": "synthetic",
+                "workload": "stub x%d envs per rank" % self.n}
+
+    def algo_bytes(self):
+        return None
+
+
+class MarketEngine(Engine):
+    """Kernel.runner configurations (VecMarket): one launch per env chunk until every env is done"""
+
+    def __init__(self, args, ctx):
+        super().__init__(args, ctx)
+        import mxabides
+        self.mx = mxabides
+        self.m = mxabides.VecMarket(args.config, self.seeds(0), device=ctx.local)
+        self.stream = self.torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
+        self.torch.cuda.set_stream(self.stream)
+        self.m.set_stream(self.stream.cuda_stream)
+        self.m.set_parity_hash(args.parity_hash)
+        self.kernel = "mxa_run_kernel<%d> (%s)" % (mxabides.CONFIG_IDS[args.config], args.config)
+
+    def step(self, k, timed):
+        m = self.m
+        m.set_seeds(self.seeds(k))
+        m.reset()
+        nl = m.run(chunk=self.args.chunk)
+        if timed:
+            self.launches += nl
+            self.kernel_ms += m.last_kernel_ms
+        m.write_records(self.records.data_ptr())
+        return self.gather(k)
+
+    def describe(self):
+        a, n = self.args, self.n
+        metric = METRIC if a.config == "rmsc03" else "env-steps/sec, %s x%d envs per GPU" % (a.config, n)
+        return {"metric": metric, "dtype": "int64", "data": "synthetic (per-env seeds; every input built on the device)",
+                "workload": "%s x%d envs per GPU, full episode per step (config build from seeds + the config's "
+                            "session), seeds %d+global_env" % (a.config, n, self.shard.SEED0),
+                "agents_per_env": self.m.n_agents}
+
+    def cpu_baseline(self, threads):
+        import numpy as np
+        import pyoracle
+        k = self.args.cpu_envs or max(2 * threads, 2048 if self.args.config in ("rmsc03", "sparse_zi_100", "value_noise")
+                                      else 8 * threads)
+        cseeds = ((self.shard.SEED0 + np.arange(k, dtype=np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+        cev, _, csec = pyoracle.run_batch(self.args.config, cseeds, threads)
+        return float(cev.sum()) / csec, "%d %s envs (seeds %d..), full episodes, C oracle (oracle/abides_oracle.c), " \
+            "%d threads, %.1f s wall" % (k, self.args.config, self.shard.SEED0, threads, csec)
+
+
+class GymEngine(Engine):
+    """GymKernel handles (rmsc03 + DummyRL from seeds, or the ABIDESEnv replay on a tape): a full
+    episode of ABIDESEnv.step calls with device-drawn actions (x ~ U(0, 0.01), level shares
+    U(0, 1), torch Philox per rank) through mxa_step_device, nothing crossing PCIe"""
+
+    def __init__(self, args, ctx):
+        super().__init__(args, ctx)
+        torch = self.torch
+        from mxabides import tape
+        from mxabides.gym import ACTION_SIZE, OBS_SIZE, VecABIDESEnv
+        self.replay = args.config == "marketreplay"
+        if self.replay:
+            self.tname = args.tape or "IBM_2003-01-14"
+            self.tp = tape.Tape.load(os.path.join(ROOT, "tests", "golden", "tape_%s.npz" % self.tname))
+            self.v = VecABIDESEnv(self.tp, self.n, device=ctx.local)
+            self.n_steps = 761  # pd.date_range(09:40, 16:00, freq="30S")
+            self.has_seeds = False
+        else:
+            self.v = VecABIDESEnv(seeds=self.seeds(0), device=ctx.local)
+            self.n_steps = 27  # pd.date_range(09:31, 09:44, "30S")
+        self.stream = torch.cuda.Stream()
+        torch.cuda.set_stream(self.stream)
+        self.v.set_stream(self.stream.cuda_stream)
+        self.v.set_parity_hash(args.parity_hash)
+        self.gen = torch.Generator(device="cuda")
+        self.gen.manual_seed(1000 + ctx.rank)
+        self.act = torch.empty((self.n_steps, self.n, ACTION_SIZE), dtype=torch.float64, device="cuda")
+        self.obs = torch.empty((self.n, OBS_SIZE), dtype=torch.float64, device="cuda")
+        self.flags = torch.empty((self.n,), dtype=torch.int32, device="cuda")
+        self.ev_pairs = []
+        self.kernel = "mxa_step_kernel<%d> (%s)" % (3 if self.replay else 4, args.config)
+
+    def step(self, k, timed):
+        torch = self.torch
+        self.v.reset(seeds=None if self.replay else self.seeds(k))
+        torch.rand(self.act.shape, generator=self.gen, dtype=torch.float64, device="cuda", out=self.act)
+        self.act[:, :, 0] *= 0.01
+        for i in range(self.n_steps):
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(self.stream)
+            self.v.step_device(self.act[i].data_ptr(), self.obs.data_ptr(), self.flags.data_ptr())
+            if timed:
+                e1.record(self.stream)
+                self.ev_pairs.append((e0, e1))
+        self.v.write_records(self.records.data_ptr())
+        return self.gather(k)
+
+    def finish_timing(self):
+        kms = [a.elapsed_time(b) for a, b in self.ev_pairs]
+        self.launches, self.kernel_ms = len(kms), sum(kms)
+
+    def describe(self):
+        n = self.n
+        if self.replay:
+            return {"metric": "env-steps/sec, ABIDESEnv market replay (%s LOBSTER tape) x%d envs per GPU" % (self.tname, n),
+                    "dtype": "int64", "data": "LOBSTER sample tape %s + device-drawn actions x~U(0,0.01), shares~U(0,1)"
+                    % self.tname, "workload": "marketreplay x%d envs per GPU, full episode (reset + %d ABIDESEnv.step) "
+                    "per bench step" % (n, self.n_steps), "tape_records": len(self.tp)}
+        return {"metric": "env-steps/sec, rmsc03 + DummyRL execution agent (GymKernel) x%d envs per GPU" % n,
+                "dtype": "int64", "data": "synthetic (seeds) + device-drawn actions x~U(0,0.01), shares~U(0,1)",
+                "workload": "rmsc03_rl x%d envs per GPU, full episode (config build + %d ABIDESEnv.step) per bench "
+                            "step, seeds %d+global_env" % (n, self.n_steps, self.shard.SEED0),
+                "agents_per_env": self.v.n_agents}
+
+    def gym_steps(self):
+        return self.n * self.ctx.world * self.n_steps
+
+    def cpu_baseline(self, threads):
+        import numpy as np
+        import pyoracle
+        k = self.args.cpu_envs or (64 * threads if self.replay else 128 * threads)
+        rs = np.random.RandomState(0)
+        acts = rs.uniform(0, 1, (self.n_steps, k, 3))
+        acts[:, :, 0] *= 0.01
+        if self.replay:
+            r = pyoracle.gym_batch(acts, threads, tape=self.tp)
+            what = "%d %s episodes" % (k, self.tname)
+        else:
+            sd = ((self.shard.SEED0 + np.arange(k, dtype=np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+            r = pyoracle.gym_batch(acts, threads, seeds=sd)
+            what = "%d rmsc03_rl episodes (seeds %d..)" % (k, self.shard.SEED0)
+        return float(r["events"].sum()) / r["seconds"], "%s, U(0, 0.01) actions, C oracle GymKernel batch " \
+            "(oracle/abides_oracle.c ora_gym_batch), %d threads, %.1f s wall" % (what, threads, r["seconds"])
+
+
+class DDQNEngine(Engine):
+    """rmsc03 + DummyRL with the DDQN execution learner in the loop (mxabides.ddqn): actions from
+    the shared Q-network (epsilon-greedy), transitions to the device replay ring, a training
+    update every 5 periods as the reference agent does.  Learner state persists across steps."""
+
+    def __init__(self, args, ctx):
+        super().__init__(args, ctx)
+        from mxabides import ddqn
+        from mxabides.gym import VecABIDESEnv
+        torch = self.torch
+        self.ddqn = ddqn
+        self.v = VecABIDESEnv(seeds=self.seeds(0), device=ctx.local)
+        self.stream = torch.cuda.Stream()
+        torch.cuda.set_stream(self.stream)
+        self.v.set_stream(self.stream.cuda_stream)
+        self.v.set_parity_hash(args.parity_hash)
+        self.learner = ddqn.DDQNLearner(device="cuda", seed=1000 + ctx.rank, batch_size=args.ddqn_batch)
+        self.task = ddqn.ExecutionTask(device="cuda")
+        self.timing = []
+        self.env_steps = torch.zeros((), dtype=torch.int64, device="cuda")
+        self.learns0 = 0
+        self.kernel = "mxa_step_kernel<4> (rmsc03_rl)"
+
+    def step(self, k, timed):
+        sh = self.shard
+        if timed and not self.timing:
+            self.learns0 = self.learner.learn_step_counter
+        r = self.ddqn.run_episode(self.v, self.learner, self.task, seeds=self.seeds(k),
+                                  timing=self.timing if timed else None)
+        if timed:
+            self.env_steps += r["env_steps"].sum()
+        self.v.write_records(self.records.data_ptr())
+        # word R_RETURN: the learner's per-env episode return (float64 bits)
+        self.records[:, sh.R_RETURN] = r["returns"].to(self.torch.float64).view(self.torch.int64)
+        return self.gather(k)
+
+    def finish_timing(self):
+        kms = [a.elapsed_time(b) for a, b in self.timing]
+        self.launches, self.kernel_ms = len(kms), sum(kms)
+
+    def describe(self):
+        n = self.n
+        return {"metric": "env-steps/sec, rmsc03 + DDQN execution learner (GymKernel) x%d envs per GPU" % n,
+                "dtype": "int64 (market), fp32 (Q-network)", "data": "synthetic (seeds); actions from the DDQN learner",
+                "workload": "rmsc03_rl x%d envs per GPU + DDQN learner (NNModel_1, batch %d, train every 5 periods), "
+                            "full episode per bench step, seeds %d+global_env" % (n, self.args.ddqn_batch, self.shard.SEED0),
+                "agents_per_env": self.v.n_agents, "learn_steps": self.learner.learn_step_counter - self.learns0}
+
+    def gym_steps(self):
+        return int(self.env_steps.item()) * self.ctx.world  # every rank steps its own envs alike
+
+
+# ----------------------------------------------------------------------------------------------
 def traffic_record(config, envs, parity_hash):
     """HBM bytes per run-kernel launch from the PMC record of THIS build (profiles/hbm_traffic_<config>.json,
     written by tools/hbm_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
     this same bench command).  A record is attached only when its build id (mxa_build_id(): a hash
     of the kernel sources and flags), config, env count and parity-hash setting all match the
     running bench; otherwise traffic is null and traffic_record says why."""
+    import mxabides
     prof = os.path.join(ROOT, "profiles", "hbm_traffic_%s.json" % config)
     if not os.path.exists(prof):
         return None, {"file": None, "match": False, "why": "no PMC record for this config"}
@@ -59,437 +407,104 @@ def traffic_record(config, envs, parity_hash):
     return p.get("bytes_per_launch"), src
 
 
-def replay_bench(args):
-    """ABIDESEnv / market replay (BASELINE configs[4] shape): n envs stepping the reference's
-    composition (Exchange + MarketReplayAgent + DummyRL) on a LOBSTER tape (IBM 2003-01-14 by
-    default; --tape GOOG_2012-06-21 has ORDER_ID 0 records) with per-env random actions.  One
-    bench step = one full episode: reset + the 761 ABIDESEnv.step calls of DummyRL's horizon
-    (09:40-16:00 every 30 s).  Actions x ~ U(0, 0.01), level shares U(0, 1) are drawn on the
-    device (torch Philox, per-rank seed) and stepped through mxa_step_device on the bench's
-    stream, so nothing crosses PCIe inside the timed region; envs that finish early stay
-    finished (the step kernel skips them)."""
-    from mxabides import tape
-    from mxabides.gym import ACTION_SIZE, OBS_SIZE, VecABIDESEnv
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    tname = args.tape or "IBM_2003-01-14"
-    tp = tape.Tape.load(os.path.join(ROOT, "tests", "golden", "tape_%s.npz" % tname))
-    n = args.envs
-    n_steps = 761  # pd.date_range(09:40, 16:00, freq="30S")
-    v = VecABIDESEnv(tp, n, device=local)
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    v.set_stream(stream.cuda_stream)
-    v.set_parity_hash(args.parity_hash)
-    gen = torch.Generator(device="cuda")
-    gen.manual_seed(1000 + rank)
-    act = torch.empty((n_steps, n, ACTION_SIZE), dtype=torch.float64, device="cuda")
-    obs = torch.empty((n, OBS_SIZE), dtype=torch.float64, device="cuda")
-    flags = torch.empty((n,), dtype=torch.int32, device="cuda")
-    res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-    ev_pairs = []
-
-    def episode(timed):
-        v.reset()
-        torch.rand(act.shape, generator=gen, dtype=torch.float64, device="cuda", out=act)
-        act[:, :, 0] *= 0.01
-        for i in range(n_steps):
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-            v.step_device(act[i].data_ptr(), obs.data_ptr(), flags.data_ptr())
-            if timed:
-                e1.record(stream)
-                ev_pairs.append((e0, e1))
-        v.write_results(res.data_ptr())
-        shard.gather_records(res, world)
-        return res[:, 0].sum()
-
-    evw = torch.zeros((), dtype=torch.int64, device="cuda")
-    for _ in range(args.warmup):  # the timed loop's exact ops
-        evw += episode(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev = torch.zeros((), dtype=torch.int64, device="cuda")
-    for _ in range(args.steps):
-        ev += episode(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    elt = torch.tensor([el], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
-        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
-    el = float(elt.item())
-    events = int(ev.item())
-    s = v.summary()
-    nerr = int((s["status"] == 2).sum())
-    if rank == 0:
-        kms = [a.elapsed_time(b) for a, b in ev_pairs]
-        avg_ms = sum(kms) / len(kms)
-        achieved = ALGO_BYTES_PER_EVENT * (events / world / len(kms)) / (avg_ms * 1e-3) / 1e9
-        out = {"metric": "env-steps/sec, ABIDESEnv market replay (%s LOBSTER tape) x%d envs per GPU" % (tname, n),
-               "value": events / el, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-               "data": "LOBSTER sample tape %s + device-drawn actions x~U(0,0.01), shares~U(0,1)" % tname,
-               "config": {"workload": "marketreplay x%d envs per GPU, full episode (reset + %d ABIDESEnv.step) per bench "
-                                      "step" % (n, n_steps),
-                          "envs_per_gpu": n, "global_envs": n * world, "tape_records": len(tp),
-                          "gym_steps_per_s": n * world * n_steps * args.steps / el,
-                          "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
-                          "parity_hash": bool(args.parity_hash),
-                          "env_errors": nerr},
-               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                            "kernel": "mxa_step_kernel<3> (marketreplay)", "avg_launch_ms": avg_ms,
-                            "launches": len(kms), "algo_bytes_per_event": ALGO_BYTES_PER_EVENT}}
-        if not args.no_cpu:
-            import pyoracle
-            k = 512  # ~10 s of one host core (8.4 M env-steps/s, ~144 k events per IBM episode)
-            t1 = time.perf_counter()
-            cev = 0
-            for i in range(k):
-                e = pyoracle.OracleGymEnv(tp)
-                r2 = np.random.RandomState(i)
-                while True:
-                    _, d_, rc = e.step([r2.uniform(0, 0.01), r2.uniform(), r2.uniform()])
-                    if d_ or rc:
-                        break
-                cev += e.events
-            cs = time.perf_counter() - t1
-            out["cpu_baseline"] = {"value": cev / cs, "unit": "env-steps/s", "cores": 1, "kind": "port",
-                                   "sample": "%d %s episodes, C oracle, 1 thread, %.1f s" % (k, tname, cs)}
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return {"nproc": os.cpu_count(), "affinity_cpus": avail, "cpu_model": model}
 
 
-def rl_bench(args):
-    """rmsc03 + DummyRL under the GymKernel step loop (BASELINE configs[3]): n envs per GPU,
-    each an rmsc03 market from its own seed with DummyRLExecutionAgent 64 stepped every 30 s
-    (09:31-09:44, 27 ABIDESEnv.step calls per episode).  Actions (x ~ U(0, 0.01), level shares
-    U(0, 1)) are drawn on the device (torch Philox, per-rank seed) and stepped through mxa_step_device on torch's
-    stream, so nothing crosses PCIe inside the timed region.  One bench step = one full
-    episode of every env (config build from seeds + 27 gym steps) + the RCCL all-gather of the
-    per-env episode records."""
-    from mxabides.gym import ACTION_SIZE, OBS_SIZE, VecABIDESEnv
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    n = args.envs
-    n_steps = 27  # pd.date_range(09:31, 09:44, "30S")
-    ACT_XMAX = 0.01  # total-volume action x ~ U(0, 0.01): up to 1,000 of the 1e5 shares per step
-    v = VecABIDESEnv(seeds=shard.env_seeds(0, rank, world, n), device=local)
-    stream = torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
-    torch.cuda.set_stream(stream)
-    v.set_stream(stream.cuda_stream)
-    v.set_parity_hash(args.parity_hash)
-    gen = torch.Generator(device="cuda")
-    gen.manual_seed(1000 + rank)
-    act = torch.empty((n_steps, n, ACTION_SIZE), dtype=torch.float64, device="cuda")
-    obs = torch.empty((n, OBS_SIZE), dtype=torch.float64, device="cuda")
-    flags = torch.empty((n,), dtype=torch.int32, device="cuda")
-    res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-    ev_pairs = []
-
-    def episode(k, timed):
-        v.reset(seeds=shard.env_seeds(k, rank, world, n))
-        torch.rand(act.shape, generator=gen, dtype=torch.float64, device="cuda", out=act)
-        act[:, :, 0] *= ACT_XMAX
-        for i in range(n_steps):
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-            v.step_device(act[i].data_ptr(), obs.data_ptr(), flags.data_ptr())
-            if timed:
-                e1.record(stream)
-                ev_pairs.append((e0, e1))
-        v.write_results(res.data_ptr())
-        shard.gather_records(res, world)
-        return res[:, 0].sum(), flags
-
-    evw = torch.zeros((), dtype=torch.int64, device="cuda")
-    dw = torch.ones((), dtype=torch.bool, device="cuda")
-    for k in range(args.warmup):  # the timed loop's exact ops (first launches of torch's kernels included)
-        e, f = episode(k, False)
-        evw += e
-        dw &= (((f & 1) != 0) | ((f & 4) != 0)).all()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev = torch.zeros((), dtype=torch.int64, device="cuda")
-    done_all = torch.ones((), dtype=torch.bool, device="cuda")
-    for k in range(args.warmup, args.warmup + args.steps):
-        e, f = episode(k, True)
-        ev += e
-        done_all &= (((f & 1) != 0) | ((f & 4) != 0)).all()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    elt = torch.tensor([el], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
-        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
-    el = float(elt.item())
-    events = int(ev.item())
-    s = v.summary()
-    n_err = int((s["status"] == 2).sum())
-    if rank == 0:
-        kms = [a.elapsed_time(b) for a, b in ev_pairs]
-        avg_ms = sum(kms) / len(kms)
-        my_ev_per_launch = events / world / len(kms)
-        achieved = ALGO_BYTES_PER_EVENT * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
-        out = {"metric": "env-steps/sec, rmsc03 + DummyRL execution agent (GymKernel) x%d envs per GPU" % n,
-               "value": events / el, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic (seeds) + device-drawn actions x~U(0,0.01), shares~U(0,1)",
-               "config": {"workload": "rmsc03_rl x%d envs per GPU, full episode (config build + %d ABIDESEnv.step) per "
-                                      "bench step, seeds %d+global_env" % (n, n_steps, SEED0),
-                          "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": v.n_agents,
-                          "gym_steps_per_s": n * world * n_steps * args.steps / el,
-                          "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
-                          "parity_hash": bool(args.parity_hash),
-                          "env_errors": n_err, "all_done": bool(done_all.item())},
-               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                            "kernel": "mxa_step_kernel<4> (rmsc03_rl)", "avg_launch_ms": avg_ms, "launches": len(kms),
-                            "algo_bytes_per_event": ALGO_BYTES_PER_EVENT}}
-        if not args.no_cpu:
-            import pyoracle
-            k = 1024  # ~12 s of one host core
-            t1 = time.perf_counter()
-            cev = 0
-            for i in range(k):
-                e = pyoracle.OracleGymEnv(seed=int(SEED0 + i))
-                r2 = np.random.RandomState(i)
-                while True:
-                    _, d_, rc = e.step([r2.uniform(0, 0.01), r2.uniform(), r2.uniform()])
-                    if d_ or rc:
-                        break
-                cev += e.events
-            cs = time.perf_counter() - t1
-            out["cpu_baseline"] = {"value": cev / cs, "unit": "env-steps/s", "cores": 1, "kind": "port",
-                                   "sample": "%d rmsc03_rl episodes, C oracle, 1 thread, %.1f s" % (k, cs)}
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-
-
-def ddqn_bench(args):
-    """rmsc03 + DummyRL (BASELINE configs[3]) with the DDQN execution learner in the loop
-    (mxabides.ddqn: the reference's DDQLearningExecutionAgent learner on PyTorch-ROCm): every
-    env's actions come from the shared Q-network (epsilon-greedy), transitions go to the device
-    replay ring and the learner trains every 5 periods, as the reference agent does. One bench
-    step = one full episode of every env (config build + 27 gym steps + learner) + the RCCL
-    all-gather of the episode records. Learner state persists across bench steps."""
-    from mxabides import ddqn
-    from mxabides.gym import VecABIDESEnv
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    n = args.envs
-    v = VecABIDESEnv(seeds=shard.env_seeds(0, rank, world, n), device=local)
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    v.set_stream(stream.cuda_stream)
-    v.set_parity_hash(args.parity_hash)
-    learner = ddqn.DDQNLearner(device="cuda", seed=1000 + rank, batch_size=args.ddqn_batch)
-    task = ddqn.ExecutionTask(device="cuda")
-    res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-    timing = []
-
-    def episode(k, timed):
-        r = ddqn.run_episode(v, learner, task, seeds=shard.env_seeds(k, rank, world, n),
-                             timing=timing if timed else None)
-        v.write_results(res.data_ptr())
-        shard.gather_records(res, world)
-        return res[:, 0].sum(), r["steps"]
-
-    evw = torch.zeros((), dtype=torch.int64, device="cuda")
-    for k in range(args.warmup):  # the timed loop's exact ops
-        evw += episode(k, False)[0]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    learns0 = learner.learn_step_counter
-    t0 = time.perf_counter()
-    ev = torch.zeros((), dtype=torch.int64, device="cuda")
-    gym_steps = 0
-    for k in range(args.warmup, args.warmup + args.steps):
-        e, ns = episode(k, True)
-        ev += e
-        gym_steps += ns
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    elt = torch.tensor([el], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
-        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
-    el = float(elt.item())
-    events = int(ev.item())
-    s = v.summary()
-    if rank == 0:
-        kms = [a.elapsed_time(b) for a, b in timing]
-        avg_ms = sum(kms) / len(kms)
-        my_ev_per_launch = events / world / len(kms)
-        achieved = ALGO_BYTES_PER_EVENT * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
-        out = {"metric": "env-steps/sec, rmsc03 + DDQN execution learner (GymKernel) x%d envs per GPU" % n,
-               "value": events / el, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "int64 (market), fp32 (Q-network)",
-               "data": "synthetic (seeds); actions from the DDQN learner",
-               "config": {"workload": "rmsc03_rl x%d envs per GPU + DDQN learner (NNModel_1, batch %d, train every "
-                                      "5 periods), full episode per bench step, seeds %d+global_env"
-                                      % (n, args.ddqn_batch, SEED0),
-                          "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": v.n_agents,
-                          "gym_steps_per_s": n * world * gym_steps / el,
-                          "learn_steps": learner.learn_step_counter - learns0,
-                          "step_kernel_ms_total": sum(kms), "wall_ms_total": 1000.0 * el,
-                          "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
-                          "parity_hash": bool(args.parity_hash),
-                          "env_errors": int((s["status"] == 2).sum())},
-               "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                            "kernel": "mxa_step_kernel<4> (rmsc03_rl)", "avg_launch_ms": avg_ms, "launches": len(kms),
-                            "algo_bytes_per_event": ALGO_BYTES_PER_EVENT}}
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+def cpu_threads(args, info):
+    if args.cpu_threads:
+        return args.cpu_threads
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(info["affinity_cpus"], omp) if omp > 0 else info["affinity_cpus"])
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--config", default="rmsc03")
-    ap.add_argument("--chunk", type=int, default=1 << 22, help="max pops per env per kernel launch")
-    ap.add_argument("--cpu-envs", type=int, default=2048, help="CPU-baseline sample size (envs)")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--parity-hash", action="store_true",
-                    help="also compute the per-pop parity hash (test instrumentation, off by default: "
-                         "tests/test_gpu_hash_switch.py shows every market result is identical either way)")
-    ap.add_argument("--ddqn-batch", type=int, default=32, help="rmsc03_ddqn: learner batch size (reference 32)")
-    ap.add_argument("--tape", default=None, help="marketreplay tape under tests/golden (IBM_2003-01-14, GOOG_2012-06-21)")
-    args = ap.parse_args()
-    if args.config == "marketreplay":
-        return replay_bench(args)
-    if args.config == "rmsc03_rl":
-        return rl_bench(args)
-    if args.config == "rmsc03_ddqn":
-        return ddqn_bench(args)
+    args = parse()
+    if args.envs is None:
+        args.envs = 4 if args.stub else DEFAULT_ENVS.get(args.config, 4096)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))  # before anything touches a GPU
+    ctx = Ctx(args)
+    torch = ctx.torch
+    if args.stub:
+        eng = StubEngine(args, ctx)
+    elif args.config in ("marketreplay", "rmsc03_rl"):
+        eng = GymEngine(args, ctx)
+    elif args.config == "rmsc03_ddqn":
+        eng = DDQNEngine(args, ctx)
+    else:
+        eng = MarketEngine(args, ctx)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    n = args.envs
-
-    def seeds_for(step):
-        return shard.env_seeds(step, rank, world, n)
-
-    m = mxabides.VecMarket(args.config, seeds_for(0), device=local)
-    stream = torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
-    torch.cuda.set_stream(stream)
-    m.set_stream(stream.cuda_stream)
-    m.set_parity_hash(args.parity_hash)
-    res = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-
-    kernel_ms, launches = [0.0], [0]
-
-    def step(k):
-        m.set_seeds(seeds_for(k))
-        m.reset()
-        launches[0] += m.run(chunk=args.chunk)
-        kernel_ms[0] += m.last_kernel_ms
-        m.write_results(res.data_ptr())
-        shard.gather_records(res, world)  # episode records over RCCL/xGMI (the only collective)
-        return res[:, 0].sum()
-
-    evw = torch.zeros((), dtype=torch.int64, device="cuda")
-    for k in range(args.warmup):
-        evw += step(k)  # the same ops as a timed step (first launches of torch's kernels included)
-    torch.cuda.synchronize()
-    kernel_ms[0], launches[0] = 0.0, 0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    dev = ctx.device
+    evw = torch.zeros((), dtype=torch.int64, device=dev)
+    for k in range(args.warmup):  # the timed loop's exact ops (first launches of torch's kernels included)
+        evw += eng.step(k, False)
+    ctx.sync()
+    ctx.barrier()
+    ctx.sync()
     t0 = time.perf_counter()
-    ev = torch.zeros((), dtype=torch.int64, device="cuda")
+    ev = torch.zeros((), dtype=torch.int64, device=dev)
     for k in range(args.warmup, args.warmup + args.steps):
-        ev += step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
-    elapsed = float(elapsed.item())
-    events = int(ev.item())
-    summ = m.summary()
-    n_err = int((summ["status"] == 2).sum())
+        ev += eng.step(k, True)
+    ctx.sync()
+    ctx.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if ctx.world > 1:
+        ctx.dist.all_reduce(el, op=ctx.dist.ReduceOp.MAX)
+        ctx.dist.all_reduce(ev, op=ctx.dist.ReduceOp.SUM)
+    elapsed, events = float(el.item()), int(ev.item())
+    if hasattr(eng, "finish_timing"):
+        eng.finish_timing()
+    chk = eng.check_gathered() if ctx.rank == 0 else None
+    n_err = eng.env_errors()
 
-    if rank == 0:
-        ms_step = 1000.0 * elapsed / args.steps
-        my_events_per_launch = events / world / max(1, launches[0])
-        avg_launch_ms = kernel_ms[0] / max(1, launches[0])
-        achieved = ALGO_BYTES_PER_EVENT * my_events_per_launch / (avg_launch_ms * 1e-3) / 1e9
-        traffic, traffic_src = traffic_record(args.config, n, bool(args.parity_hash))
-        metric = METRIC if args.config == "rmsc03" else "env-steps/sec, %s x%d envs per GPU" % (args.config, n)
-        out = {
-            "metric": metric, "value": events / elapsed, "unit": "env-steps/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": "%s x%d envs per GPU, full episode per step (config build from seeds + "
-                                   "the config's session), seeds %d+global_env" % (args.config, n, SEED0),
-                       "envs_per_gpu": n, "global_envs": n * world, "agents_per_env": m.n_agents,
-                       "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % world,
-                          "parity_hash": bool(args.parity_hash),
-                       "env_errors": n_err, "device": torch.cuda.get_device_name(local),
-                       "cus": torch.cuda.get_device_properties(local).multi_processor_count},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_record": traffic_src,
-                         "kernel": "mxa_run_kernel<%d> (%s)" % (mxabides.CONFIG_IDS[args.config], args.config), "avg_launch_ms": avg_launch_ms,
-                         "launches": launches[0], "algo_bytes_per_event": ALGO_BYTES_PER_EVENT},
-        }
-        if not args.no_cpu:
-            import pyoracle
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            cseeds = (SEED0 + np.arange(args.cpu_envs, dtype=np.int64)) & 0xFFFFFFFF
-            cev, _, csec = pyoracle.run_batch(args.config, cseeds.astype(np.uint32), threads)
-            out["cpu_baseline"] = {"value": float(cev.sum()) / csec, "unit": "env-steps/s", "cores": threads,
-                                   "kind": "port",
-                                   "sample": "%d %s envs (seeds %d..), full episodes, C oracle, %d threads, %.1f s wall "
-                                             "(~%.0f core-s)" % (args.cpu_envs, args.config, SEED0, threads, csec, csec * threads)}
+    if ctx.rank == 0:
+        d = eng.describe()
+        out = {"metric": d["metric"], "value": events / elapsed, "unit": "env-steps/s", "n_gpus": ctx.world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": d["dtype"], "data": d["data"],
+               "config": {"workload": d["workload"], "envs_per_gpu": eng.n, "global_envs": eng.n * ctx.world,
+                          "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % ctx.world,
+                          "parity_hash": bool(args.parity_hash), "env_errors": n_err, "gathered_records": chk}}
+        for key in ("agents_per_env", "tape_records", "learn_steps"):
+            if key in d:
+                out["config"][key] = d[key]
+        if hasattr(eng, "gym_steps"):
+            out["config"]["gym_steps_per_s"] = eng.gym_steps() * (args.steps if not isinstance(eng, DDQNEngine) else 1) / elapsed
+        if not args.stub:
+            out["config"]["device"] = torch.cuda.get_device_name(ctx.local)
+            out["config"]["cus"] = torch.cuda.get_device_properties(ctx.local).multi_processor_count
+            avg_ms = eng.kernel_ms / max(1, eng.launches)
+            my_ev_per_launch = events / ctx.world / max(1, eng.launches)
+            bpe = NOMINAL_BYTES_PER_EVENT
+            achieved = bpe * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
+            traffic, tsrc = (traffic_record(args.config, eng.n, bool(args.parity_hash))
+                             if isinstance(eng, MarketEngine) else (None, {"why": "no PMC record for this config"}))
+            out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_record": tsrc,
+                               "kernel": eng.kernel, "avg_launch_ms": avg_ms, "launches": eng.launches,
+                               "algo_bytes_per_event": bpe}
+            if not args.no_cpu and hasattr(eng, "cpu_baseline"):
+                info = host_info()
+                th = cpu_threads(args, info)
+                v, sample = eng.cpu_baseline(th)
+                out["cpu_baseline"] = {"value": v, "unit": "env-steps/s", "cores": th, "kind": "port", "sample": sample,
+                                       "per_core": v / th, **info}
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    ctx.close()
 
 
 if __name__ == "__main__":

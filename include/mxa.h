@@ -109,6 +109,16 @@ int mxa_set_seeds(mxa_handle* h, const uint32_t* seeds);
 /* write the per-env episode record [n_envs][4] int64 = (events, hash, status, current_time)
  * into DEVICE memory on the handle's stream (e.g. a torch tensor to all-gather over RCCL) */
 int mxa_write_results(mxa_handle* h, void* device_out);
+/* the episode record each rank contributes to the multi-GPU all-gather (replaces
+ * config/parallel.py:15-25's one-process-per-simulation result collection): DEVICE array
+ * [n_envs][MXA_RECORD_WORDS] int64 = (events, hash, status, current_time, err, seed, last_trade,
+ * order_counter, cash, holdings, gain, 0).  cash / holdings / gain: sums over the trading agents
+ * 1.. of TradingAgent.holdings['CASH'], the share position and markToMarket - starting_cash
+ * (TradingAgent.py:609-633; Kernel.py:330-341 averages the gain per agent type) for Kernel.runner
+ * handles, the execution agent's own for GymKernel handles; word 11 is the caller's (a learner's
+ * episode return).  Asynchronous on the handle's stream. */
+#define MXA_RECORD_WORDS 12
+int mxa_write_records(mxa_handle* h, void* device_out);
 /* diagnostics: copy `bytes` raw bytes of env `env`'s HBM block starting at `offset`; and
  * the block's section offsets (Layout: ag, open, rng, lat, q, book, tx, trace) */
 int mxa_read_raw(mxa_handle* h, int32_t env, int64_t offset, int64_t bytes, void* out);

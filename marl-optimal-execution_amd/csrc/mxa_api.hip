@@ -41,6 +41,48 @@ __global__ void mxa_results_kernel(const char* base, uint64_t stride, int n, int
   out[4 * i + 3] = h->cur;
 }
 
+// per-env episode record of the multi-GPU all-gather (events, status, final cash,
+// holdings, return; one wave per env): [n][MXA_RECORD_WORDS] int64, see include/mxa.h.  The cash /
+// holdings / gain words sum TradingAgent.holdings over agents 1.. (Kernel.runner configs; the gain
+// is markToMarket - starting_cash, TradingAgent.py:609-633, summed over the agents whose mean
+// Kernel.runner prints, Kernel.py:330-341) or are the execution agent's own (GymKernel handles)
+__global__ __launch_bounds__(64) void mxa_records_kernel(const char* base, uint64_t stride, int n, const uint32_t* seeds,
+                                                         uint32_t off_ag, int a0, int a1, int64_t* out) {
+  const int i = blockIdx.x, lane = threadIdx.x;
+  if (i >= n) return;
+  const char* e = base + (size_t)i * stride;
+  long long cash = 0, shares = 0, gain = 0;
+  for (int a = a0 + lane; a < a1; a += 64) {
+    const uint32_t* r = (const uint32_t*)(e + off_ag + (size_t)a * 512);
+    auto g64 = [&](int f) { return (long long)(((uint64_t)r[f + 1] << 32) | r[f]); };
+    const long long c = g64(AF_CASH), s = g64(AF_SHARES);
+    cash += c;
+    shares += s;
+    gain += c + (s ? s * g64(AF_LAST_TRADE) : 0) - g64(AF_START_CASH);
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    cash += __shfl_xor(cash, d, 64);
+    shares += __shfl_xor(shares, d, 64);
+    gain += __shfl_xor(gain, d, 64);
+  }
+  if (lane == 0) {
+    const EnvHdr* h = (const EnvHdr*)e;
+    int64_t* o = out + (size_t)MXA_RECORD_WORDS * i;
+    o[0] = h->pops;
+    o[1] = (int64_t)h->hash;
+    o[2] = h->status;
+    o[3] = h->cur;
+    o[4] = h->status == ST_ERROR ? h->err : 0;
+    o[5] = seeds[i];
+    o[6] = h->last_trade;
+    o[7] = h->order_counter;
+    o[8] = cash;
+    o[9] = shares;
+    o[10] = gain;
+    o[11] = 0;
+  }
+}
+
 // execution-agent state after a step, for a learner on the device: [n][MXA_RL_STATE_WORDS]
 // doubles = (CASH, holdings, executed qty, best bid, best ask, bid size, ask size, lob flags)
 // of DummyRLExecutionAgent (TradingAgent.holdings, ExecutionAgent.executed quantity,
@@ -460,6 +502,7 @@ int mxa_read_book_log(mxa_handle* h, int32_t env, mxa_book_rec* out, int64_t cap
   static_assert(sizeof(mxa_book_rec) == sizeof(BlRec) && offsetof(mxa_book_rec, qty) == offsetof(BlRec, qty),
                 "mxa_book_rec mirrors BlRec");
   static_assert((int)MXA_BL_FUNDAMENTAL == (int)BL_FUNDAMENTAL, "f_log record tag");
+  HIPCHK(h, hipSetDevice(h->device));
   EnvHdr hd;
   HIPCHK(h, hipMemcpyAsync(&hd, h->d_env + (size_t)env * h->P.L.env_stride, sizeof(hd), hipMemcpyDeviceToHost,
                            h->stream));
@@ -615,6 +658,18 @@ int mxa_write_results(mxa_handle* h, void* device_out) {
   int n = h->P.n_envs;
   hipLaunchKernelGGL(mxa_results_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env, h->P.L.env_stride,
                      n, (int64_t*)device_out);
+  HIPCHK(h, hipGetLastError());
+  return MXA_OK;
+}
+
+int mxa_write_records(mxa_handle* h, void* device_out) {
+  if (!h || !device_out) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  int n = h->P.n_envs;
+  // GymKernel handles: the execution agent; Kernel.runner handles: every trading agent
+  const int a0 = h->gym ? h->P.first_rl : 1, a1 = h->gym ? h->P.first_rl + 1 : h->P.n_agents;
+  hipLaunchKernelGGL(mxa_records_kernel, dim3(n), dim3(64), 0, h->stream, h->d_env, h->P.L.env_stride, n, h->d_seeds,
+                     h->P.L.off_ag, a0, a1, (int64_t*)device_out);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
 }

@@ -38,6 +38,15 @@ constexpr int sq_lds(int cfg);
 #ifndef MXA_W_RMSC02
 #define MXA_W_RMSC02 2
 #endif
+#ifndef MXA_SO_RMSC02
+#define MXA_SO_RMSC02 8
+#endif
+#ifndef MXA_SO_RFD
+#define MXA_SO_RFD 9
+#endif
+#ifndef MXA_OPEN_RFD
+#define MXA_OPEN_RFD 128
+#endif
 #ifndef MXA_W_OBI
 #define MXA_W_OBI 2
 #endif
@@ -65,21 +74,23 @@ constexpr Shape shape(int cfg) {
        // rmsc01: oracle maxima over seeds 123456789 / 7: 140 pending events, 75 resting orders;
        // wide replies for the market maker's depth-5 spread queries
        : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, MXA_RMSC01_WAVES, 8, 0}
-       // rmsc02: oracle maxima over 41 seeds: 225 pending events, 299 resting orders
-       : cfg == MXA_CFG_RMSC02 ? Shape{6, 5, true, MXA_W_RMSC02, 8, 0}
-       // obi_rmsc02: oracle maxima over 61 seeds: 211 pending events, 96 resting orders
-       : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 2, true, MXA_W_OBI, 8, 0}
+       // rmsc02: oracle maxima over the 16,384 bench seeds (batches 0-3): 225 pending events, 405
+       // resting orders (320 book slots overflowed in 0.3 % of the bench envs)
+       : cfg == MXA_CFG_RMSC02 ? Shape{6, MXA_SO_RMSC02, true, MXA_W_RMSC02, 8, 0}
+       // obi_rmsc02: oracle maxima over the 16,384 bench seeds: 211 pending events, 127 resting
+       // orders (192 book slots; 128 left one order of room)
+       : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 3, true, MXA_W_OBI, 8, 0}
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, MXA_W_Z1, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, MXA_W_VN, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
        // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
-       // maximum over 1024 seeds is 5,120 events), payload in HBM; 320 book slots (max 259)
+       // maximum over the 8,192 bench seeds is 5,125 events), payload in HBM; 320 book slots (max 279)
        // the first MXA_RFV_SQL slots per lane (24: 1,536) in LDS for events due within a second,
        // the other 72 per lane an HBM tier for the far wakeups (the two-tier queue, q_push)
        : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, MXA_RFV_WAVES, 6, 0, MXA_RFV_SQL}
-       // random_fund_diverse: the same queue; 448 book slots (oracle max 341 over 256 seeds) and
-       // wide replies for the market maker's depth-5 spread queries
-       : cfg == MXA_CFG_RANDOM_FUND_DIVERSE ? Shape{96, 7, false, MXA_RFV_WAVES, 8, 0, MXA_RFV_SQL}
+       // random_fund_diverse: the same queue; 576 book slots (oracle max 484 over the 8,192 bench
+       // seeds: 448 overflowed) and wide replies for the market maker's depth-5 spread queries
+       : cfg == MXA_CFG_RANDOM_FUND_DIVERSE ? Shape{96, MXA_SO_RFD, false, MXA_RFV_WAVES, 8, 0, MXA_RFV_SQL}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
@@ -196,7 +207,7 @@ constexpr void params_random_fund_diverse(MxaParams& P) {
   P.mom_max = 10;
   P.mom_wake = MIN;
   P.n_agents = 5127;
-  P.L.open_cap = 64;  // the market maker's ladder (oracle max 59 open orders)
+  P.L.open_cap = MXA_OPEN_RFD;  // the market maker's ladder: oracle max 78 open orders over the 8,192 bench seeds (64 overflowed)
 }
 
 // config/sparse_zi_100.py:73-334 and config/sparse_zi_1000.py

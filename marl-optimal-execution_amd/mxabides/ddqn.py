@@ -320,9 +320,11 @@ def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train
     arrival = torch.where(lob_ok, (st[:, 3] + st[:, 4]) / 2, torch.ones_like(st[:, 3]))  # mid at start_time
     rewards, actions = [], []
     stored = torch.zeros((), dtype=torch.int64, device=dev)
+    env_steps = alive.to(torch.int64)  # per env: ABIDESEnv.step calls taken while alive (the first one included)
     step_counter = 0
-    # every horizon step is enqueued without waiting for the GPU (no host read of `alive`): envs
-    # that are done stay done in the step kernel, and their rows are masked out below
+    # every horizon step is enqueued without waiting for the GPU (no host read of `alive` except
+    # on training steps): envs that are done stay done in the step kernel, and their rows are
+    # masked out below
     for _ in range(nh):
         s = task.state(obs)
         a = learner.choose_action(s)
@@ -341,15 +343,20 @@ def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train
         ok = alive & ((flags & 2) != 0) & ((flags & 4) == 0)
         r = task.reward(prev, st, arrival, task.q0)
         s2 = task.state(obs)
+        env_steps += alive.to(torch.int64)
         if learner.mode == "train":
             stored += learner.memory.add_device(s, a, s2, r, ok)
-            if step_counter % train_every == 0:
+            # the reference's agents stop training with their episode: no update on stale replay
+            # once every env is done (one host read, on training steps only)
+            if step_counter % train_every == 0 and bool(alive.any()):
                 for _ in range(updates_per_train):
                     learner.learn()
         rewards.append(torch.where(ok, r, torch.zeros_like(r)))
         actions.append(a)
         step_counter += 1
         alive = ok & ((flags & 1) == 0)
-    return {"rewards": torch.stack(rewards) if rewards else None,
-            "actions": torch.stack(actions) if actions else None,
-            "flags": flags, "arrival": arrival, "stored": stored, "steps": step_counter + 1}
+    rw = torch.stack(rewards) if rewards else None
+    return {"rewards": rw, "actions": torch.stack(actions) if actions else None,
+            "returns": rw.sum(0) if rw is not None else torch.zeros(n, dtype=torch.float64, device=dev),
+            "flags": flags, "arrival": arrival, "stored": stored, "env_steps": env_steps,
+            "steps": step_counter + 1}

@@ -90,6 +90,12 @@ class VecABIDESEnv:
         """Per-env (events, hash, status, current_time) int64 rows into device memory."""
         self._check(self.L.mxa_write_results(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_results")
 
+    def write_records(self, device_ptr):
+        """Per-env episode records [n][RECORD_WORDS] int64 into device memory (include/mxa.h
+        mxa_write_records: events, hash, status, current_time, err, seed, last_trade, order_counter,
+        cash, holdings, gain, 0), the rows bench.py all-gathers across ranks."""
+        self._check(self.L.mxa_write_records(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_records")
+
     def write_rl_state(self, device_ptr):
         """Per-env execution-agent state [n][RL_STATE_WORDS] float64 (CASH, holdings, executed,
         best bid, best ask, bid size, ask size, lob flags) into device memory, asynchronously."""

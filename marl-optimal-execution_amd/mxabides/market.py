@@ -76,6 +76,12 @@ class VecMarket:
         """Per-env (events, hash, status, current_time) int64 rows into device memory."""
         self._check(self.L.mxa_write_results(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_results")
 
+    def write_records(self, device_ptr):
+        """Per-env episode records [n][RECORD_WORDS] int64 into device memory (include/mxa.h
+        mxa_write_records: events, hash, status, current_time, err, seed, last_trade, order_counter,
+        cash, holdings, gain, 0), the rows bench.py all-gathers across ranks."""
+        self._check(self.L.mxa_write_records(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_records")
+
     def launch(self, max_pops):
         self._check(self.L.mxa_launch(self._h, max_pops), "mxa_launch")
 

@@ -12,7 +12,8 @@ import torch
 import torch.distributed as dist
 
 SEED0 = 123456789
-RECORD_WORDS = 4  # mxa_write_results: events, hash, status, current_time (int64 each)
+RECORD_WORDS = 12  # mxa_write_records (include/mxa.h MXA_RECORD_WORDS), int64 each
+R_EVENTS, R_HASH, R_STATUS, R_TIME, R_ERR, R_SEED, R_LAST, R_OCNT, R_CASH, R_HOLD, R_GAIN, R_RETURN = range(12)
 
 
 def env_seeds(batch, rank, world, n_per_rank, seed0=SEED0):
@@ -22,7 +23,7 @@ def env_seeds(batch, rank, world, n_per_rank, seed0=SEED0):
 
 
 def gather_records(local, world):
-    """All-gather the [n, 4] int64 episode records of every rank -> [world * n, 4], rank-major
+    """All-gather the [n, RECORD_WORDS] int64 episode records of every rank -> [world * n, 4], rank-major
     (= global env order).  One collective per episode batch."""
     if world == 1:
         return local

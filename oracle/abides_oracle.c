@@ -2938,6 +2938,8 @@ typedef struct {
     int64_t max_pops;
     int64_t* ev;
     uint64_t* h;
+    int32_t* err; /* optional: the env's oracle error code (0 ok, negative: fail() codes) */
+    int64_t* stats; /* optional: [n][4] ora_stats of each env */
     pthread_mutex_t mu;
     int rc;
 } batch_t;
@@ -2957,15 +2959,20 @@ static void* batch_worker(void* p) {
         ora_run(e, b->max_pops);
         b->ev[i] = e->pops;
         b->h[i] = e->hash;
+        if (b->err) b->err[i] = e->err;
+        if (b->stats) ora_stats(e, b->stats + 4 * (size_t)i);
         ora_destroy(e);
     }
     return NULL;
 }
 
-int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
-                  int64_t* events_out, uint64_t* hash_out, double* seconds_out) {
+static int run_batch_impl(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
+                          int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out,
+                          double* seconds_out) {
     batch_t b;
     memset(&b, 0, sizeof b);
+    b.err = err_out;
+    b.stats = stats_out;
     b.config = config;
     b.seeds = seeds;
     b.n = n;
@@ -2986,6 +2993,27 @@ int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads,
     return b.rc;
 }
 
+int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
+                  int64_t* events_out, uint64_t* hash_out, double* seconds_out) {
+    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, NULL, NULL, seconds_out);
+}
+
+/* the same, with each env's error code (ora_error) in err_out[n] */
+int ora_run_batch_err(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
+                      int64_t* events_out, uint64_t* hash_out, int32_t* err_out, double* seconds_out) {
+    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, err_out, NULL, seconds_out);
+}
+
+/* capacity statistics (ora_stats) of n envs: stats_out[n][4] */
+int ora_run_batch_stats(const char* config, const uint32_t* seeds, int n, int threads, int64_t* stats_out) {
+    int64_t* ev = (int64_t*)calloc(n, sizeof(int64_t));
+    uint64_t* h = (uint64_t*)calloc(n, sizeof(uint64_t));
+    int rc = run_batch_impl(config, seeds, n, threads, -1, ev, h, NULL, stats_out, NULL);
+    free(ev);
+    free(h);
+    return rc;
+}
+
 void ora_set_book_log(ora_env* e, int on) {
     e->book_log = on;
     e->nblg = 0;
@@ -2998,4 +3026,95 @@ int64_t ora_book_records(const ora_env* e, int64_t* buf, int64_t cap) {
 int64_t ora_book_log(const ora_env* e, int64_t* buf, int64_t cap) {
     if (buf) memcpy(buf, e->blg, sizeof(int64_t) * (size_t)(cap < e->nblg ? cap : e->nblg));
     return e->nblg;
+}
+
+/* ------------------------------ gym batch runner ------------------------------ */
+/* n independent GymKernel episodes (ABIDESEnv.step loop, ABIDESEnv.py:30-49), each stepped with
+ * its own action rows until done or an error: the rmsc03 + DummyRL composition from per-env seeds
+ * (config "rmsc03_rl") or the replay composition on one tape (config NULL).  Test
+ * infrastructure: bench-size parity of mxa_step against this restatement. */
+typedef struct {
+    const char* config;
+    const uint32_t* seeds;
+    const int64_t *t, *oid, *price, *size;
+    const int8_t* buy;
+    int n_rec, n, n_steps, next;
+    const double* act; /* [n_steps][n][3] */
+    int64_t* ev;
+    uint64_t* h;
+    int32_t* err;
+    int32_t* steps;
+    double* obs; /* [n][9]: the last valid observation */
+    pthread_mutex_t mu;
+    int rc;
+} gym_batch_t;
+
+static void* gym_batch_worker(void* p) {
+    gym_batch_t* b = (gym_batch_t*)p;
+    for (;;) {
+        pthread_mutex_lock(&b->mu);
+        int i = b->next++;
+        pthread_mutex_unlock(&b->mu);
+        if (i >= b->n) break;
+        ora_env* e = NULL;
+        int rc = b->config ? ora_create(b->config, b->seeds[i], &e)
+                           : ora_create_mr(b->t, b->oid, b->price, b->size, b->buy, b->n_rec, &e);
+        if (rc) {
+            b->rc = -1;
+            continue;
+        }
+        double obs[9];
+        int has = 0, done = 0, k = 0;
+        memset(b->obs + 9 * (size_t)i, 0, sizeof obs);
+        for (k = 0; k < b->n_steps; k++) {
+            int r = ora_gym_step(e, b->act + 3 * ((size_t)k * b->n + i), obs, &has, &done);
+            if (has && !r) memcpy(b->obs + 9 * (size_t)i, obs, sizeof obs);
+            if (r || done) {
+                k++;
+                break;
+            }
+        }
+        b->ev[i] = e->pops;
+        b->h[i] = e->hash;
+        b->err[i] = e->err;
+        b->steps[i] = k;
+        ora_destroy(e);
+    }
+    return NULL;
+}
+
+int ora_gym_batch(const char* config, const uint32_t* seeds, const int64_t* t, const int64_t* oid,
+                  const int64_t* price, const int64_t* size, const int8_t* buy, int n_rec, int n, int n_steps,
+                  const double* actions, int threads, int64_t* ev_out, uint64_t* hash_out, int32_t* err_out,
+                  int32_t* steps_out, double* obs_out, double* seconds_out) {
+    gym_batch_t b;
+    memset(&b, 0, sizeof b);
+    b.config = config;
+    b.seeds = seeds;
+    b.t = t;
+    b.oid = oid;
+    b.price = price;
+    b.size = size;
+    b.buy = buy;
+    b.n_rec = n_rec;
+    b.n = n;
+    b.n_steps = n_steps;
+    b.act = actions;
+    b.ev = ev_out;
+    b.h = hash_out;
+    b.err = err_out;
+    b.steps = steps_out;
+    b.obs = obs_out;
+    pthread_mutex_init(&b.mu, NULL);
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, gym_batch_worker, &b);
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (seconds_out) *seconds_out = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+    free(th);
+    pthread_mutex_destroy(&b.mu);
+    return b.rc;
 }

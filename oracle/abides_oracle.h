@@ -90,6 +90,18 @@ int ora_rl_state(const ora_env* e, int64_t* out4);
  * Each env runs at most max_pops pops (<0: to completion). Returns 0 on success. */
 int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
                   int64_t* events_out, uint64_t* hash_out, double* seconds_out);
+/* ora_run_batch plus each env's error code (0 ok; negative = the fail() code) */
+int ora_run_batch_err(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
+                      int64_t* events_out, uint64_t* hash_out, int32_t* err_out, double* seconds_out);
+/* capacity statistics of n envs run to completion: stats_out[n][4] = ora_stats */
+int ora_run_batch_stats(const char* config, const uint32_t* seeds, int n, int threads, int64_t* stats_out);
+/* n GymKernel episodes, each stepped with actions[k][i][0..2] until done or error (config
+ * "rmsc03_rl" with seeds, or NULL: the replay composition on the tape t/oid/price/size/buy).
+ * Per env: pops, hash, error code, steps taken and the last valid observation [n][9]. */
+int ora_gym_batch(const char* config, const uint32_t* seeds, const int64_t* t, const int64_t* oid,
+                  const int64_t* price, const int64_t* size, const int8_t* buy, int n_rec, int n, int n_steps,
+                  const double* actions, int threads, int64_t* ev_out, uint64_t* hash_out, int32_t* err_out,
+                  int32_t* steps_out, double* obs_out, double* seconds_out);
 
 /* numpy-legacy RNG known-answer helpers (tests) */
 typedef struct ora_rs ora_rs;

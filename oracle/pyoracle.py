@@ -58,6 +58,8 @@ def lib():
         L.ora_rl_state.argtypes = [P, ctypes.c_void_p]
         L.ora_run_batch.argtypes = [ctypes.c_char_p, ctypes.c_void_p, I32, I32, I64, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        L.ora_run_batch_err.argtypes = [ctypes.c_char_p, ctypes.c_void_p, I32, I32, I64, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         L.ora_rs_new.argtypes = [ctypes.c_uint32]
         L.ora_rs_new.restype = P
         L.ora_rs_free.argtypes = [P]
@@ -217,6 +219,64 @@ def run_batch(config, seeds, threads, max_pops=-1):
     if rc:
         raise RuntimeError("oracle batch failed")
     return ev, hs, sec.value
+
+
+def run_batch_err(config, seeds, threads, max_pops=-1):
+    """run_batch plus each env's oracle error code (0 ok, negative fail() code)"""
+    L = lib()
+    seeds = np.asarray(seeds, dtype=np.uint32)
+    ev = np.zeros(len(seeds), dtype=np.int64)
+    hs = np.zeros(len(seeds), dtype=np.uint64)
+    er = np.zeros(len(seeds), dtype=np.int32)
+    sec = ctypes.c_double()
+    rc = L.ora_run_batch_err(config.encode(), seeds.ctypes.data, len(seeds), threads, max_pops, ev.ctypes.data,
+                             hs.ctypes.data, er.ctypes.data, ctypes.byref(sec))
+    if rc:
+        raise RuntimeError("oracle batch failed")
+    return ev, hs, er, sec.value
+
+
+def batch_stats(config, seeds, threads):
+    """[n][4] capacity statistics (max pending events, max resting orders, max open orders of one
+    agent, max live transaction records) of each env run to completion"""
+    L = lib()
+    L.ora_run_batch_stats.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+    out = np.zeros((len(seeds), 4), dtype=np.int64)
+    if L.ora_run_batch_stats(config.encode(), seeds.ctypes.data, len(seeds), threads, out.ctypes.data):
+        raise RuntimeError("oracle batch failed")
+    return out
+
+
+def gym_batch(actions, threads, seeds=None, tape=None):
+    """n GymKernel episodes on host threads: actions [n_steps][n][3]; seeds -> the rmsc03 + DummyRL
+    composition, tape -> the replay composition.  Returns dict of per-env events, hash, err
+    (oracle fail() code), steps and the last valid obs [n][9], plus seconds."""
+    L = lib()
+    L.ora_gym_batch.argtypes = [ctypes.c_char_p] + [ctypes.c_void_p] * 6 + [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int] \
+        + [ctypes.c_void_p] * 5 + [ctypes.POINTER(ctypes.c_double)]
+    act = np.ascontiguousarray(actions, dtype=np.float64)
+    n_steps, n = act.shape[0], act.shape[1]
+    ev = np.zeros(n, dtype=np.int64)
+    hs = np.zeros(n, dtype=np.uint64)
+    er = np.zeros(n, dtype=np.int32)
+    st = np.zeros(n, dtype=np.int32)
+    obs = np.zeros((n, 9), dtype=np.float64)
+    sec = ctypes.c_double()
+    if tape is None:
+        sd = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
+        assert len(sd) == n
+        rc = L.ora_gym_batch(b"rmsc03_rl", sd.ctypes.data, None, None, None, None, None, 0, n, n_steps, act.ctypes.data,
+                             threads, ev.ctypes.data, hs.ctypes.data, er.ctypes.data, st.ctypes.data, obs.ctypes.data,
+                             ctypes.byref(sec))
+    else:
+        rc = L.ora_gym_batch(None, None, tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
+                             tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), n, n_steps, act.ctypes.data,
+                             threads, ev.ctypes.data, hs.ctypes.data, er.ctypes.data, st.ctypes.data, obs.ctypes.data,
+                             ctypes.byref(sec))
+    if rc:
+        raise RuntimeError("oracle gym batch failed")
+    return dict(events=ev, hash=hs, err=er, steps=st, obs=obs, seconds=sec.value)
 
 
 class OracleGymEnv(OracleEnv):
