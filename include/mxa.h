@@ -83,8 +83,15 @@ typedef struct {
 /* configuration id + per-env seeds (the reference config's -s/--seed) */
 int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device,
                int32_t trace_cap, mxa_handle** out);
-/* rebuild envs from their seeds (env_mask: NULL = all) — runs the config construction */
+/* rebuild envs from their seeds (env_mask: NULL = all) — runs the config construction.  On a
+ * GymKernel handle (mxa_create_replay, MXA_RMSC03_RL) a reset is ABIDESEnv.reset in the same
+ * process: Order.order_id / Order._order_ids carry over from the env's previous episode
+ * (util/order/Order.py:8-9, 27-42), so auto ids continue and skip
+ * every id used before; mxa_set_id_persistence(h, 0) makes every reset a fresh process. */
 int mxa_reset(mxa_handle* h, const uint8_t* env_mask);
+/* GymKernel handles only (MXA_EINVAL otherwise): 1 (the default) = consecutive episodes of one
+ * process per env, 0 = every mxa_reset starts a fresh process (order ids from 0) */
+int mxa_set_id_persistence(mxa_handle* h, int32_t on);
 /* one asynchronous launch: every running env performs up to max_pops kernel pops */
 int mxa_launch(mxa_handle* h, int64_t max_pops);
 int mxa_sync(mxa_handle* h);

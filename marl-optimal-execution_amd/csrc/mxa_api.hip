@@ -143,6 +143,9 @@ struct mxa_handle {
   double *d_act = nullptr, *d_obs = nullptr;
   int32_t* d_flags = nullptr;
   bool parity_hash = true;  // per-pop trace hash (test instrumentation); off: kernel tcap -1
+  // GymKernel handles: mxa_reset continues Order.order_id / Order._order_ids of the previous
+  // episode (one process running consecutive ABIDESEnv episodes)
+  bool persist_ids = false;
   int32_t tcap_arg() const { return (parity_hash || P.L.trace_cap > 0) ? P.L.trace_cap : -1; }
   // the run kernel of the current settings: the log variant, the instrumented one, or (hash off,
   // no trace ring) the one without the parity instrumentation
@@ -151,7 +154,7 @@ struct mxa_handle {
     return (tcap_arg() < 0 && run_fast) ? run_fast : run;
   }
   std::vector<char> tape_blob;  // host staging of the tape (uploaded by create_common)
-  size_t tb_t, tb_oid, tb_dense, tb_price, tb_size, tb_buy, tb_tm, tb_tm0;
+  size_t tb_t, tb_oid, tb_dense, tb_price, tb_size, tb_buy, tb_tm, tb_tm0, tb_uid, tb_ufirst;
 };
 
 static int hip_fail(mxa_handle* h, hipError_t e, const char* what) {
@@ -270,6 +273,8 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
     h->ctx.buy = (const int8_t*)(h->d_tape + h->tb_buy);
     h->ctx.tm = (const int64_t*)(h->d_tape + h->tb_tm);
     h->ctx.tm0 = (const int32_t*)(h->d_tape + h->tb_tm0);
+    h->ctx.uid = (const int32_t*)(h->d_tape + h->tb_uid);
+    h->ctx.ufirst = (const int32_t*)(h->d_tape + h->tb_ufirst);
   }
   if (h->gym) {
     HIPCHK(h, hipMalloc(&h->d_ctx, sizeof(RpCtx)));
@@ -279,7 +284,9 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
     HIPCHK(h, hipMalloc(&h->d_flags, sizeof(int32_t) * n_envs));
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
-  return mxa_reset(h, nullptr);
+  const int rc = mxa_reset(h, nullptr);  // a fresh process: ids from 0
+  h->persist_ids = h->gym;               // later resets continue the process (Order.py:8-9)
+  return rc;
 }
 
 // ABIDESEnv on a LOBSTER tape (agent_config.py / ABIDESEnv.py); see include/mxa.h
@@ -307,6 +314,16 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
   // happen while every auto id stays below the smallest tape id
   const int64_t auto_cap = (int64_t)P0.rl_ids + n_zero;
   if (min_id <= auto_cap) return MXA_EINVAL;
+  // Order._order_ids of the tape (for later episodes of a process): each explicit id with its
+  // first SIZE > 0 record, sorted by id
+  std::vector<std::pair<int32_t, int32_t>> uf;
+  for (int i = 0; i < n_rec; i++)
+    if (oid[i] != 0 && size[i] > 0) uf.push_back({(int32_t)oid[i], i});
+  std::sort(uf.begin(), uf.end());
+  uf.erase(std::unique(uf.begin(), uf.end(), [](const std::pair<int32_t, int32_t>& a, const std::pair<int32_t, int32_t>& b) {
+             return a.first == b.first;
+           }),
+           uf.end());  // sorted by (id, record): the first of each id is kept
   mxa_handle* h = new mxa_handle();
   if (!bind(h, MXA_CFG_MARKETREPLAY)) {
     delete h;
@@ -341,8 +358,12 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
   tm0.push_back(n_rec);
   const int ntm = (int)tm.size();
   const int C = n_rec + h->P.rl_ids;  // every placement could rest at once
+  // auto-id dense range: the episode's auto ids, the explicit ids they may skip over in a later
+  // episode (MXA_AUTO_SKIP), and one never-present index (orders.get(0) without an auto id 0)
   h->ctx.L = mxa_cfg::replay_layout(mxa_cfg::env_stride(MXA_CFG_MARKETREPLAY, trace_cap), (int)pmin, (int)(pmax - pmin + 1), C,
-                                    n_ids, (int)auto_cap, ntm, n_rec);
+                                    n_ids, (int)auto_cap + MXA_AUTO_SKIP + 1, ntm, n_rec);
+  h->ctx.nuid = (int32_t)uf.size();
+  h->ctx.umin = uf.empty() ? INT32_MAX : uf[0].first;
   h->P.L.env_stride = h->ctx.L.end;
   // tape blob: t, oid, dense, price, size, buy, tm, tm0 (256-B aligned pieces)
   auto al = [](size_t x) { return (x + 255) / 256 * 256; };
@@ -363,6 +384,10 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
   off = al(off + 8ull * ntm);
   h->tb_tm0 = off;
   off = al(off + 4ull * (ntm + 1));
+  h->tb_uid = off;
+  off = al(off + 4ull * uf.size() + 4);
+  h->tb_ufirst = off;
+  off = al(off + 4ull * uf.size() + 4);
   h->tape_blob.assign(off, 0);
   char* b = h->tape_blob.data();
   for (int i = 0; i < n_rec; i++) {
@@ -375,6 +400,10 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
   }
   memcpy(b + h->tb_tm, tm.data(), 8ull * ntm);
   memcpy(b + h->tb_tm0, tm0.data(), 4ull * (ntm + 1));
+  for (size_t i = 0; i < uf.size(); i++) {
+    ((int32_t*)(b + h->tb_uid))[i] = uf[i].first;
+    ((int32_t*)(b + h->tb_ufirst))[i] = uf[i].second;
+  }
   std::vector<uint32_t> seeds(n_envs, 0u);  // nothing in this composition draws
   return create_common(h, n_envs, seeds.data(), device, out);
 #endif
@@ -421,14 +450,29 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
   if (!h) return MXA_EINVAL;
   HIPCHK(h, hipSetDevice(h->device));
   const uint8_t* dm = nullptr;
-  if (mask) {
-    HIPCHK(h, hipMemcpyAsync(h->d_mask, mask, h->P.n_envs, hipMemcpyHostToDevice, h->stream));
+  if (h->persist_ids) {  // mask value 2: rebuild the env, keep its order-id counters
+    std::vector<uint8_t> m2(h->P.n_envs);
+    for (int i = 0; i < h->P.n_envs; i++) m2[i] = (!mask || mask[i]) ? 2 : 0;
+    HIPCHK(h, hipMemcpyAsync(h->d_mask, m2.data(), h->P.n_envs, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));  // m2 is a host temporary
+    dm = h->d_mask;
+  } else if (mask) {
+    std::vector<uint8_t> m1(h->P.n_envs);
+    for (int i = 0; i < h->P.n_envs; i++) m1[i] = mask[i] ? 1 : 0;
+    HIPCHK(h, hipMemcpyAsync(h->d_mask, m1.data(), h->P.n_envs, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     dm = h->d_mask;
   }
   h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_seeds, dm,
            h->d_ctx);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_set_id_persistence(mxa_handle* h, int32_t on) {
+  if (!h || (on && !h->gym)) return MXA_EINVAL;
+  h->persist_ids = on != 0;
   return MXA_OK;
 }
 

@@ -44,8 +44,24 @@ constexpr int sq_lds(int cfg);
 #ifndef MXA_SO_RFD
 #define MXA_SO_RFD 9
 #endif
+// random_fund_diverse with 576 book slots and 128 open orders per agent (r03 s4, x2048, same
+// results): 2 waves/SIMD 2421 ms, 1 wave 1861 ms, 1 wave + 48 LDS queue slots per lane 1810 ms
+#ifndef MXA_RFD_WAVES
+#define MXA_RFD_WAVES 1
+#endif
+#ifndef MXA_RFD_SQL
+#define MXA_RFD_SQL 48
+#endif
+// configurations whose agent-record write-back stores only the changed 128-byte quarters
+// (bit = config id; measured per configuration)
+#ifndef MXA_DIRTY_WB_MASK
+#define MXA_DIRTY_WB_MASK 0
+#endif
 #ifndef MXA_OPEN_RFD
 #define MXA_OPEN_RFD 128
+#endif
+#ifndef MXA_AUTO_SKIP
+#define MXA_AUTO_SKIP 1024  // replay: explicit tape ids one episode's auto ids may skip (Order.generateOrderId)
 #endif
 #ifndef MXA_W_OBI
 #define MXA_W_OBI 2
@@ -90,7 +106,7 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, MXA_RFV_WAVES, 6, 0, MXA_RFV_SQL}
        // random_fund_diverse: the same queue; 576 book slots (oracle max 484 over the 8,192 bench
        // seeds: 448 overflowed) and wide replies for the market maker's depth-5 spread queries
-       : cfg == MXA_CFG_RANDOM_FUND_DIVERSE ? Shape{96, MXA_SO_RFD, false, MXA_RFV_WAVES, 8, 0, MXA_RFV_SQL}
+       : cfg == MXA_CFG_RANDOM_FUND_DIVERSE ? Shape{96, MXA_SO_RFD, false, MXA_RFD_WAVES, 8, 0, MXA_RFD_SQL}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }

@@ -716,6 +716,7 @@ struct Eng {
   i32 bx[OH ? SO : 1];
   // current agent record (lane l holds dwords 2l, 2l+1)
   u32 rlo, rhi;
+  u32 rdirty;  // record quarters changed since rec_load (bit q: dwords 32q .. 32q + 31)
   i32 cur_agent;
   i64 add_delay;
   u32 dirty;  // RNG streams touched by this event: bits 0-3 G/O/K/L, bit 4 the agent's own
@@ -746,6 +747,7 @@ struct Eng {
     end_step = 0;
     add_delay = 0;
     run_skip = 0;
+    rdirty = 0;
     lane = laneid();
     qk = (LDSP u64*)lds;
     qs = (LDSP u32*)(lds + 8 * QCL);
@@ -806,12 +808,16 @@ struct Eng {
     rlo = (u32)v;
     rhi = (u32)(v >> 32);
     cur_agent = a;
+    rdirty = 0;
   }
+  // write-back of the record: with DIRTY_WB only its 128-byte quarters (whole L2 lines, 16
+  // lanes each) that an rs* call changed since rec_load (the builder writes whole records)
+  static constexpr bool DIRTY_WB = ((MXA_DIRTY_WB_MASK) >> CFG) & 1;
   DEV void rec_store() {
     const u64 v = ((u64)rhi << 32) | rlo;
     const int hs = hot_slot(cur_agent);
     if (hs >= 0) hotrec[hs * 64 + lane] = v;
-    else agent_ptr(cur_agent)[lane] = v;
+    else if (BUILD || !DIRTY_WB || ((rdirty >> (lane >> 4)) & 1)) agent_ptr(cur_agent)[lane] = v;
   }
   // Kernel.agentCurrentTimes[a] = t without loading the record (AF_ATIME: lane AF_ATIME/2's u64)
   DEV void atime_store(int a, i64 t) {
@@ -828,6 +834,7 @@ struct Eng {
   DEV double rgd(int f) { return as_d((u64)rg64(f)); }
   // record writes are lane selects (v_cndmask), not divergent branches
   DEV void rs(int f, u32 v) {
+    rdirty |= 1u << (f >> 5);  // the record quarter (dwords 32q .. 32q + 31) of field f
 #ifdef MXA_DIVERGENT_RS
     if (lane == (f >> 1)) {
       if (f & 1) rhi = v;
@@ -840,6 +847,7 @@ struct Eng {
 #endif
   }
   DEV void rs64(int f, i64 v) {
+    rdirty |= 1u << (f >> 5);
     bool me = lane == (f >> 1);
     rlo = me ? (u32)(u64)v : rlo;
     rhi = me ? (u32)((u64)v >> 32) : rhi;
@@ -1274,7 +1282,18 @@ struct Eng {
     u64 key = ((u64)t << KSH) | ((u64)agent << 2) | MT_WAKEUP;
     q_push(key, seq++, m);
   }
-  DEV i64 next_order_id() { return ocnt++; }
+  // Order.generateOrderId (Order.py:35-42): the smallest id >= the counter that no Order of this
+  // process holds; ocnt is the next candidate.  Only the replay's explicit tape ids can be met
+  // (every auto id is below ocnt), and only from the second episode of a process on
+  DEV i64 next_order_id() {
+    if constexpr (RP) {
+      i64 c = ocnt;
+      if (c >= (i64)U(rx->umin)) c = rp_skip_used(c);
+      ocnt = c + 1;
+      return c;
+    }
+    return ocnt++;
+  }
 
   // ---------------- SparseMeanRevertingOracle (SMRO:88-227)
   DEV double o_compute(i64 ts, double v_adj, i64 pt, double pv) {
@@ -2874,14 +2893,40 @@ struct Eng {
   DEV i32* idep() { return (i32*)(env + rx->L.off_idep); }
   DEV RpOrder* mro() { return (RpOrder*)(env + rx->L.off_mro); }
   DEV RpLob* ring() { return (RpLob*)(env + rx->L.off_ring); }
-  // DummyRL order ids (the global counter) map after the tape's dense ids
+  // auto ids (DummyRL's orders, the tape's ORDER_ID 0 records) map after the tape's dense ids,
+  // from this episode's first auto id on; the last dense id is never an order (orders.get(0) in
+  // a later episode of the process, when no auto id 0 exists)
   DEV i32 agent_dense(i64 oid) {
-    i32 d = U(rx->L.n_ids) + (i32)oid;
-    if (oid < 0 || d >= U(rx->L.D)) {
+    const i64 k = oid - (i64)U(rh()->id_base);
+    i32 d = U(rx->L.n_ids) + (i32)k;
+    if (k < 0 || d >= U(rx->L.D) - 1) {
       fail(ERR_RP_IDS);
       return 0;
     }
     return d;
+  }
+  DEV i32 zero_dense() { return U(rh()->id_base) == 0 ? U(rx->L.n_ids) : U(rx->L.D) - 1; }
+  // generateOrderId's skip over Order._order_ids: an explicit tape id is taken once its first
+  // SIZE > 0 record has been handled, in an earlier episode of the process or this one
+  DEV i64 rp_skip_used(i64 c) {
+    const i32 n = U(rx->nuid);
+    const RpHdr* R = rh();
+    const i32 hi = max(U(R->tape_hi), U(R->mr_done));
+    for (;;) {
+      i32 lo = 0, h2 = n - 1, f = -1;
+      while (lo <= h2) {  // uniform binary search over the sorted ids
+        const i32 mid = (lo + h2) >> 1;
+        const i64 v = (i64)U(rx->uid[mid]);
+        if (v == c) {
+          f = U(rx->ufirst[mid]);
+          break;
+        }
+        if (v < c) lo = mid + 1;
+        else h2 = mid - 1;
+      }
+      if (f < 0 || f >= hi) return c;
+      c++;
+    }
   }
   DEV i32 lvl_index(i32 price) {
     i32 x = price - U(rx->L.pmin);
@@ -3170,12 +3215,18 @@ struct Eng {
   }
 
   // ---------------- MarketReplayAgent (MarketReplayAgent.py:50-96)
-  // ORDER_ID 0 records: `orders.get(0)` finds the order whose auto id is 0 (dense index n_ids);
+  // ORDER_ID 0 records: `orders.get(0)` finds the order whose auto id is 0 (dense index n_ids in
+  // the first episode of a process; never later: zero_dense);
   // placing or modifying builds LimitOrder(order_id=0), which takes the next auto id
   // (Order.py:26), so a modify then fails isSameOrder at the exchange (OrderBook.py:343-344)
   DEV void mr_place_record(i32 r) {
-    const i32 oid = U(rx->oid[r]), d = U(rx->dense[r]), price = U(rx->price[r]), size = U(rx->size[r]);
+    const i32 oid = U(rx->oid[r]), price = U(rx->price[r]), size = U(rx->size[r]);
+    const i32 d = oid == 0 ? zero_dense() : U(rx->dense[r]);
     const int buy = (int)U((i32)rx->buy[r]);
+    mr_place_record_as(r, oid, d, price, size, buy);
+    rh()->mr_done = r + 1;  // record r's explicit id (if SIZE > 0) is in Order._order_ids now
+  }
+  DEV void mr_place_record_as(i32 r, i32 oid, i32 d, i32 price, i32 size, int buy) {
     RpOrder* O = mro() + d;
     const i32 present = U(O->present);
     if (!present && size > 0) {  // placeLimitOrder(..., order_id=ORDER_ID)
@@ -4214,7 +4265,7 @@ struct Builder : Eng<CFG, true> {
 
   // ABIDESEnv.reset (ABIDESEnv.py:51-103): agents, empty ladder book, kernelStarting wakeups.
   // No RNG stream is ever drawn in this composition.
-  DEV void build_replay() {
+  DEV void build_replay(i32 id_base, i32 tape_hi) {
     const MxaParams& P = E::PC;
     const RpLayout& L = this->rx->L;
     const i32 Pn = U(L.P), C = U(L.C), D = U(L.D);
@@ -4241,6 +4292,9 @@ struct Builder : Eng<CFG, true> {
     }
     init_gym();
     RpHdr* R = this->rh();
+    R->id_base = id_base;
+    R->tape_hi = tape_hi;
+    R->mr_done = 0;
     R->best[0] = R->best[1] = -1;
     R->free_top = C;
     R->ex_has_last = 0;  // no oracle: getDailyOpenPrice raises, last_trade stays None
@@ -4259,9 +4313,19 @@ struct Builder : Eng<CFG, true> {
     __threadfence_block();
   }
 
-  DEV void build(u32 seed) {
+  // keep_ids: ABIDESEnv.reset in the same process (Order.order_id / _order_ids carry over)
+  DEV void build(u32 seed, bool keep_ids = false) {
     const MxaParams& P = E::PC;
     LDSP EnvHdr& h = this->h;
+    i64 ocnt0 = 0;
+    i32 tape_hi0 = 0;
+    if (keep_ids) {  // the previous episode's counters, before anything is rebuilt
+      ocnt0 = U(((const EnvHdr*)this->env)->order_counter);
+      if constexpr (E::RP) {
+        const RpHdr* R = this->rh();
+        tape_hi0 = max(U(R->tape_hi), U(R->mr_done));
+      }
+    }
     {
       LDSP u32* hw = (LDSP u32*)&h;
       for (int i = this->lane; i < (int)(sizeof(EnvHdr) / 4); i += 64) hw[i] = 0;
@@ -4271,7 +4335,7 @@ struct Builder : Eng<CFG, true> {
     this->status = ST_RUNNING;
     this->err = 0;
     this->pops = 0;
-    this->ocnt = 0;
+    this->ocnt = ocnt0;
     this->seq = 0;
     this->qcount = 0;
     this->cur = P.start;
@@ -4290,7 +4354,7 @@ struct Builder : Eng<CFG, true> {
     if constexpr (E::QHIER) this->q_rescan();  // empty group mins
     for (int j = 0; j < E::SO; j++) this->bm[j] = -1;
     if constexpr (E::RP) {
-      build_replay();
+      build_replay((i32)ocnt0, tape_hi0);
       return;
     }
     mt_seed(this->rng_key(0), seed);
@@ -4579,7 +4643,7 @@ __global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stri
   if (env >= n_envs) return;
   if (mask && !mask[env]) return;
   mxa::Builder<CFG> b(base + (size_t)env * stride, lds, ctx);
-  b.build(seeds[env]);
+  b.build(seeds[env], mask && mask[env] == 2);  // 2: a later episode of the same process
 }
 
 // INSTR: the parity instrumentation (per-pop hash, trace ring) compiled in; the variant without

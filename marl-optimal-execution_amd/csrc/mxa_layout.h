@@ -187,7 +187,13 @@ typedef struct {  // per-env replay / gym state
   int32_t m_b2, m_a2, p0, p0_none;
   int32_t ph_n, ph_none, end_step, has_obs;
   double obs[9];
-  int32_t finished, pad[5];
+  int32_t finished;
+  // Order.order_id across ABIDESEnv.reset in one process (Order.py:8-9):
+  // the episode's first auto-id candidate (auto ids map to dense ids from it), and how far into
+  // the tape earlier episodes got (their explicit ids stay in Order._order_ids)
+  int32_t id_base, tape_hi;
+  int32_t mr_done;  // tape records handled this episode (their explicit ids are taken)
+  int32_t pad[2];
 } RpHdr;          // 208 B
 typedef struct {  // runtime layout of the replay sections (offsets from the env block)
   int32_t pmin, P;      // price ladder [pmin, pmin + P)
@@ -206,6 +212,12 @@ typedef struct {  // device-resident tape (shared by all envs of a handle)
   const int8_t* buy;    // [nrec]
   const int64_t* tm;    // [ntm] distinct times
   const int32_t* tm0;   // [ntm + 1] first record of each time group
+  // Order._order_ids of the tape: the distinct explicit ids that some record with SIZE > 0 turns
+  // into a LimitOrder (placing and modifying both do, MarketReplayAgent.py:69-91), sorted, and the
+  // first such record of each; generateOrderId skips an id once that record has been handled
+  const int32_t* uid;   // [nuid] sorted
+  const int32_t* ufirst;  // [nuid]
+  int32_t nuid, umin;   // umin: smallest such id (auto ids below it need no lookup)
   RpLayout L;
 } RpCtx;
 

@@ -57,12 +57,21 @@ class VecABIDESEnv:
         return rc
 
     def reset(self, seeds=None):
+        """ABIDESEnv.reset for every env (ABIDESEnv.py:51-57).  Each env is one process running
+        consecutive episodes: Order.order_id / Order._order_ids carry over from its previous
+        episode (util/order/Order.py:8-9) unless
+        set_id_persistence(False) made every reset a fresh process."""
         if seeds is not None:  # rmsc03 + DummyRL: new per-env seeds
             sd = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
             self._check(self.L.mxa_set_seeds(self._h, sd.ctypes.data), "mxa_set_seeds")
         self._check(self.L.mxa_reset(self._h, None), "mxa_reset")
         self.obs[:] = 0
         self.flags[:] = 0
+
+    def set_id_persistence(self, on):
+        """True (default): resets continue each env's order ids (one process); False: every
+        reset starts a fresh process (ids from 0)"""
+        self._check(self.L.mxa_set_id_persistence(self._h, 1 if on else 0), "mxa_set_id_persistence")
 
     def step(self, actions):
         """actions [n][3] -> (obs [n][9], done [n] bool, valid [n] bool, error [n] bool)"""

@@ -328,6 +328,11 @@ struct ora_env {
     int done, err;
     char errstr[160];
     int64_t order_counter;
+    /* Order._order_ids restricted to what generateOrderId can still meet: the explicit (tape)
+     * ids appended in this "process" (auto ids are all below order_counter).  Open addressing,
+     * carried across ora_gym_reset like the reference's class attributes (Order.py:8-9) */
+    int64_t* used_ids;
+    int used_cap, used_n;
     int64_t st_max_heap, st_max_resting, st_max_open, st_resting, st_max_hist_tx;
     char* report;
     int64_t report_len;
@@ -468,8 +473,45 @@ static void k_wakeup(ora_env* e, int sender, int64_t t) {
     heap_push(e, v);
 }
 
-/* Order.generateOrderId (util/order/Order.py:27-42): ids are consecutive per process */
-static int64_t next_order_id(ora_env* e) { return e->order_counter++; }
+/* Order._order_ids for explicit ids (Order.py:27-28: every Order appends its id) */
+static int used_has(const ora_env* e, int64_t id) {
+    if (!e->used_n) return 0;
+    for (uint64_t i = (uint64_t)id * 0x9E3779B97F4A7C15ull >> 40;; i++) {
+        int64_t k = e->used_ids[i & (uint64_t)(e->used_cap - 1)];
+        if (k == id) return 1;
+        if (k == -1) return 0;
+    }
+}
+static void used_add(ora_env* e, int64_t id) {
+    if (used_has(e, id)) return;
+    if (2 * (e->used_n + 1) > e->used_cap) {
+        int64_t* old = e->used_ids;
+        int oc = e->used_cap;
+        e->used_cap = oc ? 2 * oc : 1024;
+        e->used_ids = (int64_t*)malloc(sizeof(int64_t) * e->used_cap);
+        for (int i = 0; i < e->used_cap; i++) e->used_ids[i] = -1;
+        e->used_n = 0;
+        for (int i = 0; i < oc; i++)
+            if (old[i] != -1) used_add(e, old[i]);
+        free(old);
+    }
+    for (uint64_t i = (uint64_t)id * 0x9E3779B97F4A7C15ull >> 40;; i++) {
+        int64_t* k = &e->used_ids[i & (uint64_t)(e->used_cap - 1)];
+        if (*k == -1) {
+            *k = id;
+            e->used_n++;
+            return;
+        }
+    }
+}
+/* Order.generateOrderId (util/order/Order.py:35-42): the smallest id >= the class counter that
+ * no Order of this process has taken yet; order_counter holds the next candidate */
+static int64_t next_order_id(ora_env* e) {
+    int64_t c = e->order_counter;
+    while (used_has(e, c)) c++;
+    e->order_counter = c + 1;
+    return c;
+}
 
 /* --------------------------- oracle (SMRO) -------------------------------- */
 static void blr_push(ora_env* e, int64_t t, int64_t price, int64_t qty);
@@ -1799,12 +1841,16 @@ static void hbl_receive(ora_env* e, agent_t* a, const msg_t* m) {
  * ORDER_ID 0: `self.orders.get(0)` finds only an order whose auto id is 0, and
  * LimitOrder(..., order_id=0) takes the next auto id (Order.py:26, generateOrderId), both when
  * placing and when building the modify's new order (whose id then differs: isSameOrder fails
- * at the exchange, OrderBook.py:343-344).  Auto ids never reach the tape's explicit ids here
- * (the device host side checks that), so Order._order_ids needs no restating. */
+ * at the exchange, OrderBook.py:343-344).  In a later episode of the same process
+ * (ora_gym_reset) no order of this agent holds auto id 0, and auto ids skip every explicit id
+ * the process has used (next_order_id). */
 static void mr_place(ora_env* e, agent_t* a, int r) {
     int64_t oid = e->tp_oid[r], size = e->tp_size[r], price = e->tp_price[r];
     int buy = e->tp_buy[r];
     int slot = mr_slot(e, oid, 0);
+    /* placing and modifying both build LimitOrder(..., order_id=ORDER_ID): an explicit id joins
+     * Order._order_ids (a cancel or a size-0 record of an unknown id builds nothing) */
+    if (oid && size > 0) used_add(e, oid);
     msg_t m;
     memset(&m, 0, sizeof m);
     m.fill = -1;
@@ -2857,6 +2903,7 @@ void ora_destroy(ora_env* e) {
     free(e->tm_start);
     free(e->mr_key);
     free(e->mr_ord);
+    free(e->used_ids);
     free(e->hz);
     free(e);
 }
@@ -3026,6 +3073,27 @@ int64_t ora_book_records(const ora_env* e, int64_t* buf, int64_t cap) {
 int64_t ora_book_log(const ora_env* e, int64_t* buf, int64_t cap) {
     if (buf) memcpy(buf, e->blg, sizeof(int64_t) * (size_t)(cap < e->nblg ? cap : e->nblg));
     return e->nblg;
+}
+
+/* ABIDESEnv.reset (ABIDESEnv.py:51-57) in the same process: new agents and kernel (the
+ * rmsc03 + DummyRL composition from `seed`, or the replay composition on the same tape), while
+ * Order.order_id / Order._order_ids carry over (Order.py:8-9).
+ * *pe is replaced; a trace buffer must be set again. */
+int ora_gym_reset(ora_env** pe, uint32_t seed) {
+    ora_env* old = *pe;
+    ora_env* e = NULL;
+    int rc = old->tp_n ? ora_create_mr(old->tp_t, old->tp_oid, old->tp_price, old->tp_size, old->tp_buy, old->tp_n, &e)
+                       : ora_create(old->config, seed, &e);
+    if (rc) return rc;
+    e->order_counter = old->order_counter;
+    free(e->used_ids);
+    e->used_ids = old->used_ids;
+    e->used_cap = old->used_cap;
+    e->used_n = old->used_n;
+    old->used_ids = NULL;
+    ora_destroy(old);
+    *pe = e;
+    return 0;
 }
 
 /* ------------------------------ gym batch runner ------------------------------ */

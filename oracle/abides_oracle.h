@@ -98,6 +98,9 @@ int ora_run_batch_stats(const char* config, const uint32_t* seeds, int n, int th
 /* n GymKernel episodes, each stepped with actions[k][i][0..2] until done or error (config
  * "rmsc03_rl" with seeds, or NULL: the replay composition on the tape t/oid/price/size/buy).
  * Per env: pops, hash, error code, steps taken and the last valid observation [n][9]. */
+/* ABIDESEnv.reset in the same process: rebuild the composition (rmsc03_rl from `seed`, or the
+ * replay on the same tape), carrying Order.order_id / Order._order_ids; *pe is replaced */
+int ora_gym_reset(ora_env** pe, uint32_t seed);
 int ora_gym_batch(const char* config, const uint32_t* seeds, const int64_t* t, const int64_t* oid,
                   const int64_t* price, const int64_t* size, const int8_t* buy, int n_rec, int n, int n_steps,
                   const double* actions, int threads, int64_t* ev_out, uint64_t* hash_out, int32_t* err_out,

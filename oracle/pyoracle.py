@@ -299,6 +299,19 @@ class OracleGymEnv(OracleEnv):
             self.trace_buf = np.zeros((trace_cap, 10), dtype=np.int64)
             L.ora_set_trace(self._h, self.trace_buf.ctypes.data, trace_cap)
 
+    def reset(self, seed=None, trace_cap=0):
+        """ABIDESEnv.reset in the same process (ora_gym_reset): a new episode (rmsc03_rl: from
+        `seed`), Order.order_id / Order._order_ids carried over (SURVEY.md Appendix A #12)"""
+        L = lib()
+        L.ora_gym_reset.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32]
+        rc = L.ora_gym_reset(ctypes.byref(self._h), (int(seed) if seed is not None else 0) & 0xFFFFFFFF)
+        if rc:
+            raise ValueError("oracle: gym reset failed (%d)" % rc)
+        self.trace_buf = None
+        if trace_cap:
+            self.trace_buf = np.zeros((trace_cap, 10), dtype=np.int64)
+            L.ora_set_trace(self._h, self.trace_buf.ctypes.data, trace_cap)
+
     def step(self, action):
         """-> (obs float64[9] or None, done, rc)"""
         a = np.ascontiguousarray(action, dtype=np.float64)
