@@ -221,6 +221,18 @@ class MarketEngine(Engine):
         m.write_records(self.records.data_ptr())
         return self.gather(k)
 
+    def count(self, k):
+        """one batch of the timed workload (batch k's seeds) with the instrumentation on: the
+        event-class counters of the algorithmic-byte count (mxabides.counters)"""
+        m = self.m
+        m.set_parity_hash(True)
+        m.set_seeds(self.seeds(k))
+        m.reset()
+        m.run(chunk=self.args.chunk)
+        c = m.counters()
+        m.set_parity_hash(self.args.parity_hash)
+        return c
+
     def describe(self):
         a, n = self.args, self.n
         metric = METRIC if a.config == "rmsc03" else "env-steps/sec, %s x%d envs per GPU" % (a.config, n)
@@ -291,6 +303,16 @@ class GymEngine(Engine):
     def finish_timing(self):
         kms = [a.elapsed_time(b) for a, b in self.ev_pairs]
         self.launches, self.kernel_ms = len(kms), sum(kms)
+
+    def count(self, k):
+        """one more episode of the same workload (batch k's seeds, fresh actions of the same
+        distribution) with the instrumentation on: the algorithmic-byte counters"""
+        self.v.set_parity_hash(True)
+        self.step(k, False)
+        self.ctx.sync()
+        c = self.v.counters()
+        self.v.set_parity_hash(self.args.parity_hash)
+        return c
 
     def describe(self):
         n = self.n
@@ -365,6 +387,15 @@ class DDQNEngine(Engine):
     def finish_timing(self):
         kms = [a.elapsed_time(b) for a, b in self.timing]
         self.launches, self.kernel_ms = len(kms), sum(kms)
+
+    def count(self, k):
+        """one more learner-driven episode (batch k's seeds) with the instrumentation on"""
+        self.v.set_parity_hash(True)
+        self.ddqn.run_episode(self.v, self.learner, self.task, seeds=self.seeds(k))
+        self.ctx.sync()
+        c = self.v.counters()
+        self.v.set_parity_hash(self.args.parity_hash)
+        return c
 
     def describe(self):
         n = self.n
@@ -489,14 +520,20 @@ def main():
             out["config"]["cus"] = torch.cuda.get_device_properties(ctx.local).multi_processor_count
             avg_ms = eng.kernel_ms / max(1, eng.launches)
             my_ev_per_launch = events / ctx.world / max(1, eng.launches)
-            bpe = NOMINAL_BYTES_PER_EVENT
+            from mxabides import counters as mc
+            bpe, bparts, bunits = mc.bytes_per_event(eng.count(args.warmup))
             achieved = bpe * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
             traffic, tsrc = (traffic_record(args.config, eng.n, bool(args.parity_hash))
                              if isinstance(eng, MarketEngine) else (None, {"why": "no PMC record for this config"}))
             out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_record": tsrc,
                                "kernel": eng.kernel, "avg_launch_ms": avg_ms, "launches": eng.launches,
-                               "algo_bytes_per_event": bpe}
+                               "algo_bytes_per_event": bpe, "algo_bytes_source": "counted: device event-class counters "
+                               "of one instrumented batch of this workload (mxabides/counters.py, SURVEY.md §8(d) unit sizes)",
+                               "algo_bytes_breakdown": bparts, "algo_units_per_event": bunits,
+                               "nominal_bytes_per_event": NOMINAL_BYTES_PER_EVENT}
+            if traffic:
+                out["roofline"]["traffic_per_event"] = traffic / my_ev_per_launch
             if not args.no_cpu and hasattr(eng, "cpu_baseline"):
                 info = host_info()
                 th = cpu_threads(args, info)

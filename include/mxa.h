@@ -126,6 +126,14 @@ int mxa_write_results(mxa_handle* h, void* device_out);
  * episode return).  Asynchronous on the handle's stream. */
 #define MXA_RECORD_WORDS 12
 int mxa_write_records(mxa_handle* h, void* device_out);
+/* event-class counters since the envs' last reset, kept by instrumented runs only (parity hash on
+ * or a trace ring; the measured kernels carry none of it): HOST array [n_envs][MXA_COUNTER_WORDS]
+ * int64 = pops per message kind MK_0..MK_24 (WAKEUP pops at 0, GymKernel CANCEL_ORDER at 19),
+ * busy requeues (25), events pushed (26), RNG words drawn (27), pops (28), max pending events
+ * (29), max resting orders (30), 0.  The inputs of the SURVEY.md §8(d) algorithmic-byte count
+ * (mxabides.counters).  Synchronous. */
+#define MXA_COUNTER_WORDS 32
+int mxa_read_counters(mxa_handle* h, int64_t* out);
 /* diagnostics: copy `bytes` raw bytes of env `env`'s HBM block starting at `offset`; and
  * the block's section offsets (Layout: ag, open, rng, lat, q, book, tx, trace) */
 int mxa_read_raw(mxa_handle* h, int32_t env, int64_t offset, int64_t bytes, void* out);

@@ -83,6 +83,31 @@ __global__ __launch_bounds__(64) void mxa_records_kernel(const char* base, uint6
   }
 }
 
+// event-class counters of an instrumented run (include/mxa.h mxa_read_counters), one wave per env
+__global__ __launch_bounds__(64) void mxa_counters_kernel(const char* base, uint64_t stride, int n, uint32_t off_ag,
+                                                          int n_agents, int64_t* out) {
+  const int i = blockIdx.x, lane = threadIdx.x;
+  if (i >= n) return;
+  const char* e = base + (size_t)i * stride;
+  const EnvHdr* h = (const EnvHdr*)e;
+  long long w = 0;
+  for (int a = lane; a < n_agents; a += 64)
+    w += (long long)(((const uint32_t*)(e + off_ag + (size_t)a * 512))[AF_RS_POS] - MXA_MT_N);
+  for (int d = 32; d >= 1; d >>= 1) w += __shfl_xor(w, d, 64);
+  int64_t* o = out + (size_t)MXA_COUNTER_WORDS * i;
+  if (lane < 26) o[lane] = h->kc[lane];
+  if (lane == 0) {
+    for (int k = 0; k < 4; k++) w += h->rs_pos[k] - MXA_MT_N;
+    const int64_t req = h->kc[MXA_KC_REQUEUE];
+    o[26] = (int64_t)h->q_count - h->q0 + h->pops - req;  // every pop but a requeue removed one event
+    o[27] = w - (int64_t)h->rng0;
+    o[28] = h->pops;
+    o[29] = h->max_q;
+    o[30] = h->max_book;
+    o[31] = 0;
+  }
+}
+
 // execution-agent state after a step, for a learner on the device: [n][MXA_RL_STATE_WORDS]
 // doubles = (CASH, holdings, executed qty, best bid, best ask, bid size, ask size, lob flags)
 // of DummyRLExecutionAgent (TradingAgent.holdings, ExecutionAgent.executed quantity,
@@ -715,6 +740,21 @@ int mxa_write_records(mxa_handle* h, void* device_out) {
   hipLaunchKernelGGL(mxa_records_kernel, dim3(n), dim3(64), 0, h->stream, h->d_env, h->P.L.env_stride, n, h->d_seeds,
                      h->P.L.off_ag, a0, a1, (int64_t*)device_out);
   HIPCHK(h, hipGetLastError());
+  return MXA_OK;
+}
+
+int mxa_read_counters(mxa_handle* h, int64_t* out) {
+  if (!h || !out) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  const int n = h->P.n_envs;
+  int64_t* d = nullptr;
+  HIPCHK(h, hipMallocAsync((void**)&d, sizeof(int64_t) * MXA_COUNTER_WORDS * n, h->stream));
+  hipLaunchKernelGGL(mxa_counters_kernel, dim3(n), dim3(64), 0, h->stream, h->d_env, h->P.L.env_stride, n, h->P.L.off_ag,
+                     h->P.n_agents, d);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipMemcpyAsync(out, d, sizeof(int64_t) * MXA_COUNTER_WORDS * n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipFreeAsync(d, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;
 }
 

@@ -3714,9 +3714,15 @@ struct Eng {
 
   // ---------------- Kernel.runner event loop (Kernel.py:190-292)
   // the per-pop bookkeeping of the fast paths: currentTime, parity trace + hash, ttl_messages
+  // event class of a pop for the instrumented runs' counters (EnvHdr::kc)
+  static DEV int pop_class(u64 key, const Msg& m) {
+    const int type = (int)(key & 3);
+    return type == MT_MESSAGE ? (int)m_kind(m) : type == MT_WAKEUP ? MK_WAKEUP : MK_KCANCEL;
+  }
   DEV void account_pop(i64 t, u64 key, const Msg& m) {
     cur = t;
-    if (INSTR && (hash_on || trace)) {  // parity instrumentation (trace ring, per-pop hash)
+    if (INSTR && (hash_on || trace)) {  // parity instrumentation (trace ring, per-pop hash, class counters)
+      if (lane == 0) h.kc[pop_class(key, m)]++;
       const Rec rec = encode<PW == 8, MD, KSH>(key, m);
       if (hash_on) hash = rec_hash(hash, rec);
       if (trace && h.trace_len < trace_cap) {
@@ -4146,6 +4152,7 @@ struct Eng {
       rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
       cur = t;
       if (INSTR && (hash_on || trace)) {
+        if (lane == 0) h.kc[pop_class(key, m)]++;
         const Rec rec = encode<PW == 8, MD, KSH>(key, m);
         if (hash_on) hash = rec_hash(hash, rec);
         if (trace && h.trace_len < trace_cap) {
@@ -4168,6 +4175,7 @@ struct Eng {
       PROF_ADD(0, t0);
       if (at > t) {  // agent in the future: requeue unchanged (same uniq)
         q_rekey(slot, ((u64)at << KSH) | (key & ((1ull << KSH) - 1)));
+        if (INSTR && (hash_on || trace) && lane == 0) h.kc[MXA_KC_REQUEUE]++;
         PROF_ADD(1, t0);
         continue;
       }
@@ -4309,8 +4317,21 @@ struct Builder : Eng<CFG, true> {
     this->h.last_trade_float = 0;
     this->cur = P.start;
     for (int a = 0; a < P.n_agents; a++) this->wakeup_at(a, P.start);
+    count_base();
     this->save();
     __threadfence_block();
+  }
+  // counter baselines (EnvHdr::q0, rng0): what the build itself pushed and drew
+  DEV void count_base() {
+    const MxaParams& P = E::PC;
+    wfence();
+    u64 w = 0;
+    for (int a = this->lane; a < P.n_agents; a += 64)
+      w += (u64)(((const u32*)(this->env + P.L.off_ag + (size_t)a * 512))[AF_RS_POS] - MXA_MT_N);
+    w = (u64)wsum_i64((i64)w);
+    for (int k = 0; k < 4; k++) w += (u64)(this->h.rs_pos[k] - MXA_MT_N);
+    this->h.q0 = this->qcount;
+    this->h.rng0 = w;
   }
 
   // keep_ids: ABIDESEnv.reset in the same process (Order.order_id / _order_ids carry over)
@@ -4617,6 +4638,7 @@ struct Builder : Eng<CFG, true> {
     h.last_trade_float = 1;
     this->cur = P.start;
     for (int a = 0; a < n; a++) this->wakeup_at(a, P.start);
+    count_base();
     this->save();
     // the transaction ring (the history-epoch entry counts are header fields, zeroed above)
     TxRec* R = this->txr();

@@ -59,7 +59,9 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_last_kernel_ms", "mxa_last_error", "mxa_destroy", "mxa_rng_probe", "mxa_math_probe",
            "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout", "mxa_create_replay", "mxa_step",
            "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash",
-           "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log", "mxa_write_records", "mxa_set_id_persistence"]
+           "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log", "mxa_write_records", "mxa_set_id_persistence",
+           "mxa_read_counters"]
+COUNTER_WORDS = 32  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
 _lib = None
@@ -101,7 +103,8 @@ def load():
     L.mxa_read_raw.argtypes = [P, I32, I64, I64, P]
     L.mxa_layout.argtypes = [P, P]
     L.mxa_write_results.argtypes = [P, P]
-    for name, args in (("mxa_write_records", [P, P]), ("mxa_set_id_persistence", [P, I32])):
+    for name, args in (("mxa_write_records", [P, P]), ("mxa_set_id_persistence", [P, I32]),
+                       ("mxa_read_counters", [P, P])):
         if hasattr(L, name):  # (older single-configuration A/B builds lack them; libmxa.so has all)
             getattr(L, name).argtypes = args
     L.mxa_write_rl_state.argtypes = [P, P]

@@ -99,6 +99,13 @@ class VecABIDESEnv:
         """Per-env (events, hash, status, current_time) int64 rows into device memory."""
         self._check(self.L.mxa_write_results(self._h, ctypes.c_void_p(device_ptr)), "mxa_write_results")
 
+    def counters(self):
+        """[n_envs][COUNTER_WORDS] int64 event-class counters since the last reset (kept by
+        instrumented runs: parity hash on; include/mxa.h mxa_read_counters, mxabides.counters)"""
+        out = np.zeros((self.n_envs, _lib.COUNTER_WORDS), dtype=np.int64)
+        self._check(self.L.mxa_read_counters(self._h, out.ctypes.data), "mxa_read_counters")
+        return out
+
     def write_records(self, device_ptr):
         """Per-env episode records [n][RECORD_WORDS] int64 into device memory (include/mxa.h
         mxa_write_records: events, hash, status, current_time, err, seed, last_trade, order_counter,

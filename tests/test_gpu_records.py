@@ -56,3 +56,32 @@ def test_records_gym_handle():
     for e in range(2):
         cash, shares, _ = v.agents(e)[v.n_agents - 1]  # DummyRLExecutionAgent (id 64)
         assert rec[e, shard.R_CASH] == cash and rec[e, shard.R_HOLD] == shares
+
+
+@pytest.mark.parametrize("cfg,seed", [("rmsc03", 123456789), ("sparse_zi_100", 123456789), ("value_noise", 7)])
+def test_counters_agree_with_the_trace(cfg, seed):
+    """the event-class counters of an instrumented run (mxa_read_counters, the algorithmic-byte
+    count of bench.py) equal the per-kind histogram of the env's full parity trace, whose records
+    are the reference's (test_gpu_parity)"""
+    import mxabides
+    from mxabides import counters as mc
+    m = mxabides.VecMarket(cfg, [seed], trace_cap=400000)
+    m.run()
+    c = m.counters()[0]
+    tr = m.trace(0)
+    s = m.summary()
+    assert len(tr) == s["events"][0] == c[mc.C_POPS]
+    hist = np.bincount(tr[:, 3], minlength=26)
+    assert (c[:25] == hist[:25]).all(), (c[:25], hist[:25])
+    assert c[mc.C_PUSH] >= c[mc.C_POPS] - c[mc.C_REQUEUE] and c[mc.C_RNG] > 0
+    bpe, parts, units = mc.bytes_per_event(m.counters())
+    assert 200 < bpe < 600
+
+
+def test_counters_off_without_instrumentation():
+    import mxabides
+    m = mxabides.VecMarket("rmsc03", [7, 8])
+    m.set_parity_hash(False)
+    m.run()
+    c = m.counters()
+    assert (c[:, :26] == 0).all() and (c[:, 28] > 0).all()
