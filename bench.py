@@ -54,7 +54,9 @@ def parse():
     return ap.parse_args()
 
 
-DEFAULT_ENVS = {"marketreplay": 512, "sparse_zi_1000": 1024, "random_fund_value": 2048, "random_fund_diverse": 2048}
+DEFAULT_ENVS = {"marketreplay": 512, "sparse_zi_1000": 1024, "random_fund_value": 2048, "random_fund_diverse": 2048,
+                "hist_fund_value": 2048, "hist_fund_diverse": 2048}
+FUND = os.path.join(ROOT, "tests", "golden", "fund_JPM_20190628.npz")  # hist_fund_*: the JPM mid-price series
 
 
 # ----------------------------------------------------------------------------------------------
@@ -202,8 +204,10 @@ class MarketEngine(Engine):
     def __init__(self, args, ctx):
         super().__init__(args, ctx)
         import mxabides
+        from mxabides.fundamental import FundamentalSeries
         self.mx = mxabides
-        self.m = mxabides.VecMarket(args.config, self.seeds(0), device=ctx.local)
+        kw = {"fundamental": FundamentalSeries.load(FUND)} if args.config.startswith("hist_fund") else {}
+        self.m = mxabides.VecMarket(args.config, self.seeds(0), device=ctx.local, **kw)
         self.stream = self.torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
         self.torch.cuda.set_stream(self.stream)
         self.m.set_stream(self.stream.cuda_stream)

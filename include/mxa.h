@@ -46,7 +46,9 @@ enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKET
        MXA_RMSC02 = 7 /* config/rmsc02.py: rmsc01 with market-data subscriptions and a latency matrix */,
        MXA_OBI_RMSC02 = 8 /* config/obi_rmsc02.py: rmsc02's market with 89 ZI, 5 order-book-imbalance agents */,
        MXA_RANDOM_FUND_VALUE = 9 /* config/random_fund_value.py: 5000 noise + 100 value agents, 09:30-16:00 */,
-       MXA_RANDOM_FUND_DIVERSE = 10 /* config/random_fund_diverse.py: random_fund_value + market maker + 25 momentum */ };
+       MXA_RANDOM_FUND_DIVERSE = 10 /* config/random_fund_diverse.py: random_fund_value + market maker + 25 momentum */,
+       MXA_HIST_FUND_VALUE = 11 /* config/hist_fund_value.py: random_fund_value on an ExternalFileOracle (mxa_create_hist) */,
+       MXA_HIST_FUND_DIVERSE = 12 /* config/hist_fund_diverse.py: random_fund_diverse on an ExternalFileOracle */ };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };
@@ -83,6 +85,13 @@ typedef struct {
 /* configuration id + per-env seeds (the reference config's -s/--seed) */
 int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device,
                int32_t trace_cap, mxa_handle** out);
+/* MXA_HIST_FUND_VALUE / MXA_HIST_FUND_DIVERSE: the configuration with its ExternalFileOracle series
+ * (util/oracle/ExternalFileOracle.py:15-35 reads it from a pickled pandas Series of mid prices,
+ * util/formatting/mid_price_from_orderbook.py): n_fund time-sorted entries, fund_t ns since
+ * midnight of the simulated date, fund_v the values (cents, float).  Prices between entries are
+ * interpolated exactly as getPriceAtTime / getInterpolatedPrice do (ExternalFileOracle.py:52-159). */
+int mxa_create_hist(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device, int32_t trace_cap,
+                    const int64_t* fund_t, const double* fund_v, int32_t n_fund, mxa_handle** out);
 /* rebuild envs from their seeds (env_mask: NULL = all) — runs the config construction.  On a
  * GymKernel handle (mxa_create_replay, MXA_RMSC03_RL) a reset is ABIDESEnv.reset in the same
  * process: Order.order_id / Order._order_ids carry over from the env's previous episode

@@ -180,6 +180,8 @@ struct mxa_handle {
   }
   std::vector<char> tape_blob;  // host staging of the tape (uploaded by create_common)
   size_t tb_t, tb_oid, tb_dense, tb_price, tb_size, tb_buy, tb_tm, tb_tm0, tb_uid, tb_ufirst;
+  bool ext = false;  // ExternalFileOracle configurations: the fundamental series in d_tape
+  size_t tb_fs_t = 0, tb_fs_v = 0;
 };
 
 static int hip_fail(mxa_handle* h, hipError_t e, const char* what) {
@@ -212,6 +214,8 @@ static bool bind(mxa_handle* h, int cfg) {
   case 8: e = mxa_entry_8(); break;
   case 9: e = mxa_entry_9(); break;
   case 10: e = mxa_entry_10(); break;
+  case 11: e = mxa_entry_11(); break;
+  case 12: e = mxa_entry_12(); break;
 #endif
   default: return false;
   }
@@ -250,10 +254,14 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
                     (int)MXA_VALUE_NOISE == (int)MXA_CFG_VALUE_NOISE && (int)MXA_RMSC01 == (int)MXA_CFG_RMSC01 &&
                     (int)MXA_RMSC02 == (int)MXA_CFG_RMSC02 && (int)MXA_OBI_RMSC02 == (int)MXA_CFG_OBI_RMSC02 &&
                     (int)MXA_RANDOM_FUND_VALUE == (int)MXA_CFG_RANDOM_FUND_VALUE &&
-                    (int)MXA_RANDOM_FUND_DIVERSE == (int)MXA_CFG_RANDOM_FUND_DIVERSE,
+                    (int)MXA_RANDOM_FUND_DIVERSE == (int)MXA_CFG_RANDOM_FUND_DIVERSE &&
+                    (int)MXA_HIST_FUND_VALUE == (int)MXA_CFG_HIST_FUND_VALUE &&
+                    (int)MXA_HIST_FUND_DIVERSE == (int)MXA_CFG_HIST_FUND_DIVERSE,
                 "config ids");
-  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_RANDOM_FUND_DIVERSE + 1, "one entry per configuration");
-  if (config == MXA_MARKETREPLAY || !bind(h, config)) {  // replay handles: mxa_create_replay
+  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_HIST_FUND_DIVERSE + 1, "one entry per configuration");
+  // replay handles: mxa_create_replay; ExternalFileOracle configurations: mxa_create_hist
+  if (config == MXA_MARKETREPLAY || config == MXA_HIST_FUND_VALUE || config == MXA_HIST_FUND_DIVERSE ||
+      !bind(h, config)) {
     delete h;
     return MXA_EINVAL;
   }
@@ -265,6 +273,35 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
     h->ctx.L = mxa_cfg::replay_layout(h->P.L.env_stride, 0, 0, 0, 0, 0, 0, 0);
     h->P.L.env_stride = h->ctx.L.end;
   }
+  return create_common(h, n_envs, seeds, device, out);
+}
+
+// config/hist_fund_value.py / hist_fund_diverse.py: the ExternalFileOracle's series is the
+// handle's (shared by its envs, device-resident); see include/mxa.h
+int mxa_create_hist(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device, int32_t trace_cap,
+                    const int64_t* fund_t, const double* fund_v, int32_t n_fund, mxa_handle** out) {
+  if (!out || n_envs <= 0 || !seeds || trace_cap < 0 || !fund_t || !fund_v || n_fund <= 0) return MXA_EINVAL;
+  if (config != MXA_HIST_FUND_VALUE && config != MXA_HIST_FUND_DIVERSE) return MXA_EINVAL;
+  for (int i = 0; i < n_fund; i++)
+    if ((i && fund_t[i] < fund_t[i - 1]) || !(fund_v[i] == fund_v[i]) || fund_v[i] > 1e15 || fund_v[i] < -1e15)
+      return MXA_EINVAL;  // unsorted times or a value int(round()) cannot take (NaN raises in the reference)
+  mxa_handle* h = new mxa_handle();
+  if (!bind(h, config)) {
+    delete h;
+    return MXA_EINVAL;
+  }
+  h->P = mxa_cfg::params(config);
+  h->P.n_envs = n_envs;
+  h->P.L.trace_cap = trace_cap;
+  h->P.L.env_stride = mxa_cfg::env_stride(config, trace_cap);
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  h->tb_fs_t = 0;
+  h->tb_fs_v = al(8ull * n_fund);
+  h->tape_blob.assign(al(h->tb_fs_v + 8ull * n_fund), 0);
+  memcpy(h->tape_blob.data() + h->tb_fs_t, fund_t, 8ull * n_fund);
+  memcpy(h->tape_blob.data() + h->tb_fs_v, fund_v, 8ull * n_fund);
+  h->ctx.fs_n = n_fund;
+  h->ext = true;
   return create_common(h, n_envs, seeds, device, out);
 }
 
@@ -301,14 +338,20 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
     h->ctx.uid = (const int32_t*)(h->d_tape + h->tb_uid);
     h->ctx.ufirst = (const int32_t*)(h->d_tape + h->tb_ufirst);
   }
-  if (h->gym) {
+  if (h->ext) {
+    HIPCHK(h, hipMalloc(&h->d_tape, h->tape_blob.size()));
+    HIPCHK(h, hipMemcpyAsync(h->d_tape, h->tape_blob.data(), h->tape_blob.size(), hipMemcpyHostToDevice, h->stream));
+    h->ctx.fs_t = (const int64_t*)(h->d_tape + h->tb_fs_t);
+    h->ctx.fs_v = (const double*)(h->d_tape + h->tb_fs_v);
+  }
+  if (h->gym || h->ext) {
     HIPCHK(h, hipMalloc(&h->d_ctx, sizeof(RpCtx)));
     HIPCHK(h, hipMemcpyAsync(h->d_ctx, &h->ctx, sizeof(RpCtx), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMalloc(&h->d_act, sizeof(double) * 3 * n_envs));
     HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 9 * n_envs));
     HIPCHK(h, hipMalloc(&h->d_flags, sizeof(int32_t) * n_envs));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
   }
+  if (h->gym || h->ext) HIPCHK(h, hipStreamSynchronize(h->stream));
   const int rc = mxa_reset(h, nullptr);  // a fresh process: ids from 0
   h->persist_ids = h->gym;               // later resets continue the process (Order.py:8-9)
   return rc;
@@ -594,7 +637,7 @@ int mxa_finalize(mxa_handle* h) {
   const size_t rows = (size_t)h->P.n_envs * h->P.n_agents;
   if (!h->d_final) HIPCHK(h, hipMalloc(&h->d_final, rows * sizeof(mxa_agent_final)));
   (h->d_blog ? h->stop_log : h->stop)(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_final,
-          h->d_blog, h->blog_cap);
+          h->d_blog, h->blog_cap, h->d_ctx);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;

@@ -55,7 +55,7 @@ constexpr int sq_lds(int cfg);
 // configurations whose agent-record write-back stores only the changed 128-byte quarters
 // (bit = config id; measured per configuration)
 #ifndef MXA_DIRTY_WB_MASK
-#define MXA_DIRTY_WB_MASK 0
+#define MXA_DIRTY_WB_MASK ((1 << 9) | (1 << 10) | (1 << 11) | (1 << 12))  // r03 s5: random_fund_value 840 -> 795 ms; rmsc03 +2 %, rmsc01 +4 %
 #endif
 #ifndef MXA_OPEN_RFD
 #define MXA_OPEN_RFD 128
@@ -103,10 +103,11 @@ constexpr Shape shape(int cfg) {
        // maximum over the 8,192 bench seeds is 5,125 events), payload in HBM; 320 book slots (max 279)
        // the first MXA_RFV_SQL slots per lane (24: 1,536) in LDS for events due within a second,
        // the other 72 per lane an HBM tier for the far wakeups (the two-tier queue, q_push)
-       : cfg == MXA_CFG_RANDOM_FUND_VALUE ? Shape{96, 5, false, MXA_RFV_WAVES, 6, 0, MXA_RFV_SQL}
+       : (cfg == MXA_CFG_RANDOM_FUND_VALUE || cfg == MXA_CFG_HIST_FUND_VALUE) ? Shape{96, 5, false, MXA_RFV_WAVES, 6, 0, MXA_RFV_SQL}
        // random_fund_diverse: the same queue; 576 book slots (oracle max 484 over the 8,192 bench
        // seeds: 448 overflowed) and wide replies for the market maker's depth-5 spread queries
-       : cfg == MXA_CFG_RANDOM_FUND_DIVERSE ? Shape{96, MXA_SO_RFD, false, MXA_RFD_WAVES, 8, 0, MXA_RFD_SQL}
+       : (cfg == MXA_CFG_RANDOM_FUND_DIVERSE || cfg == MXA_CFG_HIST_FUND_DIVERSE)
+           ? Shape{96, MXA_SO_RFD, false, MXA_RFD_WAVES, 8, 0, MXA_RFD_SQL}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
@@ -224,6 +225,16 @@ constexpr void params_random_fund_diverse(MxaParams& P) {
   P.mom_wake = MIN;
   P.n_agents = 5127;
   P.L.open_cap = MXA_OPEN_RFD;  // the market maker's ladder: oracle max 78 open orders over the 8,192 bench seeds (64 overflowed)
+}
+
+// config/hist_fund_value.py / config/hist_fund_diverse.py: random_fund_value / _diverse with the
+// ExternalFileOracle (util/oracle/ExternalFileOracle.py) on a fundamental series given at create
+// time; the value agents' r_bar is the series' first value and sigma_n = r_bar / 10 (runtime)
+constexpr void params_hist_fund(MxaParams& P, bool diverse) {
+  if (diverse) params_random_fund_diverse(P);
+  else params_random_fund_value(P);
+  P.config = diverse ? MXA_CFG_HIST_FUND_DIVERSE : MXA_CFG_HIST_FUND_VALUE;
+  P.oracle_ext = 1;
 }
 
 // config/sparse_zi_100.py:73-334 and config/sparse_zi_1000.py
@@ -509,6 +520,8 @@ constexpr MxaParams params(int cfg) {
   else if (cfg == MXA_CFG_OBI_RMSC02) params_obi_rmsc02(P);
   else if (cfg == MXA_CFG_RANDOM_FUND_VALUE) params_random_fund_value(P);
   else if (cfg == MXA_CFG_RANDOM_FUND_DIVERSE) params_random_fund_diverse(P);
+  else if (cfg == MXA_CFG_HIST_FUND_VALUE) params_hist_fund(P, false);
+  else if (cfg == MXA_CFG_HIST_FUND_DIVERSE) params_hist_fund(P, true);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;

@@ -13,7 +13,8 @@ typedef void (*mxa_build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, i
                              const RpCtx*);
 typedef void (*mxa_run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, BlRec*,
                            int);
-typedef void (*mxa_stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, mxa_agent_final*, BlRec*, int);
+typedef void (*mxa_stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, mxa_agent_final*, BlRec*, int,
+                            const RpCtx*);
 typedef void (*mxa_step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*,
                             const double*, double*, int32_t*);
 
@@ -36,4 +37,6 @@ MxaEntry mxa_entry_7();
 MxaEntry mxa_entry_8();
 MxaEntry mxa_entry_9();
 MxaEntry mxa_entry_10();
-#define MXA_N_CONFIGS 11
+MxaEntry mxa_entry_11();
+MxaEntry mxa_entry_12();
+#define MXA_N_CONFIGS 13

@@ -22,8 +22,8 @@ void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t 
 }
 template <int CFG, bool LOG>
 void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, mxa_agent_final* out,
-                 BlRec* blog, int blog_cap) {
-  hipLaunchKernelGGL((mxa_stop_kernel<CFG, LOG>), g, b, lds, s, base, stride, n, out, blog, blog_cap);
+                 BlRec* blog, int blog_cap, const RpCtx* ctx) {
+  hipLaunchKernelGGL((mxa_stop_kernel<CFG, LOG>), g, b, lds, s, base, stride, n, out, blog, blog_cap, ctx);
 }
 #ifndef MXA_NO_GYM
 template <int CFG, bool INSTR>

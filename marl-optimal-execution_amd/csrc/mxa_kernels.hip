@@ -1295,6 +1295,49 @@ struct Eng {
     return ocnt++;
   }
 
+  // ---------------- ExternalFileOracle (util/oracle/ExternalFileOracle.py:52-159)
+  static constexpr bool EXT = PC.oracle_ext != 0;
+  // pandas Timedelta.total_seconds(): days * 86400 + seconds (an int) + microseconds / 1e6 of
+  // the duration floored to whole microseconds (nanoseconds dropped; measured, pandas 2.3.3)
+  static DEV double td_seconds(i64 ns) {
+    const i64 us = ns >= 0 ? ns / 1000 : -((-ns + 999) / 1000);
+    const i64 s = us >= 0 ? us / 1000000 : -((-us + 999999) / 1000000);
+    return (double)s + (double)(us - s * 1000000) / 1000000.0;
+  }
+  // getPriceAtTime (:52-97): the first / last value outside the series, else bisect_left and
+  // getInterpolatedPrice (:131-159) between the entries either side; a query at the first
+  // timestamp reads lower index -1 (Python's series[-1], the last entry), as the reference does
+  DEV double efo_price(i64 t) {
+    const i32 n = U(rx->fs_n);
+    const i64* T = rx->fs_t;
+    const double* V = rx->fs_v;
+    if (t < U(T[0])) return V[0];
+    if (t > U(T[n - 1])) return V[n - 1];
+    i32 lo = 0, hi = n;
+    while (lo < hi) {  // bisect_left
+      const i32 mid = (lo + hi) >> 1;
+      if (U(T[mid]) < t) lo = mid + 1;
+      else hi = mid;
+    }
+    i32 li = lo - 1;
+    const i32 ui = li < n - 1 ? li + 1 : li;
+    if (li < 0) li += n;
+    const double pl = V[li], ph = V[ui];
+    const i64 tl = U(T[li]), th = U(T[ui]);
+    const double slope = pl != ph ? (ph - pl) / td_seconds(th - tl) : 0.0;
+    return pl + td_seconds(t - tl) * slope;
+  }
+  // the value agents' r_bar = oracle.fundamentals[symbol].values[0] and sigma_n = r_bar / 10
+  // (config/hist_fund_value.py:80-82), else the config's constants
+  DEV double v_rbar() {
+    if constexpr (EXT) return rx->fs_v[0];
+    else return PC.v_rbar;
+  }
+  DEV double v_sigma_n() {
+    if constexpr (EXT) return rx->fs_v[0] / 10;
+    else return PC.v_sigma_n;
+  }
+
   // ---------------- SparseMeanRevertingOracle (SMRO:88-227)
   DEV double o_compute(i64 ts, double v_adj, i64 pt, double pv) {
     i64 d = ts - pt;
@@ -1335,6 +1378,14 @@ struct Eng {
     return o_compute(t, 0, pt, pv);
   }
   DEV i64 o_observe(i64 t, double sigma_n) {
+    if constexpr (EXT) {  // ExternalFileOracle.observePrice (ExternalFileOracle.py:110-129): no clamp, no draws
+      const double tp = efo_price(t);
+      if (sigma_n == 0) return py_round(tp);
+      RS A = agent_rs();
+      const i64 obs = py_round(rs_normal(A, tp, __builtin_sqrt(sigma_n)));
+      agent_rs_put(A);
+      return obs;
+    }
     double r_t = t >= PC.mkt_close ? o_advance(PC.mkt_close - 1) : o_advance(t);
     if (sigma_n == 0) return (i64)r_t;
     RS A = agent_rs();
@@ -2321,8 +2372,8 @@ struct Eng {
     rs(AF_STATE, AS_AWAITING_SPREAD);
   }
   DEV void value_place() {
-    i64 obs = o_observe(cur, PC.v_sigma_n);
-    i64 r_T = bayes_r_T(obs, PC.v_kappa, PC.v_rbar, PC.v_sigma_n, PC.v_sigma_s);
+    i64 obs = o_observe(cur, v_sigma_n());
+    i64 r_T = bayes_r_T(obs, PC.v_kappa, v_rbar(), v_sigma_n(), PC.v_sigma_s);
     i32 bid, ask;
     bool hb = known_bid(bid), ha = known_ask(ask);
     int buy;
@@ -4383,14 +4434,19 @@ struct Builder : Eng<CFG, true> {
     int n = P.n_agents;
     u32 tmp;
     if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_RL || P.config == MXA_CFG_RANDOM_FUND_VALUE ||
-        P.config == MXA_CFG_RANDOM_FUND_DIVERSE) {
+        P.config == MXA_CFG_RANDOM_FUND_DIVERSE || P.config == MXA_CFG_HIST_FUND_VALUE ||
+        P.config == MXA_CFG_HIST_FUND_DIVERSE) {
       // config/rmsc03.py, config/random_fund_value.py and config/random_fund_diverse.py: the same
-      // global-draw order (random_fund_diverse's MarketMakerAgent seed after the value agents)
+      // global-draw order (random_fund_diverse's MarketMakerAgent seed after the value agents);
+      // config/hist_fund_*.py draw the oracle's RandomState seed too, but ExternalFileOracle
+      // draws nothing at construction
       set_seed(1, g_seed(G));  // O
-      h.o_pt = P.mkt_open;
-      h.o_pv = P.o_rbar;
-      h.o_th2 = gm_pow(P.o_fundvol, 2.0);  // SMRO: theta ** 2 (SparseMeanRevertingOracle.py:105)
-      h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
+      if constexpr (!E::EXT) {
+        h.o_pt = P.mkt_open;
+        h.o_pv = P.o_rbar;
+        h.o_th2 = gm_pow(P.o_fundvol, 2.0);  // SMRO: theta ** 2 (SparseMeanRevertingOracle.py:105)
+        h.o_mst = P.mkt_open + (i64)rs_exponential(G, 1.0 / P.o_lambda);
+      }
       tmp = g_seed(G);  // exchange
       set_seed(4 + 0, tmp);
       for (int a = P.first_noise; a < P.first_noise + P.n_noise; a++) {
@@ -4407,7 +4463,7 @@ struct Builder : Eng<CFG, true> {
         i64 size = rs_randint(G, 20, 50);
         rec_init(a, AG_VALUE);
         this->rs(AF_SIZE, (u32)size);
-        this->rsd(AF_R_T, P.v_rbar);
+        this->rsd(AF_R_T, this->v_rbar());
         this->rec_store();
       }
       for (int a = P.first_mm; a < P.first_mm + P.n_mm; a++) {
@@ -4573,7 +4629,7 @@ struct Builder : Eng<CFG, true> {
     seed_streams(1);
     h.rs_pos[1] = h.rs_pos[2] = h.rs_pos[3] = MXA_MT_N;
     h.rs_m[1] = h.rs_m[2] = h.rs_m[3] = 0;
-    {  // oracle first megashock (SMRO:71-72)
+    if constexpr (!E::EXT) {  // oracle first megashock (SMRO:71-72)
       RS O = this->grs(1);
       double msv = rs_normal(O, P.o_msmean, __builtin_sqrt(P.o_msvar));
       h.o_msv = rs_randint(O, 0, 2) == 0 ? msv : -msv;
@@ -4632,10 +4688,16 @@ struct Builder : Eng<CFG, true> {
       this->agent_rs_put(A);
       this->rec_store();
     }
-    // Kernel.runner: kernelInitializing (exchange opening price = r_bar, a python float),
+    // Kernel.runner: kernelInitializing (exchange opening price = r_bar, a python float; with the
+    // ExternalFileOracle int(round(price at the open)), ExternalFileOracle.py:37-50),
     // kernelStarting (every agent wakes at startTime, in id order)
-    h.last_trade = (i64)P.o_rbar;
-    h.last_trade_float = 1;
+    if constexpr (E::EXT) {
+      h.last_trade = py_round(this->efo_price(P.mkt_open));
+      h.last_trade_float = 0;
+    } else {
+      h.last_trade = (i64)P.o_rbar;
+      h.last_trade_float = 1;
+    }
     this->cur = P.start;
     for (int a = 0; a < n; a++) this->wakeup_at(a, P.start);
     count_base();
@@ -4689,12 +4751,12 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
 
 template <int CFG, bool LOG>
 __global__ __launch_bounds__(64) void mxa_stop_kernel(char* base, uint64_t stride, int n_envs, mxa_agent_final* out,
-                                                      BlRec* blog, int blog_cap) {
+                                                      BlRec* blog, int blog_cap, const RpCtx* ctx) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int env = blockIdx.x;
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
-  mxa::Eng<CFG, false, LOG> g(e, lds, 0, nullptr, LOG ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
+  mxa::Eng<CFG, false, LOG> g(e, lds, 0, ctx, LOG ? blog + (size_t)env * blog_cap : nullptr, blog_cap);
   g.load();
   g.stop(out + (size_t)env * mxa::Eng<CFG>::PC.n_agents);  // no save(): the pass is idempotent
   // the oracle observations of the pass append to the log after the run's records; only

@@ -20,7 +20,8 @@
 enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPARSE_ZI_1000 = 2, MXA_CFG_MARKETREPLAY = 3,
                      MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6,
                      MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8, MXA_CFG_RANDOM_FUND_VALUE = 9,
-                     MXA_CFG_RANDOM_FUND_DIVERSE = 10 };
+                     MXA_CFG_RANDOM_FUND_DIVERSE = 10, MXA_CFG_HIST_FUND_VALUE = 11,
+                     MXA_CFG_HIST_FUND_DIVERSE = 12 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -226,6 +227,11 @@ typedef struct {  // device-resident tape (shared by all envs of a handle)
   const int32_t* uid;   // [nuid] sorted
   const int32_t* ufirst;  // [nuid]
   int32_t nuid, umin;   // umin: smallest such id (auto ids below it need no lookup)
+  // ExternalFileOracle fundamental series (hist_fund_* configs): time-sorted ns since midnight
+  // and values (the mid prices of util/formatting/mid_price_from_orderbook.py)
+  const int64_t* fs_t;
+  const double* fs_v;
+  int32_t fs_n, pad_fs;
   RpLayout L;
 } RpCtx;
 
@@ -311,7 +317,8 @@ typedef struct {
   int32_t md_sub, md_mk_levels, md_mom_levels, lat_asym;  // lat_asym: latency row 0 + column 0
   int64_t md_freq;
   // OrderBookImbalanceAgent (agent/OrderBookImbalanceAgent.py defaults)
-  int32_t first_obi, n_obi, obi_levels, pad6;
+  int32_t first_obi, n_obi, obi_levels;
+  int32_t oracle_ext;      // 1: util/oracle/ExternalFileOracle.py on a runtime series (RpCtx::fs_*)
   int64_t obi_freq, obi_wake;
   double obi_entry, obi_trail;
   Layout L;

@@ -3,15 +3,36 @@
 config/rmsc03.py:95-197, config/sparse_zi_100.py:177-256, config/sparse_zi_1000.py,
 config/value_noise.py:98-161 (every ValueAgent gets its own type string "ValueAgent {id}"),
 config/rmsc01.py:75-211 and config/rmsc02.py (the same agents), config/obi_rmsc02.py,
-config/random_fund_value.py:113-153, config/random_fund_diverse.py:116-198.
+config/random_fund_value.py:113-153, config/random_fund_diverse.py:116-198,
+config/hist_fund_value.py:84-148, config/hist_fund_diverse.py:86-190 (the same agents).
 """
 ZI_GROUPS = [(0, 250, "1"), (0, 500, "1"), (0, 1000, "0.8"), (0, 1000, "1"), (0, 2000, "0.8"), (250, 500, "0.8"),
              (250, 500, "1")]
 ZI_COUNTS = {"sparse_zi_100": [15, 15, 14, 14, 14, 14, 14], "sparse_zi_1000": [143] * 6 + [142]}
 
 
-def symbol_of(config):
-    return "ABM" if config in ("rmsc03", "random_fund_value", "random_fund_diverse") else "JPM"
+# configs whose script takes the ticker from -t/--ticker (config/rmsc03.py:31, random_fund_*.py,
+# hist_fund_*.py); the default is the one the fixtures and the bench use
+TICKER_CONFIGS = ("rmsc03", "random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse")
+HIST_CONFIGS = ("hist_fund_value", "hist_fund_diverse")
+
+
+def symbol_of(config, symbol=None):
+    if symbol is not None:
+        if config not in TICKER_CONFIGS:
+            raise ValueError("%s has a fixed symbol (JPM); only %s take -t/--ticker" % (config, TICKER_CONFIGS))
+        return symbol
+    if config in HIST_CONFIGS:
+        return "JPM"
+    return "ABM" if config in TICKER_CONFIGS else "JPM"
+
+
+# ExchangeAgent(book_freq=...) of each config script: 0 archives every snapshot
+# (ORDERBOOK_<sym>_FULL), None archives nothing, a pandas frequency resamples
+# (ExchangeAgent.py:389-469; value_noise / sparse_zi_* take -b, default None)
+BOOK_FREQ = {"rmsc03": 0, "rmsc02": 0, "rmsc01": "M", "obi_rmsc02": "all", "random_fund_value": None,
+             "random_fund_diverse": None, "hist_fund_value": None, "hist_fund_diverse": None, "value_noise": None,
+             "sparse_zi_100": None, "sparse_zi_1000": None}
 
 
 def agent_names(config):
@@ -24,10 +45,10 @@ def agent_names(config):
     if config == "value_noise":
         return (["Exchange Agent 0"] + ["NoiseAgent %d" % j for j in range(1, 101)] +
                 ["Value Agent %d" % j for j in range(101, 151)])
-    if config in ("random_fund_value", "random_fund_diverse"):
+    if config in ("random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse"):
         extra = ["MARKET_MAKER_AGENT_5101"] + ["MOMENTUM_AGENT_%d" % j for j in range(5102, 5127)]
         return (["EXCHANGE_AGENT"] + ["NoiseAgent %d" % j for j in range(1, 5001)] +
-                ["Value Agent %d" % j for j in range(5001, 5101)] + (extra if config == "random_fund_diverse" else []))
+                ["Value Agent %d" % j for j in range(5001, 5101)] + (extra if config.endswith("diverse") else []))
     if config == "rmsc03":
         return (["EXCHANGE_AGENT"] + ["NoiseAgent %d" % j for j in range(1, 51)] +
                 ["Value Agent %d" % j for j in range(51, 61)] + ["POV_MARKET_MAKER_AGENT_61"] +
@@ -50,8 +71,8 @@ def agent_type_names(config):
                 ["HeuristicBeliefLearningAgent"] * 25 + ["MomentumAgent"] * 24)
     if config == "value_noise":
         return ["ExchangeAgent"] + ["NoiseAgent"] * 100 + ["ValueAgent %d" % j for j in range(101, 151)]
-    if config in ("random_fund_value", "random_fund_diverse"):
-        extra = ["MarketMakerAgent"] + ["MomentumAgent"] * 25 if config == "random_fund_diverse" else []
+    if config in ("random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse"):
+        extra = ["MarketMakerAgent"] + ["MomentumAgent"] * 25 if config.endswith("diverse") else []
         return ["ExchangeAgent"] + ["NoiseAgent"] * 5000 + ["ValueAgent"] * 100 + extra
     if config == "rmsc03":
         return ["ExchangeAgent"] + ["NoiseAgent"] * 50 + ["ValueAgent"] * 10 + ["POVMarketMakerAgent"] + ["MomentumAgent"] * 2

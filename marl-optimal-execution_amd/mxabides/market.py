@@ -10,28 +10,46 @@ import os
 import numpy as np
 
 from . import _lib
-from .configs import agent_names, agent_type_names, symbol_of
+from .configs import BOOK_FREQ, HIST_CONFIGS, agent_names, agent_type_names, symbol_of
 
 CHUNK_DEFAULT = 1 << 20
 
 
 class VecMarket:
-    def __init__(self, config, seeds, device=0, trace_cap=0, book_log=0):
+    def __init__(self, config, seeds, device=0, trace_cap=0, book_log=0, symbol=None, fundamental=None,
+                 book_freq="config"):
         """book_log: records per env of the book-update log (0 off), the input of the exchange's
         order-book outputs (orderbook_snapshots, exchange_events; include/mxa.h
-        mxa_set_book_log).  A limit order takes 2-4 records, a cancellation 1."""
+        mxa_set_book_log).  A limit order takes 2-4 records, a cancellation 1.
+        symbol: the -t/--ticker of the configs that take one (output names only).
+        fundamental: the ExternalFileOracle series of hist_fund_value / hist_fund_diverse
+        (mxabides.fundamental.FundamentalSeries).  book_freq: the exchange's (default: the config
+        script's, configs.BOOK_FREQ), which decides the order-book file write_logs writes."""
         if config not in _lib.CONFIG_IDS:
             raise ValueError("unknown config %r (supported: %s)" % (config, sorted(_lib.CONFIG_IDS)))
         self.L = _lib.load()
         self.config = config
+        self.symbol = symbol_of(config, symbol)
+        self.book_freq = BOOK_FREQ[config] if book_freq == "config" else book_freq
         self.seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
         self.n_envs = len(self.seeds)
         self.device = device
         self.trace_cap = trace_cap
         self._h = ctypes.c_void_p()
-        rc = self.L.mxa_create(_lib.CONFIG_IDS[config], self.n_envs, self.seeds.ctypes.data, device, trace_cap,
-                               ctypes.byref(self._h))
-        self._check(rc, "mxa_create")
+        self.fundamental = fundamental
+        if config in HIST_CONFIGS:
+            if fundamental is None:
+                raise ValueError("%s needs its ExternalFileOracle series (fundamental=FundamentalSeries)" % config)
+            f = fundamental
+            rc = self.L.mxa_create_hist(_lib.CONFIG_IDS[config], self.n_envs, self.seeds.ctypes.data, device, trace_cap,
+                                        f.t.ctypes.data, f.v.ctypes.data, len(f), ctypes.byref(self._h))
+            self._check(rc, "mxa_create_hist")
+        else:
+            if fundamental is not None:
+                raise ValueError("%s runs the SparseMeanRevertingOracle; a fundamental series is for %s" % (config, HIST_CONFIGS))
+            rc = self.L.mxa_create(_lib.CONFIG_IDS[config], self.n_envs, self.seeds.ctypes.data, device, trace_cap,
+                                   ctypes.byref(self._h))
+            self._check(rc, "mxa_create")
         self.n_agents = self.L.mxa_n_agents(self._h)
         self.book_log_cap = int(book_log)
         if book_log:
@@ -162,7 +180,7 @@ class VecMarket:
         lines (TradingAgent.py:121-126) and Kernel's mean ending value per agent type
         (Kernel.py:337-341)."""
         FL_LAST_FLOAT = 1024
-        names, tnames, sym = agent_names(self.config), agent_type_names(self.config), symbol_of(self.config)
+        names, tnames, sym = agent_names(self.config), agent_type_names(self.config), self.symbol
         lines, gains, counts, order = [], {}, {}, []
         for a, st in enumerate(self.agents(env)):
             if a == 0:
@@ -253,7 +271,7 @@ class VecMarket:
         """the exchange's BEST_BID / BEST_ASK / LAST_TRADE log rows (OrderBook.py:114-141) as a
         DataFrame indexed by EventTime"""
         from .booklog import exchange_events_frame
-        return exchange_events_frame(self.book_log_rows(env), symbol_of(self.config))
+        return exchange_events_frame(self.book_log_rows(env), self.symbol)
 
     def orderbook_snapshots(self, env, wide_book=False):
         """ExchangeAgent.logOrderBookSnapshots' DataFrame with book_freq 0 (ORDERBOOK_<sym>_FULL)"""
@@ -270,21 +288,29 @@ class VecMarket:
 
     def write_logs(self, env, log_dir, wide_book=False):
         """env's run directory as the reference writes it at termination (Kernel.writeLog /
-        writeSummaryLog, Kernel.py:520-565): summary_log.bz2, fundamental_<sym>.bz2 and
-        ORDERBOOK_<sym>_FULL.bz2 (book_freq 0), each a bz2-pickled DataFrame.  Returns the paths."""
-        sym = symbol_of(self.config)
+        writeSummaryLog, Kernel.py:520-565; ExchangeAgent.kernelTerminating, ExchangeAgent.py:106-126):
+        summary_log.bz2, fundamental_<sym>.bz2 and, with book_freq 0, ORDERBOOK_<sym>_FULL.bz2, each
+        a bz2-pickled DataFrame; with book_freq None no order-book file.  Returns the paths."""
+        if self.book_freq is not None and self.book_freq != 0:
+            # "M" (rmsc01) goes through pd.date_range(..., closed="right"), which pandas 2 rejects,
+            # and "all" (obi_rmsc02) is no pandas frequency: the reference raises in both
+            raise NotImplementedError("book_freq %r: the resampled ORDERBOOK_%s_FREQ_* file is not restated"
+                                      % (self.book_freq, self.symbol))
+        if self.config in HIST_CONFIGS:
+            raise NotImplementedError("the ExternalFileOracle's f_log (fundamental_%s) is not restated" % self.symbol)
         os.makedirs(log_dir, exist_ok=True)
         paths = [self.write_summary_log(env, log_dir)]
-        p = os.path.join(log_dir, "fundamental_%s.bz2" % sym)
+        p = os.path.join(log_dir, "fundamental_%s.bz2" % self.symbol)
         self.fundamental_log(env).to_pickle(p, compression="bz2")
         paths.append(p)
-        paths.append(self.write_orderbook_log(env, log_dir, wide_book))
+        if self.book_freq == 0:
+            paths.append(self.write_orderbook_log(env, log_dir, wide_book))
         return paths
 
     def write_orderbook_log(self, env, log_dir, wide_book=False):
         """log_dir/ORDERBOOK_<sym>_FULL.bz2 as Kernel.writeLog pickles it (Kernel.py:537-547)"""
         os.makedirs(log_dir, exist_ok=True)
-        path = os.path.join(log_dir, "ORDERBOOK_%s_FULL.bz2" % symbol_of(self.config))
+        path = os.path.join(log_dir, "ORDERBOOK_%s_FULL.bz2" % self.symbol)
         self.orderbook_snapshots(env, wide_book).to_pickle(path, compression="bz2")
         return path
 

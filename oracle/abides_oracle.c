@@ -287,6 +287,7 @@ struct ora_env {
     /* SparseMeanRevertingOracle (one symbol) */
     ora_rs O;
     double o_rbar, o_kappa, o_fundvol, o_lambda, o_msmean, o_msvar;
+    int efo; /* ExternalFileOracle (hist_fund_* configs) instead of the SparseMeanRevertingOracle */
     int64_t o_open, o_close, o_pt, o_mst;
     double o_pv, o_msv;
     /* global / kernel / latency RNGs */
@@ -546,8 +547,52 @@ static double o_advance(ora_env* e, int64_t t) {
     }
     return o_compute(e, t, 0, pt, pv);
 }
-/* observePrice (SMRO:210-227) with sigma_n > 0 */
+/* ExternalFileOracle (util/oracle/ExternalFileOracle.py) on a series set once per process
+ * (ora_set_fundamental; test infrastructure like the rest of this file) */
+static int64_t* g_fs_t;
+static double* g_fs_v;
+static int g_fs_n;
+void ora_set_fundamental(const int64_t* t, const double* v, int n) {
+    free(g_fs_t);
+    free(g_fs_v);
+    g_fs_t = (int64_t*)malloc(sizeof(int64_t) * n);
+    g_fs_v = (double*)malloc(sizeof(double) * n);
+    memcpy(g_fs_t, t, sizeof(int64_t) * n);
+    memcpy(g_fs_v, v, sizeof(double) * n);
+    g_fs_n = n;
+}
+/* pandas Timedelta.total_seconds(): days * 86400 + seconds + microseconds / 1e6 of the duration
+ * floored to whole microseconds */
+static int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+static double td_seconds(int64_t ns) {
+    int64_t us = floor_div(ns, 1000), s = floor_div(us, 1000000);
+    return (double)s + (double)(us - s * 1000000) / 1000000.0;
+}
+/* getPriceAtTime (ExternalFileOracle.py:52-97) + getInterpolatedPrice (:131-159) */
+static double efo_price(int64_t t) {
+    int n = g_fs_n;
+    if (t < g_fs_t[0]) return g_fs_v[0];
+    if (t > g_fs_t[n - 1]) return g_fs_v[n - 1];
+    int lo = 0, hi = n;
+    while (lo < hi) { /* bisect_left */
+        int mid = (lo + hi) / 2;
+        if (g_fs_t[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    int li = lo - 1, ui = li < n - 1 ? li + 1 : li;
+    if (li < 0) li += n; /* fundamental_series[-1] */
+    double pl = g_fs_v[li], ph = g_fs_v[ui];
+    double slope = pl != ph ? (ph - pl) / td_seconds(g_fs_t[ui] - g_fs_t[li]) : 0.0;
+    return pl + td_seconds(t - g_fs_t[li]) * slope;
+}
+
+/* observePrice (SMRO:210-227; ExternalFileOracle.py:110-129) */
 static int64_t o_observe(ora_env* e, int64_t t, double sigma_n, ora_rs* rs) {
+    if (e->efo) {
+        double tp = efo_price(t);
+        if (sigma_n == 0) return py_round(tp);
+        return py_round(rs_normal(rs, tp, sqrt(sigma_n)));
+    }
     double r_t = t >= e->o_close ? o_advance(e, e->o_close - 1) : o_advance(e, t);
     if (sigma_n == 0) return (int64_t)r_t;
     return py_round(rs_normal(rs, r_t, sqrt(sigma_n)));
@@ -2451,11 +2496,26 @@ static int build_sparse_zi(ora_env* e, uint32_t seed, int big) {
  * wakeup_time then seed then size, per value agent seed then size, [market maker, momentum],
  * kernel seed); random_fund_value has 5000 noise agents waking in 09:30-16:00, 100 value agents
  * (lambda_a 1e-12), no market maker or momentum agents, market 09:30-16:00, kernel 09:30-16:01 */
+/* rfv: 0 rmsc03, 1 random_fund_value, 2 random_fund_diverse, 3 / 4 hist_fund_value / _diverse
+ * (config/hist_fund_*.py: the same agents on an ExternalFileOracle, which draws nothing at
+ * construction; the value agents' r_bar is the series' first value, sigma_n = r_bar / 10) */
 static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv) {
+    const int hist = rfv >= 3;
+    if (hist) {
+        if (!g_fs_n) return -2; /* ora_set_fundamental first */
+        rfv -= 2;
+    }
     rs_seed(&e->G, seed);
     int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = rfv ? 16 * NS_HOUR : 9 * NS_HOUR + 45 * NS_MIN;
     rs_seed(&e->O, seed_u32(&e->G));
-    oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+    if (hist) {
+        e->efo = 1;
+        e->o_open = open;
+        e->o_close = close;
+    } else {
+        oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+    }
+    const double vr_bar = hist ? g_fs_v[0] : 1e5;
     agent_t* ex = add_agent(e, AG_EXCHANGE);
     rs_seed(&ex->rs, seed_u32(&e->G));
     snprintf(ex->name, 96, "EXCHANGE_AGENT");
@@ -2483,12 +2543,12 @@ static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv) {
         snprintf(a->name, 96, "Value Agent %d", a->id);
         snprintf(a->tname, 96, "ValueAgent");
         trading_init(a, 10000000);
-        a->sigma_n = 1e5 / 10;
-        a->r_bar = 1e5;
+        a->sigma_n = vr_bar / 10;
+        a->r_bar = vr_bar;
         a->kappa = 1.67e-15;
         a->sigma_s = 100000;
         a->lambda_a = rfv ? 1e-12 : 7e-11;
-        a->r_t = 1e5;
+        a->r_t = vr_bar;
         a->sigma_t = 0;
     }
     for (int j = 0; j < (rfv ? 0 : 1); j++) {
@@ -2850,6 +2910,8 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     else if (!strcmp(config, "rmsc03")) rc = build_rmsc03_like(e, seed, 0);
     else if (!strcmp(config, "random_fund_value")) rc = build_rmsc03_like(e, seed, 1);
     else if (!strcmp(config, "random_fund_diverse")) rc = build_rmsc03_like(e, seed, 2);
+    else if (!strcmp(config, "hist_fund_value")) rc = build_rmsc03_like(e, seed, 3);
+    else if (!strcmp(config, "hist_fund_diverse")) rc = build_rmsc03_like(e, seed, 4);
     else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
     else if (!strcmp(config, "value_noise")) rc = build_value_noise(e, seed);
     else if (!strcmp(config, "rmsc01")) rc = build_rmsc0x(e, seed, 0, 0);
@@ -2862,9 +2924,15 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     }
     e->nhist = 1; /* history = [{}] */
     e->hash = FNV_OFF;
-    /* kernelInitializing: exchange opening price = oracle.getDailyOpenPrice = r_bar (a float) */
-    e->last_trade = (int64_t)e->o_rbar;
-    e->last_trade_float = 1;
+    /* kernelInitializing: exchange opening price = oracle.getDailyOpenPrice = r_bar (a float); the
+     * ExternalFileOracle's is int(round(price at the open)) (ExternalFileOracle.py:37-50) */
+    if (e->efo) {
+        e->last_trade = py_round(efo_price(e->ex_open));
+        e->last_trade_float = 0;
+    } else {
+        e->last_trade = (int64_t)e->o_rbar;
+        e->last_trade_float = 1;
+    }
     e->ex_has_last = 1;
     /* kernelStarting: every agent requests a wakeup at startTime, in id order */
     for (int i = 0; i < e->n; i++) k_wakeup(e, i, e->start);

@@ -40,6 +40,9 @@ typedef struct ora_env ora_env;
 
 /* config: sparse_zi_100, sparse_zi_1000 or rmsc03 */
 int ora_create(const char* config, uint32_t seed, ora_env** out);
+/* the ExternalFileOracle series of hist_fund_value / hist_fund_diverse (process-wide): n
+ * time-sorted entries, ns since midnight and values */
+void ora_set_fundamental(const int64_t* t, const double* v, int n);
 void ora_destroy(ora_env* e);
 /* run up to max_pops kernel pops (<0: unlimited); returns pops performed by this call */
 int64_t ora_run(ora_env* e, int64_t max_pops);

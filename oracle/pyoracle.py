@@ -10,7 +10,19 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libabides_oracle.so")
+# the ExternalFileOracle series of the hist_fund_* fixtures (tests/golden/gen_fixtures.py fund_series)
+DEFAULT_FUND = os.path.join(os.path.dirname(HERE), "tests", "golden", "fund_JPM_20190628.npz")
+HIST_CONFIGS = ("hist_fund_value", "hist_fund_diverse")
 _lib = None
+_fund_set = False
+
+
+def _ensure_fundamental(config):
+    """hist_fund_* envs read the process-wide series: the fixtures' one unless set_fundamental ran"""
+    global _fund_set
+    if config in HIST_CONFIGS and not _fund_set:
+        z = np.load(DEFAULT_FUND, allow_pickle=False)
+        _set_arrays(z["t"], z["v"])
 
 
 def build():
@@ -79,11 +91,28 @@ def lib():
     return _lib
 
 
+def set_fundamental(series):
+    """the ExternalFileOracle series (mxabides.fundamental.FundamentalSeries) of the hist_fund_*
+    configs, for every oracle env created afterwards in this process"""
+    _set_arrays(series.t, series.v)
+
+
+def _set_arrays(t, v):
+    global _fund_set
+    L = lib()
+    L.ora_set_fundamental.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    t = np.ascontiguousarray(t, dtype=np.int64)
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    L.ora_set_fundamental(t.ctypes.data, v.ctypes.data, len(t))
+    _fund_set = True
+
+
 class OracleEnv:
     """One reference-semantics simulation (config + seed)."""
 
     def __init__(self, config, seed, trace_cap=0):
         L = lib()
+        _ensure_fundamental(config)
         self._h = ctypes.c_void_p()
         rc = L.ora_create(config.encode(), seed & 0xFFFFFFFF, ctypes.byref(self._h))
         if rc:
@@ -210,6 +239,7 @@ class OracleEnv:
 
 def run_batch(config, seeds, threads, max_pops=-1):
     L = lib()
+    _ensure_fundamental(config)
     seeds = np.asarray(seeds, dtype=np.uint32)
     ev = np.zeros(len(seeds), dtype=np.int64)
     hs = np.zeros(len(seeds), dtype=np.uint64)
@@ -224,6 +254,7 @@ def run_batch(config, seeds, threads, max_pops=-1):
 def run_batch_err(config, seeds, threads, max_pops=-1):
     """run_batch plus each env's oracle error code (0 ok, negative fail() code)"""
     L = lib()
+    _ensure_fundamental(config)
     seeds = np.asarray(seeds, dtype=np.uint32)
     ev = np.zeros(len(seeds), dtype=np.int64)
     hs = np.zeros(len(seeds), dtype=np.uint64)
@@ -241,6 +272,7 @@ def batch_stats(config, seeds, threads):
     agent, max live transaction records) of each env run to completion"""
     L = lib()
     L.ora_run_batch_stats.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    _ensure_fundamental(config)
     seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
     out = np.zeros((len(seeds), 4), dtype=np.int64)
     if L.ora_run_batch_stats(config.encode(), seeds.ctypes.data, len(seeds), threads, out.ctypes.data):

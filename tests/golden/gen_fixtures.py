@@ -271,11 +271,16 @@ def run_config(cfg, seed, out, full):
     date = {"sparse_zi_100": "2019-06-28", "sparse_zi_1000": "2019-06-28", "rmsc03": "2019-06-28",
             "value_noise": "2019-06-28", "rmsc01": "2019-06-28", "rmsc02": "2019-06-28",
             "obi_rmsc02": "2019-06-28", "random_fund_value": "2019-06-28",
-            "random_fund_diverse": "2019-06-28"}[cfg]
+            "random_fund_diverse": "2019-06-28", "hist_fund_value": "2019-06-28",
+            "hist_fund_diverse": "2019-06-28"}[cfg]
     MIDNIGHT = int(pd.Timestamp(date).value)
     argv = ["abides.py", "-c", cfg, "-s", str(seed)]
     if cfg in ("rmsc03", "random_fund_value", "random_fund_diverse"):
         argv += ["-t", "ABM", "-d", "20190628"]
+    if cfg in ("hist_fund_value", "hist_fund_diverse"):  # ExternalFileOracle on the JPM mid-price series
+        fp = os.path.abspath("fund_JPM_20190628.pkl")
+        write_fund_files(fp)
+        argv += ["-t", "JPM", "-d", "20190628", "-f", fp]
     sys.argv = argv
     buf = io.StringIO()
     real_stdout = sys.stdout
@@ -355,6 +360,31 @@ def run_config(cfg, seed, out, full):
 
 
 CAPTURE = {}
+
+FUND_CSV = os.path.join(REF, "data", "JPM_2019-06-28_34200_57571_orderbook_1.csv")
+
+
+def fund_series():
+    """The ExternalFileOracle input of the hist_fund_* fixtures: a mid-price series built the way
+    util/formatting/mid_price_from_orderbook.py builds one ((ask_price_1 + bid_price_1) / 2 per
+    book timestamp), from the level-1 book the reference ships (data/JPM_2019-06-28_..._orderbook_1.csv;
+    the series its scripts name, scripts/hist_fund_value.sh, is not in the repository).  Rows
+    with an empty side have no mid and are dropped."""
+    import pandas as pd
+    df = pd.read_csv(FUND_CSV)
+    mid = (df["ask_price_1"] + df["bid_price_1"]) / 2
+    s = pd.Series(mid.to_numpy(dtype=np.float64), index=pd.DatetimeIndex(pd.to_datetime(df["time"])))
+    return s.dropna()
+
+
+def write_fund_files(pickle_path):
+    """our own series file for the reference's ExternalFileOracle (read_pickle of a file this
+    script wrote) and the committed arrays the device and the oracle read"""
+    import pandas as pd
+    s = fund_series()
+    s.to_pickle(pickle_path)
+    mid0 = int(pd.Timestamp("2019-06-28").value)
+    np.savez_compressed(os.path.join(HERE, "fund_JPM_20190628.npz"), t=s.index.asi8 - mid0, v=s.to_numpy())
 
 
 def save_booklog(ex, ob, sym, orig_snapshots, out):
@@ -487,7 +517,11 @@ def main():
             # the whole 09:30-16:00 session; ~5,100 pending events in the queue
             ("random_fund_value", 7, False), ("random_fund_value", 123456789, False),
             # random_fund_diverse: random_fund_value plus a MarketMakerAgent and 25 momentum agents
-            ("random_fund_diverse", 7, False), ("random_fund_diverse", 123456789, False)]
+            ("random_fund_diverse", 7, False), ("random_fund_diverse", 123456789, False),
+            # hist_fund_value / hist_fund_diverse: the same markets on an ExternalFileOracle (the
+            # fundamental is the JPM level-1 mid-price series, interpolated; fund_series())
+            ("hist_fund_value", 7, False), ("hist_fund_value", 123456789, False),
+            ("hist_fund_diverse", 7, False), ("hist_fund_diverse", 123456789, False)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2]]
     procs = []

@@ -10,7 +10,20 @@ FIXTURES = [("sparse_zi_100", 123456789), ("rmsc03", 123456789), ("rmsc03", 1008
             ("rmsc02", 7), ("rmsc02", 123456789), ("rmsc01", 7), ("rmsc01", 99),
             ("obi_rmsc02", 7), ("obi_rmsc02", 123456789), ("obi_rmsc02", 30), ("obi_rmsc02", 107),
             ("random_fund_value", 7), ("random_fund_value", 123456789),
-            ("random_fund_diverse", 7), ("random_fund_diverse", 123456789)]
+            ("random_fund_diverse", 7), ("random_fund_diverse", 123456789),
+            ("hist_fund_value", 7), ("hist_fund_value", 123456789),
+            ("hist_fund_diverse", 7), ("hist_fund_diverse", 123456789)]
+HIST_CONFIGS = ("hist_fund_value", "hist_fund_diverse")
+FUND = os.path.join(GOLDEN, "fund_JPM_20190628.npz")  # gen_fixtures.py fund_series()
+
+
+def market_kw(cfg):
+    """VecMarket keyword arguments a configuration needs: the ExternalFileOracle series of the
+    hist_fund_* fixtures"""
+    if cfg in HIST_CONFIGS:
+        from mxabides.fundamental import FundamentalSeries
+        return {"fundamental": FundamentalSeries.load(FUND)}
+    return {}
 
 
 def load(cfg, seed):

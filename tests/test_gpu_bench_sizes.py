@@ -48,9 +48,11 @@ def _check_batch(s, ev, hs, er):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("cfg,n,batches", [("rmsc02", 4096, (0, 1, 2)), ("obi_rmsc02", 4096, (0,)),
                                            ("rmsc01", 4096, (0,)), ("random_fund_value", 2048, (0,)),
-                                           ("random_fund_diverse", 2048, (0,))])
+                                           ("random_fund_diverse", 2048, (0,)), ("hist_fund_value", 2048, (0,)),
+                                           ("hist_fund_diverse", 2048, (0,))])
 def test_gpu_bench_batches_equal_oracle(mx, cfg, n, batches):
-    m = mx.VecMarket(cfg, shard.env_seeds(batches[0], 0, 1, n))
+    from golden_util import market_kw
+    m = mx.VecMarket(cfg, shard.env_seeds(batches[0], 0, 1, n), **market_kw(cfg))
     for b in batches:
         seeds = shard.env_seeds(b, 0, 1, n)
         m.set_seeds(seeds)

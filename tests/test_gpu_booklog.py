@@ -101,7 +101,7 @@ def test_gpu_fundamental_log_equals_reference(mx, cfg, seed, tmp_path):
     the reference's; write_logs writes the run directory's frames"""
     import pandas as pd
     z = np.load(os.path.join(GOLDEN, "%s_%d_booklog.npz" % (cfg, seed)))
-    m = mx.VecMarket(cfg, [seed], book_log=CAP)
+    m = mx.VecMarket(cfg, [seed], book_log=CAP, book_freq=0)  # the fixtures' -b 0 (rmsc03's own default)
     m.run()
     df = m.fundamental_log(0)
     assert np.array_equal(df.index.asi8 - pd.Timestamp(bl.SESSION_DATE).value, z["fund_time"])
@@ -128,3 +128,22 @@ def test_gpu_fundamental_records_equal_oracle(mx):
         assert len(r) == len(ref)
         assert np.array_equal(r["t"], ref[:, 0]) and np.array_equal(r["price"], ref[:, 1])
         assert np.array_equal(r["qty"], ref[:, 2])
+
+
+def test_gpu_write_logs_follows_the_config_book_freq(mx, tmp_path):
+    """ExchangeAgent.kernelTerminating (ExchangeAgent.py:106-126): with book_freq None
+    (random_fund_value, value_noise's default) no order-book file; the ticker names the files;
+    a resampling frequency (rmsc01 "M", obi_rmsc02 "all") is not restated and says so"""
+    import pandas as pd
+    m = mx.VecMarket("value_noise", [7], book_log=CAP)
+    m.run()
+    paths = m.write_logs(0, str(tmp_path / "vn"))
+    assert sorted(os.path.basename(p) for p in paths) == ["fundamental_JPM.bz2", "summary_log.bz2"]
+    r = mx.VecMarket("random_fund_value", [7], book_log=1 << 20, symbol="IBM")
+    r.run()
+    paths = r.write_logs(0, str(tmp_path / "rfv"))
+    assert sorted(os.path.basename(p) for p in paths) == ["fundamental_IBM.bz2", "summary_log.bz2"]
+    assert len(pd.read_pickle(paths[1] if "fund" in paths[1] else paths[0], compression="bz2")) > 0
+    q = mx.VecMarket("rmsc01", [7], book_log=CAP)
+    with pytest.raises(NotImplementedError):
+        q.write_logs(0, str(tmp_path / "r1"))

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import pyoracle
-from golden_util import FIXTURES, first_mismatch, kat_lines, load
+from golden_util import market_kw, FIXTURES, first_mismatch, kat_lines, load
 
 pytestmark = pytest.mark.gpu
 
@@ -72,7 +72,7 @@ def test_device_glibc_math(mx):
 @pytest.mark.parametrize("cfg,seed", FIXTURES)
 def test_gpu_trace_matches_reference(mx, cfg, seed):
     d, ref = load(cfg, seed)
-    m = mx.VecMarket(cfg, [seed], trace_cap=len(ref))
+    m = mx.VecMarket(cfg, [seed], trace_cap=len(ref), **market_kw(cfg))
     m.run()
     s = m.summary()
     tr = m.trace(0)
@@ -100,7 +100,7 @@ def test_gpu_sparse_zi_1000_known_answer(mx):
 @pytest.mark.parametrize("cfg,n", [("rmsc03", 96), ("sparse_zi_100", 64), ("value_noise", 1024)])
 def test_gpu_batch_equals_oracle(mx, cfg, n):
     seeds = (np.arange(n, dtype=np.int64) * 7919 + 11) & 0xFFFFFFFF
-    m = mx.VecMarket(cfg, seeds)
+    m = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     m.run()
     s = m.summary()
     ev, hs, _ = pyoracle.run_batch(cfg, seeds.astype(np.uint32), threads=8)
@@ -128,7 +128,7 @@ def test_gpu_config_bench_workload_equals_oracle(mx, cfg, n):
     per env: sparse_zi_1000 x1024 is BASELINE configs[2] at full size"""
     from mxabides import shard
     seeds = shard.env_seeds(0, 0, 1, n)
-    m = mx.VecMarket(cfg, seeds)
+    m = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     m.run()
     s = m.summary()
     ev, hs, _ = pyoracle.run_batch(cfg, seeds, threads=min(16, os.cpu_count() or 1))
@@ -140,7 +140,7 @@ def test_gpu_config_bench_workload_equals_oracle(mx, cfg, n):
 @pytest.mark.parametrize("cfg,n", [("sparse_zi_1000", 8)])
 def test_gpu_wide_config_equals_oracle(mx, cfg, n):
     seeds = (np.arange(n, dtype=np.int64) * 104729 + 3) & 0xFFFFFFFF
-    m = mx.VecMarket(cfg, seeds)
+    m = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     m.run()
     s = m.summary()
     ev, hs, _ = pyoracle.run_batch(cfg, seeds.astype(np.uint32), threads=8)
@@ -159,9 +159,9 @@ def test_gpu_chunked_launches_equal_single(mx, cfg, seeds):
     """many save/restore cycles of the queue (LDS) and the book (VGPRs): the reload refills the
     queue from the saved events and, in grouped mode, rebuilds the group minima from a
     non-empty queue"""
-    a = mx.VecMarket(cfg, seeds)
+    a = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     a.run(chunk=1 << 30)
-    b = mx.VecMarket(cfg, seeds)
+    b = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     b.run(chunk=977)
     sa, sb = a.summary(), b.summary()
     assert (sa["status"] == 1).all() and (sb["status"] == 1).all()
@@ -211,7 +211,7 @@ def test_gpu_summary_log_matches_reference(mx, cfg, seed, tmp_path):
     import pandas as pd
     with open(os.path.join(os.path.dirname(__file__), "golden", "%s_%d_summary.json" % (cfg, seed))) as f:
         ref = json.load(f)
-    m = mx.VecMarket(cfg, [seed])
+    m = mx.VecMarket(cfg, [seed], **market_kw(cfg))
     m.run()
     got = m.summary_log(0)
     assert len(got) == len(ref)
@@ -226,7 +226,7 @@ def test_gpu_summary_log_matches_reference(mx, cfg, seed, tmp_path):
 @pytest.mark.parametrize("cfg,n", [("rmsc03", 64), ("sparse_zi_100", 16), ("value_noise", 64)])
 def test_gpu_summary_log_batch_equals_oracle(mx, cfg, n):
     seeds = (np.arange(n, dtype=np.int64) * 7919 + 11) & 0xFFFFFFFF
-    m = mx.VecMarket(cfg, seeds)
+    m = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     m.run()
     m.finalize()
     for i, s in enumerate(seeds):

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import pyoracle
+from golden_util import market_kw
 
 pytestmark = pytest.mark.gpu
 
@@ -21,13 +22,15 @@ def mx():
     return mxabides
 
 
-CONFIGS = ["random_fund_value", "random_fund_diverse"]
+# hist_fund_*: the same markets on the ExternalFileOracle (config/hist_fund_value.py,
+# hist_fund_diverse.py) with the fixtures' JPM mid-price series
+CONFIGS = ["random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse"]
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
 def test_gpu_random_fund_batch_equals_oracle(mx, cfg):
     seeds = (np.arange(64, dtype=np.int64) * 7919 + 11) & 0xFFFFFFFF
-    m = mx.VecMarket(cfg, seeds)
+    m = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     m.run()
     s = m.summary()
     ev, hs, _ = pyoracle.run_batch(cfg, seeds.astype(np.uint32), threads=8)
@@ -41,7 +44,7 @@ def test_gpu_random_fund_chunked_launches_equal_oracle(mx, cfg):
     """997-pop launches: the 6,144-slot queue (payloads in HBM) and the 128-bit free-slot masks
     are saved and rebuilt ~100-200 times per env"""
     seeds = [123456789, 7, 42]
-    m = mx.VecMarket(cfg, seeds)
+    m = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     m.run(chunk=997)
     s = m.summary()
     ev, hs, _ = pyoracle.run_batch(cfg, np.array(seeds, dtype=np.uint32), threads=3)
@@ -52,7 +55,7 @@ def test_gpu_random_fund_chunked_launches_equal_oracle(mx, cfg):
 @pytest.mark.parametrize("cfg", CONFIGS)
 def test_gpu_random_fund_state_and_summary_equal_oracle(mx, cfg):
     seeds = [7, 1008]
-    m = mx.VecMarket(cfg, seeds)
+    m = mx.VecMarket(cfg, seeds, **market_kw(cfg))
     m.run()
     for i, sd in enumerate(seeds):
         o = pyoracle.OracleEnv(cfg, sd)
