@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--ddqn-batch", type=int, default=32, help="rmsc03_ddqn: learner batch size (reference 32)")
     ap.add_argument("--tape", default=None, help="marketreplay tape under tests/golden (IBM_2003-01-14, GOOG_2012-06-21)")
     ap.add_argument("--stub", action="store_true", help="launcher self-test on CPU/gloo with a synthetic engine")
+    ap.add_argument("--no-count", action="store_true",
+                    help="skip the instrumented batch that counts the algorithmic bytes (PMC passes of "
+                         "tools/profile_round.sh: only the timed kernel launches)")
     return ap.parse_args()
 
 
@@ -525,15 +528,19 @@ def main():
             avg_ms = eng.kernel_ms / max(1, eng.launches)
             my_ev_per_launch = events / ctx.world / max(1, eng.launches)
             from mxabides import counters as mc
-            bpe, bparts, bunits = mc.bytes_per_event(eng.count(args.warmup))
+            if args.no_count:
+                bpe, bparts, bunits = float(NOMINAL_BYTES_PER_EVENT), None, None
+            else:
+                bpe, bparts, bunits = mc.bytes_per_event(eng.count(args.warmup))
             achieved = bpe * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
             traffic, tsrc = (traffic_record(args.config, eng.n, bool(args.parity_hash))
                              if isinstance(eng, MarketEngine) else (None, {"why": "no PMC record for this config"}))
             out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_record": tsrc,
                                "kernel": eng.kernel, "avg_launch_ms": avg_ms, "launches": eng.launches,
-                               "algo_bytes_per_event": bpe, "algo_bytes_source": "counted: device event-class counters "
-                               "of one instrumented batch of this workload (mxabides/counters.py, SURVEY.md §8(d) unit sizes)",
+                               "algo_bytes_per_event": bpe, "algo_bytes_source": "nominal (--no-count)" if args.no_count else
+                               "counted: device event-class counters of one instrumented batch of this workload "
+                               "(mxabides/counters.py, SURVEY.md §8(d) unit sizes)",
                                "algo_bytes_breakdown": bparts, "algo_units_per_event": bunits,
                                "nominal_bytes_per_event": NOMINAL_BYTES_PER_EVENT}
             if traffic:

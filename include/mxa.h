@@ -139,9 +139,10 @@ int mxa_write_records(mxa_handle* h, void* device_out);
  * or a trace ring; the measured kernels carry none of it): HOST array [n_envs][MXA_COUNTER_WORDS]
  * int64 = pops per message kind MK_0..MK_24 (WAKEUP pops at 0, GymKernel CANCEL_ORDER at 19),
  * busy requeues (25), events pushed (26), RNG words drawn (27), pops (28), max pending events
- * (29), max resting orders (30), 0.  The inputs of the SURVEY.md §8(d) algorithmic-byte count
- * (mxabides.counters).  Synchronous. */
-#define MXA_COUNTER_WORDS 32
+ * (29), max resting orders (30), agent-record round trips (31), pops handled inside batched event
+ * runs (32), 0.  The inputs of the SURVEY.md §8(d) algorithmic-byte count (mxabides.counters).
+ * Synchronous. */
+#define MXA_COUNTER_WORDS 34
 int mxa_read_counters(mxa_handle* h, int64_t* out);
 /* diagnostics: copy `bytes` raw bytes of env `env`'s HBM block starting at `offset`; and
  * the block's section offsets (Layout: ag, open, rng, lat, q, book, tx, trace) */

@@ -104,7 +104,9 @@ __global__ __launch_bounds__(64) void mxa_counters_kernel(const char* base, uint
     o[28] = h->pops;
     o[29] = h->max_q;
     o[30] = h->max_book;
-    o[31] = 0;
+    o[31] = h->kc[MXA_KC_REC];
+    o[32] = h->kc[MXA_KC_RUN];
+    o[33] = 0;
   }
 }
 

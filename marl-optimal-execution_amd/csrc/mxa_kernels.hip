@@ -809,6 +809,9 @@ struct Eng {
     rhi = (u32)(v >> 32);
     cur_agent = a;
     rdirty = 0;
+    if constexpr (INSTR && !BUILD) {
+      if ((hash_on || trace) && lane == 0) h.kc[MXA_KC_REC]++;  // class counters (mxa_read_counters)
+    }
   }
   // write-back of the record: with DIRTY_WB only its 128-byte quarters (whole L2 lines, 16
   // lanes each) that an rs* call changed since rec_load (the builder writes whole records)
@@ -3833,6 +3836,7 @@ struct Eng {
   // per-pop accounting of the members, in member order
   DEV void run_account(u64 key, i64 t, const Msg& mm, int n) {
     if (INSTR && (hash_on || trace)) {
+      if (lane == 0) h.kc[MXA_KC_RUN] += n;
       for (int i = 0; i < n; i++) {
         Msg m;
         for (int w = 0; w < 8; w++) m.w[w] = w < PW ? rdl(mm.w[w], i) : 0u;

@@ -102,13 +102,16 @@ typedef struct {
   int64_t md_next_due;           // no freq > 0 subscription is due before this update time (0: unknown)
   // event-class counters of instrumented runs (parity hash on / trace ring): pops per message
   // kind (MK_*; WAKEUP pops at MK_WAKEUP, GymKernel CANCEL_ORDER pops at MK_KCANCEL), then busy
-  // requeues at MXA_KC_REQUEUE; the algorithmic-byte count of bench.py (mxa_read_counters)
-  uint32_t kc[26];
+  // requeues at MXA_KC_REQUEUE, agent-record round trips (MXA_KC_REC) and pops handled as members
+  // of a batched event run (MXA_KC_RUN); the algorithmic-byte count of bench.py (mxa_read_counters)
+  uint32_t kc[28];
   int32_t q0;                    // queue occupancy when the build ended (the kernelStarting wakeups)
   int32_t pad4;
   uint64_t rng0;                 // RNG words the build drew (sum over streams of position - 624)
 } EnvHdr;
 #define MXA_KC_REQUEUE 25
+#define MXA_KC_REC 26
+#define MXA_KC_RUN 27
 
 #ifdef __cplusplus
 static_assert(sizeof(EnvHdr) % 8 == 0 && sizeof(EnvHdr) <= 512, "EnvHdr: copied by 64 lanes x 8 B, 512 B of LDS");

@@ -64,7 +64,7 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash",
            "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log", "mxa_write_records", "mxa_set_id_persistence",
            "mxa_read_counters", "mxa_create_hist"]
-COUNTER_WORDS = 32  # include/mxa.h MXA_COUNTER_WORDS
+COUNTER_WORDS = 34  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
 _lib = None

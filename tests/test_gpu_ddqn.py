@@ -28,6 +28,7 @@ def test_gpu_ddqn_episode_matches_oracle_replay():
     v.set_stream(stream.cuda_stream)
     learner = ddqn.DDQNLearner(device="cuda", seed=1, batch_size=32)
     task = ddqn.ExecutionTask(device="cuda")
+    oras = [None] * len(SEEDS)  # one oracle "process" per env: episode 2 continues its order ids
     for ep in range(2):
         seeds = [s + 1000 * ep for s in SEEDS]
         rec = []
@@ -42,7 +43,11 @@ def test_gpu_ddqn_episode_matches_oracle_replay():
         st = st.cpu().numpy()
         rl_id = v.n_agents - 1
         for e, seed in enumerate(seeds):
-            o = pyoracle.OracleGymEnv(seed=seed)
+            if oras[e] is None:
+                oras[e] = pyoracle.OracleGymEnv(seed=seed)
+            else:
+                oras[e].reset(seed=seed)
+            o = oras[e]
             cash0, ex0 = _oracle_rl(o, rl_id)
             ref_r = []
             for i in range(len(acts)):

@@ -13,7 +13,7 @@ ENVS=${3:-4096}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp
-B="$R/bench.py --config $CFG --envs $ENVS --no-cpu"
+B="$R/bench.py --config $CFG --envs $ENVS --no-cpu --no-count"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 $B > $OUT/trace.log 2>&1 || { echo "trace pass failed"; tail $OUT/trace.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o pmc -- \
@@ -23,6 +23,6 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -
 cd $R
 python3 tools/hbm_summary.py $OUT --record $CFG $ENVS 0 \
   "tools/profile_round.sh $TAG: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of" \
-  "'bench.py --config $CFG --envs $ENVS --steps 1 --warmup 0 --no-cpu' (parity hash off, as bench.py runs);" \
+  "'bench.py --config $CFG --envs $ENVS --steps 1 --warmup 0 --no-cpu --no-count' (parity hash off, as bench.py runs);" \
   "reads doubled per MI355X_MICROARCH.md HBM section (gfx950 FETCH_SIZE reports half); L2 memory-side" \
   "requests, Infinity-Cache hits included"
