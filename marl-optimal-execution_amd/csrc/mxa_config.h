@@ -41,6 +41,9 @@ constexpr int sq_lds(int cfg);
 #ifndef MXA_SO_RMSC02
 #define MXA_SO_RMSC02 8
 #endif
+#ifndef MXA_SO_Z1K
+#define MXA_SO_Z1K 13  // sparse_zi_1000 book slots per lane (832; oracle max 734 resting orders over the 4,096 bench seeds); r03 s9 run kernel: 16 slots 1004 ms, 14 952, 13 925
+#endif
 #ifndef MXA_SO_RFD
 #define MXA_SO_RFD 9
 #endif
@@ -98,7 +101,7 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 3, true, MXA_W_OBI, 8, 0}
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, MXA_W_Z1, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, MXA_W_VN, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
-       : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, 16, false, 1, 6, MXA_HOT_RECORDS}
+       : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, MXA_SO_Z1K, false, 1, 6, MXA_HOT_RECORDS}
        // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
        // maximum over the 8,192 bench seeds is 5,125 events), payload in HBM; 320 book slots (max 279)
        // the first MXA_RFV_SQL slots per lane (24: 1,536) in LDS for events due within a second,

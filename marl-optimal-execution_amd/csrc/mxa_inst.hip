@@ -44,9 +44,10 @@ MxaEntry make_entry() {
     e.run_log = launch_run<CFG, true, true>;
     // measured per configuration (one box, hash off, run kernel): without the instrumentation
     // rmsc03 44.1 vs 44.6 ms, sparse_zi_100 132.5 vs 135.1, value_noise 22.1 vs 22.5, rmsc02
-    // 1190 vs 1245; but rmsc01 1201 vs 1147 and sparse_zi_1000 986 vs 976 (their register
-    // allocation comes out worse), so those two keep the instrumented kernel
-    constexpr bool fast = CFG != MXA_CFG_RMSC01 && CFG != MXA_CFG_SPARSE_ZI_1000;
+    // 1190 vs 1245; rmsc01 and sparse_zi_1000 measured the other way in round 2 (1201 vs 1147,
+    // 986 vs 976), but with the event-class counters in the instrumented kernel (round 3, s10)
+    // the plain one wins there too: rmsc01 1047 vs 1082 ms, sparse_zi_1000 916 vs 920
+    constexpr bool fast = true;
 #ifndef MXA_NO_FAST
     if constexpr (fast) e.run_fast = launch_run<CFG, false, false>;
 #endif

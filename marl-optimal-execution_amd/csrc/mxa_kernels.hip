@@ -1010,7 +1010,7 @@ struct Eng {
       if constexpr (TIER) {  // unrolled: a rolled loop indexes gk/gs/gj dynamically (scratch)
 #pragma unroll
         for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
-      } else {
+      } else {  // (unrolled here too: the same time for sparse_zi_1000, +0.5-2 % for sparse_zi_100 and value_noise, r03 s9)
         for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
       }
       q_lanemin();
@@ -3746,7 +3746,10 @@ struct Eng {
       e.key = qkey(j);
       e.seq = qseq(j);
       e.pad = 0;
-      for (int i = 0; i < 8; i++) e.pl[i] = (PL_LDS && i < PW) ? qpl[slot * PW + i] : 0u;
+      // an empty slot saves no payload: its LDS words are whatever the slot last held (or, in a
+      // slot never used since the build, LDS contents of an earlier kernel)
+      const bool live = e.key != KEY_EMPTY;
+      for (int i = 0; i < 8; i++) e.pl[i] = (live && PL_LDS && i < PW) ? qpl[slot * PW + i] : 0u;
       sq[slot] = e;
     }
     SavedOrder* so = (SavedOrder*)(env + PC.L.off_book);

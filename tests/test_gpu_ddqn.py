@@ -80,3 +80,44 @@ def test_gpu_qnet_matches_host():
         ref = net(x)
         got = net.cuda()(x.cuda()).cpu()
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3)
+
+
+def _layers(net):
+    return [(lin.weight.detach().cpu().numpy().T.astype(np.float64), lin.bias.detach().cpu().numpy().astype(np.float64))
+            for lin in list(net.hidden) + [net.logits]]
+
+
+def _batch(n, seed):
+    rs = np.random.RandomState(seed)
+    return (rs.randint(0, 200, (n, 2)).astype(np.float64), rs.randint(0, 24, n), rs.randint(0, 200, (n, 2)).astype(np.float64),
+            rs.normal(0, 50, n))
+
+
+@pytest.mark.parametrize("dtype,rtol,atol", [(torch.float64, 1e-9, 1e-9), (torch.float32, 2e-3, 2e-4)])
+def test_gpu_learner_updates_match_numpy_reference(dtype, rtol, atol):
+    """train_neural_nets on the device (ddqlearning_execution_agent.py:448-515: the target from
+    the target net, MSE, Keras RMSprop with eps outside the sqrt, the target copy every
+    replace_target_iter updates) against oracle/ddqn_ref.py in float64, step by step: exact to
+    1e-9 in float64, within fp32 tolerance for the fp32 learner the bench runs"""
+    import ddqn_ref
+    L = ddqn.DDQNLearner(device="cuda", dropout=0.0, seed=3, batch_size=32)
+    L.eval_model.to(dtype)
+    L.target_model.to(dtype)
+    L.opt = torch.optim.RMSprop(L.eval_model.parameters(), lr=0.01, alpha=0.9, eps=1e-7)
+    lay = _layers(L.eval_model)
+    rms = [(np.zeros_like(W), np.zeros_like(b)) for W, b in lay]
+    T = lay
+    for it in range(12):
+        s, a, s2, r = _batch(32, 100 + it)
+        if it % L.replace_target_iter == 0:
+            T = [(W.copy(), b.copy()) for W, b in lay]
+        tgt = ddqn_ref.q_target(lay, T, s, a, s2, r, 0.98)
+        loss, grads = ddqn_ref.mse_grads(lay, s, tgt)
+        lay, rms = ddqn_ref.rmsprop_step(lay, grads, rms, 0.01)
+        dv = lambda x: torch.from_numpy(x).to("cuda", dtype)
+        cost = L.learn_on(dv(s), torch.from_numpy(a).cuda(), dv(s2), dv(r))
+        assert abs(float(cost) - loss) <= max(rtol, 1e-9) * max(1.0, loss) * (1 if dtype == torch.float64 else 10), it
+        for (W, b), (W2, b2) in zip(_layers(L.eval_model), lay):
+            np.testing.assert_allclose(W, W2, rtol=rtol, atol=atol, err_msg="update %d" % it)
+            np.testing.assert_allclose(b, b2, rtol=rtol, atol=atol, err_msg="update %d" % it)
+    assert L.learn_step_counter == 12

@@ -16,29 +16,18 @@ HASH_OFF = 16  # EnvHdr.hash (include/mxa.h layout: cur, pops, hash, ...)
 KC_OFF, KC_END = 368, 368 + 28 * 4  # EnvHdr.kc: the event-class counters instrumented runs keep
 
 
-SAVED_EVENT = 48  # include/mxa.h SavedEvent: u64 key, u32 seq, u32 pad, u32 payload[8]
-KEY_EMPTY = 0xFFFFFFFFFFFFFFFF
-
 
 def _blocks(m, envs):
-    """env blocks with the hash field, the event-class counters (mxa_read_counters) and the
-    payload words of EMPTY saved-queue slots zeroed:
-    a freed slot keeps the payload words of its last message, including words that message's
-    kind leaves unset (register contents at the push, never read), which is the only place
-    besides the hash where the two runs can differ."""
+    """env blocks with the hash field and the event-class counters (mxa_read_counters) zeroed:
+    the only two places where the instrumented and the plain run may differ.  (Empty saved-queue
+    slots carry no payload words: save() writes zeros there, so stale LDS contents cannot leak
+    into the env block.)"""
     n = m.env_bytes
-    lay = m.layout()
-    q0, q1 = lay["q"], lay["book"]
     out = []
     for e in envs:
         b = m.raw(int(e), 0, n)
         b[HASH_OFF:HASH_OFF + 8] = 0
         b[KC_OFF:KC_END] = 0
-        q = b[q0:q1].view(np.uint8)
-        nslot = (q1 - q0) // SAVED_EVENT
-        keys = q[:nslot * SAVED_EVENT].reshape(nslot, SAVED_EVENT)[:, :8].copy().view(np.uint64).ravel()
-        for sl in np.nonzero(keys == KEY_EMPTY)[0]:
-            b[q0 + sl * SAVED_EVENT + 16:q0 + (sl + 1) * SAVED_EVENT] = 0
         out.append(b)
     return out
 
