@@ -48,7 +48,8 @@ enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKET
        MXA_RANDOM_FUND_VALUE = 9 /* config/random_fund_value.py: 5000 noise + 100 value agents, 09:30-16:00 */,
        MXA_RANDOM_FUND_DIVERSE = 10 /* config/random_fund_diverse.py: random_fund_value + market maker + 25 momentum */,
        MXA_HIST_FUND_VALUE = 11 /* config/hist_fund_value.py: random_fund_value on an ExternalFileOracle (mxa_create_hist) */,
-       MXA_HIST_FUND_DIVERSE = 12 /* config/hist_fund_diverse.py: random_fund_diverse on an ExternalFileOracle */ };
+       MXA_HIST_FUND_DIVERSE = 12 /* config/hist_fund_diverse.py: random_fund_diverse on an ExternalFileOracle */,
+       MXA_MARKETREPLAY_RUNNER = 13 /* config/marketreplay.py: exchange + MarketReplayAgent under Kernel.runner */ };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };
@@ -165,6 +166,12 @@ void mxa_destroy(mxa_handle* h);
 int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                       const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
                       mxa_handle** out);
+/* config/marketreplay.py (config/marketreplay.py:60-140): the exchange and the MarketReplayAgent on
+ * the same tape under Kernel.runner, midnight to 16:01 — a plain Kernel.runner handle (mxa_run,
+ * mxa_finalize, the readers); the tape format of mxa_create_replay */
+int mxa_create_replay_runner(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                             const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
+                             mxa_handle** out);
 /* (replay and MXA_RMSC03_RL handles) one ABIDESEnv.step per env: actions [n][3] (float64) -> obs [n][9] (float64) and flags [n]
  * (bit0 done, bit1 observation valid, bit2 env error).  Host arrays; synchronous. */
 int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags);

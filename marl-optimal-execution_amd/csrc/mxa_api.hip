@@ -218,6 +218,7 @@ static bool bind(mxa_handle* h, int cfg) {
   case 10: e = mxa_entry_10(); break;
   case 11: e = mxa_entry_11(); break;
   case 12: e = mxa_entry_12(); break;
+  case 13: e = mxa_entry_13(); break;
 #endif
   default: return false;
   }
@@ -258,12 +259,13 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
                     (int)MXA_RANDOM_FUND_VALUE == (int)MXA_CFG_RANDOM_FUND_VALUE &&
                     (int)MXA_RANDOM_FUND_DIVERSE == (int)MXA_CFG_RANDOM_FUND_DIVERSE &&
                     (int)MXA_HIST_FUND_VALUE == (int)MXA_CFG_HIST_FUND_VALUE &&
-                    (int)MXA_HIST_FUND_DIVERSE == (int)MXA_CFG_HIST_FUND_DIVERSE,
+                    (int)MXA_HIST_FUND_DIVERSE == (int)MXA_CFG_HIST_FUND_DIVERSE &&
+                    (int)MXA_MARKETREPLAY_RUNNER == (int)MXA_CFG_MARKETREPLAY_RUNNER,
                 "config ids");
-  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_HIST_FUND_DIVERSE + 1, "one entry per configuration");
-  // replay handles: mxa_create_replay; ExternalFileOracle configurations: mxa_create_hist
-  if (config == MXA_MARKETREPLAY || config == MXA_HIST_FUND_VALUE || config == MXA_HIST_FUND_DIVERSE ||
-      !bind(h, config)) {
+  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_MARKETREPLAY_RUNNER + 1, "one entry per configuration");
+  // replay handles: mxa_create_replay(_runner); ExternalFileOracle configurations: mxa_create_hist
+  if (config == MXA_MARKETREPLAY || config == MXA_MARKETREPLAY_RUNNER || config == MXA_HIST_FUND_VALUE ||
+      config == MXA_HIST_FUND_DIVERSE || !bind(h, config)) {
     delete h;
     return MXA_EINVAL;
   }
@@ -346,23 +348,37 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
     h->ctx.fs_t = (const int64_t*)(h->d_tape + h->tb_fs_t);
     h->ctx.fs_v = (const double*)(h->d_tape + h->tb_fs_v);
   }
-  if (h->gym || h->ext) {
+  if (h->gym || h->ext || h->replay) {
     HIPCHK(h, hipMalloc(&h->d_ctx, sizeof(RpCtx)));
     HIPCHK(h, hipMemcpyAsync(h->d_ctx, &h->ctx, sizeof(RpCtx), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMalloc(&h->d_act, sizeof(double) * 3 * n_envs));
     HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 9 * n_envs));
     HIPCHK(h, hipMalloc(&h->d_flags, sizeof(int32_t) * n_envs));
   }
-  if (h->gym || h->ext) HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->gym || h->ext || h->replay) HIPCHK(h, hipStreamSynchronize(h->stream));
   const int rc = mxa_reset(h, nullptr);  // a fresh process: ids from 0
   h->persist_ids = h->gym;               // later resets continue the process (Order.py:8-9)
   return rc;
 }
 
-// ABIDESEnv on a LOBSTER tape (agent_config.py / ABIDESEnv.py); see include/mxa.h
+// ABIDESEnv on a LOBSTER tape (agent_config.py / ABIDESEnv.py), or config/marketreplay.py under
+// Kernel.runner (cfg MXA_CFG_MARKETREPLAY_RUNNER); see include/mxa.h
+static int create_replay(int cfg, const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                         const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
+                         mxa_handle** out);
 int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                       const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
                       mxa_handle** out) {
+  return create_replay(MXA_CFG_MARKETREPLAY, t, oid, price, size, buy, n_rec, n_envs, device, trace_cap, out);
+}
+int mxa_create_replay_runner(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                             const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
+                             mxa_handle** out) {
+  return create_replay(MXA_CFG_MARKETREPLAY_RUNNER, t, oid, price, size, buy, n_rec, n_envs, device, trace_cap, out);
+}
+static int create_replay(int cfg, const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                         const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
+                         mxa_handle** out) {
   if (!out || !t || !oid || !price || !size || !buy || n_rec <= 0 || n_envs <= 0 || trace_cap < 0) return MXA_EINVAL;
 #ifdef MXA_NO_GYM
   return MXA_EINVAL;
@@ -378,7 +394,7 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
     if (oid[i] == 0) n_zero++;
     else min_id = std::min(min_id, oid[i]);
   }
-  const MxaParams P0 = mxa_cfg::params(MXA_CFG_MARKETREPLAY);
+  const MxaParams P0 = mxa_cfg::params(cfg);
   // auto ids (DummyRL's orders and the tape's ORDER_ID 0 records) count up from 0 in one
   // global sequence; Order.generateOrderId would skip explicit tape ids it met, which cannot
   // happen while every auto id stays below the smallest tape id
@@ -395,7 +411,7 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
            }),
            uf.end());  // sorted by (id, record): the first of each id is kept
   mxa_handle* h = new mxa_handle();
-  if (!bind(h, MXA_CFG_MARKETREPLAY)) {
+  if (!bind(h, cfg)) {
     delete h;
     return MXA_EINVAL;
   }
@@ -430,7 +446,7 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
   const int C = n_rec + h->P.rl_ids;  // every placement could rest at once
   // auto-id dense range: the episode's auto ids, the explicit ids they may skip over in a later
   // episode (MXA_AUTO_SKIP), and one never-present index (orders.get(0) without an auto id 0)
-  h->ctx.L = mxa_cfg::replay_layout(mxa_cfg::env_stride(MXA_CFG_MARKETREPLAY, trace_cap), (int)pmin, (int)(pmax - pmin + 1), C,
+  h->ctx.L = mxa_cfg::replay_layout(mxa_cfg::env_stride(cfg, trace_cap), (int)pmin, (int)(pmax - pmin + 1), C,
                                     n_ids, (int)auto_cap + MXA_AUTO_SKIP + 1, ntm, n_rec);
   h->ctx.nuid = (int32_t)uf.size();
   h->ctx.umin = uf.empty() ? INT32_MAX : uf[0].first;
@@ -593,7 +609,8 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
 // book-update log (OrderBook.book_log / the exchange's BEST_BID, BEST_ASK, LAST_TRADE events):
 // `cap` records per env in one device buffer; every env's record count restarts at 0
 int mxa_set_book_log(mxa_handle* h, int32_t cap) {
-  if (!h || h->gym || !h->run_log || cap < 0) return MXA_EINVAL;
+  // (the replay book is a price ladder the log does not follow: not for replay handles)
+  if (!h || h->gym || h->replay || !h->run_log || cap < 0) return MXA_EINVAL;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->d_blog) HIPCHK(h, hipFree(h->d_blog));

@@ -111,7 +111,7 @@ constexpr Shape shape(int cfg) {
        // seeds: 448 overflowed) and wide replies for the market maker's depth-5 spread queries
        : (cfg == MXA_CFG_RANDOM_FUND_DIVERSE || cfg == MXA_CFG_HIST_FUND_DIVERSE)
            ? Shape{96, MXA_SO_RFD, false, MXA_RFD_WAVES, 8, 0, MXA_RFD_SQL}
-                                       : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay: book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
+                                       : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay (both): book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
 constexpr size_t lds_bytes(int cfg) {
@@ -320,6 +320,17 @@ constexpr void params_marketreplay(MxaParams& P) {
   P.L.lat_len = 0;
 }
 
+// config/marketreplay.py:60-140: the exchange and the MarketReplayAgent alone under
+// Kernel.runner (midnight to 16:01, compute delay 0, latency 0, noise [0.0]); nothing draws
+constexpr void params_marketreplay_runner(MxaParams& P) {
+  params_marketreplay(P);
+  P.config = MXA_CFG_MARKETREPLAY_RUNNER;
+  P.stop = 16 * HOUR + MIN;
+  P.first_rl = 0;
+  P.n_rl = 0;
+  P.n_agents = 2;
+}
+
 // rmsc03 + DummyRL (BASELINE.json configs[3]; tests/golden/gen_rl_fixtures.py): rmsc03's 64
 // agents under a GymKernel with DummyRLExecutionAgent 64 (agent_config.py:115-137 parameters:
 // BUY 1e5, 30 s, order_level 2, spread depth 500), horizon pd.date_range(09:31, 09:44, "30S").
@@ -517,6 +528,7 @@ constexpr MxaParams params(int cfg) {
   if (cfg == MXA_CFG_RMSC03) params_rmsc03(P);
   else if (cfg == MXA_CFG_RMSC03_RL) params_rmsc03_rl(P);
   else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);
+  else if (cfg == MXA_CFG_MARKETREPLAY_RUNNER) params_marketreplay_runner(P);
   else if (cfg == MXA_CFG_VALUE_NOISE) params_value_noise(P);
   else if (cfg == MXA_CFG_RMSC01) params_rmsc01(P);
   else if (cfg == MXA_CFG_RMSC02) params_rmsc02(P);

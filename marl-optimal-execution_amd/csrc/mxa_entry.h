@@ -39,4 +39,5 @@ MxaEntry mxa_entry_9();
 MxaEntry mxa_entry_10();
 MxaEntry mxa_entry_11();
 MxaEntry mxa_entry_12();
-#define MXA_N_CONFIGS 13
+MxaEntry mxa_entry_13();
+#define MXA_N_CONFIGS 14

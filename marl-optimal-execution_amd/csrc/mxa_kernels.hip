@@ -543,8 +543,9 @@ struct Eng {
 #endif
   static constexpr int NG = QHIER ? SQ / QG : 1;
   static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
-  static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY;     // ABIDESEnv / replay composition
-  static constexpr bool GYM = RP || CFG == MXA_CFG_RMSC03_RL;  // a GymKernel with a DummyRL agent
+  // the replay book + tape (ABIDESEnv's composition, or config/marketreplay.py under Kernel.runner)
+  static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_MARKETREPLAY_RUNNER;
+  static constexpr bool GYM = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL;  // a GymKernel with a DummyRL agent
   // ORDER_ACCEPTED to a background TradingAgent is a no-op (TradingAgent.orderAccepted only
   // logs, TradingAgent.py:409-420; no ZI/Noise/Value/POV-MM/Momentum branch reacts to it, and the
   // POV-MM's both-replies-in test cannot fire on it). With every computation delay 0 the busy
@@ -4369,8 +4370,10 @@ struct Builder : Eng<CFG, true> {
     this->rec_store();
     rec_init(P.first_replay, AG_REPLAY);
     this->rec_store();
-    rec_init(P.first_rl, AG_DUMMYRL);
-    this->rec_store();
+    if constexpr (E::PC.n_rl > 0) {
+      rec_init(P.first_rl, AG_DUMMYRL);
+      this->rec_store();
+    }
     this->h.last_trade = 0;
     this->h.last_trade_float = 0;
     this->cur = P.start;

@@ -21,7 +21,7 @@ enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPAR
                      MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6,
                      MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8, MXA_CFG_RANDOM_FUND_VALUE = 9,
                      MXA_CFG_RANDOM_FUND_DIVERSE = 10, MXA_CFG_HIST_FUND_VALUE = 11,
-                     MXA_CFG_HIST_FUND_DIVERSE = 12 };
+                     MXA_CFG_HIST_FUND_DIVERSE = 12, MXA_CFG_MARKETREPLAY_RUNNER = 13 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {

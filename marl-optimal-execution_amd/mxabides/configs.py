@@ -13,8 +13,10 @@ ZI_COUNTS = {"sparse_zi_100": [15, 15, 14, 14, 14, 14, 14], "sparse_zi_1000": [1
 
 # configs whose script takes the ticker from -t/--ticker (config/rmsc03.py:31, random_fund_*.py,
 # hist_fund_*.py); the default is the one the fixtures and the bench use
-TICKER_CONFIGS = ("rmsc03", "random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse")
+TICKER_CONFIGS = ("rmsc03", "random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse",
+                  "marketreplay_runner")
 HIST_CONFIGS = ("hist_fund_value", "hist_fund_diverse")
+REPLAY_CONFIGS = ("marketreplay_runner",)  # config/marketreplay.py: a LOBSTER tape, no oracle
 
 
 def symbol_of(config, symbol=None):
@@ -24,6 +26,8 @@ def symbol_of(config, symbol=None):
         return symbol
     if config in HIST_CONFIGS:
         return "JPM"
+    if config in REPLAY_CONFIGS:
+        return "IBM"
     return "ABM" if config in TICKER_CONFIGS else "JPM"
 
 
@@ -32,10 +36,12 @@ def symbol_of(config, symbol=None):
 # (ExchangeAgent.py:389-469; value_noise / sparse_zi_* take -b, default None)
 BOOK_FREQ = {"rmsc03": 0, "rmsc02": 0, "rmsc01": "M", "obi_rmsc02": "all", "random_fund_value": None,
              "random_fund_diverse": None, "hist_fund_value": None, "hist_fund_diverse": None, "value_noise": None,
-             "sparse_zi_100": None, "sparse_zi_1000": None}
+             "sparse_zi_100": None, "sparse_zi_1000": None, "marketreplay_runner": 0}
 
 
 def agent_names(config):
+    if config == "marketreplay_runner":  # config/marketreplay.py:66-110
+        return ["EXCHANGE_AGENT", "MARKET_REPLAY_AGENT"]
     if config == "obi_rmsc02":
         return (["EXCHANGE_AGENT", "MARKET_MAKER_AGENT_1"] + ["ZI_AGENT_%d" % j for j in range(2, 91)] +
                 ["OBI_AGENT_%d" % j for j in range(91, 96)] + ["MOMENTUM_AGENT_%d" % j for j in range(96, 101)])
@@ -63,6 +69,8 @@ def agent_names(config):
 
 
 def agent_type_names(config):
+    if config == "marketreplay_runner":
+        return ["ExchangeAgent", "MarketReplayAgent"]
     if config == "obi_rmsc02":
         return (["ExchangeAgent", "MarketMakerAgent"] + ["ZeroIntelligenceAgent"] * 89 +
                 ["OrderBookImbalanceAgent"] * 5 + ["MomentumAgent"] * 5)

@@ -10,21 +10,23 @@ import os
 import numpy as np
 
 from . import _lib
-from .configs import BOOK_FREQ, HIST_CONFIGS, agent_names, agent_type_names, symbol_of
+from .configs import BOOK_FREQ, HIST_CONFIGS, REPLAY_CONFIGS, agent_names, agent_type_names, symbol_of
 
 CHUNK_DEFAULT = 1 << 20
 
 
 class VecMarket:
     def __init__(self, config, seeds, device=0, trace_cap=0, book_log=0, symbol=None, fundamental=None,
-                 book_freq="config"):
+                 book_freq="config", tape=None):
         """book_log: records per env of the book-update log (0 off), the input of the exchange's
         order-book outputs (orderbook_snapshots, exchange_events; include/mxa.h
         mxa_set_book_log).  A limit order takes 2-4 records, a cancellation 1.
         symbol: the -t/--ticker of the configs that take one (output names only).
         fundamental: the ExternalFileOracle series of hist_fund_value / hist_fund_diverse
         (mxabides.fundamental.FundamentalSeries).  book_freq: the exchange's (default: the config
-        script's, configs.BOOK_FREQ), which decides the order-book file write_logs writes."""
+        script's, configs.BOOK_FREQ), which decides the order-book file write_logs writes.
+        tape: the LOBSTER tape (mxabides.tape.Tape) of marketreplay_runner, config/marketreplay.py
+        (the seeds only count the envs there: nothing in that composition draws)."""
         if config not in _lib.CONFIG_IDS:
             raise ValueError("unknown config %r (supported: %s)" % (config, sorted(_lib.CONFIG_IDS)))
         self.L = _lib.load()
@@ -37,7 +39,15 @@ class VecMarket:
         self.trace_cap = trace_cap
         self._h = ctypes.c_void_p()
         self.fundamental = fundamental
-        if config in HIST_CONFIGS:
+        if config in REPLAY_CONFIGS:
+            if tape is None:
+                raise ValueError("%s replays a LOBSTER tape (tape=mxabides.tape.Tape)" % config)
+            self.tape = tape
+            rc = self.L.mxa_create_replay_runner(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
+                                                 tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), self.n_envs,
+                                                 device, trace_cap, ctypes.byref(self._h))
+            self._check(rc, "mxa_create_replay_runner")
+        elif config in HIST_CONFIGS:
             if fundamental is None:
                 raise ValueError("%s needs its ExternalFileOracle series (fundamental=FundamentalSeries)" % config)
             f = fundamental
@@ -144,11 +154,13 @@ class VecMarket:
         """OrderBook.bids (side 0) / asks (side 1): list of levels, each a FIFO list of
         [order_id, agent_id, quantity, price]."""
         cap = 4096
-        buf = np.zeros((cap, 4), dtype=np.int64)
-        n = self._check(self.L.mxa_read_book(self._h, env, side, buf.ctypes.data, cap), "mxa_read_book")
+        while True:  # mxa_read_book returns the side's order count; a replay book holds thousands
+            buf = np.zeros((cap, 4), dtype=np.int64)
+            n = self._check(self.L.mxa_read_book(self._h, env, side, buf.ctypes.data, cap), "mxa_read_book")
+            if n <= cap:
+                break
+            cap = n
         levels = []
-        if n > cap:
-            raise _lib.MxaError("book side holds %d orders (> %d)" % (n, cap))
         for o in buf[:n].tolist():
             if levels and levels[-1][0][3] == o[3]:
                 levels[-1].append(o)
@@ -298,6 +310,8 @@ class VecMarket:
                                       % (self.book_freq, self.symbol))
         if self.config in HIST_CONFIGS:
             raise NotImplementedError("the ExternalFileOracle's f_log (fundamental_%s) is not restated" % self.symbol)
+        if self.config in REPLAY_CONFIGS:
+            raise NotImplementedError("ORDERBOOK_%s_FULL of the replay's price-ladder book is not restated" % self.symbol)
         os.makedirs(log_dir, exist_ok=True)
         paths = [self.write_summary_log(env, log_dir)]
         p = os.path.join(log_dir, "fundamental_%s.bz2" % self.symbol)

@@ -334,6 +334,7 @@ struct ora_env {
      * carried across ora_gym_reset like the reference's class attributes (Order.py:8-9) */
     int64_t* used_ids;
     int used_cap, used_n;
+    char sym[16]; /* the report's symbol when set (ora_set_symbol): -t/--ticker of replay configs */
     int64_t st_max_heap, st_max_resting, st_max_open, st_resting, st_max_hist_tx;
     char* report;
     int64_t report_len;
@@ -2315,7 +2316,8 @@ static void final_valuation(ora_env* e, agent_t* a) {
 /* TradingAgent.kernelStopping (TradingAgent.py:112-138) + Kernel mean print (Kernel.py:337-341) */
 int ora_finish(ora_env* e) {
     char line[512];
-    const char* sym = strncmp(e->config, "rmsc03", 6) == 0 || strncmp(e->config, "random_fund_", 12) == 0 ? "ABM" : "JPM";
+    const char* sym = e->sym[0] ? e->sym
+                      : strncmp(e->config, "rmsc03", 6) == 0 || strncmp(e->config, "random_fund_", 12) == 0 ? "ABM" : "JPM";
     /* one entry per distinct agent type string (value_noise names every ValueAgent's type apart) */
     char (*tnames)[96] = (char (*)[96])malloc(sizeof(char[96]) * (size_t)e->n);
     long long* gains = (long long*)malloc(sizeof(long long) * (size_t)e->n);
@@ -2821,14 +2823,18 @@ static int build_rmsc03_rl(ora_env* e, uint32_t seed) {
  * Exchange (id 0), MarketReplayAgent (1) on a LOBSTER tape, DummyRLExecutionAgent (2);
  * GymKernel start = midnight, stop = 16:10, compute delays 0, latencies 0, noise [1.0].
  * Nothing in this composition draws from an RNG. */
-int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
-                  const int8_t* buy, int n, ora_env** out) {
+/* runner 0: ABIDESEnv's composition (agent_config.py: Exchange, MarketReplayAgent, DummyRL under
+ * a GymKernel); runner 1: config/marketreplay.py (Exchange and MarketReplayAgent under
+ * Kernel.runner, midnight to 16:01, agents named as that script names them) */
+static int create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                     const int8_t* buy, int n, int runner, ora_env** out) {
     if (n <= 0) return -1;
     ora_env* e = (ora_env*)calloc(1, sizeof(ora_env));
-    snprintf(e->config, sizeof e->config, "marketreplay");
+    snprintf(e->config, sizeof e->config, runner ? "marketreplay_runner" : "marketreplay");
     int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
     agent_t* x = add_agent(e, AG_EXCHANGE);
-    snprintf(x->name, sizeof x->name, "0_EXCHANGE_AGENT");
+    snprintf(x->name, sizeof x->name, runner ? "EXCHANGE_AGENT" : "0_EXCHANGE_AGENT");
+    snprintf(x->tname, sizeof x->tname, "ExchangeAgent");
     e->ex_open = open;
     e->ex_close = close;
     e->ex_pipeline = 0;
@@ -2836,10 +2842,14 @@ int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, co
     e->stream_history = 10;
     agent_t* a = add_agent(e, AG_REPLAY);
     trading_init(a, 0);
-    snprintf(a->name, sizeof a->name, "1_MARKET_REPLAY_AGENT");
-    agent_t* r = add_agent(e, AG_DUMMYRL);
-    trading_init(r, 0);
-    snprintf(r->name, sizeof r->name, "2_DUMMY_RL_EXECUTION_AGENT");
+    snprintf(a->name, sizeof a->name, runner ? "MARKET_REPLAY_AGENT" : "1_MARKET_REPLAY_AGENT");
+    snprintf(a->tname, sizeof a->tname, "MarketReplayAgent");
+    agent_t* r = NULL;
+    if (!runner) {
+        r = add_agent(e, AG_DUMMYRL);
+        trading_init(r, 0);
+        snprintf(r->name, sizeof r->name, "2_DUMMY_RL_EXECUTION_AGENT");
+    }
     e->tp_n = n;
     e->tp_t = (int64_t*)malloc(sizeof(int64_t) * n);
     e->tp_oid = (int64_t*)malloc(sizeof(int64_t) * n);
@@ -2867,20 +2877,22 @@ int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, co
     for (int i = 0; i < e->mr_cap; i++) e->mr_key[i] = -1;
     e->mr_ord = (aord_t*)calloc(e->mr_cap, sizeof(aord_t));
     a = &e->ag[1]; /* add_agent reallocs: re-fetch */
-    r = &e->ag[2];
     a->wake_freq = e->tm[0] - open;
-    /* execution_time_horizon = pd.date_range(09:40, 16:00, freq="30S") */
-    e->nhz = 761;
-    e->hz = (int64_t*)malloc(sizeof(int64_t) * e->nhz);
-    for (int i = 0; i < e->nhz; i++) e->hz[i] = 9 * NS_HOUR + 40 * NS_MIN + (int64_t)i * 30 * NS_SEC;
-    r->wake_freq = e->hz[0] - open;
-    e->rl_quantity = 100000;
-    e->rl_rem = 100000;
-    e->rl_trade = 1;
-    e->rl_id = 2;
-    e->gym = 1;
+    if (!runner) {
+        r = &e->ag[2];
+        /* execution_time_horizon = pd.date_range(09:40, 16:00, freq="30S") */
+        e->nhz = 761;
+        e->hz = (int64_t*)malloc(sizeof(int64_t) * e->nhz);
+        for (int i = 0; i < e->nhz; i++) e->hz[i] = 9 * NS_HOUR + 40 * NS_MIN + (int64_t)i * 30 * NS_SEC;
+        r->wake_freq = e->hz[0] - open;
+        e->rl_quantity = 100000;
+        e->rl_rem = 100000;
+        e->rl_trade = 1;
+        e->rl_id = 2;
+        e->gym = 1;
+    }
     e->start = 0;
-    e->stop = 16 * NS_HOUR + 10 * NS_MIN;
+    e->stop = runner ? 16 * NS_HOUR + NS_MIN : 16 * NS_HOUR + 10 * NS_MIN;
     e->lat_mode = 0;
     e->noise_len = 1;
     e->agent_time = (int64_t*)calloc(e->n, sizeof(int64_t));
@@ -2892,6 +2904,15 @@ int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, co
     e->cur = e->start;
     *out = e;
     return 0;
+}
+int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                  const int8_t* buy, int n, ora_env** out) {
+    return create_mr(t, oid, price, size, buy, n, 0, out);
+}
+void ora_set_symbol(ora_env* e, const char* sym) { snprintf(e->sym, sizeof e->sym, "%s", sym); }
+int ora_create_mr_runner(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                         const int8_t* buy, int n, ora_env** out) {
+    return create_mr(t, oid, price, size, buy, n, 1, out);
 }
 int ora_rl_state(const ora_env* e, int64_t* out4) {
     out4[0] = e->rl_rem;
@@ -3150,7 +3171,8 @@ int64_t ora_book_log(const ora_env* e, int64_t* buf, int64_t cap) {
 int ora_gym_reset(ora_env** pe, uint32_t seed) {
     ora_env* old = *pe;
     ora_env* e = NULL;
-    int rc = old->tp_n ? ora_create_mr(old->tp_t, old->tp_oid, old->tp_price, old->tp_size, old->tp_buy, old->tp_n, &e)
+    int rc = old->tp_n ? create_mr(old->tp_t, old->tp_oid, old->tp_price, old->tp_size, old->tp_buy, old->tp_n,
+                                   !old->gym, &e)
                        : ora_create(old->config, seed, &e);
     if (rc) return rc;
     e->order_counter = old->order_counter;

@@ -84,6 +84,10 @@ int64_t ora_report(const ora_env* e, char* buf, int64_t cap);
  * midnight), order id, price (cents), size, side; time-sorted, file order within a time. */
 int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                   const int8_t* buy, int n, ora_env** out);
+/* config/marketreplay.py: the exchange and the MarketReplayAgent under Kernel.runner (ora_run) */
+void ora_set_symbol(ora_env* e, const char* sym);
+int ora_create_mr_runner(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                         const int8_t* buy, int n, ora_env** out);
 /* ABIDESEnv.step(action[3]): obs_out[9] (valid when *has_obs), *done; returns 0 or an error */
 int ora_gym_step(ora_env* e, const double* action, double* obs_out, int* has_obs, int* done_out);
 /* DummyRL: remaining quantity, executed quantity, trade flag; replay agent's open orders */

@@ -311,6 +311,27 @@ def gym_batch(actions, threads, seeds=None, tape=None):
     return dict(events=ev, hash=hs, err=er, steps=st, obs=obs, seconds=sec.value)
 
 
+class OracleReplayRunner(OracleEnv):
+    """config/marketreplay.py: the exchange and the MarketReplayAgent on a tape under Kernel.runner
+    (run / finish / report / summary_log / book / agents as OracleEnv)"""
+
+    def __init__(self, tape, symbol="IBM", trace_cap=0):
+        L = lib()
+        L.ora_create_mr_runner.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.ora_set_symbol.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        self._h = ctypes.c_void_p()
+        self._tape = tape
+        rc = L.ora_create_mr_runner(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
+                                    tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), ctypes.byref(self._h))
+        if rc:
+            raise ValueError("oracle: bad tape (%d)" % rc)
+        L.ora_set_symbol(self._h, symbol.encode())
+        self.trace_buf = None
+        if trace_cap:
+            self.trace_buf = np.zeros((trace_cap, 10), dtype=np.int64)
+            L.ora_set_trace(self._h, self.trace_buf.ctypes.data, trace_cap)
+
+
 class OracleGymEnv(OracleEnv):
     """GymKernel restatement: ABIDESEnv (Exchange + MarketReplayAgent + DummyRL on a LOBSTER tape),
     or with `tape=None, seed=s` the rmsc03 + DummyRL composition (config "rmsc03_rl")."""

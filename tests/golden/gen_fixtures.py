@@ -268,15 +268,32 @@ def run_config(cfg, seed, out, full):
     from agent.TradingAgent import TradingAgent
     TradingAgent.getTransactedVolume = TradingAgent.get_transacted_volume  # SURVEY.md key finding 3
 
+    replay = None
+    if cfg.startswith("marketreplay:"):  # config/marketreplay.py TICKER DATE (Kernel.runner replay)
+        _, ticker, rdate = cfg.split(":")
+        replay = (ticker, rdate)
+        cfg = "marketreplay"
+        # the script's relative paths: the LOBSTER message file under data/lobster/ (linked to the
+        # one the reference ships) and an empty processed-orders folder (the processor parses the
+        # CSV; the committed pickles are never loaded)
+        d = os.path.join("data", "lobster", "LOBSTER_SampleFile_%s_%s_1" % (ticker, rdate))
+        os.makedirs(d, exist_ok=True)
+        os.makedirs(os.path.join("data", "marketreplay", "level_1"), exist_ok=True)
+        fn = "%s_%s_34200000_57600000_message_1.csv" % (ticker, rdate)
+        src = os.path.join(REF, "data", "lobster", "LOBSTER_SampleFile_%s_1" % ticker, fn)
+        if not os.path.exists(os.path.join(d, fn)):
+            os.symlink(src, os.path.join(d, fn))
     date = {"sparse_zi_100": "2019-06-28", "sparse_zi_1000": "2019-06-28", "rmsc03": "2019-06-28",
             "value_noise": "2019-06-28", "rmsc01": "2019-06-28", "rmsc02": "2019-06-28",
             "obi_rmsc02": "2019-06-28", "random_fund_value": "2019-06-28",
             "random_fund_diverse": "2019-06-28", "hist_fund_value": "2019-06-28",
-            "hist_fund_diverse": "2019-06-28"}[cfg]
+            "hist_fund_diverse": "2019-06-28", "marketreplay": replay[1] if replay else None}[cfg]
     MIDNIGHT = int(pd.Timestamp(date).value)
     argv = ["abides.py", "-c", cfg, "-s", str(seed)]
     if cfg in ("rmsc03", "random_fund_value", "random_fund_diverse"):
         argv += ["-t", "ABM", "-d", "20190628"]
+    if replay:
+        argv += ["-t", replay[0], "-d", replay[1]]
     if cfg in ("hist_fund_value", "hist_fund_diverse"):  # ExternalFileOracle on the JPM mid-price series
         fp = os.path.abspath("fund_JPM_20190628.pkl")
         write_fund_files(fp)
@@ -521,12 +538,14 @@ def main():
             # hist_fund_value / hist_fund_diverse: the same markets on an ExternalFileOracle (the
             # fundamental is the JPM level-1 mid-price series, interpolated; fund_series())
             ("hist_fund_value", 7, False), ("hist_fund_value", 123456789, False),
-            ("hist_fund_diverse", 7, False), ("hist_fund_diverse", 123456789, False)]
+            ("hist_fund_diverse", 7, False), ("hist_fund_diverse", 123456789, False),
+            # config/marketreplay.py: the exchange and the MarketReplayAgent under Kernel.runner
+            ("marketreplay:IBM:2003-01-14", 1, False), ("marketreplay:GOOG:2012-06-21", 1, False)]
     if len(sys.argv) > 2:
-        jobs = [j for j in jobs if j[0] == sys.argv[2]]
+        jobs = [j for j in jobs if j[0] == sys.argv[2] or j[0].startswith(sys.argv[2] + ":")]
     procs = []
     for cfg, seed, full in jobs:
-        out = os.path.join(HERE, "%s_%d" % (cfg, seed))
+        out = os.path.join(HERE, "%s_%d" % (cfg.replace(":", "_"), seed))
         cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out] + (["--full"] if full else []) + extra
         wd = tempfile.mkdtemp(prefix="gf_")
         procs.append((cfg, seed, subprocess.Popen(cmd, cwd=wd, env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))))
