@@ -107,6 +107,16 @@ int mxa_launch(mxa_handle* h, int64_t max_pops);
 int mxa_sync(mxa_handle* h);
 /* launches of `chunk` pops until every env is done/errored (or max_launches reached) */
 int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launches_out);
+/* Kernel.runner(startTime, stopTime) with a caller's stopTime (Kernel.py:50-64, 190-196): every env
+ * of a Kernel.runner handle stops at its first pop with currentTime past t_stop_ns (ns since the
+ * simulated midnight; that event is handled, as the reference's loop test comes before its get)
+ * instead of the config script's kernelStopTime.  Kept across mxa_reset; t_stop_ns <= 0 restores
+ * the config's.  Set it before the run: an env already stopped stays stopped.  GymKernel handles:
+ * MXA_EINVAL. */
+int mxa_set_stop_time(mxa_handle* h, int64_t t_stop_ns);
+/* mxa_set_stop_time + mxa_run to the end of every env (chunks of 2^20 pops); events_out
+ * (nullable, [n_envs]): each env's ttl_messages.  The §8(b) mxa_run_until entry point. */
+int mxa_run_until(mxa_handle* h, int64_t t_stop_ns, int64_t* events_out);
 /* Kernel.runner's kernelStopping pass for every env once the run is over: the agents'
  * FINAL_VALUATION entries of the summary log (ZeroIntelligenceAgent.py:80-112, NoiseAgent.py:44-68,
  * ValueAgent.py:66-86), observing the oracle in agent order.  Idempotent (state is not saved);

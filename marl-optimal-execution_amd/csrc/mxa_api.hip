@@ -31,6 +31,12 @@ __global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int 
   if (i < n && ((const EnvHdr*)(base + (size_t)i * stride))->status == ST_RUNNING) atomicAdd(out, 1);
 }
 
+// Kernel.runner's stopTime of every env (EnvHdr::t_stop; 0 = the config's own)
+__global__ void mxa_set_stop_kernel(char* base, uint64_t stride, int n, int64_t t_stop) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ((EnvHdr*)(base + (size_t)i * stride))->t_stop = t_stop;
+}
+
 __global__ void mxa_results_kernel(const char* base, uint64_t stride, int n, int64_t* out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -173,6 +179,7 @@ struct mxa_handle {
   // GymKernel handles: mxa_reset continues Order.order_id / Order._order_ids of the previous
   // episode (one process running consecutive ABIDESEnv episodes)
   bool persist_ids = false;
+  int64_t t_stop = 0;  // mxa_set_stop_time: Kernel.runner's stopTime override (0: the config's)
   int32_t tcap_arg() const { return (parity_hash || P.L.trace_cap > 0) ? P.L.trace_cap : -1; }
   // the run kernel of the current settings: the log variant, the instrumented one, or (hash off,
   // no trace ring) the one without the parity instrumentation
@@ -552,7 +559,39 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
   h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_seeds, dm,
            h->d_ctx);
   HIPCHK(h, hipGetLastError());
+  if (h->t_stop > 0) {  // the build cleared the header: the override outlives resets
+    const int n = h->P.n_envs;
+    hipLaunchKernelGGL(mxa_set_stop_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env,
+                       h->P.L.env_stride, n, h->t_stop);
+    HIPCHK(h, hipGetLastError());
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_set_stop_time(mxa_handle* h, int64_t t_stop_ns) {
+  if (!h || h->gym) return MXA_EINVAL;  // GymKernel handles: ABIDESEnv's own stop (ABIDESEnv.py:42-46)
+  HIPCHK(h, hipSetDevice(h->device));
+  h->t_stop = t_stop_ns > 0 ? t_stop_ns : 0;
+  const int n = h->P.n_envs;
+  hipLaunchKernelGGL(mxa_set_stop_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env, h->P.L.env_stride,
+                     n, h->t_stop);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_run_until(mxa_handle* h, int64_t t_stop_ns, int64_t* events_out) {
+  if (!h || h->gym) return MXA_EINVAL;
+  int rc = mxa_set_stop_time(h, t_stop_ns);
+  if (rc != MXA_OK) return rc;
+  if ((rc = mxa_run(h, (int64_t)1 << 20, 0, nullptr)) != MXA_OK) return rc;
+  if (events_out) {
+    const int n = h->P.n_envs;
+    std::vector<mxa_env_summary> s(n);
+    if ((rc = mxa_read_summary(h, s.data())) != MXA_OK) return rc;
+    for (int i = 0; i < n; i++) events_out[i] = s[i].events;
+  }
   return MXA_OK;
 }
 

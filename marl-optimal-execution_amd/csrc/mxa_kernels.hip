@@ -580,6 +580,7 @@ struct Eng {
   LDSP EnvHdr& h;  // cold header fields live in LDS for the duration of a launch
   // hot header fields in SGPRs
   i64 cur, pops, ocnt;
+  i64 stop_t;  // Kernel.runner's stopTime: the config's unless the header overrides it (EnvHdr::t_stop)
   u64 hash;
   u32 seq;
   i32 status, err, qcount;
@@ -3687,6 +3688,7 @@ struct Eng {
     if (lane < (int)(sizeof(EnvHdr) / 8)) dst[lane] = src[lane];
     wfence();
     cur = h.cur;
+    stop_t = h.t_stop > 0 ? h.t_stop : PC.stop;
     pops = h.pops;
     ocnt = h.order_counter;
     hash = h.hash;
@@ -4105,7 +4107,7 @@ struct Eng {
       u64 key;
       u32 eseq;
       int slot = q_peek(key, eseq);
-      if (slot < 0 || !(cur <= PC.stop)) {
+      if (slot < 0 || !(cur <= stop_t)) {
         status = ST_DONE;
         break;
       }
@@ -4115,7 +4117,7 @@ struct Eng {
       int type = (int)(key & 3);
       if constexpr (RUNS) {
         // a run past stopTime is not batched: the loop stops after its first member
-        if (type == MT_MESSAGE && (m.w[0] & MF_RUN) && t <= PC.stop && eseq >= run_skip) {
+        if (type == MT_MESSAGE && (m.w[0] & MF_RUN) && t <= stop_t && eseq >= run_skip) {
           const u32 k = m_kind(m);
           const bool exr = rcp == 0 && (k == MK_CANCEL || k == MK_LIMIT) && !(t > PC.mkt_close) && !BLOG && !MD;
           const bool ackr = rcp > 0 && rcp < ACK_LIMIT && (k == MK_ACCEPTED || k == MK_CANCELLED);

@@ -108,6 +108,7 @@ typedef struct {
   int32_t q0;                    // queue occupancy when the build ended (the kernelStarting wakeups)
   int32_t pad4;
   uint64_t rng0;                 // RNG words the build drew (sum over streams of position - 624)
+  int64_t t_stop;                // Kernel.runner's stopTime if > 0 (mxa_set_stop_time), else the config's
 } EnvHdr;
 #define MXA_KC_REQUEUE 25
 #define MXA_KC_REC 26

@@ -66,7 +66,8 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_set_seeds", "mxa_write_results", "mxa_read_raw", "mxa_layout", "mxa_create_replay", "mxa_step",
            "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash",
            "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log", "mxa_write_records", "mxa_set_id_persistence",
-           "mxa_read_counters", "mxa_create_hist", "mxa_create_replay_runner"]
+           "mxa_read_counters", "mxa_create_hist", "mxa_create_replay_runner",
+           "mxa_set_stop_time", "mxa_run_until"]
 COUNTER_WORDS = 34  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
@@ -112,7 +113,8 @@ def load():
     for name, args in (("mxa_write_records", [P, P]), ("mxa_set_id_persistence", [P, I32]),
                        ("mxa_read_counters", [P, P]),
                        ("mxa_create_hist", [I32, I32, P, I32, I32, P, P, I32, ctypes.POINTER(P)]),
-                       ("mxa_create_replay_runner", [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)])):
+                       ("mxa_create_replay_runner", [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)]),
+                       ("mxa_set_stop_time", [P, I64]), ("mxa_run_until", [P, I64, P])):
         if hasattr(L, name):  # (older single-configuration A/B builds lack them; libmxa.so has all)
             getattr(L, name).argtypes = args
     L.mxa_write_rl_state.argtypes = [P, P]

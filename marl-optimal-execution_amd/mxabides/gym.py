@@ -170,6 +170,44 @@ class VecABIDESEnv:
             pass
 
 
+class Box:
+    """What a learner reads of the reference's gym.spaces.Box (ABIDESEnv.py:22-26; gym is not a
+    dependency here): low, high, shape, dtype (float32 as gym's default), sample(), contains(),
+    seed().  gym.spaces.Box(low, high) itself is used when gym is importable."""
+
+    def __init__(self, low, high, dtype=np.float32):
+        self.dtype = np.dtype(dtype)
+        self.low = np.asarray(low, dtype=self.dtype)
+        self.high = np.asarray(high, dtype=self.dtype)
+        assert self.low.shape == self.high.shape
+        self.shape = self.low.shape
+        self._rs = np.random.RandomState()
+
+    def seed(self, seed=None):
+        self._rs = np.random.RandomState(seed)
+        return [seed]
+
+    def sample(self):
+        return self._rs.uniform(self.low, self.high, self.shape).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+    __contains__ = contains
+
+    def __repr__(self):
+        return "Box(%s, %s, %s, %s)" % (self.low.min(), self.high.max(), self.shape, self.dtype)
+
+
+def _box(low, high):
+    try:
+        import gym
+        return gym.spaces.Box(np.array(low), np.array(high))
+    except ImportError:
+        return Box(low, high)
+
+
 class ABIDESEnv:
     """Drop-in for the reference ABIDESEnv(ticker, date, log_dir=None, seed=None) on a LOBSTER
     message file `data/lobster/LOBSTER_SampleFile_{ticker}_1/{ticker}_{date}_34200000_57600000_message_1.csv`
@@ -182,8 +220,8 @@ class ABIDESEnv:
         self.ticker, self.date, self.log_dir = ticker, date, log_dir
         self.seed = np.random.randint(low=0, high=2 ** 31 - 1) if seed is None else seed  # agents draw nothing
         self._v = VecABIDESEnv(tape, 1, device=device)
-        self.action_space = (np.zeros(ACTION_SIZE), np.ones(ACTION_SIZE))
-        self.observation_space = (np.zeros(10), np.zeros(10))  # as declared by the reference
+        self.action_space = _box([0.0] * ACTION_SIZE, [1.0] * ACTION_SIZE)
+        self.observation_space = _box([0] * 10, [0] * 10)  # as declared by the reference (ABIDESEnv.py:23)
         self._obs = []
 
     def reset(self):

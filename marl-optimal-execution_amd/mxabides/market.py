@@ -129,6 +129,19 @@ class VecMarket:
         self._check(self.L.mxa_run(self._h, chunk, max_launches, ctypes.byref(n)), "mxa_run")
         return n.value
 
+    def set_stop_time(self, t_stop_ns):
+        """Kernel.runner's stopTime (ns since the simulated midnight) instead of the config
+        script's kernelStopTime, kept across resets; None or <= 0 restores the config's
+        (include/mxa.h mxa_set_stop_time)"""
+        self._check(self.L.mxa_set_stop_time(self._h, int(t_stop_ns or 0)), "mxa_set_stop_time")
+
+    def run_until(self, t_stop_ns):
+        """Kernel.runner(startTime, stopTime=t_stop_ns) for every env: run to the first pop past
+        t_stop_ns (handled, as in the reference); returns each env's ttl_messages"""
+        ev = np.zeros(self.n_envs, dtype=np.int64)
+        self._check(self.L.mxa_run_until(self._h, int(t_stop_ns), ev.ctypes.data), "mxa_run_until")
+        return ev
+
     @property
     def last_kernel_ms(self):
         return self.L.mxa_last_kernel_ms(self._h)

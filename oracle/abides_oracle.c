@@ -2910,6 +2910,9 @@ int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, co
     return create_mr(t, oid, price, size, buy, n, 0, out);
 }
 void ora_set_symbol(ora_env* e, const char* sym) { snprintf(e->sym, sizeof e->sym, "%s", sym); }
+/* Kernel.runner(startTime, stopTime=...) with another stopTime than the config script's
+ * (Kernel.py:50-64; the loop test `currentTime <= stopTime`, Kernel.py:190-196) */
+void ora_set_stop(ora_env* e, int64_t t_stop) { e->stop = t_stop; }
 int ora_create_mr_runner(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                          const int8_t* buy, int n, ora_env** out) {
     return create_mr(t, oid, price, size, buy, n, 1, out);

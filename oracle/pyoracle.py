@@ -128,6 +128,12 @@ class OracleEnv:
     def finish(self):
         lib().ora_finish(self._h)
 
+    def set_stop(self, t_stop):
+        """Kernel.runner's stopTime (ns since midnight) instead of the config's; before run()"""
+        L = lib()
+        L.ora_set_stop.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        L.ora_set_stop(self._h, int(t_stop))
+
     @property
     def done(self):
         return bool(lib().ora_done(self._h))

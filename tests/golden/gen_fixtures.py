@@ -268,6 +268,15 @@ def run_config(cfg, seed, out, full):
     from agent.TradingAgent import TradingAgent
     TradingAgent.getTransactedVolume = TradingAgent.get_transacted_volume  # SURVEY.md key finding 3
 
+    stop_at = None
+    if "@" in cfg:  # CFG@HH:MM:SS: Kernel.runner(stopTime=that time of the day) instead of the script's
+        cfg, stop_at = cfg.split("@")
+        orig_runner = K.Kernel.runner
+
+        def runner(self, *a, **k):
+            k["stopTime"] = k["startTime"].normalize() + pd.Timedelta(stop_at)
+            return orig_runner(self, *a, **k)
+        K.Kernel.runner = runner
     replay = None
     if cfg.startswith("marketreplay:"):  # config/marketreplay.py TICKER DATE (Kernel.runner replay)
         _, ticker, rdate = cfg.split(":")
@@ -540,12 +549,16 @@ def main():
             ("hist_fund_value", 7, False), ("hist_fund_value", 123456789, False),
             ("hist_fund_diverse", 7, False), ("hist_fund_diverse", 123456789, False),
             # config/marketreplay.py: the exchange and the MarketReplayAgent under Kernel.runner
-            ("marketreplay:IBM:2003-01-14", 1, False), ("marketreplay:GOOG:2012-06-21", 1, False)]
+            ("marketreplay:IBM:2003-01-14", 1, False), ("marketreplay:GOOG:2012-06-21", 1, False),
+            # Kernel.runner with a caller's stopTime (the scripts' own kernelStopTime replaced)
+            ("rmsc03@11:00:00", 123456789, True), ("value_noise@10:15:00", 7, True),
+            ("sparse_zi_100@09:45:30", 123456789, True)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2] or j[0].startswith(sys.argv[2] + ":")]
     procs = []
     for cfg, seed, full in jobs:
-        out = os.path.join(HERE, "%s_%d" % (cfg.replace(":", "_"), seed))
+        out = os.path.join(HERE, "%s_%d" % (cfg.replace("@", "_stop").replace(":", ""), seed) if "@" in cfg
+                           else "%s_%d" % (cfg.replace(":", "_"), seed))
         cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out] + (["--full"] if full else []) + extra
         wd = tempfile.mkdtemp(prefix="gf_")
         procs.append((cfg, seed, subprocess.Popen(cmd, cwd=wd, env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))))

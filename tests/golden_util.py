@@ -52,3 +52,21 @@ def kat_lines():
                 break
             means.append(l.strip())
     return holdings, means
+
+
+# Kernel.runner with a caller's stopTime (gen_fixtures.py "CFG@HH:MM:SS"): (config, seed, stop
+# as ns since midnight, fixture name)
+NS_S = 1_000_000_000
+STOP_FIXTURES = [("rmsc03", 123456789, 11 * 3600 * NS_S, "rmsc03_stop110000_123456789"),
+                 ("value_noise", 7, (10 * 3600 + 15 * 60) * NS_S, "value_noise_stop101500_7"),
+                 ("sparse_zi_100", 123456789, (9 * 3600 + 45 * 60 + 30) * NS_S, "sparse_zi_100_stop094530_123456789")]
+
+
+def load_named(name):
+    """(fixture dict, trace, summary rows) of tests/golden/<name>.*"""
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        d = json.load(f)
+    with open(os.path.join(GOLDEN, name + "_summary.json")) as f:
+        summ = json.load(f)
+    tr = np.load(os.path.join(GOLDEN, name + ".npz"))["trace"]
+    return d, tr, summ

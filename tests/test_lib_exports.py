@@ -27,7 +27,8 @@ def test_layout_header_is_self_consistent(tmp_path):
     import subprocess
     src = tmp_path / "sz.cpp"
     src.write_text("""#include "mxa_config.h"
-static_assert(sizeof(EnvHdr) == 496, "EnvHdr");
+static_assert(sizeof(EnvHdr) == 504, "EnvHdr");
+static_assert(offsetof(EnvHdr, t_stop) == 496, "EnvHdr.t_stop");
 static_assert(offsetof(EnvHdr, kc) == 368, "EnvHdr.kc (tests/test_gpu_hash_switch.py KC_OFF)");
 static_assert(sizeof(SubRec) == 32, "SubRec");
 static_assert(sizeof(BlRec) == 16, "BlRec");
