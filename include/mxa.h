@@ -49,7 +49,8 @@ enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKET
        MXA_RANDOM_FUND_DIVERSE = 10 /* config/random_fund_diverse.py: random_fund_value + market maker + 25 momentum */,
        MXA_HIST_FUND_VALUE = 11 /* config/hist_fund_value.py: random_fund_value on an ExternalFileOracle (mxa_create_hist) */,
        MXA_HIST_FUND_DIVERSE = 12 /* config/hist_fund_diverse.py: random_fund_diverse on an ExternalFileOracle */,
-       MXA_MARKETREPLAY_RUNNER = 13 /* config/marketreplay.py: exchange + MarketReplayAgent under Kernel.runner */ };
+       MXA_MARKETREPLAY_RUNNER = 13 /* config/marketreplay.py: exchange + MarketReplayAgent under Kernel.runner */,
+       MXA_MARKETREPLAY_TWAP = 14 /* config/execution/marketreplay/execution_marketreplay.py: + TWAPExecutionAgent */ };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };
@@ -182,6 +183,15 @@ int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price
 int mxa_create_replay_runner(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                              const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
                              mxa_handle** out);
+/* config/execution/marketreplay/execution_marketreplay.py (:55-160): the handle of
+ * mxa_create_replay_runner plus TWAP_EXECUTION_AGENT 2 (TWAPExecutionAgent, twap_agent.py:9-63:
+ * BUY 12e3 over pd.date_range(10:00, 12:00, "60S"), QUERY_SPREAD depth 500).  trade = the script's
+ * -e flag; with it the agent's first placeOrders raises the reference's KeyError (a 30 s Interval
+ * looked up in its 60 s schedule, execution_agent.py:118) and every env ends in error
+ * 25 (ERR_TWAP_SCHEDULE) at 10:00, as the reference run does. */
+int mxa_create_replay_twap(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                           const int8_t* buy, int32_t n_rec, int32_t trade, int32_t n_envs, int32_t device,
+                           int32_t trace_cap, mxa_handle** out);
 /* (replay and MXA_RMSC03_RL handles) one ABIDESEnv.step per env: actions [n][3] (float64) -> obs [n][9] (float64) and flags [n]
  * (bit0 done, bit1 observation valid, bit2 env error).  Host arrays; synchronous. */
 int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags);

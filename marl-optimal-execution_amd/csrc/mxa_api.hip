@@ -226,6 +226,7 @@ static bool bind(mxa_handle* h, int cfg) {
   case 11: e = mxa_entry_11(); break;
   case 12: e = mxa_entry_12(); break;
   case 13: e = mxa_entry_13(); break;
+  case 14: e = mxa_entry_14(); break;
 #endif
   default: return false;
   }
@@ -267,11 +268,13 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
                     (int)MXA_RANDOM_FUND_DIVERSE == (int)MXA_CFG_RANDOM_FUND_DIVERSE &&
                     (int)MXA_HIST_FUND_VALUE == (int)MXA_CFG_HIST_FUND_VALUE &&
                     (int)MXA_HIST_FUND_DIVERSE == (int)MXA_CFG_HIST_FUND_DIVERSE &&
-                    (int)MXA_MARKETREPLAY_RUNNER == (int)MXA_CFG_MARKETREPLAY_RUNNER,
+                    (int)MXA_MARKETREPLAY_RUNNER == (int)MXA_CFG_MARKETREPLAY_RUNNER &&
+                    (int)MXA_MARKETREPLAY_TWAP == (int)MXA_CFG_MARKETREPLAY_TWAP,
                 "config ids");
-  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_MARKETREPLAY_RUNNER + 1, "one entry per configuration");
+  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_MARKETREPLAY_TWAP + 1, "one entry per configuration");
   // replay handles: mxa_create_replay(_runner); ExternalFileOracle configurations: mxa_create_hist
-  if (config == MXA_MARKETREPLAY || config == MXA_MARKETREPLAY_RUNNER || config == MXA_HIST_FUND_VALUE ||
+  if (config == MXA_MARKETREPLAY || config == MXA_MARKETREPLAY_RUNNER || config == MXA_MARKETREPLAY_TWAP ||
+      config == MXA_HIST_FUND_VALUE ||
       config == MXA_HIST_FUND_DIVERSE || !bind(h, config)) {
     delete h;
     return MXA_EINVAL;
@@ -372,7 +375,7 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
 // Kernel.runner (cfg MXA_CFG_MARKETREPLAY_RUNNER); see include/mxa.h
 static int create_replay(int cfg, const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                          const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
-                         mxa_handle** out);
+                         mxa_handle** out, int32_t twap_trade = 0);
 int mxa_create_replay(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                       const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
                       mxa_handle** out) {
@@ -383,9 +386,15 @@ int mxa_create_replay_runner(const int64_t* t, const int64_t* oid, const int64_t
                              mxa_handle** out) {
   return create_replay(MXA_CFG_MARKETREPLAY_RUNNER, t, oid, price, size, buy, n_rec, n_envs, device, trace_cap, out);
 }
+int mxa_create_replay_twap(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                           const int8_t* buy, int32_t n_rec, int32_t trade, int32_t n_envs, int32_t device,
+                           int32_t trace_cap, mxa_handle** out) {
+  return create_replay(MXA_CFG_MARKETREPLAY_TWAP, t, oid, price, size, buy, n_rec, n_envs, device, trace_cap, out,
+                       trade != 0);
+}
 static int create_replay(int cfg, const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                          const int8_t* buy, int32_t n_rec, int32_t n_envs, int32_t device, int32_t trace_cap,
-                         mxa_handle** out) {
+                         mxa_handle** out, int32_t twap_trade) {
   if (!out || !t || !oid || !price || !size || !buy || n_rec <= 0 || n_envs <= 0 || trace_cap < 0) return MXA_EINVAL;
 #ifdef MXA_NO_GYM
   return MXA_EINVAL;
@@ -456,6 +465,7 @@ static int create_replay(int cfg, const int64_t* t, const int64_t* oid, const in
   h->ctx.L = mxa_cfg::replay_layout(mxa_cfg::env_stride(cfg, trace_cap), (int)pmin, (int)(pmax - pmin + 1), C,
                                     n_ids, (int)auto_cap + MXA_AUTO_SKIP + 1, ntm, n_rec);
   h->ctx.nuid = (int32_t)uf.size();
+  h->ctx.twap_trade = twap_trade;
   h->ctx.umin = uf.empty() ? INT32_MAX : uf[0].first;
   h->P.L.env_stride = h->ctx.L.end;
   // tape blob: t, oid, dense, price, size, buy, tm, tm0 (256-B aligned pieces)

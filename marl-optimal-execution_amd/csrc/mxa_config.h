@@ -331,6 +331,23 @@ constexpr void params_marketreplay_runner(MxaParams& P) {
   P.n_agents = 2;
 }
 
+// config/execution/marketreplay/execution_marketreplay.py:55-160: config/marketreplay.py's exchange
+// and MarketReplayAgent plus TWAP_EXECUTION_AGENT 2 (TWAPExecutionAgent: BUY 12e3 over
+// execution_time_horizon = pd.date_range(10:00, 12:00, "60S"), spread depth 500); whether it
+// trades (the script's -e flag) is a runtime choice (RpCtx::twap_trade)
+constexpr void params_marketreplay_twap(MxaParams& P) {
+  params_marketreplay_runner(P);
+  P.config = MXA_CFG_MARKETREPLAY_TWAP;
+  P.n_agents = 3;
+  P.first_twap = 2;
+  P.n_twap = 1;
+  P.rl_quantity = 12000;
+  P.rl_h0 = 10 * HOUR;
+  P.rl_hstep = 60 * NS;
+  P.rl_nh = 121;
+  P.rl_depth = 500;
+}
+
 // rmsc03 + DummyRL (BASELINE.json configs[3]; tests/golden/gen_rl_fixtures.py): rmsc03's 64
 // agents under a GymKernel with DummyRLExecutionAgent 64 (agent_config.py:115-137 parameters:
 // BUY 1e5, 30 s, order_level 2, spread depth 500), horizon pd.date_range(09:31, 09:44, "30S").
@@ -529,6 +546,7 @@ constexpr MxaParams params(int cfg) {
   else if (cfg == MXA_CFG_RMSC03_RL) params_rmsc03_rl(P);
   else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);
   else if (cfg == MXA_CFG_MARKETREPLAY_RUNNER) params_marketreplay_runner(P);
+  else if (cfg == MXA_CFG_MARKETREPLAY_TWAP) params_marketreplay_twap(P);
   else if (cfg == MXA_CFG_VALUE_NOISE) params_value_noise(P);
   else if (cfg == MXA_CFG_RMSC01) params_rmsc01(P);
   else if (cfg == MXA_CFG_RMSC02) params_rmsc02(P);

@@ -40,4 +40,5 @@ MxaEntry mxa_entry_10();
 MxaEntry mxa_entry_11();
 MxaEntry mxa_entry_12();
 MxaEntry mxa_entry_13();
-#define MXA_N_CONFIGS 14
+MxaEntry mxa_entry_14();
+#define MXA_N_CONFIGS 15

@@ -544,7 +544,8 @@ struct Eng {
   static constexpr int NG = QHIER ? SQ / QG : 1;
   static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
   // the replay book + tape (ABIDESEnv's composition, or config/marketreplay.py under Kernel.runner)
-  static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_MARKETREPLAY_RUNNER;
+  static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_MARKETREPLAY_RUNNER ||
+                             CFG == MXA_CFG_MARKETREPLAY_TWAP;
   static constexpr bool GYM = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL;  // a GymKernel with a DummyRL agent
   // ORDER_ACCEPTED to a background TradingAgent is a no-op (TradingAgent.orderAccepted only
   // logs, TradingAgent.py:409-420; no ZI/Noise/Value/POV-MM/Momentum branch reacts to it, and the
@@ -712,6 +713,7 @@ struct Eng {
   // HBL configurations: OrderBook.history restated as an order-history ring in HBM (one OhRec
   // per handled limit order); a resting order keeps its record index to flag its transactions
   static constexpr bool OH = PC.n_hbl > 0;
+  static constexpr bool TW = PC.n_twap > 0;  // a TWAPExecutionAgent (execution_marketreplay.py)
   // market-data subscription configs (rmsc02): the exchange publishes after book changes
   static constexpr bool MD = PC.md_sub != 0;
   static_assert(!MD || PW == 8, "MARKET_DATA carries its level counts and slot tag in w6 / w7");
@@ -2118,6 +2120,9 @@ struct Eng {
     if (type == AG_OBI) return PC.obi_wake;      // pd.Timedelta("1s") (OrderBookImbalanceAgent.py:187-188)
     if constexpr (RP) {
       if (type == AG_REPLAY) return U(rx->tm[0]) - PC.mkt_open;  // MarketReplayAgent.py:94-96
+      if constexpr (TW) {
+        if (type == AG_TWAP) return PC.rl_h0 - PC.mkt_open;  // ExecutionAgent.getWakeFrequency
+      }
     }
     if constexpr (GYM) {
       if (type == AG_DUMMYRL) return PC.rl_h0 - PC.mkt_open;     // execution_agent.py:129-130
@@ -3558,6 +3563,38 @@ struct Eng {
     if (U(R->rl_trade)) fail(ERR_RP_STOPPING);
   }
 
+  // ---------------- TWAPExecutionAgent (agent/execution/baselines/twap_agent.py:9-63) on the
+  // replay: ExecutionAgent.wakeup / receiveMessage / placeOrders (execution_agent.py:65-123).
+  // The horizon is pd.date_range(rl_h0, ..., rl_hstep) (rl_nh times); RpHdr::rl_trade = -e.
+  DEV void tw_wakeup() {
+    if (!ta_wakeup()) return;
+    if (!U(rh()->rl_trade)) return;
+    // [time for time in execution_time_horizon if time > currentTime][0] (IndexError: none)
+    const i32 k = cur < PC.rl_h0 ? 0 : (i32)((cur - PC.rl_h0) / PC.rl_hstep) + 1;
+    if (k < PC.rl_nh) wakeup_at(cur_agent, PC.rl_h0 + (i64)k * PC.rl_hstep);
+    get_spread(PC.rl_depth);
+    rs(AF_STATE, AS_AWAITING_SPREAD);
+  }
+  // The schedule is keyed by the 60 s bins of pd.interval_range(start, end, freq) (twap_agent.py:
+  // 50-55) and read with a 30 s Interval (execution_agent.py:118): the first limit order raises
+  // KeyError, so no TWAP order reaches the exchange (nothing executes, rem_quantity stays > 0)
+  DEV void tw_receive(const Msg& m) {
+    ta_receive(m, AG_TWAP);
+    if (rgi(AF_STATE) != AS_AWAITING_SPREAD || m_kind(m) != MK_SPREAD) return;
+    // cancelOrders(): self.orders is empty.  placeOrders(currentTime):
+    const i64 d = cur - PC.rl_h0;
+    if (d < 0 || d % PC.rl_hstep != 0 || d / PC.rl_hstep >= PC.rl_nh) return;  // not a horizon time
+    const i64 k = d / PC.rl_hstep;
+    if (k == PC.rl_nh - 2) {
+      fail(ERR_TWAP_MARKET);
+      return;
+    }
+    if (k < PC.rl_nh - 2) {
+      const u32 f = flags();
+      fail((f & FL_NB) && (f & FL_NA) ? ERR_TWAP_SCHEDULE : ERR_TWAP_QUOTE);
+    }
+  }
+
   // agent classes absent from the configuration are compiled out
   DEV void dispatch(int type, bool wake, const Msg& m) {
     if (wake) {
@@ -3579,6 +3616,9 @@ struct Eng {
         if (type == AG_OBI) return obi_wakeup();
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_wakeup();
+        if constexpr (TW) {
+          if (type == AG_TWAP) return tw_wakeup();
+        }
       }
       if constexpr (GYM) {
         if (type == AG_DUMMYRL) return rl_wakeup();
@@ -3604,6 +3644,9 @@ struct Eng {
         if (type == AG_OBI) return obi_receive(m);
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_receive(m);
+        if constexpr (TW) {
+          if (type == AG_TWAP) return tw_receive(m);
+        }
       }
       if constexpr (GYM) {
         if (type == AG_DUMMYRL) return rl_receive(m);
@@ -4375,6 +4418,11 @@ struct Builder : Eng<CFG, true> {
     if constexpr (E::PC.n_rl > 0) {
       rec_init(P.first_rl, AG_DUMMYRL);
       this->rec_store();
+    }
+    if constexpr (E::PC.n_twap > 0) {  // TWAP_EXECUTION_AGENT: trades only with -e
+      rec_init(P.first_twap, AG_TWAP);
+      this->rec_store();
+      R->rl_trade = U(this->rx->twap_trade);
     }
     this->h.last_trade = 0;
     this->h.last_trade_float = 0;

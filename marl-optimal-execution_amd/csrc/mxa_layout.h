@@ -21,7 +21,8 @@ enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPAR
                      MXA_CFG_RMSC03_RL = 4, MXA_CFG_VALUE_NOISE = 5, MXA_CFG_RMSC01 = 6,
                      MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8, MXA_CFG_RANDOM_FUND_VALUE = 9,
                      MXA_CFG_RANDOM_FUND_DIVERSE = 10, MXA_CFG_HIST_FUND_VALUE = 11,
-                     MXA_CFG_HIST_FUND_DIVERSE = 12, MXA_CFG_MARKETREPLAY_RUNNER = 13 };
+                     MXA_CFG_HIST_FUND_DIVERSE = 12, MXA_CFG_MARKETREPLAY_RUNNER = 13,
+                     MXA_CFG_MARKETREPLAY_TWAP = 14 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -37,7 +38,7 @@ enum { MT_MESSAGE = 1, MT_WAKEUP = 2, MT_CANCEL_ORDER = 3 };
 
 // agent classes
 enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_MOMENTUM = 5, AG_REPLAY = 6, AG_DUMMYRL = 7,
-       AG_MKTMAKER = 8, AG_HBL = 9, AG_OBI = 10 };
+       AG_MKTMAKER = 8, AG_HBL = 9, AG_OBI = 10, AG_TWAP = 11 };
 
 // env status flags (EnvHdr::status)
 enum { ST_RUNNING = 0, ST_DONE = 1, ST_ERROR = 2 };
@@ -62,7 +63,11 @@ enum {
   ERR_MD_NO_UPDATE = 21,  // a publish before the book's first change: None > Timestamp (TypeError)
   ERR_MD_SUBS = 22,       // more subscriptions than the device table (64)
   ERR_MD_KEYERROR = 23,   // cancelling a subscription that does not exist (KeyError)
-  ERR_MD_SLOT = 24        // a second MARKET_DATA in flight to one agent (freq below the latency)
+  ERR_MD_SLOT = 24,       // a second MARKET_DATA in flight to one agent (freq below the latency)
+  // TWAPExecutionAgent (ExecutionAgent.placeOrders, execution_agent.py:108-123)
+  ERR_TWAP_SCHEDULE = 25, // schedule[Interval(t, t + 30 s)] of a 60 s schedule (KeyError)
+  ERR_TWAP_QUOTE = 26,    // (bid + ask) / 2 with a None side (TypeError)
+  ERR_TWAP_MARKET = 27    // placeMarketOrder at horizon[-2] (not restated; unreachable in the script)
 };
 
 // per-env scalar header (first bytes of the env block)
@@ -235,7 +240,8 @@ typedef struct {  // device-resident tape (shared by all envs of a handle)
   // and values (the mid prices of util/formatting/mid_price_from_orderbook.py)
   const int64_t* fs_t;
   const double* fs_v;
-  int32_t fs_n, pad_fs;
+  int32_t fs_n;
+  int32_t twap_trade;   // execution_marketreplay.py -e: the TWAP agent trades
   RpLayout L;
 } RpCtx;
 
@@ -310,13 +316,13 @@ typedef struct {
   // marketreplay / ABIDESEnv composition (agent_config.py:30-160)
   int32_t first_replay, n_replay, first_rl, n_rl;
   int64_t rl_quantity, rl_h0, rl_hstep;   // DummyRL: BUY 1e5 over date_range(h0, ..., hstep)
-  int32_t rl_nh, rl_depth, rl_ids, pad3;  // horizon length, spread depth, agent-id capacity
+  int32_t rl_nh, rl_depth, rl_ids, n_twap;  // horizon length, spread depth, agent-id capacity; TWAP agents (the horizon is rl_*)
   // MarketMakerAgent (agent/market_makers/MarketMakerAgent.py, polling mode)
   int32_t first_mk, n_mk, mk_min, mk_max;
   int32_t mk_depth, pad4;
   int64_t mk_wake, mk_last_spread;
   // HeuristicBeliefLearningAgent (ZI parameters of group 0, plus L)
-  int32_t first_hbl, n_hbl, hbl_L, pad5;
+  int32_t first_hbl, n_hbl, hbl_L, first_twap;
   // market-data subscriptions (rmsc02: MarketMakerAgent / MomentumAgent subscribe=True)
   int32_t md_sub, md_mk_levels, md_mom_levels, lat_asym;  // lat_asym: latency row 0 + column 0
   int64_t md_freq;

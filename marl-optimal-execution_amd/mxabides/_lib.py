@@ -18,13 +18,16 @@ MXA_RANDOM_FUND_DIVERSE = 10
 MXA_HIST_FUND_VALUE = 11
 MXA_HIST_FUND_DIVERSE = 12
 MXA_MARKETREPLAY_RUNNER = 13
+MXA_MARKETREPLAY_TWAP = 14
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000,
               "value_noise": MXA_VALUE_NOISE, "rmsc01": MXA_RMSC01, "rmsc02": MXA_RMSC02,
               "obi_rmsc02": MXA_OBI_RMSC02, "random_fund_value": MXA_RANDOM_FUND_VALUE,
               "random_fund_diverse": MXA_RANDOM_FUND_DIVERSE, "hist_fund_value": MXA_HIST_FUND_VALUE,
               "hist_fund_diverse": MXA_HIST_FUND_DIVERSE,
               # config/marketreplay.py (Kernel.runner; ABIDESEnv's GymKernel replay is mxabides.gym)
-              "marketreplay_runner": MXA_MARKETREPLAY_RUNNER}
+              "marketreplay_runner": MXA_MARKETREPLAY_RUNNER,
+              # config/execution/marketreplay/execution_marketreplay.py (TWAP agent passive / -e)
+              "marketreplay_twap": MXA_MARKETREPLAY_TWAP, "marketreplay_twap_e": MXA_MARKETREPLAY_TWAP}
 ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
 ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",
              4: "transaction history capacity", 5: "get_transacted_volume without transactions (pandas error)",
@@ -40,7 +43,10 @@ ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: 
              21: "market data published before the book's first change (the reference's TypeError)",
              22: "more market-data subscriptions than the device table",
              23: "cancelled a market-data subscription that does not exist (KeyError)",
-             24: "two MARKET_DATA messages in flight to one agent (subscription freq below the latency)"}
+             24: "two MARKET_DATA messages in flight to one agent (subscription freq below the latency)",
+             25: "ExecutionAgent.placeOrders: schedule[Interval(t, t + 30 s)] of a 60 s TWAP schedule (KeyError)",
+             26: "ExecutionAgent.placeOrders: (bid + ask) / 2 with a None side (TypeError)",
+             27: "ExecutionAgent.placeOrders: placeMarketOrder at horizon[-2] (not restated)"}
 
 
 class EnvSummary(ctypes.Structure):
@@ -67,7 +73,7 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash",
            "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log", "mxa_write_records", "mxa_set_id_persistence",
            "mxa_read_counters", "mxa_create_hist", "mxa_create_replay_runner",
-           "mxa_set_stop_time", "mxa_run_until"]
+           "mxa_set_stop_time", "mxa_run_until", "mxa_create_replay_twap"]
 COUNTER_WORDS = 34  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
@@ -114,7 +120,8 @@ def load():
                        ("mxa_read_counters", [P, P]),
                        ("mxa_create_hist", [I32, I32, P, I32, I32, P, P, I32, ctypes.POINTER(P)]),
                        ("mxa_create_replay_runner", [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)]),
-                       ("mxa_set_stop_time", [P, I64]), ("mxa_run_until", [P, I64, P])):
+                       ("mxa_set_stop_time", [P, I64]), ("mxa_run_until", [P, I64, P]),
+                       ("mxa_create_replay_twap", [P, P, P, P, P, I32, I32, I32, I32, I32, ctypes.POINTER(P)])):
         if hasattr(L, name):  # (older single-configuration A/B builds lack them; libmxa.so has all)
             getattr(L, name).argtypes = args
     L.mxa_write_rl_state.argtypes = [P, P]

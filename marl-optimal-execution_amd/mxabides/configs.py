@@ -14,9 +14,11 @@ ZI_COUNTS = {"sparse_zi_100": [15, 15, 14, 14, 14, 14, 14], "sparse_zi_1000": [1
 # configs whose script takes the ticker from -t/--ticker (config/rmsc03.py:31, random_fund_*.py,
 # hist_fund_*.py); the default is the one the fixtures and the bench use
 TICKER_CONFIGS = ("rmsc03", "random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse",
-                  "marketreplay_runner")
+                  "marketreplay_runner", "marketreplay_twap", "marketreplay_twap_e")
 HIST_CONFIGS = ("hist_fund_value", "hist_fund_diverse")
-REPLAY_CONFIGS = ("marketreplay_runner",)  # config/marketreplay.py: a LOBSTER tape, no oracle
+# config/marketreplay.py (a LOBSTER tape, no oracle) and config/execution/marketreplay/
+# execution_marketreplay.py (the same plus TWAP_EXECUTION_AGENT; _e: its -e flag, the agent trades)
+REPLAY_CONFIGS = ("marketreplay_runner", "marketreplay_twap", "marketreplay_twap_e")
 
 
 def symbol_of(config, symbol=None):
@@ -36,12 +38,15 @@ def symbol_of(config, symbol=None):
 # (ExchangeAgent.py:389-469; value_noise / sparse_zi_* take -b, default None)
 BOOK_FREQ = {"rmsc03": 0, "rmsc02": 0, "rmsc01": "M", "obi_rmsc02": "all", "random_fund_value": None,
              "random_fund_diverse": None, "hist_fund_value": None, "hist_fund_diverse": None, "value_noise": None,
-             "sparse_zi_100": None, "sparse_zi_1000": None, "marketreplay_runner": 0}
+             "sparse_zi_100": None, "sparse_zi_1000": None, "marketreplay_runner": 0,
+             "marketreplay_twap": 0, "marketreplay_twap_e": 0}
 
 
 def agent_names(config):
     if config == "marketreplay_runner":  # config/marketreplay.py:66-110
         return ["EXCHANGE_AGENT", "MARKET_REPLAY_AGENT"]
+    if config in ("marketreplay_twap", "marketreplay_twap_e"):  # execution_marketreplay.py:66-140
+        return ["EXCHANGE_AGENT", "MARKET_REPLAY_AGENT", "TWAP_EXECUTION_AGENT"]
     if config == "obi_rmsc02":
         return (["EXCHANGE_AGENT", "MARKET_MAKER_AGENT_1"] + ["ZI_AGENT_%d" % j for j in range(2, 91)] +
                 ["OBI_AGENT_%d" % j for j in range(91, 96)] + ["MOMENTUM_AGENT_%d" % j for j in range(96, 101)])
@@ -71,6 +76,8 @@ def agent_names(config):
 def agent_type_names(config):
     if config == "marketreplay_runner":
         return ["ExchangeAgent", "MarketReplayAgent"]
+    if config in ("marketreplay_twap", "marketreplay_twap_e"):
+        return ["ExchangeAgent", "MarketReplayAgent", "ExecutionAgent"]
     if config == "obi_rmsc02":
         return (["ExchangeAgent", "MarketMakerAgent"] + ["ZeroIntelligenceAgent"] * 89 +
                 ["OrderBookImbalanceAgent"] * 5 + ["MomentumAgent"] * 5)

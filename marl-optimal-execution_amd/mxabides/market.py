@@ -43,10 +43,14 @@ class VecMarket:
             if tape is None:
                 raise ValueError("%s replays a LOBSTER tape (tape=mxabides.tape.Tape)" % config)
             self.tape = tape
-            rc = self.L.mxa_create_replay_runner(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
-                                                 tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), self.n_envs,
-                                                 device, trace_cap, ctypes.byref(self._h))
-            self._check(rc, "mxa_create_replay_runner")
+            tp = (tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data, tape.size.ctypes.data,
+                  tape.buy.ctypes.data, len(tape))
+            if config == "marketreplay_runner":
+                rc = self.L.mxa_create_replay_runner(*tp, self.n_envs, device, trace_cap, ctypes.byref(self._h))
+            else:
+                rc = self.L.mxa_create_replay_twap(*tp, 1 if config == "marketreplay_twap_e" else 0, self.n_envs,
+                                                   device, trace_cap, ctypes.byref(self._h))
+            self._check(rc, "mxa_create_replay_%s" % config.split("_", 1)[1])
         elif config in HIST_CONFIGS:
             if fundamental is None:
                 raise ValueError("%s needs its ExternalFileOracle series (fundamental=FundamentalSeries)" % config)

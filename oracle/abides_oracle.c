@@ -206,7 +206,8 @@ typedef struct {
 /* ------------------------------------------------------------------------- */
 /* agents                                                                     */
 /* ------------------------------------------------------------------------- */
-enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL, AG_MKTMAKER, AG_HBL, AG_OBI };
+enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL, AG_MKTMAKER, AG_HBL, AG_OBI,
+       AG_TWAP };
 enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE, ST_AWAITING_STREAM, ST_AWAITING_MARKET_DATA };
 
 typedef struct {
@@ -1302,6 +1303,7 @@ static int64_t wake_frequency(agent_t* a) {
     case AG_OBI: return NS_SEC;           /* pd.Timedelta("1s") (OrderBookImbalanceAgent.py:187-188) */
     case AG_REPLAY: return a->wake_freq;  /* first tape time - mkt_open (MarketReplayAgent.py:94-96) */
     case AG_DUMMYRL: return a->wake_freq; /* horizon[0] - mkt_open (execution_agent.py:129-130) */
+    case AG_TWAP: return a->wake_freq;    /* the same ExecutionAgent.getWakeFrequency */
     default: return rs_randint(&a->rs, 0, 100);
     }
 }
@@ -1993,6 +1995,44 @@ static void rl_wakeup(ora_env* e, agent_t* a) {
     get_spread(e, a, 500);
     a->state = ST_AWAITING_SPREAD;
 }
+/* TWAPExecutionAgent (agent/execution/baselines/twap_agent.py:9-63) runs ExecutionAgent.wakeup
+ * (execution_agent.py:65-76): the next horizon time strictly after now (IndexError: no wakeup),
+ * then QUERY_SPREAD at depth 500 */
+static void tw_wakeup(ora_env* e, agent_t* a) {
+    if (!ta_wakeup(e, a)) return;
+    if (!e->rl_trade) return;
+    for (int i = 0; i < e->nhz; i++)
+        if (e->hz[i] > e->cur) {
+            k_wakeup(e, a->id, e->hz[i]);
+            break;
+        }
+    get_spread(e, a, 500);
+    a->state = ST_AWAITING_SPREAD;
+}
+/* ExecutionAgent.receiveMessage / placeOrders (execution_agent.py:78-123).  The schedule is keyed
+ * by the 60 s intervals of pd.interval_range(start, end, freq) (twap_agent.py:50-55) and looked up
+ * with a 30 s interval (execution_agent.py:118): the first limit order raises KeyError, so no
+ * TWAP order ever reaches the exchange and ORDER_EXECUTED / ORDER_ACCEPTED never arrive. */
+static void tw_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    if (e->rl_rem > 0 && a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        /* cancelOrders(): self.orders is empty; placeOrders(currentTime) */
+        int k = -1;
+        for (int i = 0; i < e->nhz; i++)
+            if (e->hz[i] == e->cur) { k = i; break; }
+        if (k >= 0 && k == e->nhz - 2) {
+            fail(e, -19, "ExecutionAgent.placeOrders: placeMarketOrder at horizon[-2] (not restated)");
+            return;
+        }
+        if (k >= 0 && k < e->nhz - 2) {
+            if (!a->nb || !a->na) {
+                fail(e, -18, "ExecutionAgent.placeOrders: (bid + ask) / 2 with a None side (TypeError)");
+                return;
+            }
+            fail(e, -17, "ExecutionAgent.placeOrders: schedule[Interval(t, t + 30 s)] (KeyError)");
+        }
+    }
+}
 /* ABIDESEnvMetrics.addLOB (ABIDESEnvMetrics.py:68-94): deque(maxlen=100), newest first */
 static void metrics_add(ora_env* e, const msg_t* m) {
     if (e->ph_n == 0) {
@@ -2140,6 +2180,7 @@ static void dispatch_wakeup(ora_env* e, int id) {
     case AG_MOMENTUM: mom_wakeup(e, a); break;
     case AG_REPLAY: mr_wakeup(e, a); break;
     case AG_DUMMYRL: rl_wakeup(e, a); break;
+    case AG_TWAP: tw_wakeup(e, a); break;
     case AG_MKTMAKER: mk_wakeup(e, a); break;
     case AG_HBL: hbl_wakeup(e, a); break;
     case AG_OBI: obi_wakeup(e, a); break;
@@ -2158,6 +2199,7 @@ static void dispatch_message(ora_env* e, int id, const msg_t* m) {
     case AG_POVMM: mm_receive(e, a, m); break;
     case AG_MOMENTUM: mom_receive(e, a, m); break;
     case AG_REPLAY: mr_receive(e, a, m); break;
+    case AG_TWAP: tw_receive(e, a, m); break;
     case AG_DUMMYRL:
         rl_receive(e, a, m);
         if (m->kind == K_SPREAD) { /* GymKernel: the step ends at the RL agent's spread reply */
@@ -2825,12 +2867,14 @@ static int build_rmsc03_rl(ora_env* e, uint32_t seed) {
  * Nothing in this composition draws from an RNG. */
 /* runner 0: ABIDESEnv's composition (agent_config.py: Exchange, MarketReplayAgent, DummyRL under
  * a GymKernel); runner 1: config/marketreplay.py (Exchange and MarketReplayAgent under
- * Kernel.runner, midnight to 16:01, agents named as that script names them) */
+ * Kernel.runner, midnight to 16:01, agents named as that script names them); runner 2 / 3:
+ * config/execution/marketreplay/execution_marketreplay.py, the same plus TWAP_EXECUTION_AGENT 2
+ * (BUY 12e3 over pd.date_range(10:00, 12:00, "60S"); 3: -e, the agent trades) */
 static int create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                      const int8_t* buy, int n, int runner, ora_env** out) {
     if (n <= 0) return -1;
     ora_env* e = (ora_env*)calloc(1, sizeof(ora_env));
-    snprintf(e->config, sizeof e->config, runner ? "marketreplay_runner" : "marketreplay");
+    snprintf(e->config, sizeof e->config, runner >= 2 ? "marketreplay_twap" : runner ? "marketreplay_runner" : "marketreplay");
     int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
     agent_t* x = add_agent(e, AG_EXCHANGE);
     snprintf(x->name, sizeof x->name, runner ? "EXCHANGE_AGENT" : "0_EXCHANGE_AGENT");
@@ -2849,6 +2893,11 @@ static int create_mr(const int64_t* t, const int64_t* oid, const int64_t* price,
         r = add_agent(e, AG_DUMMYRL);
         trading_init(r, 0);
         snprintf(r->name, sizeof r->name, "2_DUMMY_RL_EXECUTION_AGENT");
+    } else if (runner >= 2) {
+        r = add_agent(e, AG_TWAP);
+        trading_init(r, 0);
+        snprintf(r->name, sizeof r->name, "TWAP_EXECUTION_AGENT");
+        snprintf(r->tname, sizeof r->tname, "ExecutionAgent");
     }
     e->tp_n = n;
     e->tp_t = (int64_t*)malloc(sizeof(int64_t) * n);
@@ -2890,6 +2939,15 @@ static int create_mr(const int64_t* t, const int64_t* oid, const int64_t* price,
         e->rl_trade = 1;
         e->rl_id = 2;
         e->gym = 1;
+    } else if (runner >= 2) {
+        r = &e->ag[2];
+        e->nhz = 121; /* pd.date_range(10:00, 12:00, freq="60S") */
+        e->hz = (int64_t*)malloc(sizeof(int64_t) * e->nhz);
+        for (int i = 0; i < e->nhz; i++) e->hz[i] = 10 * NS_HOUR + (int64_t)i * 60 * NS_SEC;
+        r->wake_freq = e->hz[0] - open;
+        e->rl_quantity = 12000;
+        e->rl_rem = 12000;
+        e->rl_trade = runner == 3;
     }
     e->start = 0;
     e->stop = runner ? 16 * NS_HOUR + NS_MIN : 16 * NS_HOUR + 10 * NS_MIN;
@@ -2916,6 +2974,10 @@ void ora_set_stop(ora_env* e, int64_t t_stop) { e->stop = t_stop; }
 int ora_create_mr_runner(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                          const int8_t* buy, int n, ora_env** out) {
     return create_mr(t, oid, price, size, buy, n, 1, out);
+}
+int ora_create_mr_twap(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                       const int8_t* buy, int n, int trade, ora_env** out) {
+    return create_mr(t, oid, price, size, buy, n, trade ? 3 : 2, out);
 }
 int ora_rl_state(const ora_env* e, int64_t* out4) {
     out4[0] = e->rl_rem;

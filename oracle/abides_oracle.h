@@ -87,6 +87,10 @@ int ora_create_mr(const int64_t* t, const int64_t* oid, const int64_t* price, co
 /* config/marketreplay.py: the exchange and the MarketReplayAgent under Kernel.runner (ora_run) */
 void ora_set_symbol(ora_env* e, const char* sym);
 void ora_set_stop(ora_env* e, int64_t t_stop);
+/* config/execution/marketreplay/execution_marketreplay.py: the replay of ora_create_mr_runner plus
+ * TWAPExecutionAgent 2; trade = the script's -e flag */
+int ora_create_mr_twap(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
+                       const int8_t* buy, int n, int trade, ora_env** out);
 int ora_create_mr_runner(const int64_t* t, const int64_t* oid, const int64_t* price, const int64_t* size,
                          const int8_t* buy, int n, ora_env** out);
 /* ABIDESEnv.step(action[3]): obs_out[9] (valid when *has_obs), *done; returns 0 or an error */

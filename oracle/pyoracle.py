@@ -321,14 +321,21 @@ class OracleReplayRunner(OracleEnv):
     """config/marketreplay.py: the exchange and the MarketReplayAgent on a tape under Kernel.runner
     (run / finish / report / summary_log / book / agents as OracleEnv)"""
 
-    def __init__(self, tape, symbol="IBM", trace_cap=0):
+    def __init__(self, tape, symbol="IBM", trace_cap=0, twap=None):
+        """twap: None = config/marketreplay.py; False / True = config/execution/marketreplay/
+        execution_marketreplay.py without / with -e (the TWAP execution agent trades)"""
         L = lib()
         L.ora_create_mr_runner.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.ora_create_mr_twap.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.ora_set_symbol.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         self._h = ctypes.c_void_p()
         self._tape = tape
-        rc = L.ora_create_mr_runner(tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data,
-                                    tape.size.ctypes.data, tape.buy.ctypes.data, len(tape), ctypes.byref(self._h))
+        args = (tape.t.ctypes.data, tape.oid.ctypes.data, tape.price.ctypes.data, tape.size.ctypes.data,
+                tape.buy.ctypes.data, len(tape))
+        if twap is None:
+            rc = L.ora_create_mr_runner(*args, ctypes.byref(self._h))
+        else:
+            rc = L.ora_create_mr_twap(*args, 1 if twap else 0, ctypes.byref(self._h))
         if rc:
             raise ValueError("oracle: bad tape (%d)" % rc)
         L.ora_set_symbol(self._h, symbol.encode())

@@ -278,6 +278,12 @@ def run_config(cfg, seed, out, full):
             return orig_runner(self, *a, **k)
         K.Kernel.runner = runner
     replay = None
+    twap = None
+    if cfg.startswith(("twap:", "twap_e:")):
+        # config/execution/marketreplay/execution_marketreplay.py TICKER DATE: the replay plus a
+        # TWAPExecutionAgent; twap_e adds -e (execution_agents: the agent trades)
+        twap = cfg.startswith("twap_e:")
+        cfg = "marketreplay:" + cfg.split(":", 1)[1]
     if cfg.startswith("marketreplay:"):  # config/marketreplay.py TICKER DATE (Kernel.runner replay)
         _, ticker, rdate = cfg.split(":")
         replay = (ticker, rdate)
@@ -303,6 +309,12 @@ def run_config(cfg, seed, out, full):
         argv += ["-t", "ABM", "-d", "20190628"]
     if replay:
         argv += ["-t", replay[0], "-d", replay[1]]
+    module = "config." + cfg
+    if twap is not None:
+        module = "config.execution.marketreplay.execution_marketreplay"
+        argv[2] = "execution_marketreplay"
+        if twap:
+            argv.append("-e")
     if cfg in ("hist_fund_value", "hist_fund_diverse"):  # ExternalFileOracle on the JPM mid-price series
         fp = os.path.abspath("fund_JPM_20190628.pkl")
         write_fund_files(fp)
@@ -313,7 +325,7 @@ def run_config(cfg, seed, out, full):
     sys.stdout = buf
     stop_error = None
     try:
-        importlib.import_module("config." + cfg)
+        importlib.import_module(module)
     except Exception as ex:  # e.g. ZeroIntelligenceAgent.kernelStopping's IndexError (rmsc01)
         if "kernel" not in CAPTURE:
             raise
@@ -552,7 +564,11 @@ def main():
             ("marketreplay:IBM:2003-01-14", 1, False), ("marketreplay:GOOG:2012-06-21", 1, False),
             # Kernel.runner with a caller's stopTime (the scripts' own kernelStopTime replaced)
             ("rmsc03@11:00:00", 123456789, True), ("value_noise@10:15:00", 7, True),
-            ("sparse_zi_100@09:45:30", 123456789, True)]
+            ("sparse_zi_100@09:45:30", 123456789, True),
+            # config/execution/marketreplay/execution_marketreplay.py: the replay plus the TWAP
+            # execution agent, passive (no -e) and trading (-e)
+            ("twap:IBM:2003-01-14", 1, False), ("twap_e:IBM:2003-01-14", 1, True),
+            ("twap:GOOG:2012-06-21", 1, False), ("twap_e:GOOG:2012-06-21", 1, True)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2] or j[0].startswith(sys.argv[2] + ":")]
     procs = []

@@ -16,8 +16,13 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 REPLAY_FIXTURES = [("IBM", "2003-01-14"), ("GOOG", "2012-06-21")]
 
 
-def load_replay(ticker, date):
-    name = "marketreplay_%s_%s_1" % (ticker, date)
+TWAP_FIXTURES = [(t, d, trade) for t, d in REPLAY_FIXTURES for trade in (False, True)]
+# oracle fail() codes of the TWAP agent's crash path (ExecutionAgent.placeOrders KeyError)
+TWAP_KEYERROR = -17
+
+
+def load_replay(ticker, date, prefix="marketreplay"):
+    name = "%s_%s_%s_1" % (prefix, ticker, date)
     with open(os.path.join(GOLD, name + ".json")) as f:
         d = json.load(f)
     with open(os.path.join(GOLD, name + "_summary.json")) as f:
@@ -43,6 +48,37 @@ def test_oracle_replay_runner_matches_reference(ticker, date):
     assert max(e.order_counter - 1, 0) == d["order_id_counter"]
     (ag,) = d["agents"]
     assert e.agents()[ag["id"]] == (ag["cash"], ag["shares"], len(ag["open_orders"]))
+    e.finish()
+    rep = e.report()
+    assert [l for l in rep if l.startswith("Final holdings")] == d["final_holdings_lines"]
+    assert [l for l in rep if not l.startswith("Final holdings")] == d["mean_lines"]
+    got = e.summary_log()
+    assert got == summ and all(type(a["Event"]) is type(b["Event"]) for a, b in zip(got, summ))
+
+
+@pytest.mark.parametrize("ticker,date,trade", TWAP_FIXTURES)
+def test_oracle_twap_execution_matches_reference(ticker, date, trade):
+    """config/execution/marketreplay/execution_marketreplay.py: the replay plus TWAP_EXECUTION_AGENT.
+    Without -e it only learns the market hours and wakes at 10:00; with -e its first placeOrders
+    raises KeyError (a 30 s Interval looked up in the 60 s schedule, execution_agent.py:118,
+    twap_agent.py:50-55) and the reference run ends there"""
+    d, summ, trace, tp = load_replay(ticker, date, "twap_e" if trade else "twap")
+    e = pyoracle.OracleReplayRunner(tp, symbol=ticker, trace_cap=len(trace), twap=trade)
+    e.run()
+    assert (e.trace() == trace).all()
+    assert e.events == d["events"] and "%016x" % e.hash == d["hash"]
+    assert e.book(0) == d["bids"] and e.book(1) == d["asks"]
+    assert max(e.order_counter - 1, 0) == d["order_id_counter"]
+    for ag in d["agents"]:
+        assert e.agents()[ag["id"]] == (ag["cash"], ag["shares"], len(ag["open_orders"]))
+    if trade:
+        assert d["stop_error"].startswith("KeyError: Interval(") and e.error[0] == TWAP_KEYERROR
+        assert d["final_time"] == 10 * 3600 * 10 ** 9
+        # kernelStarting's rows only: the crash skips kernelStopping
+        assert summ == [{"AgentID": a, "AgentStrategy": t, "EventType": "STARTING_CASH", "Event": 0}
+                        for a, t in ((1, "MarketReplayAgent"), (2, "ExecutionAgent"))]
+        return
+    assert e.error[0] == 0 and d["stop_error"] is None
     e.finish()
     rep = e.report()
     assert [l for l in rep if l.startswith("Final holdings")] == d["final_holdings_lines"]
