@@ -38,7 +38,11 @@ typedef int64_t i64;
 typedef uint32_t u32;
 typedef int32_t i32;
 
+#ifdef MXA_DEV_NOINLINE  // diagnostics build: every engine helper a real call
+#define DEV __device__ __attribute__((noinline))
+#else
 #define DEV __device__ __forceinline__
+#endif
 #define FNV_OFF 0xCBF29CE484222325ull
 #define FNV_PRIME 0x100000001B3ull
 #define KEY_EMPTY 0xFFFFFFFFFFFFFFFFull
