@@ -534,7 +534,7 @@ def main():
                 bpe, bparts, bunits = mc.bytes_per_event(eng.count(args.warmup))
             achieved = bpe * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
             traffic, tsrc = (traffic_record(args.config, eng.n, bool(args.parity_hash))
-                             if isinstance(eng, MarketEngine) else (None, {"why": "no PMC record for this config"}))
+                             if isinstance(eng, (MarketEngine, GymEngine)) else (None, {"why": "no PMC record for this config"}))
             out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_record": tsrc,
                                "kernel": eng.kernel, "avg_launch_ms": avg_ms, "launches": eng.launches,

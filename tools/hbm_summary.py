@@ -37,7 +37,8 @@ def pmc(sub, name):
 
 fetch, fc = pmc("fetch", "FETCH_SIZE")
 write, _ = pmc("write", "WRITE_SIZE")
-run = [k for k in fetch if "mxa_run_kernel" in k]
+# the dominant kernel: the run kernel (Kernel.runner configs) or the step kernel (GymKernel ones)
+run = [k for k in fetch if "mxa_run_kernel" in k or "mxa_step_kernel" in k]
 res = {}
 for k in run:
     n = len({d for (kk, d) in fc if kk == k}) or 1
@@ -57,7 +58,7 @@ if "--record" in sys.argv:
     source = " ".join(sys.argv[i + 4:])
     sys.path.insert(0, os.path.join(ROOT, "marl-optimal-execution_amd"))
     import mxabides
-    assert len(res) == 1, "expected exactly one run-kernel instantiation, got %s" % list(res)
+    assert len(res) == 1, "expected exactly one run- or step-kernel instantiation, got %s" % list(res)
     (k, r), = res.items()
     rec = {"config": cfg, "envs": envs, "kernel": k, "build_id": mxabides.build_id(), "parity_hash": ph}
     rec.update({x: r[x] for x in ("bytes_per_launch", "read_bytes_corrected", "write_bytes", "fetch_size_kib",
