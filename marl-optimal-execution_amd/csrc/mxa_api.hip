@@ -613,6 +613,7 @@ int mxa_set_id_persistence(mxa_handle* h, int32_t on) {
 
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
   if (!h || h->gym) return MXA_EINVAL;  // GymKernel handles advance by mxa_step
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   h->run_kernel()(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
          h->d_ctx, h->d_blog, h->blog_cap);
   HIPCHK(h, hipGetLastError());
@@ -621,6 +622,7 @@ int mxa_launch(mxa_handle* h, int64_t max_pops) {
 
 int mxa_sync(mxa_handle* h) {
   if (!h) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;
 }
@@ -713,6 +715,7 @@ int mxa_finalize(mxa_handle* h) {
 
 int mxa_read_final(mxa_handle* h, int32_t env, mxa_agent_final* out, int32_t cap) {
   if (!h || !h->d_final || env < 0 || env >= h->P.n_envs || !out || cap < h->P.n_agents) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   HIPCHK(h, hipMemcpyAsync(out, h->d_final + (size_t)env * h->P.n_agents, sizeof(mxa_agent_final) * h->P.n_agents,
                            hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -721,6 +724,7 @@ int mxa_read_final(mxa_handle* h, int32_t env, mxa_agent_final* out, int32_t cap
 
 int mxa_read_summary(mxa_handle* h, mxa_env_summary* out) {
   if (!h || !out) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   int n = h->P.n_envs;
   std::vector<EnvHdr> hd(n);
   HIPCHK(h, hipMemcpy2DAsync(hd.data(), sizeof(EnvHdr), h->d_env, h->P.L.env_stride, sizeof(EnvHdr), n,
@@ -742,6 +746,7 @@ int mxa_read_summary(mxa_handle* h, mxa_env_summary* out) {
 
 int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t cap) {
   if (!h || env < 0 || env >= h->P.n_envs) return MXA_ERANGE;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   int n = std::min(cap, h->P.n_agents);
   std::vector<uint32_t> rec((size_t)h->P.n_agents * 128);
   HIPCHK(h, hipMemcpy(rec.data(), h->d_env + (size_t)env * h->P.L.env_stride + h->P.L.off_ag, rec.size() * 4,
@@ -770,6 +775,7 @@ int mxa_read_agents(mxa_handle* h, int32_t env, mxa_agent_state* out, int32_t ca
 
 int mxa_read_book(mxa_handle* h, int32_t env, int32_t side, int64_t* out4, int32_t cap) {
   if (!h || env < 0 || env >= h->P.n_envs) return MXA_ERANGE;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   if (h->replay) {  // price ladder: levels best-first, FIFO lists
     const RpLayout& L = h->ctx.L;
     char* e = h->d_env + (size_t)env * h->P.L.env_stride;
@@ -817,6 +823,7 @@ int mxa_read_book(mxa_handle* h, int32_t env, int32_t side, int64_t* out4, int32
 
 int mxa_read_trace(mxa_handle* h, int32_t env, int64_t* out, int64_t cap, int64_t* nout) {
   if (!h || env < 0 || env >= h->P.n_envs) return MXA_ERANGE;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   EnvHdr hd;
   char* e = h->d_env + (size_t)env * h->P.L.env_stride;
   HIPCHK(h, hipMemcpy(&hd, e, sizeof hd, hipMemcpyDeviceToHost));
@@ -828,6 +835,7 @@ int mxa_read_trace(mxa_handle* h, int32_t env, int64_t* out, int64_t cap, int64_
 
 int mxa_set_seeds(mxa_handle* h, const uint32_t* seeds) {
   if (!h || !seeds) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   HIPCHK(h, hipMemcpyAsync(h->d_seeds, seeds, sizeof(uint32_t) * h->P.n_envs, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return MXA_OK;
@@ -835,6 +843,7 @@ int mxa_set_seeds(mxa_handle* h, const uint32_t* seeds) {
 
 int mxa_write_results(mxa_handle* h, void* device_out) {
   if (!h || !device_out) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   int n = h->P.n_envs;
   hipLaunchKernelGGL(mxa_results_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env, h->P.L.env_stride,
                      n, (int64_t*)device_out);
@@ -888,6 +897,7 @@ int mxa_write_rl_state(mxa_handle* h, double* device_out) {
 int mxa_read_raw(mxa_handle* h, int32_t env, int64_t offset, int64_t bytes, void* out) {
   if (!h || env < 0 || env >= h->P.n_envs || offset < 0 || bytes < 0 || offset + bytes > (int64_t)h->P.L.env_stride)
     return MXA_ERANGE;
+  HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipMemcpy(out, h->d_env + (size_t)env * h->P.L.env_stride + offset, bytes, hipMemcpyDeviceToHost));
   return MXA_OK;
