@@ -28,6 +28,7 @@ struct Shape {
   int sql = 0;  // queue slots per lane in LDS (0: all sq); the rest are an HBM tier (far events)
 };
 constexpr int sq_lds(int cfg);
+constexpr int lat_lds(int cfg);
 #ifndef MXA_RMSC03_WAVES
 #define MXA_RMSC03_WAVES 4
 #endif
@@ -40,6 +41,15 @@ constexpr int sq_lds(int cfg);
 #endif
 #ifndef MXA_SO_RMSC02
 #define MXA_SO_RMSC02 8
+#endif
+#ifndef MXA_SQ_Z1K
+#define MXA_SQ_Z1K 36  // sparse_zi_1000 queue slots per lane (2,304; the oracle's maximum over the bench seeds is
+                       // 2,004 pending events); r03 s22 run kernel: 48 slots 821 ms, 36 slots 796
+#endif
+// configurations whose exchange latency row (the only row Kernel.sendMessage reads with a
+// symmetric matrix) is copied to LDS for each launch (bit = config id)
+#ifndef MXA_LAT_LDS_MASK
+#define MXA_LAT_LDS_MASK (1 << MXA_CFG_SPARSE_ZI_1000)  // r03 s22: 796 -> 784 ms (8 KB row, room from the 36-slot queue)
 #endif
 #ifndef MXA_SO_Z1K
 #define MXA_SO_Z1K 13  // sparse_zi_1000 book slots per lane (832; oracle max 734 resting orders over the 4,096 bench seeds); r03 s9 run kernel: 16 slots 1004 ms, 14 952, 13 925
@@ -101,7 +111,7 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 3, true, MXA_W_OBI, 8, 0}
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, MXA_W_Z1, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, MXA_W_VN, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
-       : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{48, MXA_SO_Z1K, false, 1, 6, MXA_HOT_RECORDS}
+       : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{MXA_SQ_Z1K, MXA_SO_Z1K, false, 1, 6, MXA_HOT_RECORDS}
        // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
        // maximum over the 8,192 bench seeds is 5,125 events), payload in HBM; 320 book slots (max 279)
        // the first MXA_RFV_SQL slots per lane (24: 1,536) in LDS for events due within a second,
@@ -118,6 +128,7 @@ constexpr size_t lds_bytes(int cfg) {
   return (size_t)sq_lds(cfg) * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
          + 1024                                                                               // RNG stream windows
+         + (size_t)lat_lds(cfg) * 8                                                           // exchange latency row
 #ifdef MXA_QREG
          + 768  // batched-push scratch: slot table + staged keys
 #else
@@ -558,6 +569,11 @@ constexpr MxaParams params(int cfg) {
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
   layout(P, cfg);
   return P;
+}
+// doubles of the latency row held in LDS (MXA_LAT_LDS_MASK): the exchange's row of a symmetric
+// matrix (lat_mode 1 without lat_asym), else none
+constexpr int lat_lds(int cfg) {
+  return (((MXA_LAT_LDS_MASK) >> cfg) & 1) && params(cfg).lat_mode == 1 && !params(cfg).lat_asym ? (int)params(cfg).L.lat_len : 0;
 }
 
 // runtime stride of one env block with `trace_cap` trace records

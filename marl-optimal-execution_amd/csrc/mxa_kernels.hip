@@ -546,6 +546,15 @@ struct Eng {
   static_assert(!QHIER || SQ % QG == 0, "queue groups must tile the lane's slots (MXA_QG)");
 #endif
   static constexpr int NG = QHIER ? SQ / QG : 1;
+  // group rescans as one batch of loads and a select tree (q_scan): groups of 4 and more slots.
+  // r03 s20, same per-env results: sparse_zi_1000 916 -> 826 ms, random_fund_value 778 -> 575,
+  // sparse_zi_100 132.5 -> 125.7, value_noise 22.0 -> 21.2; rmsc02 (groups of 3) 1053 -> 1086, so
+  // it keeps the serial scan
+#ifdef MXA_SERIAL_QSCAN
+  static constexpr bool QTREE = false;
+#else
+  static constexpr bool QTREE = QHIER && QG >= 4;
+#endif
   static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
   // the replay book + tape (ABIDESEnv's composition, or config/marketreplay.py under Kernel.runner)
   static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_MARKETREPLAY_RUNNER ||
@@ -743,6 +752,10 @@ struct Eng {
   LDSP u64* prof;
 #endif
   LDSP u64* hotrec;  // [HOT][64]: the exchange's (and the market maker's) agent record
+  // the exchange's latency row in LDS for the launch (MXA_LAT_LDS_MASK): every send reads one
+  // entry, which from HBM is a dependent memory round trip on the event chain
+  static constexpr int LATL = BUILD ? 0 : mxa_cfg::lat_lds(CFG);
+  LDSP double* latl;
   LDSP i32* scr;     // [64] rank -> queue slot, then [64] u64 staged keys (MXA_QREG)
   LDSP u32* rwin;    // [4][64] output windows of the global RNG streams (RSt::lw)
 
@@ -780,6 +793,7 @@ struct Eng {
 #else
     hotrec = (LDSP u64*)(lds + LDS_Q + 512);
 #endif
+    latl = (LDSP double*)(hotrec + mxa_cfg::shape(CFG).hot * 64);
   }
 
   // ---------------- env block accessors
@@ -940,8 +954,50 @@ struct Eng {
   }
 
   // ---------------- event queue
+  // (k, s, j) = lexicographic min of itself and (k2, s2, j2): lane selects, no branch
+  static DEV void q_min2(u64& k, u32& s, i32& j, u64 k2, u32 s2, i32 j2) {
+    const bool lt = (k2 < k) | ((k2 == k) & (s2 < s));
+    k = lt ? k2 : k;
+    s = lt ? s2 : s;
+    j = lt ? j2 : j;
+  }
   // min (key, seq, slot) over this lane's slots [j0, j0 + n)
   DEV void q_scan(int j0, int n, u64& bk, u32& bs, i32& bj) {
+    if constexpr (QTREE) {
+      // every load of the group first, then a pairwise tree of selects: one memory latency per
+      // rescan instead of QG dependent load -> compare -> branch steps (the serial scan was
+      // 21 % of sparse_zi_1000's cycles, r03 s8).  Ties (only empty slots) keep the lower slot,
+      // as the serial scan does; an all-empty group still reports j = -1.
+      u64 k[QG];
+      u32 s[QG];
+      i32 j[QG];
+      if (TIER && j0 >= SQL) {
+        const GLBP u64* K = hqk() + (j0 - SQL) * 64 + lane;
+        const GLBP u32* S = hqs() + (j0 - SQL) * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < QG; i++) {
+          k[i] = K[i * 64];
+          s[i] = S[i * 64];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < QG; i++) {
+          k[i] = qk[(j0 + i) * 64 + lane];
+          s[i] = qs[(j0 + i) * 64 + lane];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < QG; i++) j[i] = j0 + i;
+#pragma unroll
+      for (int w = 1; w < QG; w *= 2) {
+#pragma unroll
+        for (int i = 0; i + w < QG; i += 2 * w) q_min2(k[i], s[i], j[i], k[i + w], s[i + w], j[i + w]);
+      }
+      bk = k[0];
+      bs = s[0];
+      bj = (k[0] == KEY_EMPTY && s[0] == 0xFFFFFFFFu) ? -1 : j[0];
+      return;
+    }
     bk = KEY_EMPTY;
     bs = 0xFFFFFFFFu;
     bj = -1;
@@ -976,11 +1032,16 @@ struct Eng {
     u64 bk = gk[0];
     u32 bs = gs[0];
     i32 bj = gj[0];
-    for (int g = 1; g < NG; g++) {
-      if (gk[g] < bk || (gk[g] == bk && gs[g] < bs)) {
-        bk = gk[g];
-        bs = gs[g];
-        bj = gj[g];
+    if constexpr (QTREE) {
+#pragma unroll
+      for (int g = 1; g < NG; g++) q_min2(bk, bs, bj, gk[g], gs[g], gj[g]);
+    } else {
+      for (int g = 1; g < NG; g++) {
+        if (gk[g] < bk || (gk[g] == bk && gs[g] < bs)) {
+          bk = gk[g];
+          bs = gs[g];
+          bj = gj[g];
+        }
       }
     }
     mk = bk;
@@ -994,6 +1055,7 @@ struct Eng {
     u32 s;
     i32 j;
     q_scan(g * QG, QG, k, s, j);
+#pragma unroll
     for (int gg = 0; gg < NG; gg++) {
       if (gg == g) {
         gk[gg] = k;
@@ -1005,11 +1067,21 @@ struct Eng {
   }
   DEV void q_gupd(int j, u64 k, u32 s) {  // QHIER: slot j of this lane now holds (k, s)
     const int g = j / QG;
-    for (int gg = 0; gg < NG; gg++) {
-      if (gg == g && (k < gk[gg] || (k == gk[gg] && s < gs[gg]))) {
-        gk[gg] = k;
-        gs[gg] = s;
-        gj[gg] = j;
+    if constexpr (QTREE) {
+#pragma unroll
+      for (int gg = 0; gg < NG; gg++) {  // selects: g differs between lanes
+        const bool w = (gg == g) & ((k < gk[gg]) | ((k == gk[gg]) & (s < gs[gg])));
+        gk[gg] = w ? k : gk[gg];
+        gs[gg] = w ? s : gs[gg];
+        gj[gg] = w ? j : gj[gg];
+      }
+    } else {
+      for (int gg = 0; gg < NG; gg++) {
+        if (gg == g && (k < gk[gg] || (k == gk[gg] && s < gs[gg]))) {
+          gk[gg] = k;
+          gs[gg] = s;
+          gj[gg] = j;
+        }
       }
     }
   }
@@ -1271,7 +1343,11 @@ struct Eng {
       deliver = sent + (i64)l;
     } else {
       double l = 0.0;
-      if (PC.lat_mode == 1) l = lat()[cur_agent == 0 ? recipient : (PC.lat_asym ? PC.n_agents : 0) + cur_agent];
+      if (PC.lat_mode == 1) {
+        const int li = cur_agent == 0 ? recipient : (PC.lat_asym ? PC.n_agents : 0) + cur_agent;
+        if constexpr (LATL > 0) l = latl[li];
+        else l = lat()[li];
+      }
       i64 noise = 0;
       if (PC.noise_len > 1) {
         RS K = grs(2);
@@ -3765,6 +3841,7 @@ struct Eng {
   DEV void load() {
     hdr_from_global();
     for (int hs = 0; hs < HOT; hs++) hotrec[hs * 64 + lane] = agent_ptr(hot_agent(hs))[lane];
+    for (int i = lane; i < LATL; i += 64) latl[i] = lat()[i];
     SavedEvent* sq = (SavedEvent*)(env + PC.L.off_q);
     qfree = 0;
     for (int j = 0; j < SQ; j++) {
