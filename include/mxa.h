@@ -8,6 +8,7 @@
  *
  * Reference interfaces replaced (file:line in yutiansut/marl-optimal-execution):
  *   mxa_create ......... config/{rmsc01,rmsc02,obi_rmsc02,rmsc03,sparse_zi_100,sparse_zi_1000,value_noise}.py module body
+ *                        (and rmsc03 with SpreadBasedMarketMakerAgent.py:17-297, MXA_RMSC03_SBMM*)
  *                        (agent/oracle/kernel construction, global-RNG draw order) and
  *                        Kernel.__init__ (Kernel.py:13-46)
  *   mxa_reset .......... Kernel.runner kernelInitializing/kernelStarting (Kernel.py:143-177),
@@ -50,7 +51,11 @@ enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKET
        MXA_HIST_FUND_VALUE = 11 /* config/hist_fund_value.py: random_fund_value on an ExternalFileOracle (mxa_create_hist) */,
        MXA_HIST_FUND_DIVERSE = 12 /* config/hist_fund_diverse.py: random_fund_diverse on an ExternalFileOracle */,
        MXA_MARKETREPLAY_RUNNER = 13 /* config/marketreplay.py: exchange + MarketReplayAgent under Kernel.runner */,
-       MXA_MARKETREPLAY_TWAP = 14 /* config/execution/marketreplay/execution_marketreplay.py: + TWAPExecutionAgent */ };
+       MXA_MARKETREPLAY_TWAP = 14 /* config/execution/marketreplay/execution_marketreplay.py: + TWAPExecutionAgent */,
+       /* config/rmsc03.py with agent/market_makers/SpreadBasedMarketMakerAgent.py in the market maker's
+        * slot (no reference config uses that agent; composition of tests/golden/gen_fixtures.py):
+        * subscribe=True (level-1 MARKET_DATA every 10 s) and the polling mode (QUERY_SPREAD every second) */
+       MXA_RMSC03_SBMM = 15, MXA_RMSC03_SBMM_POLL = 16 };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };

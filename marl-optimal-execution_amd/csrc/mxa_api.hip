@@ -227,6 +227,8 @@ static bool bind(mxa_handle* h, int cfg) {
   case 12: e = mxa_entry_12(); break;
   case 13: e = mxa_entry_13(); break;
   case 14: e = mxa_entry_14(); break;
+  case 15: e = mxa_entry_15(); break;
+  case 16: e = mxa_entry_16(); break;
 #endif
   default: return false;
   }
@@ -248,9 +250,9 @@ extern "C" {
 #ifdef MXA_PROF
 // diagnostics build only (not in include/mxa.h): phase cycle totals, then cleared
 int mxa_prof_read(uint64_t* out64) {
-  if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(mxa::g_mxa_prof), 64 * 8) != hipSuccess) return MXA_EHIP;
-  static const uint64_t z[64] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(mxa::g_mxa_prof), z, 64 * 8) != hipSuccess) return MXA_EHIP;
+  if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(mxa::g_mxa_prof), 128 * 8) != hipSuccess) return MXA_EHIP;
+  static const uint64_t z[128] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(mxa::g_mxa_prof), z, 128 * 8) != hipSuccess) return MXA_EHIP;
   return MXA_OK;
 }
 #endif
@@ -269,9 +271,11 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
                     (int)MXA_HIST_FUND_VALUE == (int)MXA_CFG_HIST_FUND_VALUE &&
                     (int)MXA_HIST_FUND_DIVERSE == (int)MXA_CFG_HIST_FUND_DIVERSE &&
                     (int)MXA_MARKETREPLAY_RUNNER == (int)MXA_CFG_MARKETREPLAY_RUNNER &&
-                    (int)MXA_MARKETREPLAY_TWAP == (int)MXA_CFG_MARKETREPLAY_TWAP,
+                    (int)MXA_MARKETREPLAY_TWAP == (int)MXA_CFG_MARKETREPLAY_TWAP &&
+                    (int)MXA_RMSC03_SBMM == (int)MXA_CFG_RMSC03_SBMM &&
+                    (int)MXA_RMSC03_SBMM_POLL == (int)MXA_CFG_RMSC03_SBMM_POLL,
                 "config ids");
-  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_MARKETREPLAY_TWAP + 1, "one entry per configuration");
+  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_RMSC03_SBMM_POLL + 1, "one entry per configuration");
   // replay handles: mxa_create_replay(_runner); ExternalFileOracle configurations: mxa_create_hist
   if (config == MXA_MARKETREPLAY || config == MXA_MARKETREPLAY_RUNNER || config == MXA_MARKETREPLAY_TWAP ||
       config == MXA_HIST_FUND_VALUE ||

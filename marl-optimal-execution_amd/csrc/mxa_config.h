@@ -99,6 +99,9 @@ constexpr Shape shape(int cfg) {
   // rmsc03_rl episodes 146), so 16 waves per CU fit the queue, the header and the exchange and
   // market-maker records in LDS
   return cfg == MXA_CFG_RMSC03 ? Shape{3, 2, true, MXA_RMSC03_WAVES, 6, 2 * MXA_HOT_RECORDS}
+       // rmsc03 + SpreadBasedMarketMakerAgent: MARKET_DATA carries level counts (8 payload words)
+       : cfg == MXA_CFG_RMSC03_SBMM ? Shape{3, 2, true, 4, 8, 0}
+       : cfg == MXA_CFG_RMSC03_SBMM_POLL ? Shape{3, 2, true, 4, 6, 0}
        : cfg == MXA_CFG_RMSC03_RL ? Shape{3, 2, true, 4, 8, 2 * MXA_HOT_RECORDS}  // wide spread replies (depth 500)
        // rmsc01: oracle maxima over seeds 123456789 / 7: 140 pending events, 75 resting orders;
        // wide replies for the market maker's depth-5 spread queries
@@ -135,7 +138,7 @@ constexpr size_t lds_bytes(int cfg) {
          + 256  // batched-push scratch: slot table
 #endif
 #ifdef MXA_PROF
-         + 512  // phase counters (64 x u64)
+         + 1024  // phase counters and inclusive function timers (128 x u64)
 #endif
       ;
 }
@@ -194,6 +197,28 @@ constexpr void params_rmsc03(MxaParams& P) {
   P.L.open_cap = 128;
   P.L.tx_cap = 256;
   P.L.lat_len = 0;
+}
+
+// rmsc03 with a SpreadBasedMarketMakerAgent in its market maker's slot (agent 61), built from the
+// same script arguments (window 5, 20 ticks, wake-up 1 s, order_size = --mm-min-order-size);
+// tests/golden/gen_fixtures.py rmsc03_sbmm / rmsc03_sbmm_poll.  subscribe=True requests level-1
+// MARKET_DATA every 10e9 ns (SpreadBasedMarketMakerAgent.py:28-30, 78-80)
+constexpr void params_rmsc03_sbmm(MxaParams& P, bool subscribe) {
+  params_rmsc03(P);
+  P.config = subscribe ? MXA_CFG_RMSC03_SBMM : MXA_CFG_RMSC03_SBMM_POLL;
+  P.first_mm = 0;
+  P.n_mm = 0;
+  P.first_sb = 61;
+  P.n_sb = 1;
+  P.sb_sub = subscribe ? 1 : 0;
+  P.sb_size = 20;
+  P.sb_window = 5;
+  P.sb_ticks = 20;
+  P.sb_wake = NS;
+  P.md_sub = subscribe ? 1 : 0;
+  P.md_mk_levels = 1;
+  P.md_mom_levels = 1;
+  P.md_freq = 10 * NS;
 }
 
 // config/random_fund_value.py:59-180: rmsc03's agent classes at 5,100 agents over a whole day:
@@ -554,6 +579,7 @@ constexpr void params_value_noise(MxaParams& P) {
 constexpr MxaParams params(int cfg) {
   MxaParams P{};
   if (cfg == MXA_CFG_RMSC03) params_rmsc03(P);
+  else if (cfg == MXA_CFG_RMSC03_SBMM || cfg == MXA_CFG_RMSC03_SBMM_POLL) params_rmsc03_sbmm(P, cfg == MXA_CFG_RMSC03_SBMM);
   else if (cfg == MXA_CFG_RMSC03_RL) params_rmsc03_rl(P);
   else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);
   else if (cfg == MXA_CFG_MARKETREPLAY_RUNNER) params_marketreplay_runner(P);

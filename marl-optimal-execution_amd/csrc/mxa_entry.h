@@ -41,4 +41,6 @@ MxaEntry mxa_entry_11();
 MxaEntry mxa_entry_12();
 MxaEntry mxa_entry_13();
 MxaEntry mxa_entry_14();
-#define MXA_N_CONFIGS 15
+MxaEntry mxa_entry_15();
+MxaEntry mxa_entry_16();
+#define MXA_N_CONFIGS 17

@@ -500,7 +500,7 @@ DEV i64 U(i64 v) {
 }
 #ifdef MXA_PROF
 // diagnostics build only: per-phase shader-cycle totals over all envs (tools/prof_phases.py)
-__device__ unsigned long long g_mxa_prof[64];
+__device__ unsigned long long g_mxa_prof[128];
 DEV u64 stamp() {
   u64 t;
   __builtin_amdgcn_sched_barrier(0);
@@ -511,7 +511,27 @@ DEV u64 stamp() {
 #define PROF_T(v) u64 v = stamp()
 #define PROF_ADD(b, v) do { u64 _t = stamp(); if (lane == 0) prof[b] += _t - (v); v = _t; } while (0)
 #define PROF_CNT(b) do { if (lane == 0) prof[b] += 1; } while (0)
+// inclusive function timers (slots 64..95, call counts at +32): nested inside the phases above
+#define PROF_IN(v) u64 v = stamp()
+#define PROF_OUT(b, v) do { u64 _t = stamp(); if (lane == 0) { prof[b] += _t - (v); prof[(b) + 32] += 1; } } while (0)
+struct ProfScope {
+  LDSP unsigned long long* p;
+  int b, lane;
+  unsigned long long t0;
+  DEV ProfScope(LDSP unsigned long long* p_, int b_, int l) : p(p_), b(b_), lane(l), t0(stamp()) {}
+  DEV ~ProfScope() {
+    const unsigned long long t = stamp();
+    if (lane == 0) {
+      p[b] += t - t0;
+      p[b + 32] += 1;
+    }
+  }
+};
+#define PROF_SCOPE(b) ProfScope _pscope((LDSP unsigned long long*)prof, b, lane)
 #else
+#define PROF_SCOPE(b)
+#define PROF_IN(v)
+#define PROF_OUT(b, v)
 #define PROF_T(v)
 #define PROF_ADD(b, v)
 #define PROF_CNT(b)
@@ -769,6 +789,7 @@ struct Eng {
     add_delay = 0;
     run_skip = 0;
     rdirty = 0;
+    bok = 0;
     lane = laneid();
     qk = (LDSP u64*)lds;
     qs = (LDSP u32*)(lds + 8 * QCL);
@@ -780,6 +801,7 @@ struct Eng {
 #ifdef MXA_PROF
     prof = (LDSP u64*)(lds + LDS_Q + sizeof(EnvHdr));
     prof[lane] = 0;
+    prof[64 + lane] = 0;
 #endif
     trace = tcap > 0 ? (i64*)(env + PC.L.off_trace) : nullptr;
 #ifdef MXA_QREG
@@ -789,7 +811,7 @@ struct Eng {
 #endif
     rwin = (LDSP u32*)((LDSP char*)scr - 1024);
 #ifdef MXA_PROF
-    hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 512);
+    hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 1024);
 #else
     hotrec = (LDSP u64*)(lds + LDS_Q + 512);
 #endif
@@ -823,6 +845,7 @@ struct Eng {
     return -1;
   }
   DEV void rec_load(int a) {
+    PROF_SCOPE(77);
     const int hs = hot_slot(a);
     u64 v;
     if (hs >= 0) v = hotrec[hs * 64 + lane];
@@ -902,7 +925,19 @@ struct Eng {
     rs(AF_RS_M, (u32)r.m);
     rs(AF_RS_HASG, (u32)r.hasg);
     rsd(AF_RS_GAUSS, r.gauss);
-    dirty |= 16;
+    dirty |= rs_needs_maint(r) ? 16u : 0u;
+  }
+  // whether rng_maint has work for a stream in this state: a look-ahead overrun to report, or
+  // no materialized block after the one holding position p.  Decided where the state is put
+  // (registers) instead of re-read from the header and the record at the event's end
+  DEV bool rs_needs_maint(const RS& r) {
+#ifdef MXA_MAINT_AT_END
+    (void)r;
+    return true;
+#else
+    if constexpr (BUILD) return true;
+    return (r.hasg & 2) || r.m < r.p / MXA_MT_N + 1;
+#endif
   }
   // global streams: 0 = G (np.random), 1 = O (oracle symbol), 2 = K (kernel), 3 = L (latency)
   DEV RS grs(int s) {
@@ -931,10 +966,11 @@ struct Eng {
       h.rs_w0[s] = r.lw0;
       h.rs_wn[s] = r.lwn;
     }
-    dirty |= 1u << s;
+    dirty |= rs_needs_maint(r) ? 1u << s : 0u;
   }
   // event boundary: keep one MT block of look-ahead for every stream this event drew from
   DEV void rng_maint() {
+    PROF_SCOPE(78);
 #pragma unroll 1
     for (int k = 0; k < 5; k++) {
       if (!((dirty >> k) & 1)) continue;
@@ -1096,6 +1132,30 @@ struct Eng {
       q_lanemin();
       return;
     }
+#if !defined(MXA_SERIAL_FLAT) && !defined(MXA_QREG)
+    // every slot's load first, then a select tree (as q_scan).  r03 s24, same per-env results:
+    // rmsc03 43.8 -> 41.4 ms, rmsc01 1073 -> 963, obi_rmsc02 386 -> 373
+    if constexpr (!TIER) {
+      u64 k[SQ];
+      u32 s[SQ];
+      i32 j[SQ];
+#pragma unroll
+      for (int i = 0; i < SQ; i++) {
+        k[i] = qk[i * 64 + lane];
+        s[i] = qs[i * 64 + lane];
+        j[i] = i;
+      }
+#pragma unroll
+      for (int w = 1; w < SQ; w *= 2) {
+#pragma unroll
+        for (int i = 0; i + w < SQ; i += 2 * w) q_min2(k[i], s[i], j[i], k[i + w], s[i + w], j[i + w]);
+      }
+      mk = k[0];
+      ms = s[0];
+      mj = (k[0] == KEY_EMPTY && s[0] == 0xFFFFFFFFu) ? -1 : j[0];
+      return;
+    }
+#endif
     u64 bk = KEY_EMPTY;
     u32 bs = 0xFFFFFFFFu;
     i32 bj = -1;
@@ -1129,6 +1189,7 @@ struct Eng {
     return m;
   }
   DEV void q_push(u64 key, u32 seq, const Msg& m) {
+    PROF_SCOPE(65);
     QM use = qfree;
     if constexpr (TIER) {  // due within a second: an LDS slot; later: an HBM slot (either if full)
       const QM lm = ((QM)1 << SQL) - 1;
@@ -1332,6 +1393,7 @@ struct Eng {
   // ---------------- kernel services
   // Kernel.sendMessage (Kernel.py:347-425)
   DEV void send(int recipient, const Msg& m, i64 delay) {
+    PROF_SCOPE(64);
     i64 sent = cur + rg64(AF_COMP) + add_delay + delay;
     i64 deliver;
     if (PC.lat_mode == 2) {
@@ -1465,6 +1527,7 @@ struct Eng {
     return o_compute(t, 0, pt, pv);
   }
   DEV i64 o_observe(i64 t, double sigma_n) {
+    PROF_SCOPE(69);
     if constexpr (EXT) {  // ExternalFileOracle.observePrice (ExternalFileOracle.py:110-129): no clamp, no draws
       const double tp = efo_price(t);
       if (sigma_n == 0) return py_round(tp);
@@ -1482,13 +1545,42 @@ struct Eng {
   }
 
   // ---------------- order book pool (VGPR resident)
+  // best-price cache (BEST_CACHE): side s's best price while bok bit s is set.  A new order
+  // can only improve it; removing an order AT the cached price clears the bit (the level may
+  // have emptied); bulk book writes (launch load, event runs) clear both.  b_best rescans the
+  // pool only when the bit is clear
+#ifdef MXA_BEST_CACHE
+  static constexpr bool BEST_CACHE = true;
+#else
+  static constexpr bool BEST_CACHE = false;
+#endif
+  i32 bbest[2];
+  u32 bok;
+  DEV void b_inval() { bok = 0; }
   DEV i32 b_best(int buy_side) {  // best bid (max) or best ask (min); INT_MIN/INT_MAX if empty
+    PROF_SCOPE(68);
+    if constexpr (BEST_CACHE) {
+      if ((bok >> buy_side) & 1) return buy_side ? bbest[1] : bbest[0];
+    }
     i32 v = buy_side ? INT32_MIN : INT32_MAX;
     for (int j = 0; j < SO; j++) {
       bool m = bm[j] >= 0 && (bm[j] & 1) == buy_side;
       if (m) v = buy_side ? (bp[j] > v ? bp[j] : v) : (bp[j] < v ? bp[j] : v);
     }
-    return buy_side ? wmax_i32(v) : wmin_i32(v);
+    v = buy_side ? wmax_i32(v) : wmin_i32(v);
+    if constexpr (BEST_CACHE) {
+      if (buy_side) bbest[1] = v;
+      else bbest[0] = v;
+      bok |= 1u << buy_side;
+    }
+    return v;
+  }
+  // an order of side `buy` at `price` left the pool
+  DEV void b_gone(int buy, i32 price) {
+    if constexpr (BEST_CACHE) {
+      const i32 c = buy ? bbest[1] : bbest[0];
+      if (c == price) bok &= ~(1u << buy);
+    }
   }
   DEV i64 b_level_qty(int buy_side, i32 price) {
     i64 s = 0;
@@ -1570,6 +1662,10 @@ struct Eng {
       }
     h.b_count++;
     if (h.b_count > h.max_book) h.max_book = h.b_count;
+    if constexpr (BEST_CACHE) {
+      if (is_buy) bbest[1] = price > bbest[1] ? price : bbest[1];
+      else bbest[0] = price < bbest[0] ? price : bbest[0];
+    }
   }
   DEV void b_free(int s) {
     b_set(bm, s, -1);
@@ -1734,6 +1830,7 @@ struct Eng {
     if (n >= blog_cap) fail(ERR_BOOK_LOG_FULL);
   }
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
+    PROF_SCOPE(66);
     if (qty <= 0) return;
     if constexpr (BLOG) bl_put(cur, price, is_buy ? qty : -qty);
     i32 hep = h.epoch;
@@ -1756,6 +1853,7 @@ struct Eng {
         if (qty >= hq) {
           mq = hq;
           b_free(s);
+          b_gone(opp, best);
         } else {
           mq = qty;
           b_set(bq, s, hq - qty);
@@ -1797,11 +1895,13 @@ struct Eng {
     }
   }
   DEV void cancel_order(const Msg& m) {
+    PROF_SCOPE(67);
     int buy = m_buy(m);
     int s = b_find(buy, (i32)m.w[3], (i32)m.w[1]);
     if (s < 0) return;
     i32 q = b_get(bq, s), o = b_get(bo, s), mm = b_get(bm, s), p = b_get(bp, s);
     b_free(s);
+    b_gone(buy, p);
     if constexpr (BLOG) bl_put(cur, -p, buy ? q : -q);
     Msg r = msg_order(MK_CANCELLED, o, mm >> 1, mm & 1, q, p, 0);
     ex_notify(m_agent(m), r);
@@ -1930,6 +2030,7 @@ struct Eng {
 
   // ExchangeAgent.receiveMessage (ExchangeAgent.py:129-340)
   DEV void ex_receive(const Msg& m) {
+    PROF_SCOPE(73);
     rs64(AF_COMP, PC.ex_comp);
     u32 k = m_kind(m);
     i32 sender = m_agent(m);
@@ -2063,7 +2164,12 @@ struct Eng {
   }
   // placeLimitOrder (TradingAgent.py:309-349)
   DEV void place_limit(i64 qty, int is_buy, i64 price) {
-    i64 oid = next_order_id();
+    PROF_SCOPE(72);
+    place_limit_oid(qty, is_buy, price, next_order_id());
+  }
+  // placeLimitOrder with the order's id: an auto id (LimitOrder() consumed it even for a zero
+  // quantity) or the caller's order_id (SpreadBasedMarketMakerAgent)
+  DEV void place_limit_oid(i64 qty, int is_buy, i64 price, i64 oid) {
     if (qty > 0) {
       i32 n = rgi(AF_NORD);
       if (n >= PC.L.open_cap) {
@@ -2098,6 +2204,7 @@ struct Eng {
   DEV u64 ex_key() { return ((u64)(cur + rg64(AF_COMP) + add_delay) << KSH) | MT_MESSAGE; }
   // cancelOrder for every open order in dict (= list) order
   DEV void cancel_all() {
+    PROF_SCOPE(71);
     if constexpr (BATCH) {
       const i32 u = rgi(AF_NUSED);
       const OpenOrder* oo = open_ptr(cur_agent);
@@ -2184,6 +2291,7 @@ struct Eng {
 
   // TradingAgent.wakeup (TradingAgent.py:142-158)
   DEV bool ta_wakeup() {
+    PROF_SCOPE(75);
     u32 f = flags();
     if (f & FL_FIRST_WAKE) rs(AF_FLAGS, f & ~FL_FIRST_WAKE);
     if (!(f & FL_HAS_OPEN)) {
@@ -2198,6 +2306,7 @@ struct Eng {
     if (type == AG_MOMENTUM) return PC.mom_wake;
     if (type == AG_MKTMAKER) return PC.mk_wake;  // pd.Timedelta(wake_up_freq) (MarketMakerAgent.py:148-149)
     if (type == AG_OBI) return PC.obi_wake;      // pd.Timedelta("1s") (OrderBookImbalanceAgent.py:187-188)
+    if (type == AG_SBMM) return PC.sb_wake;      // pd.Timedelta(wake_up_freq) (SpreadBasedMarketMakerAgent.py:290-292)
     if constexpr (RP) {
       if (type == AG_REPLAY) return U(rx->tm[0]) - PC.mkt_open;  // MarketReplayAgent.py:94-96
       if constexpr (TW) {
@@ -2221,6 +2330,7 @@ struct Eng {
   }
   // TradingAgent.receiveMessage (TradingAgent.py:181-268)
   DEV void ta_receive(const Msg& m, int type) {
+    PROF_SCOPE(74);
     u32 f0 = flags();
     bool had = (f0 & FL_HAS_OPEN) && (f0 & FL_HAS_CLOSE);
     switch (m_kind(m)) {
@@ -2333,6 +2443,7 @@ struct Eng {
 
   // Bayesian estimate shared by ZI (ZI.py:215-263) and Value (ValueAgent.py:153-201)
   DEV i64 bayes_r_T(i64 obs, double kappa, double r_bar, double sigma_n, double sigma_s) {
+    PROF_SCOPE(70);
     if (!fl(FL_PREV_WAKE)) {
       fl_set(FL_PREV_WAKE, true);
       rs64(AF_PREV_WAKE, rg64(AF_MKT_OPEN));
@@ -2594,6 +2705,132 @@ struct Eng {
     Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, (i32)sz, price, 0);
     lm.w[0] = (lm.w[0] & 0xFFFFu) | ((u32)cur_agent << 16);
     q_push_lanes(act, ex_key(), lm);
+  }
+
+  // ---------------- SpreadBasedMarketMakerAgent (agent/market_makers/SpreadBasedMarketMakerAgent.py)
+  // The Chakraborty-Kearns ladder: num_ticks + 1 one-cent levels per side around the mid, shifted
+  // by whole ticks as the mid moves.  current_bids / current_asks are rings of order ids in the
+  // record (AF_SB_IDS: bids, then asks) with one head and one length; their prices run from
+  // AF_SB_BLO / AF_SB_ALO up by one cent per entry
+  static constexpr int SBC = PC.n_sb > 0 ? PC.sb_ticks + 1 : 1;
+  static_assert(PC.n_sb == 0 || AF_SB_IDS + 2 * SBC <= AF_RS_M, "SpreadBased ladder ids inside the agent record");
+  static DEV int sb_wrap(int r) { return r >= SBC ? r - SBC : r; }
+  // cancelOrders (:166-179): self.orders[id] -> cancelOrder; an id no longer open (KeyError) is skipped
+  DEV void cancel_oid(i32 oid) {
+    OpenOrder o;
+    if (find_open(oid, o) < 0) return;
+    send_ex(msg_order(MK_CANCEL, oid, cur_agent, o.is_buy, o.qty, o.price, 0));
+  }
+  // computeOrdersToCancel + cancelOrders + computeOrdersToPlace + placeOrders (:111-113, :128-130)
+  // at `mid`; AF_LAST_MID still holds the previous mid
+  DEV void sb_update(i64 mid) {
+    i32 n = rgi(AF_SB_N);
+    if (fl(FL_SB_INIT)) {  // computeOrdersToCancel (:134-164)
+      const i64 k = mid - rg64(AF_LAST_MID);
+      const i64 ak = k > 0 ? k : -k;
+      for (i64 i = 0; i < ak && n > 0; i++) {  // popleft on a rise, pop on a fall; empty deques ignored
+        const i32 hd = rgi(AF_SB_HEAD);
+        const int r = k > 0 ? hd : sb_wrap(hd + n - 1);
+        const i32 bo = rgi(AF_SB_IDS + r), ao = rgi(AF_SB_IDS + SBC + r);
+        if (k > 0) {
+          rs(AF_SB_HEAD, (u32)sb_wrap(hd + 1));
+          rs(AF_SB_BLO, (u32)(rgi(AF_SB_BLO) + 1));
+          rs(AF_SB_ALO, (u32)(rgi(AF_SB_ALO) + 1));
+        }
+        n--;
+        rs(AF_SB_N, (u32)n);
+        cancel_oid(bo);  // the list order: bid, ask, bid, ask, ...
+        cancel_oid(ao);
+      }
+    }
+    if (!fl(FL_SB_INIT) || n == 0) {  // `not self.current_asks or not self.current_bids`
+      cancel_all();                    // cancelAllOrders (:294-297)
+      // initialiseBidsAsksDeques (:257-277), anchor "bottom": ids for the bids, then the asks
+      const i64 lb = mid - 1 - PC.sb_ticks, la = mid + PC.sb_window;
+      const i32 c0 = rgi(AF_SB_CNT);
+      for (int i = 0; i < SBC; i++) {
+        rs(AF_SB_IDS + i, (u32)(MXA_SB_ID_BASE + c0 + 1 + i));
+        rs(AF_SB_IDS + SBC + i, (u32)(MXA_SB_ID_BASE + c0 + 1 + SBC + i));
+      }
+      rs(AF_SB_CNT, (u32)(c0 + 2 * SBC));
+      rs(AF_SB_HEAD, 0u);
+      rs(AF_SB_N, (u32)SBC);
+      rs(AF_SB_BLO, (u32)lb);
+      rs(AF_SB_ALO, (u32)la);
+      fl_set(FL_SB_INIT, true);
+      for (int i = 0; i < SBC; i++) place_limit_oid(PC.sb_size, 1, lb + i, MXA_SB_ID_BASE + c0 + 1 + i);
+      for (int i = 0; i < SBC; i++) place_limit_oid(PC.sb_size, 0, la + i, MXA_SB_ID_BASE + c0 + 1 + SBC + i);
+      return;
+    }
+    const i64 k = fl(FL_LAST_MID) ? mid - rg64(AF_LAST_MID) : 0;
+    if (k == 0) return;
+    // new levels beyond the moving end, one id each, bid before ask (generateNewOrderId order);
+    // |k| < the deque length here (a longer move emptied the deques above)
+    const i32 c0 = rgi(AF_SB_CNT);
+    const i64 ak = k > 0 ? k : -k;
+    const i64 b0 = k > 0 ? rgi(AF_SB_BLO) + n - 1 : rgi(AF_SB_BLO);
+    const i64 a0 = k > 0 ? rgi(AF_SB_ALO) + n - 1 : rgi(AF_SB_ALO);
+    for (i64 inc = 1; inc <= ak; inc++) {
+      const i32 bo = MXA_SB_ID_BASE + c0 + (i32)(2 * inc - 1), ao = bo + 1;
+      i32 hd = rgi(AF_SB_HEAD);
+      int r;
+      if (k > 0) {  // append
+        r = sb_wrap(hd + n);
+      } else {      // appendleft
+        hd = sb_wrap(hd + SBC - 1);
+        r = hd;
+        rs(AF_SB_HEAD, (u32)hd);
+        rs(AF_SB_BLO, (u32)(rgi(AF_SB_BLO) - 1));
+        rs(AF_SB_ALO, (u32)(rgi(AF_SB_ALO) - 1));
+      }
+      rs(AF_SB_IDS + r, (u32)bo);
+      rs(AF_SB_IDS + SBC + r, (u32)ao);
+      n++;
+    }
+    rs(AF_SB_N, (u32)n);
+    rs(AF_SB_CNT, (u32)(c0 + 2 * ak));
+    const i64 dir = k > 0 ? 1 : -1;
+    for (i64 inc = 1; inc <= ak; inc++) place_limit_oid(PC.sb_size, 1, b0 + dir * inc, MXA_SB_ID_BASE + c0 + 2 * inc - 1);
+    for (i64 inc = 1; inc <= ak; inc++) place_limit_oid(PC.sb_size, 0, a0 + dir * inc, MXA_SB_ID_BASE + c0 + 2 * inc);
+  }
+  DEV void sb_wakeup() {  // wakeup (:75-84)
+    const bool can = ta_wakeup();
+    if constexpr (PC.sb_sub) {
+      if (!fl(FL_SUB_REQ)) request_subscription(1);  // level 1 every subscribe_freq (10e9 ns)
+      return;
+    }
+    if (can) {
+      get_spread(1);
+      rs(AF_STATE, AS_AWAITING_SPREAD);
+    }
+  }
+  DEV void sb_receive(const Msg& m) {  // receiveMessage (:86-132)
+    ta_receive(m, AG_SBMM);
+    const u32 k = m_kind(m);
+    i32 bid, ask;
+    if constexpr (!PC.sb_sub) {
+      if (!(rgi(AF_STATE) == AS_AWAITING_SPREAD && k == MK_SPREAD)) return;
+      const bool hb = known_bid(bid), ha = known_ask(ask);  // getKnownBidAsk; `if bid and ask`
+      i64 mid = rg64(AF_LAST_MID);
+      if (hb && ha) mid = (i64)((double)((i64)ask + bid) / 2);
+      else if (!fl(FL_LAST_MID)) {  // `mid` never bound
+        fail(ERR_SB_MID);
+        return;
+      }
+      sb_update(mid);
+      wakeup_at(cur_agent, cur + PC.sb_wake);
+      rs(AF_STATE, AS_AWAITING_WAKEUP);
+      rs64(AF_LAST_MID, mid);
+      fl_set(FL_LAST_MID, true);
+    } else {
+      if (!(rgi(AF_STATE) == AS_AWAITING_MD && k == MK_MARKET_DATA)) return;
+      const bool hb = known_bid(bid), ha = known_ask(ask);  // known_bids[symbol][0][0] if known_bids[symbol] else None
+      if (!(hb && ha)) return;
+      const i64 mid = (i64)((double)((i64)ask + bid) / 2);
+      sb_update(mid);
+      rs64(AF_LAST_MID, mid);
+      fl_set(FL_LAST_MID, true);
+    }
   }
 
   // ---------------- MarketMakerAgent (agent/market_makers/MarketMakerAgent.py, polling mode)
@@ -3694,6 +3931,8 @@ struct Eng {
         if (type == AG_HBL) return hbl_wakeup();
       if constexpr (PC.n_obi > 0)
         if (type == AG_OBI) return obi_wakeup();
+      if constexpr (PC.n_sb > 0)
+        if (type == AG_SBMM) return sb_wakeup();
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_wakeup();
         if constexpr (TW) {
@@ -3722,6 +3961,8 @@ struct Eng {
         if (type == AG_HBL) return hbl_receive(m);
       if constexpr (PC.n_obi > 0)
         if (type == AG_OBI) return obi_receive(m);
+      if constexpr (PC.n_sb > 0)
+        if (type == AG_SBMM) return sb_receive(m);
       if constexpr (RP) {
         if (type == AG_REPLAY) return mr_receive(m);
         if constexpr (TW) {
@@ -4023,6 +4264,7 @@ struct Eng {
       found = s >= 0;
       for (int j = 0; j < SO; j++) bm[j] = hit[j] >= 0 ? -1 : bm[j];  // b_free
       h.b_count -= nfreed;
+      b_inval();
     } else {
       for (int i = 0; i < n; i++) {
         const u32 w0 = rdl(mm.w[0], i);
@@ -4030,6 +4272,7 @@ struct Eng {
         if (s >= 0) {
           const i32 q = b_get(bq, s), mt = b_get(bm, s);
           b_free(s);
+          b_inval();
           const bool me = lane == i;
           found = me || found;
           nq = me ? q : nq;
@@ -4105,6 +4348,7 @@ struct Eng {
         }
         base += __popcll(fb);
       }
+      b_inval();
       h.arrival = arr0 + (u32)m;
       h.b_count += m;
       if (h.b_count > h.max_book) h.max_book = h.b_count;
@@ -4373,6 +4617,16 @@ struct Eng {
       if (type == MT_MESSAGE && m_kind(m) == MK_SPREAD && rgi(AF_TYPE) == AG_VALUE) pb = 53, pc = 61;
       if (type == MT_MESSAGE && m_kind(m) == MK_SPREAD && rgi(AF_TYPE) == AG_POVMM) pb = 54, pc = 62;
       if (type == MT_MESSAGE && m_kind(m) == MK_TV) pb = 55, pc = 63;
+      if (type == MT_MESSAGE && rcp == 0) {  // the exchange by request kind (as the fast path)
+        const u32 kk = m_kind(m);
+        pb = kk == MK_SPREAD_REQ ? 48 : kk == MK_TV_REQ ? 49 : kk == MK_LIMIT ? 50 : kk == MK_CANCEL ? 51 : 52;
+        pc = pb + 8;
+      }
+      if (type == MT_MESSAGE && rgi(AF_TYPE) == AG_ZI) {  // ZI messages: 80 SPREAD, 81 ACCEPTED, 82 EXECUTED, 83 other
+        const u32 kk = m_kind(m);
+        pb = kk == MK_SPREAD ? 80 : kk == MK_ACCEPTED ? 81 : kk == MK_EXECUTED ? 82 : 83;
+        pc = pb + 32;
+      }
 #endif
       dispatch(rgi(AF_TYPE), type == MT_WAKEUP, m);
       PROF_ADD(pb, t0);
@@ -4575,6 +4829,7 @@ struct Builder : Eng<CFG, true> {
     int n = P.n_agents;
     u32 tmp;
     if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_RL || P.config == MXA_CFG_RANDOM_FUND_VALUE ||
+        P.config == MXA_CFG_RMSC03_SBMM || P.config == MXA_CFG_RMSC03_SBMM_POLL ||
         P.config == MXA_CFG_RANDOM_FUND_DIVERSE || P.config == MXA_CFG_HIST_FUND_VALUE ||
         P.config == MXA_CFG_HIST_FUND_DIVERSE) {
       // config/rmsc03.py, config/random_fund_value.py and config/random_fund_diverse.py: the same
@@ -4611,6 +4866,11 @@ struct Builder : Eng<CFG, true> {
         set_seed(4 + a, g_seed(G));
         rec_init(a, AG_POVMM);
         this->rs(AF_ORDER_SIZE, (u32)P.mm_min_size);
+        this->rec_store();
+      }
+      for (int a = P.first_sb; a < P.first_sb + P.n_sb; a++) {  // rmsc03_sbmm*: the market maker's slot and draw
+        set_seed(4 + a, g_seed(G));
+        rec_init(a, AG_SBMM);
         this->rec_store();
       }
       for (int a = P.first_mk; a < P.first_mk + P.n_mk; a++) {  // random_fund_diverse
@@ -4887,6 +5147,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(
   g.save();
 #ifdef MXA_PROF
   atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
+  atomicAdd(&mxa::g_mxa_prof[64 + g.lane], (unsigned long long)g.prof[64 + g.lane]);
 #endif
 }
 
@@ -4944,6 +5205,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
   if (g.lane == 0) flags[env] = done | (hobs ? 2 : 0) | (g.status == ST_ERROR ? 4 : 0);
 #ifdef MXA_PROF
   atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
+  atomicAdd(&mxa::g_mxa_prof[64 + g.lane], (unsigned long long)g.prof[64 + g.lane]);
 #endif
 }
 #endif

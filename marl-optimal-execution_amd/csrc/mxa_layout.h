@@ -22,7 +22,10 @@ enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPAR
                      MXA_CFG_RMSC02 = 7, MXA_CFG_OBI_RMSC02 = 8, MXA_CFG_RANDOM_FUND_VALUE = 9,
                      MXA_CFG_RANDOM_FUND_DIVERSE = 10, MXA_CFG_HIST_FUND_VALUE = 11,
                      MXA_CFG_HIST_FUND_DIVERSE = 12, MXA_CFG_MARKETREPLAY_RUNNER = 13,
-                     MXA_CFG_MARKETREPLAY_TWAP = 14 };
+                     MXA_CFG_MARKETREPLAY_TWAP = 14,
+                     // rmsc03 with a SpreadBasedMarketMakerAgent in the market maker's slot: subscribe=True
+                     // (the agent's default) and the polling mode
+                     MXA_CFG_RMSC03_SBMM = 15, MXA_CFG_RMSC03_SBMM_POLL = 16 };
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -38,7 +41,11 @@ enum { MT_MESSAGE = 1, MT_WAKEUP = 2, MT_CANCEL_ORDER = 3 };
 
 // agent classes
 enum { AG_EXCHANGE = 0, AG_ZI = 1, AG_NOISE = 2, AG_VALUE = 3, AG_POVMM = 4, AG_MOMENTUM = 5, AG_REPLAY = 6, AG_DUMMYRL = 7,
-       AG_MKTMAKER = 8, AG_HBL = 9, AG_OBI = 10, AG_TWAP = 11 };
+       AG_MKTMAKER = 8, AG_HBL = 9, AG_OBI = 10, AG_TWAP = 11, AG_SBMM = 12 };
+// SpreadBasedMarketMakerAgent's string order ids "<name>_<id>_<n>" (generateNewOrderId,
+// SpreadBasedMarketMakerAgent.py:279-288) are carried as MXA_SB_ID_BASE + n: compared for
+// identity only, never equal to an auto id
+#define MXA_SB_ID_BASE 0x40000000
 
 // env status flags (EnvHdr::status)
 enum { ST_RUNNING = 0, ST_DONE = 1, ST_ERROR = 2 };
@@ -67,7 +74,10 @@ enum {
   // TWAPExecutionAgent (ExecutionAgent.placeOrders, execution_agent.py:108-123)
   ERR_TWAP_SCHEDULE = 25, // schedule[Interval(t, t + 30 s)] of a 60 s schedule (KeyError)
   ERR_TWAP_QUOTE = 26,    // (bid + ask) / 2 with a None side (TypeError)
-  ERR_TWAP_MARKET = 27    // placeMarketOrder at horizon[-2] (not restated; unreachable in the script)
+  ERR_TWAP_MARKET = 27,   // placeMarketOrder at horizon[-2] (not restated; unreachable in the script)
+  // SpreadBasedMarketMakerAgent.receiveMessage: a QUERY_SPREAD with a missing side before any mid
+  // was known leaves `mid` unbound (UnboundLocalError)
+  ERR_SB_MID = 28
 };
 
 // per-env scalar header (first bytes of the env block)
@@ -263,6 +273,10 @@ enum {
   AF_WAKEUP_TIME = 30, AF_RS_POS = 32, AF_RS_HASG = 33, AF_RS_GAUSS = 34, AF_LAST_MID = 36,
   AF_ORDER_SIZE = 38, AF_NMID = 39, AF_N20 = 40, AF_N50 = 41, AF_AVG20 = 42, AF_AVG50 = 44,
   AF_THETA = 46,      // 20 x int32
+  // SpreadBasedMarketMakerAgent (its own fields in the ZI / momentum areas): the two ladder deques
+  // current_bids / current_asks as rings of order ids with one head and one length (they always
+  // have equal lengths), prices contiguous from the left end's
+  AF_SB_N = 39, AF_SB_HEAD = 40, AF_SB_BLO = 41, AF_SB_ALO = 42, AF_SB_CNT = 43, AF_SB_IDS = 46,
   AF_MIDS = 66,       // 50 x int32 (2*mid ring), momentum
   AF_STREAM_N = 66,   // HBL: epochs of the last QUERY_ORDER_STREAM reply (momentum's AF_MIDS area)
   AF_STREAM_HI = 68,  // HBL: absolute history epoch of its first entry (history[1]), int64
@@ -278,7 +292,8 @@ enum {
   FL_TRADING = 32, FL_HAS_KNOWN = 64, FL_NB = 128, FL_NA = 256, FL_HAS_LAST = 512,
   FL_LAST_FLOAT = 1024, FL_PREV_WAKE = 2048, FL_AW_SPREAD = 4096, FL_AW_TV = 8192, FL_LAST_MID = 16384,
   FL_HAS_STREAM = 32768, FL_SUB_REQ = 65536,
-  FL_OBI_LONG = 131072, FL_OBI_SHORT = 262144  // OrderBookImbalanceAgent.is_long / is_short
+  FL_OBI_LONG = 131072, FL_OBI_SHORT = 262144,  // OrderBookImbalanceAgent.is_long / is_short
+  FL_SB_INIT = 524288  // SpreadBasedMarketMakerAgent: current_bids / current_asks are not None
 };
 enum { AF_OBI_STOP = AF_R_T };  // OrderBookImbalanceAgent.trailing_stop (double; OBI has no r_t)
 enum { AS_AWAITING_WAKEUP = 0, AS_INACTIVE = 1, AS_AWAITING_SPREAD = 2, AS_ACTIVE = 3, AS_AWAITING_STREAM = 4,
@@ -331,6 +346,9 @@ typedef struct {
   int32_t oracle_ext;      // 1: util/oracle/ExternalFileOracle.py on a runtime series (RpCtx::fs_*)
   int64_t obi_freq, obi_wake;
   double obi_entry, obi_trail;
+  // SpreadBasedMarketMakerAgent (agent/market_makers/SpreadBasedMarketMakerAgent.py)
+  int32_t first_sb, n_sb, sb_sub, sb_size, sb_window, sb_ticks;
+  int64_t sb_wake;
   Layout L;
 } MxaParams;
 

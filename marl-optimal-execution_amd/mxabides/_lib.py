@@ -19,6 +19,8 @@ MXA_HIST_FUND_VALUE = 11
 MXA_HIST_FUND_DIVERSE = 12
 MXA_MARKETREPLAY_RUNNER = 13
 MXA_MARKETREPLAY_TWAP = 14
+MXA_RMSC03_SBMM = 15
+MXA_RMSC03_SBMM_POLL = 16
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000,
               "value_noise": MXA_VALUE_NOISE, "rmsc01": MXA_RMSC01, "rmsc02": MXA_RMSC02,
               "obi_rmsc02": MXA_OBI_RMSC02, "random_fund_value": MXA_RANDOM_FUND_VALUE,
@@ -27,7 +29,9 @@ CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_
               # config/marketreplay.py (Kernel.runner; ABIDESEnv's GymKernel replay is mxabides.gym)
               "marketreplay_runner": MXA_MARKETREPLAY_RUNNER,
               # config/execution/marketreplay/execution_marketreplay.py (TWAP agent passive / -e)
-              "marketreplay_twap": MXA_MARKETREPLAY_TWAP, "marketreplay_twap_e": MXA_MARKETREPLAY_TWAP}
+              "marketreplay_twap": MXA_MARKETREPLAY_TWAP, "marketreplay_twap_e": MXA_MARKETREPLAY_TWAP,
+              # rmsc03 with a SpreadBasedMarketMakerAgent in the market maker's slot (subscribe / polling)
+              "rmsc03_sbmm": MXA_RMSC03_SBMM, "rmsc03_sbmm_poll": MXA_RMSC03_SBMM_POLL}
 ENV_RUNNING, ENV_DONE, ENV_ERROR = 0, 1, 2
 ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: "open-order list capacity",
              4: "transaction history capacity", 5: "get_transacted_volume without transactions (pandas error)",
@@ -46,7 +50,8 @@ ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: 
              24: "two MARKET_DATA messages in flight to one agent (subscription freq below the latency)",
              25: "ExecutionAgent.placeOrders: schedule[Interval(t, t + 30 s)] of a 60 s TWAP schedule (KeyError)",
              26: "ExecutionAgent.placeOrders: (bid + ask) / 2 with a None side (TypeError)",
-             27: "ExecutionAgent.placeOrders: placeMarketOrder at horizon[-2] (not restated)"}
+             27: "ExecutionAgent.placeOrders: placeMarketOrder at horizon[-2] (not restated)",
+             28: "SpreadBasedMarketMakerAgent: mid unbound (UnboundLocalError)"}
 
 
 class EnvSummary(ctypes.Structure):

@@ -13,7 +13,7 @@ ZI_COUNTS = {"sparse_zi_100": [15, 15, 14, 14, 14, 14, 14], "sparse_zi_1000": [1
 
 # configs whose script takes the ticker from -t/--ticker (config/rmsc03.py:31, random_fund_*.py,
 # hist_fund_*.py); the default is the one the fixtures and the bench use
-TICKER_CONFIGS = ("rmsc03", "random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse",
+TICKER_CONFIGS = ("rmsc03", "rmsc03_sbmm", "rmsc03_sbmm_poll", "random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse",
                   "marketreplay_runner", "marketreplay_twap", "marketreplay_twap_e")
 HIST_CONFIGS = ("hist_fund_value", "hist_fund_diverse")
 # config/marketreplay.py (a LOBSTER tape, no oracle) and config/execution/marketreplay/
@@ -36,7 +36,7 @@ def symbol_of(config, symbol=None):
 # ExchangeAgent(book_freq=...) of each config script: 0 archives every snapshot
 # (ORDERBOOK_<sym>_FULL), None archives nothing, a pandas frequency resamples
 # (ExchangeAgent.py:389-469; value_noise / sparse_zi_* take -b, default None)
-BOOK_FREQ = {"rmsc03": 0, "rmsc02": 0, "rmsc01": "M", "obi_rmsc02": "all", "random_fund_value": None,
+BOOK_FREQ = {"rmsc03": 0, "rmsc03_sbmm": 0, "rmsc03_sbmm_poll": 0, "rmsc02": 0, "rmsc01": "M", "obi_rmsc02": "all", "random_fund_value": None,
              "random_fund_diverse": None, "hist_fund_value": None, "hist_fund_diverse": None, "value_noise": None,
              "sparse_zi_100": None, "sparse_zi_1000": None, "marketreplay_runner": 0,
              "marketreplay_twap": 0, "marketreplay_twap_e": 0}
@@ -60,9 +60,10 @@ def agent_names(config):
         extra = ["MARKET_MAKER_AGENT_5101"] + ["MOMENTUM_AGENT_%d" % j for j in range(5102, 5127)]
         return (["EXCHANGE_AGENT"] + ["NoiseAgent %d" % j for j in range(1, 5001)] +
                 ["Value Agent %d" % j for j in range(5001, 5101)] + (extra if config.endswith("diverse") else []))
-    if config == "rmsc03":
+    if config in ("rmsc03", "rmsc03_sbmm", "rmsc03_sbmm_poll"):
+        mm = "POV_MARKET_MAKER_AGENT_61" if config == "rmsc03" else "SPREAD_BASED_MARKET_MAKER_AGENT_61"
         return (["EXCHANGE_AGENT"] + ["NoiseAgent %d" % j for j in range(1, 51)] +
-                ["Value Agent %d" % j for j in range(51, 61)] + ["POV_MARKET_MAKER_AGENT_61"] +
+                ["Value Agent %d" % j for j in range(51, 61)] + [mm] +
                 ["MOMENTUM_AGENT_%d" % j for j in (62, 63)])
     names, a = ["Exchange Agent 0"], 1
     for g, cnt in enumerate(ZI_COUNTS[config]):
@@ -89,8 +90,9 @@ def agent_type_names(config):
     if config in ("random_fund_value", "random_fund_diverse", "hist_fund_value", "hist_fund_diverse"):
         extra = ["MarketMakerAgent"] + ["MomentumAgent"] * 25 if config.endswith("diverse") else []
         return ["ExchangeAgent"] + ["NoiseAgent"] * 5000 + ["ValueAgent"] * 100 + extra
-    if config == "rmsc03":
-        return ["ExchangeAgent"] + ["NoiseAgent"] * 50 + ["ValueAgent"] * 10 + ["POVMarketMakerAgent"] + ["MomentumAgent"] * 2
+    if config in ("rmsc03", "rmsc03_sbmm", "rmsc03_sbmm_poll"):
+        mm = "POVMarketMakerAgent" if config == "rmsc03" else "SpreadBasedMarketMakerAgent"
+        return ["ExchangeAgent"] + ["NoiseAgent"] * 50 + ["ValueAgent"] * 10 + [mm] + ["MomentumAgent"] * 2
     out = ["ExchangeAgent"]
     for g, cnt in enumerate(ZI_COUNTS[config]):
         lo, hi, eta = ZI_GROUPS[g]

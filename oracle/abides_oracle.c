@@ -207,7 +207,12 @@ typedef struct {
 /* agents                                                                     */
 /* ------------------------------------------------------------------------- */
 enum { AG_EXCHANGE = 0, AG_ZI, AG_NOISE, AG_VALUE, AG_POVMM, AG_MOMENTUM, AG_REPLAY, AG_DUMMYRL, AG_MKTMAKER, AG_HBL, AG_OBI,
-       AG_TWAP };
+       AG_TWAP, AG_SBMM };
+/* SpreadBasedMarketMakerAgent's string order ids "<name>_<id>_<n>" (generateNewOrderId,
+ * SpreadBasedMarketMakerAgent.py:279-288) as SB_ID_BASE + n: only ever compared for identity, and
+ * never equal to an auto id (Order.generateOrderId tests ints against a list of mixed ids) */
+#define SB_ID_BASE 0x40000000LL
+#define SB_MAX 32 /* ladder deque capacity (2 x num_ticks + 1 = 21 per side at most) */
 enum { ST_AWAITING_WAKEUP = 0, ST_INACTIVE, ST_AWAITING_SPREAD, ST_ACTIVE, ST_AWAITING_STREAM, ST_AWAITING_MARKET_DATA };
 
 typedef struct {
@@ -267,6 +272,11 @@ typedef struct {
     /* OrderBookImbalanceAgent: position state and trailing stop */
     int obi_long, obi_short;
     double obi_stop;
+    /* SpreadBasedMarketMakerAgent: current_bids / current_asks (deques of (price, id), index 0 =
+     * the left end; both always hold the same number of entries), None until the first ladder */
+    int64_t sb_bpx[SB_MAX], sb_bid[SB_MAX], sb_apx[SB_MAX], sb_aid[SB_MAX];
+    int sb_n, sb_init;
+    int64_t sb_cnt; /* order_id_counter */
 } agent_t;
 
 #define HIST_RETIRED 48
@@ -1304,6 +1314,7 @@ static int64_t wake_frequency(agent_t* a) {
     case AG_REPLAY: return a->wake_freq;  /* first tape time - mkt_open (MarketReplayAgent.py:94-96) */
     case AG_DUMMYRL: return a->wake_freq; /* horizon[0] - mkt_open (execution_agent.py:129-130) */
     case AG_TWAP: return a->wake_freq;    /* the same ExecutionAgent.getWakeFrequency */
+    case AG_SBMM: return a->wake_freq;    /* pd.Timedelta(wake_up_freq) (SpreadBasedMarketMakerAgent.py:290-292) */
     default: return rs_randint(&a->rs, 0, 100);
     }
 }
@@ -1724,6 +1735,176 @@ static void mk_receive(ora_env* e, agent_t* a, const msg_t* m) {
     }
     k_wakeup(e, a->id, e->cur + a->wake_freq);
     a->state = ST_AWAITING_WAKEUP;
+}
+
+/* ------------------------ SpreadBasedMarketMakerAgent ------------------------ */
+/* agent/market_makers/SpreadBasedMarketMakerAgent.py: the Chakraborty-Kearns ladder of num_ticks + 1
+ * one-cent levels per side around the mid, shifted by whole ticks as the mid moves */
+/* placeLimitOrder(..., order_id=<the ladder's id>) (TradingAgent.py:309-349) */
+static void place_limit_id(ora_env* e, agent_t* a, int64_t qty, int is_buy, int64_t price, int64_t oid) {
+    if (qty <= 0) return;
+    if (a->nord == a->capord) {
+        a->capord = a->capord ? 2 * a->capord : 8;
+        a->ord = (aord_t*)realloc(a->ord, sizeof(aord_t) * a->capord);
+    }
+    aord_t o = {oid, is_buy, qty, price};
+    a->ord[a->nord++] = o;
+    if (a->nord > e->st_max_open) e->st_max_open = a->nord;
+    msg_t m;
+    memset(&m, 0, sizeof m);
+    m.kind = K_LIMIT;
+    m.oid = oid;
+    m.oagent = a->id;
+    m.is_buy = is_buy;
+    m.qty = qty;
+    m.price = price;
+    m.fill = -1;
+    ta_send_ex(e, a, &m);
+}
+/* cancelOrders (:166-179): self.orders[id] -> cancelOrder; an id no longer open is a KeyError, skipped */
+static void cancel_oid(ora_env* e, agent_t* a, int64_t oid) {
+    int i = find_ord(a, oid);
+    if (i < 0) return;
+    msg_t m;
+    memset(&m, 0, sizeof m);
+    m.kind = K_CANCEL;
+    m.oid = oid;
+    m.oagent = a->id;
+    m.is_buy = a->ord[i].is_buy;
+    m.qty = a->ord[i].qty;
+    m.price = a->ord[i].price;
+    m.fill = -1;
+    ta_send_ex(e, a, &m);
+}
+static int64_t sb_new_id(agent_t* a) { return SB_ID_BASE + ++a->sb_cnt; } /* generateNewOrderId */
+static void sb_pop(int64_t* px, int64_t* id, int n, int left, int64_t* out_id) {
+    if (left) {
+        *out_id = id[0];
+        memmove(px, px + 1, sizeof(int64_t) * (n - 1));
+        memmove(id, id + 1, sizeof(int64_t) * (n - 1));
+    } else {
+        *out_id = id[n - 1];
+    }
+}
+static void sb_push(int64_t* px, int64_t* id, int n, int left, int64_t p, int64_t oid) {
+    if (left) {
+        memmove(px + 1, px, sizeof(int64_t) * n);
+        memmove(id + 1, id, sizeof(int64_t) * n);
+        px[0] = p;
+        id[0] = oid;
+    } else {
+        px[n] = p;
+        id[n] = oid;
+    }
+}
+/* computeOrdersToCancel + cancelOrders + placeOrders (receiveMessage :111-113 / :128-130) at `mid`;
+ * self.last_mid is still the previous mid here */
+static void sb_update(ora_env* e, agent_t* a, int64_t mid) {
+    /* computeOrdersToCancel (:134-164): per tick of the move one order from each deque, the lowest
+     * levels on a rise (popleft), the highest on a fall (pop); an empty deque is ignored */
+    int64_t cancel[2 * SB_MAX];
+    int nc = 0;
+    if (a->sb_init) {
+        const int64_t k = mid - a->last_mid;
+        for (int64_t i = 0; i < (k > 0 ? k : -k) && a->sb_n > 0; i++) {
+            sb_pop(a->sb_bpx, a->sb_bid, a->sb_n, k > 0, &cancel[nc++]);
+            sb_pop(a->sb_apx, a->sb_aid, a->sb_n, k > 0, &cancel[nc++]);
+            a->sb_n--;
+        }
+    }
+    for (int i = 0; i < nc; i++) cancel_oid(e, a, cancel[i]);
+    /* computeOrdersToPlace (:181-238), placeOrders (:240-255): bids first, then asks */
+    int64_t bp[SB_MAX], bi[SB_MAX], ap[SB_MAX], ai[SB_MAX];
+    int np = 0;
+    if (!a->sb_init || a->sb_n == 0) {
+        cancel_all(e, a); /* cancelAllOrders (:294-297): every order of self.orders */
+        /* initialiseBidsAsksDeques (:257-277), anchor "bottom" */
+        const int64_t hb = mid - 1, la = mid + a->window, lb = hb - a->num_ticks, ha = la + a->num_ticks;
+        const int nl = (int)(hb - lb + 1);
+        if (nl > SB_MAX || nl <= 0) {
+            fail(e, -19, "SpreadBasedMarketMakerAgent: ladder width beyond the restated deque");
+            return;
+        }
+        for (int i = 0; i < nl; i++) {
+            a->sb_bpx[i] = lb + i;
+            a->sb_bid[i] = sb_new_id(a);
+        }
+        for (int i = 0; i < nl; i++) {
+            a->sb_apx[i] = la + i;
+            a->sb_aid[i] = sb_new_id(a);
+        }
+        (void)ha;
+        a->sb_n = nl;
+        a->sb_init = 1;
+        for (int i = 0; i < nl; i++) place_limit_id(e, a, a->order_size, 1, a->sb_bpx[i], a->sb_bid[i]);
+        for (int i = 0; i < nl; i++) place_limit_id(e, a, a->order_size, 0, a->sb_apx[i], a->sb_aid[i]);
+        return;
+    }
+    const int64_t k = a->has_last_mid ? mid - a->last_mid : 0;
+    if (k > 0) {
+        const int64_t b0 = a->sb_bpx[a->sb_n - 1], a0 = a->sb_apx[a->sb_n - 1];
+        for (int64_t inc = 1; inc <= k; inc++) {
+            bp[np] = b0 + inc;
+            bi[np] = sb_new_id(a);
+            ap[np] = a0 + inc;
+            ai[np] = sb_new_id(a);
+            sb_push(a->sb_bpx, a->sb_bid, a->sb_n, 0, bp[np], bi[np]);
+            sb_push(a->sb_apx, a->sb_aid, a->sb_n, 0, ap[np], ai[np]);
+            a->sb_n++;
+            np++;
+        }
+    } else if (k < 0) {
+        const int64_t b0 = a->sb_bpx[0], a0 = a->sb_apx[0];
+        for (int64_t inc = 1; inc <= -k; inc++) {
+            bp[np] = b0 - inc;
+            bi[np] = sb_new_id(a);
+            ap[np] = a0 - inc;
+            ai[np] = sb_new_id(a);
+            sb_push(a->sb_bpx, a->sb_bid, a->sb_n, 1, bp[np], bi[np]);
+            sb_push(a->sb_apx, a->sb_aid, a->sb_n, 1, ap[np], ai[np]);
+            a->sb_n++;
+            np++;
+        }
+    }
+    for (int i = 0; i < np; i++) place_limit_id(e, a, a->order_size, 1, bp[i], bi[i]);
+    for (int i = 0; i < np; i++) place_limit_id(e, a, a->order_size, 0, ap[i], ai[i]);
+}
+/* wakeup (:75-84) */
+static void sb_wakeup(ora_env* e, agent_t* a) {
+    int can_trade = ta_wakeup(e, a);
+    if (a->subscribe && !a->sub_requested) {
+        request_subscription(e, a, 1, 10000000000LL); /* subscribe_num_levels 1, subscribe_freq 10e9 */
+        a->state = ST_AWAITING_MARKET_DATA;
+    } else if (can_trade && !a->subscribe) {
+        get_spread(e, a, 1);
+        a->state = ST_AWAITING_SPREAD;
+    }
+}
+/* receiveMessage (:86-132) */
+static void sb_receive(ora_env* e, agent_t* a, const msg_t* m) {
+    ta_receive(e, a, m);
+    if (!a->subscribe && a->state == ST_AWAITING_SPREAD && m->kind == K_SPREAD) {
+        int64_t mid = a->last_mid;
+        /* getKnownBidAsk: the best levels or None; `if bid and ask` */
+        if (a->nb && a->na && a->bid && a->ask) {
+            mid = (int64_t)((double)(a->ask + a->bid) / 2);
+        } else if (!a->has_last_mid) { /* `mid` never bound: UnboundLocalError */
+            fail(e, -18, "SpreadBasedMarketMakerAgent: no spread and no last mid (UnboundLocalError)");
+            return;
+        }
+        sb_update(e, a, mid);
+        k_wakeup(e, a->id, e->cur + a->wake_freq);
+        a->state = ST_AWAITING_WAKEUP;
+        a->last_mid = mid;
+        a->has_last_mid = 1;
+    } else if (a->subscribe && a->state == ST_AWAITING_MARKET_DATA && m->kind == K_MARKET_DATA) {
+        /* known_bids[symbol][0][0] if known_bids[symbol] else None */
+        if (!(a->nb && a->na && a->kb[0] && a->ka[0])) return;
+        const int64_t mid = (int64_t)((double)(a->ka[0] + a->kb[0]) / 2);
+        sb_update(e, a, mid);
+        a->last_mid = mid;
+        a->has_last_mid = 1;
+    }
 }
 
 /* ------------------------- OrderBookImbalanceAgent ---------------------------- */
@@ -2184,6 +2365,7 @@ static void dispatch_wakeup(ora_env* e, int id) {
     case AG_MKTMAKER: mk_wakeup(e, a); break;
     case AG_HBL: hbl_wakeup(e, a); break;
     case AG_OBI: obi_wakeup(e, a); break;
+    case AG_SBMM: sb_wakeup(e, a); break;
     }
 }
 static void dispatch_message(ora_env* e, int id, const msg_t* m) {
@@ -2194,6 +2376,7 @@ static void dispatch_message(ora_env* e, int id, const msg_t* m) {
     case AG_HBL: hbl_receive(e, a, m); break;
     case AG_MKTMAKER: mk_receive(e, a, m); break;
     case AG_OBI: obi_receive(e, a, m); break;
+    case AG_SBMM: sb_receive(e, a, m); break;
     case AG_NOISE: noise_receive(e, a, m); break;
     case AG_VALUE: value_receive(e, a, m); break;
     case AG_POVMM: mm_receive(e, a, m); break;
@@ -2684,6 +2867,29 @@ static void zi_params(agent_t* a, int64_t rmin, int64_t rmax, double sigma_n, do
  * U(21000, 13e6)[n][n] drawn after the kernel seed (not symmetrised) with 6-way noise */
 /* config/obi_rmsc02.py: rmsc02's market with 89 ZI agents, 5 OrderBookImbalanceAgent (built
  * after the ZI agents, each drawing only its seed) and 5 momentum agents; no HBL */
+/* rmsc03 with its market-maker slot (config/rmsc03.py:158-177) a SpreadBasedMarketMakerAgent built
+ * from the same arguments (tests/golden/gen_fixtures.py rmsc03_sbmm*): window 5, 20 ticks, wake-up
+ * 1 s, order_size = --mm-min-order-size (20); the random_state draw is the POV maker's */
+static int build_rmsc03_sbmm(ora_env* e, uint32_t seed, int subscribe) {
+    int rc = build_rmsc03_like(e, seed, 0);
+    if (rc) return rc;
+    agent_t* a = &e->ag[61];
+    a->type = AG_SBMM;
+    snprintf(a->name, 96, "SPREAD_BASED_MARKET_MAKER_AGENT_%d", a->id);
+    snprintf(a->tname, 96, "SpreadBasedMarketMakerAgent");
+    a->order_size = 20;
+    a->window = 5;
+    a->num_ticks = 20;
+    a->wake_freq = NS_SEC;
+    a->subscribe = subscribe;
+    a->sub_requested = 0;
+    a->state = ST_AWAITING_WAKEUP;
+    a->has_last_mid = 0;
+    a->sb_n = 0;
+    a->sb_init = 0;
+    a->sb_cnt = 0;
+    return 0;
+}
 static int build_rmsc0x(ora_env* e, uint32_t seed, int v2, int obi) {
     rs_seed(&e->G, seed);
     int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
@@ -2994,6 +3200,8 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     if (!strcmp(config, "sparse_zi_100")) rc = build_sparse_zi(e, seed, 0);
     else if (!strcmp(config, "sparse_zi_1000")) rc = build_sparse_zi(e, seed, 1);
     else if (!strcmp(config, "rmsc03")) rc = build_rmsc03_like(e, seed, 0);
+    else if (!strcmp(config, "rmsc03_sbmm")) rc = build_rmsc03_sbmm(e, seed, 1);
+    else if (!strcmp(config, "rmsc03_sbmm_poll")) rc = build_rmsc03_sbmm(e, seed, 0);
     else if (!strcmp(config, "random_fund_value")) rc = build_rmsc03_like(e, seed, 1);
     else if (!strcmp(config, "random_fund_diverse")) rc = build_rmsc03_like(e, seed, 2);
     else if (!strcmp(config, "hist_fund_value")) rc = build_rmsc03_like(e, seed, 3);

@@ -79,8 +79,19 @@ def _price(p):
     return int(p)
 
 
+SB_ID_BASE = 0x40000000  # SpreadBasedMarketMakerAgent's string ids "<name>_<id>_<n>" -> SB_ID_BASE + n
+
+
+def _oid(x):
+    """order id as the device carries it: ints as they are; SpreadBasedMarketMakerAgent's string
+    ids (generateNewOrderId, SpreadBasedMarketMakerAgent.py:279-288) by their counter"""
+    if isinstance(x, str):
+        return SB_ID_BASE + int(x.rsplit("_", 1)[1])
+    return int(x)
+
+
 def _order_fields(o, with_qty=True):
-    return [int(o.order_id), int(o.agent_id), 1 if o.is_buy_order else 0,
+    return [_oid(o.order_id), int(o.agent_id), 1 if o.is_buy_order else 0,
             int(o.quantity) if with_qty else 0, _price(o.limit_price)]
 
 
@@ -268,6 +279,27 @@ def run_config(cfg, seed, out, full):
     from agent.TradingAgent import TradingAgent
     TradingAgent.getTransactedVolume = TradingAgent.get_transacted_volume  # SURVEY.md key finding 3
 
+    if cfg.startswith("rmsc03_sbmm"):
+        # rmsc03 with its market maker slot (config/rmsc03.py:158-177) a SpreadBasedMarketMakerAgent
+        # (agent/market_makers/SpreadBasedMarketMakerAgent.py; no reference config uses it): the
+        # script's own arguments (window 5, 20 ticks, wake-up 1 s, random_state drawn in place),
+        # order_size = --mm-min-order-size (20); subscribe=True (the agent's default) or, for
+        # rmsc03_sbmm_poll, False
+        from agent.market_makers.SpreadBasedMarketMakerAgent import SpreadBasedMarketMakerAgent
+        sub = cfg == "rmsc03_sbmm"
+
+        def factory(id, name, type, symbol, starting_cash, pov, min_order_size, window_size, num_ticks,
+                    wake_up_freq, log_orders, random_state):
+            return SpreadBasedMarketMakerAgent(
+                id, "SPREAD_BASED_MARKET_MAKER_AGENT_{}".format(id), "SpreadBasedMarketMakerAgent", symbol,
+                starting_cash, order_size=min_order_size, window_size=window_size, num_ticks=num_ticks,
+                wake_up_freq=wake_up_freq, subscribe=sub, log_orders=log_orders, random_state=random_state)
+        stub = types.ModuleType("agent.market_makers.POVMarketMakerAgent")
+        stub.POVMarketMakerAgent = factory
+        sys.modules["agent.market_makers.POVMarketMakerAgent"] = stub
+        cfg_script = "rmsc03"
+    else:
+        cfg_script = cfg
     stop_at = None
     if "@" in cfg:  # CFG@HH:MM:SS: Kernel.runner(stopTime=that time of the day) instead of the script's
         cfg, stop_at = cfg.split("@")
@@ -302,14 +334,15 @@ def run_config(cfg, seed, out, full):
             "value_noise": "2019-06-28", "rmsc01": "2019-06-28", "rmsc02": "2019-06-28",
             "obi_rmsc02": "2019-06-28", "random_fund_value": "2019-06-28",
             "random_fund_diverse": "2019-06-28", "hist_fund_value": "2019-06-28",
-            "hist_fund_diverse": "2019-06-28", "marketreplay": replay[1] if replay else None}[cfg]
+            "hist_fund_diverse": "2019-06-28", "marketreplay": replay[1] if replay else None,
+            "rmsc03_sbmm": "2019-06-28", "rmsc03_sbmm_poll": "2019-06-28"}[cfg]
     MIDNIGHT = int(pd.Timestamp(date).value)
-    argv = ["abides.py", "-c", cfg, "-s", str(seed)]
-    if cfg in ("rmsc03", "random_fund_value", "random_fund_diverse"):
+    argv = ["abides.py", "-c", cfg_script, "-s", str(seed)]
+    if cfg_script in ("rmsc03", "random_fund_value", "random_fund_diverse"):
         argv += ["-t", "ABM", "-d", "20190628"]
     if replay:
         argv += ["-t", replay[0], "-d", replay[1]]
-    module = "config." + cfg
+    module = "config." + cfg_script
     if twap is not None:
         module = "config.execution.marketreplay.execution_marketreplay"
         argv[2] = "execution_marketreplay"
@@ -342,7 +375,7 @@ def run_config(cfg, seed, out, full):
     ob = ex.order_books[sym]
 
     def lvl(side):
-        return [[[int(o.order_id), int(o.agent_id), int(o.quantity), _price(o.limit_price)] for o in level] for level in side]
+        return [[[_oid(o.order_id), int(o.agent_id), int(o.quantity), _price(o.limit_price)] for o in level] for level in side]
 
     final = {
         "config": cfg, "seed": seed, "events": len(TRACE),
@@ -369,7 +402,7 @@ def run_config(cfg, seed, out, full):
         h = {k: int(v) for k, v in a.holdings.items()}
         final["agents"].append({
             "id": a.id, "cash": h.get("CASH"), "shares": h.get(sym, 0),
-            "open_orders": [[int(o.order_id), 1 if o.is_buy_order else 0, int(o.quantity), _price(o.limit_price)]
+            "open_orders": [[_oid(o.order_id), 1 if o.is_buy_order else 0, int(o.quantity), _price(o.limit_price)]
                             for o in a.orders.values()],
         })
     tr = np.asarray(TRACE, dtype=np.int64)
@@ -568,7 +601,14 @@ def main():
             # config/execution/marketreplay/execution_marketreplay.py: the replay plus the TWAP
             # execution agent, passive (no -e) and trading (-e)
             ("twap:IBM:2003-01-14", 1, False), ("twap_e:IBM:2003-01-14", 1, True),
-            ("twap:GOOG:2012-06-21", 1, False), ("twap_e:GOOG:2012-06-21", 1, True)]
+            ("twap:GOOG:2012-06-21", 1, False), ("twap_e:GOOG:2012-06-21", 1, True),
+            # rmsc03 with a SpreadBasedMarketMakerAgent in the market maker's slot: subscribe=True
+            # (MARKET_DATA every 10 s) and polling (QUERY_SPREAD every second)
+            ("rmsc03_sbmm", 123456789, True), ("rmsc03_sbmm", 7, False),
+            ("rmsc03_sbmm_poll", 123456789, True), ("rmsc03_sbmm_poll", 7, False),
+            # a polling seed whose first QUERY_SPREAD finds a side empty before any mid was known:
+            # receiveMessage's UnboundLocalError ends the reference's run after 649 pops
+            ("rmsc03_sbmm_poll", 123456798, True)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2] or j[0].startswith(sys.argv[2] + ":")]
     procs = []

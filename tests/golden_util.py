@@ -12,7 +12,8 @@ FIXTURES = [("sparse_zi_100", 123456789), ("rmsc03", 123456789), ("rmsc03", 1008
             ("random_fund_value", 7), ("random_fund_value", 123456789),
             ("random_fund_diverse", 7), ("random_fund_diverse", 123456789),
             ("hist_fund_value", 7), ("hist_fund_value", 123456789),
-            ("hist_fund_diverse", 7), ("hist_fund_diverse", 123456789)]
+            ("hist_fund_diverse", 7), ("hist_fund_diverse", 123456789),
+            ("rmsc03_sbmm", 123456789), ("rmsc03_sbmm", 7), ("rmsc03_sbmm_poll", 123456789), ("rmsc03_sbmm_poll", 7)]
 HIST_CONFIGS = ("hist_fund_value", "hist_fund_diverse")
 FUND = os.path.join(GOLDEN, "fund_JPM_20190628.npz")  # gen_fixtures.py fund_series()
 

@@ -7,6 +7,8 @@ divergence and fails these tests.
 Workloads (seeds as bench.py draws them, shard.env_seeds(batch, rank 0, world 1, n)):
 * rmsc02 x4096, batches 0-2 (bench: warmup 1 + 2 timed steps), obi_rmsc02 x4096, rmsc01 x4096,
   random_fund_value / random_fund_diverse x2048 — Kernel.runner configs (Kernel.py:190-292);
+* rmsc03 with a SpreadBasedMarketMakerAgent (subscribe / polling) x4096: 899 polling envs end in
+  the agent's own UnboundLocalError (oracle -18, device 28);
 * rmsc03_rl x4096 — GymKernel.stepRunner (GymKernel.py:158-306) with a fixed host action stream of
   the bench's distribution (x ~ U(0, 0.01), level shares U(0, 1));
 * marketreplay IBM 2003-01-14 and GOOG 2012-06-21 x512 — ABIDESEnv.step over a whole episode.
@@ -24,7 +26,7 @@ THREADS = min(16, os.cpu_count() or 1)
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 # oracle fail() code -> device env error code (mxa_layout.h ERR_*) for the reference's own crash paths
-ORACLE_TO_DEVICE = {-3: 6, -5: 5, -6: 7, -7: 13, -8: 14, -11: 17, -13: 19, -14: 21, -16: 23}
+ORACLE_TO_DEVICE = {-3: 6, -5: 5, -6: 7, -7: 13, -8: 14, -11: 17, -13: 19, -14: 21, -16: 23, -18: 28}
 GYM_ERR = {-8: (14, 15)}  # get_observation/get_reward (14) or ExecutionAgent.kernelStopping (15)
 
 
@@ -49,7 +51,8 @@ def _check_batch(s, ev, hs, er):
 @pytest.mark.parametrize("cfg,n,batches", [("rmsc02", 4096, (0, 1, 2)), ("obi_rmsc02", 4096, (0,)),
                                            ("rmsc01", 4096, (0,)), ("random_fund_value", 2048, (0,)),
                                            ("random_fund_diverse", 2048, (0,)), ("hist_fund_value", 2048, (0,)),
-                                           ("hist_fund_diverse", 2048, (0,))])
+                                           ("hist_fund_diverse", 2048, (0,)), ("rmsc03_sbmm", 4096, (0,)),
+                                           ("rmsc03_sbmm_poll", 4096, (0,))])
 def test_gpu_bench_batches_equal_oracle(mx, cfg, n, batches):
     from golden_util import market_kw
     m = mx.VecMarket(cfg, shard.env_seeds(batches[0], 0, 1, n), **market_kw(cfg))

@@ -236,3 +236,17 @@ def test_gpu_summary_log_batch_equals_oracle(mx, cfg, n):
         ref = o.summary_log()
         got = m.summary_log(i)
         assert got == ref, (cfg, int(s))
+
+
+def test_gpu_sbmm_unbound_mid_matches_reference(mx):
+    """rmsc03 + SpreadBasedMarketMakerAgent (polling), seed 123456798: the reference's run ends in
+    the agent's UnboundLocalError after 649 pops; the device stops at the same pop with env error
+    28 (ERR_SB_MID) and the same trace"""
+    d, ref = load("rmsc03_sbmm_poll", 123456798)
+    m = mx.VecMarket("rmsc03_sbmm_poll", [123456798], trace_cap=len(ref) + 10)
+    m.run()
+    s = m.summary()
+    assert int(s["status"][0]) == 2 and int(s["err"][0]) == 28
+    assert int(s["events"][0]) == d["events"] == 649
+    tr = m.trace(0)
+    assert first_mismatch(tr, ref) == -1 and len(tr) == len(ref)

@@ -108,3 +108,17 @@ def test_oracle_rmsc01_kernel_stopping_index_error():
     with open(os.path.join(GOLDEN, "rmsc01_123456789_summary.json")) as f:
         summ = json.load(f)
     assert e.summary_log()[:len(summ)] == summ
+
+
+def test_oracle_sbmm_unbound_mid_matches_reference():
+    """rmsc03 + SpreadBasedMarketMakerAgent (polling), seed 123456798: the agent's first
+    QUERY_SPREAD reply has an empty side and no last mid, so receiveMessage reads an unbound `mid`
+    (SpreadBasedMarketMakerAgent.py:100-111) and the reference's run ends in UnboundLocalError
+    after 649 pops; the oracle stops at the same pop with error -18"""
+    d, ref = load("rmsc03_sbmm_poll", 123456798)
+    assert d["stop_error"].startswith("UnboundLocalError")
+    e = pyoracle.OracleEnv("rmsc03_sbmm_poll", 123456798, trace_cap=len(ref) + 10)
+    e.run()
+    assert e.error[0] == -18
+    assert e.events == d["events"] == 649
+    assert first_mismatch(e.trace(), ref) == -1 and len(e.trace()) == len(ref)

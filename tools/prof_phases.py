@@ -14,7 +14,7 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "rmsc03"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 m = mxabides.VecMarket(cfg, (123456789 + np.arange(n)) & 0xFFFFFFFF)
 m.set_parity_hash(os.environ.get("MXA_PROF_HASH", "0") == "1")  # off, as bench.py times it
-buf = (ctypes.c_uint64 * 64)()
+buf = (ctypes.c_uint64 * 128)()
 lib = _lib.load()
 lib.mxa_prof_read(buf)  # clear
 m.reset()
@@ -24,7 +24,7 @@ v = list(buf)
 ev = int(m.summary()["events"].sum())
 names = ["pop+hash+rec_load", "requeue"] + ["%s.%s" % (a, w) for a in ["EX", "ZI", "NOISE", "VALUE", "MM", "MOM"] for w in ["msg", "wake"]]
 names += ["ACCEPTED fast", "CANCELLED fast"]  # phases 14, 15 (counts 28, 29)
-tot = v[0] + v[1] + sum(v[2:16]) + v[30] + v[31] + v[32] + v[33] + sum(v[34:38]) + v[46] + sum(v[48:56])
+tot = v[0] + v[1] + sum(v[2:16]) + v[30] + v[31] + v[32] + v[33] + sum(v[34:38]) + v[46] + sum(v[48:56]) + sum(v[80:84])
 print("events %d  total cycles/event (sum over waves) %.0f" % (ev, tot / ev))
 print("%-20s %8s %10s %12s" % ("phase", "share", "cyc/event", "cyc/call"))
 for i, nm in enumerate(names):
@@ -45,3 +45,13 @@ for i, nm in enumerate(["EX SPREAD_REQ", "EX TV_REQ", "EX LIMIT (single)", "EX C
                         "VALUE SPREAD (place)", "MM SPREAD", "MM TV"]):
     c = v[56 + i]
     print("%-20s %7.1f%% %10.0f %12s" % (nm, 100 * v[48 + i] / tot, v[48 + i] / ev, ("%.0f (%d calls)" % (v[48 + i] / c, c)) if c else ""))
+for i, nm in enumerate(["ZI SPREAD (place)", "ZI ACCEPTED", "ZI EXECUTED", "ZI other msg"]):
+    c = v[112 + i]
+    print("%-20s %7.1f%% %10.0f %12s" % (nm, 100 * v[80 + i] / tot, v[80 + i] / ev, ("%.0f (%d calls)" % (v[80 + i] / c, c)) if c else ""))
+print("inclusive function timers (nested inside the phases above; cycles per call)")
+for slot, nm in [(64, "send"), (65, "q_push"), (66, "handle_limit"), (67, "cancel_order"), (68, "b_best"),
+                 (69, "o_observe"), (70, "bayes_r_T"), (71, "cancel_all"), (72, "place_limit"), (73, "ex_receive"),
+                 (74, "ta_receive"), (75, "ta_wakeup"), (77, "rec_load"), (78, "rng_maint")]:
+    c = v[slot + 32]
+    if c:
+        print("%-20s %10.0f cyc/event %8.0f cyc/call %6.2f calls/event" % (nm, v[slot] / ev, v[slot] / c, c / ev))
