@@ -573,7 +573,11 @@ struct Eng {
 #ifdef MXA_SERIAL_QSCAN
   static constexpr bool QTREE = false;
 #else
+#ifdef MXA_QTREE_ALL
+  static constexpr bool QTREE = QHIER;
+#else
   static constexpr bool QTREE = QHIER && QG >= 4;
+#endif
 #endif
   static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
   // the replay book + tape (ABIDESEnv's composition, or config/marketreplay.py under Kernel.runner)
@@ -1188,6 +1192,18 @@ struct Eng {
     for (int i = PW; i < 8; i++) m.w[i] = 0;
     return m;
   }
+  // the queue's high-water mark (EnvHdr::max_q, a diagnostic): a register for the launch (loaded
+  // and saved with the header) instead of an LDS read-modify-write on every push
+#ifdef MXA_MAXQ_LDS
+  static constexpr bool MAXQ_REG = false;
+#else
+  static constexpr bool MAXQ_REG = !BUILD;
+#endif
+  i32 maxq;
+  DEV void note_max_q() {
+    if constexpr (MAXQ_REG) maxq = qcount > maxq ? qcount : maxq;
+    else if (qcount > h.max_q) h.max_q = qcount;
+  }
   DEV void q_push(u64 key, u32 seq, const Msg& m) {
     PROF_SCOPE(65);
     QM use = qfree;
@@ -1223,7 +1239,7 @@ struct Eng {
       if (lane < PW) qpl[slot * PW + lane] = msel(m, lane);
     }
     qcount++;
-    if (qcount > h.max_q) h.max_q = qcount;
+    note_max_q();
   }
   // One q_push per active lane, in lane order (ranks 0..n-1, seqs seq..seq+n-1): the same
   // (key, seq, message) set as n q_push calls, so the pop order is unchanged; only the slot
@@ -1299,7 +1315,7 @@ struct Eng {
     }
     seq += (u32)n;
     qcount += n;
-    if (qcount > h.max_q) h.max_q = qcount;
+    note_max_q();
   }
   // lexicographic wave-min of the per-lane cached (key, seq); returns winning slot or -1
 #ifdef MXA_KEY96
@@ -4060,6 +4076,7 @@ struct Eng {
     status = h.status;
     err = h.err;
     qcount = h.q_count;
+    maxq = h.max_q;
     if (lane < 4) h.rs_wn[lane] = 0;  // the LDS stream windows did not survive the last launch
     wfence();
   }
@@ -4073,6 +4090,7 @@ struct Eng {
       h.status = status;
       h.err = err;
       h.q_count = qcount;
+      if constexpr (MAXQ_REG) h.max_q = maxq;
     }
     wfence();
     const u64* src = (const u64*)&h;

@@ -154,6 +154,8 @@ def test_gpu_wide_config_equals_oracle(mx, cfg, n):
     ("value_noise", [3, 5, 123456789]),             # grouped queue: 2 groups of 3 slots
     ("sparse_zi_1000", [123456789, 5]),             # grouped queue: 4 groups of 12, payload in HBM
     ("random_fund_value", [123456789, 5]),          # two-tier queue: 2 LDS groups + 6 HBM groups of 12
+    ("rmsc03_sbmm", [123456789, 7]),                # ladder deques in the record, MARKET_DATA subscription
+    ("rmsc03_sbmm_poll", [123456789, 7]),
 ])
 def test_gpu_chunked_launches_equal_single(mx, cfg, seeds):
     """many save/restore cycles of the queue (LDS) and the book (VGPRs): the reload refills the
