@@ -217,7 +217,7 @@ constexpr void params_rmsc03_sbmm(MxaParams& P, bool subscribe) {
   P.sb_wake = NS;
   P.md_sub = subscribe ? 1 : 0;
   P.md_mk_levels = 1;
-  P.md_mom_levels = 1;
+  P.md_mom_levels = 0;  // rmsc03's momentum agents poll (subscribe=False, config/rmsc03.py:180-197)
   P.md_freq = 10 * NS;
 }
 

@@ -554,7 +554,9 @@ struct Eng {
 #define MXA_QG 12  // group size at SQ >= 16 (measured, sparse_zi_1000: 4 -> 1194 ms, 6/8 -> 973, 12 -> 958)
 #endif
 #ifndef MXA_QHIER_MIN
-#define MXA_QHIER_MIN 6  // below 16 slots: two groups (sparse_zi_100, 8 slots: 149 -> 144 ms)
+// grouped minima from 7 slots per lane; 6 slots and fewer take the flat select tree (r03 s29, same
+// per-env results: value_noise 20.7 -> 18.9 ms, rmsc02 1087 -> 1003 ms against two groups of 3)
+#define MXA_QHIER_MIN 7
 #endif
   static constexpr int QG = SQ >= 16 ? MXA_QG : SQ / 2;
 #ifdef MXA_QREG
@@ -1194,10 +1196,14 @@ struct Eng {
   }
   // the queue's high-water mark (EnvHdr::max_q, a diagnostic): a register for the launch (loaded
   // and saved with the header) instead of an LDS read-modify-write on every push
+#ifndef MXA_MAXQ_REG_MASK
+  // r03 s28, same results: sparse_zi_1000 762 -> 736 ms, rmsc02 1096 -> 1084; rmsc03 40.7 -> 42.8 (not set)
+#define MXA_MAXQ_REG_MASK ((1 << MXA_CFG_SPARSE_ZI_1000) | (1 << MXA_CFG_RMSC02))
+#endif
 #ifdef MXA_MAXQ_LDS
   static constexpr bool MAXQ_REG = false;
 #else
-  static constexpr bool MAXQ_REG = !BUILD;
+  static constexpr bool MAXQ_REG = !BUILD && (((MXA_MAXQ_REG_MASK) >> CFG) & 1);
 #endif
   i32 maxq;
   DEV void note_max_q() {
@@ -3219,9 +3225,11 @@ struct Eng {
     double x = ((double)s2 / 2.0) / (double)n;
     return __builtin_rint(x * 100.0) / 100.0;
   }
+  // MomentumAgent subscribe=True (rmsc02 / obi_rmsc02): md_mom_levels > 0; rmsc03's poll
+  static constexpr bool MOM_SUB = MD && PC.md_mom_levels > 0;
   DEV void mom_wakeup() {
     const bool can = ta_wakeup();
-    if constexpr (MD) {  // subscribe=True (MomentumAgent.py:54-62): level-1 data every 10 s
+    if constexpr (MOM_SUB) {  // subscribe=True (MomentumAgent.py:54-62): level-1 data every 10 s
       if (!fl(FL_SUB_REQ)) request_subscription(PC.md_mom_levels);
       return;
     }
@@ -3232,7 +3240,7 @@ struct Eng {
   }
   DEV void mom_receive(const Msg& m) {
     ta_receive(m, AG_MOMENTUM);
-    if constexpr (MD) {  // MomentumAgent.py:71-75: `if bids and asks`, then placeOrders(best bid, best ask)
+    if constexpr (MOM_SUB) {  // MomentumAgent.py:71-75: `if bids and asks`, then placeOrders(best bid, best ask)
       if (rgi(AF_STATE) == AS_AWAITING_MD && m_kind(m) == MK_MARKET_DATA) {
         i32 bid, ask;
         const bool hb = known_bid(bid), ha = known_ask(ask);
