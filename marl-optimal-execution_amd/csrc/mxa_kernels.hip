@@ -554,9 +554,10 @@ struct Eng {
 #define MXA_QG 12  // group size at SQ >= 16 (measured, sparse_zi_1000: 4 -> 1194 ms, 6/8 -> 973, 12 -> 958)
 #endif
 #ifndef MXA_QHIER_MIN
-// grouped minima from 7 slots per lane; 6 slots and fewer take the flat select tree (r03 s29, same
-// per-env results: value_noise 20.7 -> 18.9 ms, rmsc02 1087 -> 1003 ms against two groups of 3)
-#define MXA_QHIER_MIN 7
+// grouped minima from 9 slots per lane; 8 slots and fewer take the flat select tree (same per-env
+// results: r03 s29 value_noise 20.7 -> 18.9 ms, rmsc02 1087 -> 1003 ms against two groups of 3;
+// s31 sparse_zi_100 120.1 -> 116.8 ms against two groups of 4)
+#define MXA_QHIER_MIN 9
 #endif
   static constexpr int QG = SQ >= 16 ? MXA_QG : SQ / 2;
 #ifdef MXA_QREG
@@ -1197,8 +1198,10 @@ struct Eng {
   // the queue's high-water mark (EnvHdr::max_q, a diagnostic): a register for the launch (loaded
   // and saved with the header) instead of an LDS read-modify-write on every push
 #ifndef MXA_MAXQ_REG_MASK
-  // r03 s28, same results: sparse_zi_1000 762 -> 736 ms, rmsc02 1096 -> 1084; rmsc03 40.7 -> 42.8 (not set)
-#define MXA_MAXQ_REG_MASK ((1 << MXA_CFG_SPARSE_ZI_1000) | (1 << MXA_CFG_RMSC02))
+  // same results: r03 s28 sparse_zi_1000 762 -> 736 ms, rmsc02 1096 -> 1084; s31 random_fund_value
+  // 553 -> 541; not set where it cost: rmsc03 40.7 -> 42.8 (s28), rmsc01 1013 -> 1051 (s31)
+#define MXA_MAXQ_REG_MASK ((1 << MXA_CFG_SPARSE_ZI_1000) | (1 << MXA_CFG_RMSC02) | (1 << MXA_CFG_RANDOM_FUND_VALUE) | \
+                           (1 << MXA_CFG_RANDOM_FUND_DIVERSE) | (1 << MXA_CFG_HIST_FUND_VALUE) | (1 << MXA_CFG_HIST_FUND_DIVERSE))
 #endif
 #ifdef MXA_MAXQ_LDS
   static constexpr bool MAXQ_REG = false;

@@ -150,9 +150,9 @@ def test_gpu_wide_config_equals_oracle(mx, cfg, n):
 
 @pytest.mark.parametrize("cfg,seeds", [
     ("rmsc03", [3, 5, 123456789, 1008]),            # flat queue (3 slots per lane)
-    ("sparse_zi_100", [3, 5, 123456789]),           # grouped queue: 2 groups of 4 slots
+    ("sparse_zi_100", [3, 5, 123456789]),           # flat queue (8 slots per lane, select tree)
     ("value_noise", [3, 5, 123456789]),             # flat queue (6 slots per lane, select tree)
-    ("sparse_zi_1000", [123456789, 5]),             # grouped queue: 4 groups of 12, payload in HBM
+    ("sparse_zi_1000", [123456789, 5]),             # grouped queue: 3 groups of 12, payload in HBM
     ("random_fund_value", [123456789, 5]),          # two-tier queue: 2 LDS groups + 6 HBM groups of 12
     ("rmsc03_sbmm", [123456789, 7]),                # ladder deques in the record, MARKET_DATA subscription
     ("rmsc03_sbmm_poll", [123456789, 7]),
