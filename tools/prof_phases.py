@@ -24,7 +24,7 @@ v = list(buf)
 ev = int(m.summary()["events"].sum())
 names = ["pop+hash+rec_load", "requeue"] + ["%s.%s" % (a, w) for a in ["EX", "ZI", "NOISE", "VALUE", "MM", "MOM"] for w in ["msg", "wake"]]
 names += ["ACCEPTED fast", "CANCELLED fast"]  # phases 14, 15 (counts 28, 29)
-tot = v[0] + v[1] + sum(v[2:16]) + v[30] + v[31] + v[32] + v[33] + sum(v[34:38]) + v[46] + sum(v[48:56]) + sum(v[80:84])
+tot = v[0] + v[1] + sum(v[2:16]) + v[30] + v[31] + v[32] + v[33] + sum(v[34:38]) + v[46] + v[47] + sum(v[48:56]) + v[79] + sum(v[80:84])
 print("events %d  total cycles/event (sum over waves) %.0f" % (ev, tot / ev))
 print("%-20s %8s %10s %12s" % ("phase", "share", "cyc/event", "cyc/call"))
 for i, nm in enumerate(names):
@@ -55,3 +55,6 @@ for slot, nm in [(64, "send"), (65, "q_push"), (66, "handle_limit"), (67, "cance
     c = v[slot + 32]
     if c:
         print("%-20s %10.0f cyc/event %8.0f cyc/call %6.2f calls/event" % (nm, v[slot] / ev, v[slot] / c, c / ev))
+if v[47] or v[79]:  # MXA_PROF_WAITS builds
+    print("%-20s %7.1f%% %10.0f" % ("payload wait", 100 * v[47] / tot, v[47] / ev))
+    print("%-20s %7.1f%% %10.0f" % ("record wait", 100 * v[79] / tot, v[79] / ev))
