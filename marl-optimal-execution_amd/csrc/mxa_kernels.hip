@@ -4509,12 +4509,6 @@ struct Eng {
         break;
       }
       Msg m = pl_read(slot);
-#ifdef MXA_PROF_WAITS
-      // diagnostics: the payload's memory latency as a phase of its own (slot 47)
-      PROF_ADD(0, t0);
-      for (int i = 0; i < PW; i++) asm volatile("" ::"v"(m.w[i]));
-      PROF_ADD(47, t0);
-#endif
       i64 t = (i64)(key >> KSH);
       int rcp = (int)((key >> 2) & KRCP);
       int type = (int)(key & 3);
@@ -4614,11 +4608,6 @@ struct Eng {
 #endif
       PROF_ADD(0, t0);
       rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
-#ifdef MXA_PROF_WAITS
-      PROF_ADD(0, t0);
-      asm volatile("" ::"v"(rlo), "v"(rhi));  // the record's latency (slot 79), after the payload's
-      PROF_ADD(79, t0);
-#endif
       cur = t;
       if (INSTR && (hash_on || trace)) {
         if (lane == 0) h.kc[pop_class(key, m)]++;
