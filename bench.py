@@ -417,7 +417,7 @@ class DDQNEngine(Engine):
 
 
 # ----------------------------------------------------------------------------------------------
-def traffic_record(config, envs, parity_hash):
+def traffic_record(config, envs, parity_hash, tape=None):
     """HBM bytes per run-kernel launch from the PMC record of THIS build (profiles/hbm_traffic_<config>.json,
     written by tools/hbm_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
     this same bench command).  A record is attached only when its build id (mxa_build_id(): a hash
@@ -436,6 +436,8 @@ def traffic_record(config, envs, parity_hash):
         why.append("measured on another build")
     if p.get("config") != config or p.get("envs") != envs:
         why.append("other workload")
+    if config == "marketreplay" and p.get("tape", "IBM_2003-01-14") != (tape or "IBM_2003-01-14"):
+        why.append("other tape")  # records without a tape field were measured on the default tape
     if bool(p.get("parity_hash")) != parity_hash:
         why.append("parity hash setting differs")
     src["match"] = not why
@@ -533,7 +535,7 @@ def main():
             else:
                 bpe, bparts, bunits = mc.bytes_per_event(eng.count(args.warmup))
             achieved = bpe * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
-            traffic, tsrc = (traffic_record(args.config, eng.n, bool(args.parity_hash))
+            traffic, tsrc = (traffic_record(args.config, eng.n, bool(args.parity_hash), args.tape)
                              if isinstance(eng, (MarketEngine, GymEngine)) else (None, {"why": "no PMC record for this config"}))
             out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_record": tsrc,
