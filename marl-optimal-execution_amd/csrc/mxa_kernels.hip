@@ -968,20 +968,23 @@ struct Eng {
   // the launch instead of the LDS header (MXA_KREG_MASK): loaded and saved with the header, the
   // window itself stays in LDS
 #ifndef MXA_KREG_MASK
-// r03 s38, same per-env results: rmsc02 1002 -> 927 ms, obi_rmsc02 356 -> 346, value_noise 19.2 -> 18.5,
-// sparse_zi_1000 736 -> 731
-#define MXA_KREG_MASK ((1 << MXA_CFG_SPARSE_ZI_1000) | (1 << MXA_CFG_VALUE_NOISE) | (1 << MXA_CFG_RMSC02) | (1 << MXA_CFG_OBI_RMSC02))
+// same per-env results: r03 s38 rmsc02 1002 -> 927 ms, obi_rmsc02 356 -> 346, value_noise 19.2 -> 18.5,
+// sparse_zi_1000 736 -> 731; s40 (the L stream of the cubic latency model) sparse_zi_100 116.8 -> 114.6
+#define MXA_KREG_MASK ((1 << MXA_CFG_SPARSE_ZI_1000) | (1 << MXA_CFG_VALUE_NOISE) | (1 << MXA_CFG_RMSC02) | \
+                       (1 << MXA_CFG_OBI_RMSC02) | (1 << MXA_CFG_SPARSE_ZI_100))
 #endif
-  static constexpr bool KREG = !BUILD && (((MXA_KREG_MASK) >> CFG) & 1) && PC.lat_mode != 2 && PC.noise_len > 1;
+  // the stream a send draws from: L (latency model, lat_mode 2) or K (the noise of lat_mode 0/1)
+  static constexpr int KS = PC.lat_mode == 2 ? 3 : 2;
+  static constexpr bool KREG = !BUILD && (((MXA_KREG_MASK) >> CFG) & 1) && (PC.lat_mode == 2 || PC.noise_len > 1);
   i32 kp, km, khg, kw0, kwn;
   DEV RS grs_k() {
     RS r;
-    r.key = rng_key(2);
+    r.key = rng_key(KS);
     r.p = kp;
     r.m = km;
     r.hasg = khg;
-    r.gauss = 0.0;  // randint never reads or writes it; the header keeps K's cached gauss
-    r.lw = rwin + 2 * 64;
+    r.gauss = 0.0;  // randint / uniform never read or write it; the header keeps the cached gauss
+    r.lw = rwin + KS * 64;
     r.lw0 = kw0;
     r.lwn = kwn;
     return r;
@@ -992,7 +995,7 @@ struct Eng {
     khg = r.hasg;
     kw0 = r.lw0;
     kwn = r.lwn;
-    dirty |= rs_needs_maint(r) ? 4u : 0u;
+    dirty |= rs_needs_maint(r) ? 1u << KS : 0u;
   }
   DEV void grs_put(int s, const RS& r) {
     h.rs_pos[s] = r.p;
@@ -1011,7 +1014,7 @@ struct Eng {
 #pragma unroll 1
     for (int k = 0; k < 5; k++) {
       if (!((dirty >> k) & 1)) continue;
-      const bool kr = KREG && k == 2;
+      const bool kr = KREG && k == KS;
       const i32 p = kr ? kp : k < 4 ? h.rs_pos[k] : rgi(AF_RS_POS), m = kr ? km : k < 4 ? h.rs_m[k] : rgi(AF_RS_M);
       const i32 hg = kr ? khg : k < 4 ? h.rs_has_gauss[k] : rgi(AF_RS_HASG);
       if (hg & 2) fail(ERR_RNG_OVERRUN);
@@ -1455,9 +1458,16 @@ struct Eng {
     i64 sent = cur + rg64(AF_COMP) + add_delay + delay;
     i64 deliver;
     if (PC.lat_mode == 2) {
-      RS L = grs(3);
-      double x = rs_uniform(L, PC.clip, 1.0);
-      grs_put(3, L);
+      double x;
+      if constexpr (KREG) {
+        RS L = grs_k();
+        x = rs_uniform(L, PC.clip, 1.0);
+        grs_put_k(L);
+      } else {
+        RS L = grs(3);
+        x = rs_uniform(L, PC.clip, 1.0);
+        grs_put(3, L);
+      }
       double mn = cur_agent == 0 ? lat()[recipient] : lat()[PC.n_agents + cur_agent];
       double l = mn + ((PC.jitter / gm_pow(x, 3.0)) * (mn / PC.unit));
       deliver = sent + (i64)l;
@@ -4130,10 +4140,10 @@ struct Eng {
     if (lane < 4) h.rs_wn[lane] = 0;  // the LDS stream windows did not survive the last launch
     wfence();
     if constexpr (KREG) {
-      kp = h.rs_pos[2];
-      km = h.rs_m[2];
-      khg = h.rs_has_gauss[2];
-      kw0 = h.rs_w0[2];
+      kp = h.rs_pos[KS];
+      km = h.rs_m[KS];
+      khg = h.rs_has_gauss[KS];
+      kw0 = h.rs_w0[KS];
       kwn = 0;
     }
   }
@@ -4149,11 +4159,11 @@ struct Eng {
       h.q_count = qcount;
       if constexpr (MAXQ_REG) h.max_q = maxq;
       if constexpr (KREG) {
-        h.rs_pos[2] = kp;
-        h.rs_m[2] = km;
-        h.rs_has_gauss[2] = khg;
-        h.rs_w0[2] = kw0;
-        h.rs_wn[2] = kwn;
+        h.rs_pos[KS] = kp;
+        h.rs_m[KS] = km;
+        h.rs_has_gauss[KS] = khg;
+        h.rs_w0[KS] = kw0;
+        h.rs_wn[KS] = kwn;
       }
     }
     wfence();
