@@ -68,7 +68,9 @@ constexpr int lat_lds(int cfg);
 // configurations whose agent-record write-back stores only the changed 128-byte quarters
 // (bit = config id; measured per configuration)
 #ifndef MXA_DIRTY_WB_MASK
-#define MXA_DIRTY_WB_MASK ((1 << 9) | (1 << 10) | (1 << 11) | (1 << 12))  // r03 s5: random_fund_value 840 -> 795 ms; rmsc03 +2 %, rmsc01 +4 %
+// r03 s5: random_fund_value 840 -> 795 ms; rmsc03 +2 % (s38 on the final build: +5 %); rmsc01 +4 % in s5, but
+// -4.6 % on the final build (s48: 1023 -> 976 ms); rmsc02 unchanged (s48)
+#define MXA_DIRTY_WB_MASK ((1 << 9) | (1 << 10) | (1 << 11) | (1 << 12) | (1 << MXA_CFG_RMSC01))
 #endif
 #ifndef MXA_OPEN_RFD
 #define MXA_OPEN_RFD 128
