@@ -149,13 +149,16 @@ class Engine:
         self.records = torch.zeros((self.n, shard.RECORD_WORDS), dtype=torch.int64, device=ctx.device)
         self.gathered = None
         self.last_batch = None
+        self.errs = torch.zeros((), dtype=torch.int64, device=ctx.device)  # envs in error, every timed batch
 
     def seeds(self, k):
         return self.shard.env_seeds(k, self.ctx.rank, self.ctx.world, self.n)
 
-    def gather(self, k):
+    def gather(self, k, timed=False):
         self.last_batch = k
         self.gathered = self.shard.gather_records(self.records, self.ctx.world)
+        if timed:
+            self.errs += (self.records[:, self.shard.R_STATUS] == 2).sum()
         return self.records[:, self.shard.R_EVENTS].sum()
 
     def check_gathered(self):
@@ -171,8 +174,12 @@ class Engine:
         return {"own_rows_in_place": own, "global_env_order": bool((got == want).all())}
 
     def env_errors(self):
-        g = self.gathered
-        return int((g[:, self.shard.R_STATUS] == 2).sum())
+        """envs that ended in an error over every timed batch of every rank (their events are
+        counted like any other's: the reference's own crash paths end an env the same way)"""
+        e = self.errs.clone()
+        if self.ctx.world > 1:
+            self.ctx.dist.all_reduce(e, op=self.ctx.dist.ReduceOp.SUM)
+        return int(e.item())
 
     has_seeds = True
 
@@ -191,7 +198,7 @@ class StubEngine(Engine):
         r[:, sh.R_STATUS] = 1
         r[:, sh.R_SEED] = s
         self.launches += 1
-        return self.gather(k)
+        return self.gather(k, timed)
 
     def describe(self):
         return {"metric": "launcher self-test (stub engine, no market)", "dtype": "int64", "data": "synthetic",
@@ -207,9 +214,16 @@ class MarketEngine(Engine):
     def __init__(self, args, ctx):
         super().__init__(args, ctx)
         import mxabides
+        from mxabides.configs import REPLAY_CONFIGS
         from mxabides.fundamental import FundamentalSeries
         self.mx = mxabides
         kw = {"fundamental": FundamentalSeries.load(FUND)} if args.config.startswith("hist_fund") else {}
+        self.tname = None
+        if args.config in REPLAY_CONFIGS:  # config/marketreplay.py & co. replay a LOBSTER tape (--tape)
+            from mxabides import tape
+            self.tname = args.tape or "IBM_2003-01-14"
+            kw["tape"] = tape.Tape.load(os.path.join(ROOT, "tests", "golden", "tape_%s.npz" % self.tname))
+            self.has_seeds = False  # nothing in these compositions draws
         self.m = mxabides.VecMarket(args.config, self.seeds(0), device=ctx.local, **kw)
         self.stream = self.torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
         self.torch.cuda.set_stream(self.stream)
@@ -226,7 +240,7 @@ class MarketEngine(Engine):
             self.launches += nl
             self.kernel_ms += m.last_kernel_ms
         m.write_records(self.records.data_ptr())
-        return self.gather(k)
+        return self.gather(k, timed)
 
     def count(self, k):
         """one batch of the timed workload (batch k's seeds) with the instrumentation on: the
@@ -243,6 +257,11 @@ class MarketEngine(Engine):
     def describe(self):
         a, n = self.args, self.n
         metric = METRIC if a.config == "rmsc03" else "env-steps/sec, %s x%d envs per GPU" % (a.config, n)
+        if self.tname:
+            return {"metric": metric + " (%s LOBSTER tape)" % self.tname, "dtype": "int64",
+                    "data": "LOBSTER sample tape %s (every env replays it; nothing draws)" % self.tname,
+                    "workload": "%s x%d envs per GPU, full Kernel.runner episode per step" % (a.config, n),
+                    "agents_per_env": self.m.n_agents}
         return {"metric": metric, "dtype": "int64", "data": "synthetic (per-env seeds; every input built on the device)",
                 "workload": "%s x%d envs per GPU, full episode per step (config build from seeds + the config's "
                             "session), seeds %d+global_env" % (a.config, n, self.shard.SEED0),
@@ -251,6 +270,15 @@ class MarketEngine(Engine):
     def cpu_baseline(self, threads):
         import numpy as np
         import pyoracle
+        if self.tname:  # identical envs: one Kernel.runner episode of the oracle, single-threaded
+            cfg = self.args.config
+            t0 = time.perf_counter()
+            o = pyoracle.OracleReplayRunner(self.m.tape, symbol=self.m.symbol,
+                                            twap=None if cfg == "marketreplay_runner" else cfg.endswith("_e"))
+            o.run()
+            sec = time.perf_counter() - t0
+            return float(o.events) / sec, "1 %s episode on %s, C oracle (oracle/abides_oracle.c), 1 thread, %.1f s " \
+                "wall (reported per thread: every env is the same episode)" % (cfg, self.tname, sec)
         k = self.args.cpu_envs or max(2 * threads, 2048 if self.args.config in ("rmsc03", "sparse_zi_100", "value_noise")
                                       else 8 * threads)
         cseeds = ((self.shard.SEED0 + np.arange(k, dtype=np.int64)) & 0xFFFFFFFF).astype(np.uint32)
@@ -305,7 +333,7 @@ class GymEngine(Engine):
                 e1.record(self.stream)
                 self.ev_pairs.append((e0, e1))
         self.v.write_records(self.records.data_ptr())
-        return self.gather(k)
+        return self.gather(k, timed)
 
     def finish_timing(self):
         kms = [a.elapsed_time(b) for a, b in self.ev_pairs]
@@ -389,7 +417,7 @@ class DDQNEngine(Engine):
         self.v.write_records(self.records.data_ptr())
         # word R_RETURN: the learner's per-env episode return (float64 bits)
         self.records[:, sh.R_RETURN] = r["returns"].to(self.torch.float64).view(self.torch.int64)
-        return self.gather(k)
+        return self.gather(k, timed)
 
     def finish_timing(self):
         kms = [a.elapsed_time(b) for a, b in self.timing]

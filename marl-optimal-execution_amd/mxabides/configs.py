@@ -21,7 +21,9 @@ HIST_CONFIGS = ("hist_fund_value", "hist_fund_diverse")
 REPLAY_CONFIGS = ("marketreplay_runner", "marketreplay_twap", "marketreplay_twap_e")
 
 
-def symbol_of(config, symbol=None):
+def symbol_of(config, symbol=None, tape=None):
+    """the ticker of a configuration's outputs: the caller's -t for the configs that take one; a
+    replay config's default is its tape's ticker (a replay has no default of its own)"""
     if symbol is not None:
         if config not in TICKER_CONFIGS:
             raise ValueError("%s has a fixed symbol (JPM); only %s take -t/--ticker" % (config, TICKER_CONFIGS))
@@ -29,7 +31,10 @@ def symbol_of(config, symbol=None):
     if config in HIST_CONFIGS:
         return "JPM"
     if config in REPLAY_CONFIGS:
-        return "IBM"
+        sym = getattr(tape, "symbol", None)
+        if not sym:
+            raise ValueError("%s: the tape carries no ticker; pass symbol=" % config)
+        return sym
     return "ABM" if config in TICKER_CONFIGS else "JPM"
 
 

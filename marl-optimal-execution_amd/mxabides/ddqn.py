@@ -13,9 +13,9 @@ parallel envs on one device:
   TargetModel (QNets.py:54-60); NNModel_2 (:30-51) by name;
 * epsilon-greedy `choose_action` (:333-362): exploit when U < epsilon and enough experience,
   else `randint(0, n_actions)`; epsilon = epsilon_max unless an increment is given (:100);
-* `train_neural_nets` (:448-515): uniform sampling with replacement, target copy every
-  `replace_target_iter` learn steps before the update, q_next AND q_eval4next both from the
-  TARGET net (so the "double" argmax is the target's own: kept as written), no terminal mask,
+* `train_neural_nets` (:448-515): uniform sampling with replacement; q_next AND q_eval4next
+  from the target net as it stands, THEN the eval -> target copy every `replace_target_iter`
+  learn steps (:508-510), then the update; both from the TARGET net (so the "double" argmax is the target's own: kept as written), no terminal mask,
   one Keras `train_on_batch` (MSE, RMSprop lr 0.01, rho 0.9, eps 1e-7 outside the sqrt,
   TF 2.1 optimizer_v2), then the epsilon update that may overshoot epsilon_max by one step;
 * `compute_reward` (:409-446): per fill (1 - (fill - arrival)/arrival) * qty/q0 * 1e4 (BUY).
@@ -37,8 +37,8 @@ and never under ABIDESEnv. What the composition changes, and why:
 * one learner serves every env (shared replay, one policy); `batch_size`, `train_every` and
   `updates_per_train` default to the reference's 32, 5 and 1.
 
-Everything runs on the device stream the env steps on; the only host reads per step are the
-stored-transition count and the any-env-alive check.
+Everything runs on the device stream the env steps on; the only host read is the stored-transition
+count, when the replay ring's host-side bounds cannot decide the batch-size test.
 """
 import math
 
@@ -163,38 +163,74 @@ class ReplayRing:
 
 
 class DDQNLearner:
-    """DDQLearningExecutionAgent's learner (ddqlearning_execution_agent.py:40-131, 333-362, 448-515)."""
+    """DDQLearningExecutionAgent's learner (ddqlearning_execution_agent.py:40-131, 333-362, 448-515).
+
+    Eval and target parameters each live in one flat device buffer (`eflat`, `tflat`; the
+    modules' parameters are views of it), so the target copy and the RMSprop step are single
+    elementwise passes and every update can be masked on the device: `learn(live=...)` with a
+    device bool makes the whole update (target copy, RMSprop step and its state, epsilon,
+    `learn_step_counter`) a no-op when it is false, without a host read. The counter and epsilon
+    are device scalars for the same reason."""
 
     def __init__(self, n_state=2, n_actions=N_ACTIONS, replace_target_iter=5, batch_size=32, learning_rate=0.01,
                  epsilon_increment=None, epsilon_max=0.9, reward_decay=0.98, mode="train", model="NNModel_1",
-                 dropout=0.1, capacity=1 << 20, device="cuda", seed=0):
+                 dropout=0.1, capacity=1 << 20, device="cuda", seed=0, dtype=torch.float32):
         self.device = torch.device(device)
+        self.dtype = dtype
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         cpu = torch.Generator()
         cpu.manual_seed(seed)
-        self.eval_model = QNet(n_state, n_actions, model, dropout, cpu).to(self.device)
-        self.target_model = QNet(n_state, n_actions, model, dropout, cpu).to(self.device)
+        # EvalModel and TargetModel are two separately initialised Keras models (QNets.py:54-60):
+        # two draws from the same generator, not a copy
+        self.eval_model, self.eflat = self._flat(QNet(n_state, n_actions, model, dropout, cpu))
+        self.target_model, self.tflat = self._flat(QNet(n_state, n_actions, model, dropout, cpu))
         self.n_actions = n_actions
         self.replace_target_iter = replace_target_iter
         self.batch_size = batch_size
         self.learning_rate = learning_rate
         self.epsilon_increment = epsilon_increment
         self.epsilon_max = epsilon_max
-        self.epsilon = 0 if epsilon_increment is not None else epsilon_max  # :100
+        eps0 = 0.0 if epsilon_increment is not None else epsilon_max  # :100
+        self._eps = torch.tensor(eps0, dtype=torch.float64, device=self.device)
         self.reward_decay = reward_decay
         self.mode = mode
-        self.learn_step_counter = 0
-        self.cost_hist = []
+        self._counter = torch.zeros((), dtype=torch.int64, device=self.device)
+        self._costs = []  # (loss, live) device scalars per learn() call
         # Keras RMSprop (TF 2.1 optimizer_v2, momentum 0, not centered): rho 0.9, epsilon 1e-7
-        self.opt = torch.optim.RMSprop(self.eval_model.parameters(), lr=learning_rate, alpha=0.9, eps=1e-7)
+        self.rho, self.rms_eps = 0.9, 1e-7
+        self.rms = torch.zeros_like(self.eflat)
         self.memory = ReplayRing(capacity, n_state, self.device)
+
+    def _flat(self, net):
+        net = net.to(self.device, self.dtype)
+        params = list(net.parameters())
+        flat = torch.cat([p.detach().reshape(-1) for p in params]).contiguous()
+        off = 0
+        for p in params:
+            k = p.numel()
+            p.data = flat[off:off + k].view_as(p)
+            off += k
+        return net, flat
+
+    @property
+    def learn_step_counter(self):
+        return int(self._counter.item())
+
+    @property
+    def epsilon(self):
+        return float(self._eps.item())
+
+    @property
+    def cost_hist(self):
+        """the losses of the updates that ran (host read; not on the step path)"""
+        return [c for c, live in self._costs if bool(live)]
 
     # ---- acting (choose_action, :333-362)
     def q_values(self, s):
         self.eval_model.eval()  # Keras predict(): training=False, no dropout
         with torch.no_grad():
-            return self.eval_model(s.to(self.eval_model.logits.weight.dtype))
+            return self.eval_model(s.to(self.dtype))
 
     def choose_action(self, s):
         """s [n, n_state] -> actions [n] int64 (epsilon-greedy per env in train mode)."""
@@ -204,15 +240,16 @@ class DDQNLearner:
             return greedy
         u = torch.rand(n, generator=self.gen, device=self.device, dtype=torch.float64)
         rnd = torch.randint(0, self.n_actions, (n,), generator=self.gen, device=self.device)
-        exploit = (u < self.epsilon) & self.memory.more_than(self.batch_size - 1)  # len + 1 > batch_size
+        exploit = (u < self._eps) & self.memory.more_than(self.batch_size - 1)  # len + 1 > batch_size
         return torch.where(exploit, greedy, rnd)
 
     # ---- learning (train_neural_nets, :448-515)
     def q_target(self, s, a, s2, r):
-        """the reference's target: both q_next and q_eval4next from the target net."""
+        """the reference's target: both q_next and q_eval4next from the target net (:486-505)."""
         self.target_model.eval()
         self.eval_model.eval()
         with torch.no_grad():
+            s, s2, r = s.to(self.dtype), s2.to(self.dtype), r.to(self.dtype)
             q_next = self.target_model(s2)
             q_eval4next = self.target_model(s2)
             q_eval = self.eval_model(s)
@@ -222,21 +259,40 @@ class DDQNLearner:
             tgt[idx, a] = r + self.reward_decay * q_next[idx, best]
         return tgt
 
-    def learn_on(self, s, a, s2, r):
-        """one train_neural_nets update on a given batch; returns the cost (a device scalar)."""
-        if self.learn_step_counter % self.replace_target_iter == 0:
-            self.target_model.load_state_dict(self.eval_model.state_dict())
+    def learn_on(self, s, a, s2, r, live=None):
+        """one train_neural_nets update on a given batch, in the reference's order: the target
+        from the target net as it stands (:486-505), THEN the eval -> target copy when
+        learn_step_counter % replace_target_iter == 0 (:508-510), then train_on_batch (:513).
+        `live` (device bool, default true) masks the whole update. Returns the loss."""
+        if live is None:
+            live = torch.ones((), dtype=torch.bool, device=self.device)
         tgt = self.q_target(s, a, s2, r)
+        with torch.no_grad():
+            do_copy = live & (self._counter % self.replace_target_iter == 0)
+            self.tflat.copy_(torch.where(do_copy, self.eflat, self.tflat))
         self.eval_model.train()  # train_on_batch: training=True (dropout active)
-        self.opt.zero_grad(set_to_none=True)
-        loss = torch.mean((self.eval_model(s) - tgt) ** 2)
+        for p in self.eval_model.parameters():
+            p.grad = None
+        loss = torch.mean((self.eval_model(s.to(self.dtype)) - tgt) ** 2)
         loss.backward()
-        self.opt.step()
-        self.epsilon = self.epsilon + self.epsilon_increment if self.epsilon < self.epsilon_max else self.epsilon_max
-        self.learn_step_counter += 1
-        return loss.detach()
+        with torch.no_grad():
+            g = torch.cat([p.grad.reshape(-1) for p in self.eval_model.parameters()])
+            rms = self.rho * self.rms + (1 - self.rho) * g * g
+            self.rms.copy_(torch.where(live, rms, self.rms))
+            step = self.learning_rate * g / (torch.sqrt(self.rms) + self.rms_eps)
+            self.eflat.sub_(torch.where(live, step, torch.zeros_like(step)))
+            if self.epsilon_increment is not None:  # :515, may overshoot epsilon_max by one step
+                e = torch.where(self._eps < self.epsilon_max, self._eps + self.epsilon_increment,
+                                torch.full_like(self._eps, self.epsilon_max))
+                self._eps.copy_(torch.where(live, e, self._eps))
+            self._counter += live.to(torch.int64)
+        for p in self.eval_model.parameters():
+            p.grad = None
+        loss = loss.detach()
+        self._costs.append((loss, live))
+        return loss
 
-    def learn(self):
+    def learn(self, live=None):
         """sample a batch with replacement (np.random.choice(current_size, batch)) and update."""
         m = self.memory
         if not m.more_than(self.batch_size):
@@ -244,9 +300,7 @@ class DDQNLearner:
         size = torch.clamp(m.n_dev, max=m.cap).to(torch.float64)  # the current size, on the device
         u = torch.rand(self.batch_size, generator=self.gen, device=self.device, dtype=torch.float64)
         idx = torch.clamp((u * size).to(torch.int64), max=m.cap - 1)
-        cost = self.learn_on(m.s[idx], m.a[idx], m.s2[idx], m.r[idx])
-        self.cost_hist.append(cost)
-        return cost
+        return self.learn_on(m.s[idx], m.a[idx], m.s2[idx], m.r[idx], live=live)
 
 
 class ExecutionTask:
@@ -347,10 +401,11 @@ def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train
         if learner.mode == "train":
             stored += learner.memory.add_device(s, a, s2, r, ok)
             # the reference's agents stop training with their episode: no update on stale replay
-            # once every env is done (one host read, on training steps only)
-            if step_counter % train_every == 0 and bool(alive.any()):
+            # once every env is done; decided on the device (a masked no-op), no host read
+            if step_counter % train_every == 0:
+                live = alive.any()
                 for _ in range(updates_per_train):
-                    learner.learn()
+                    learner.learn(live=live)
         rewards.append(torch.where(ok, r, torch.zeros_like(r)))
         actions.append(a)
         step_counter += 1

@@ -216,7 +216,8 @@ class ABIDESEnv:
     def __init__(self, ticker, date, log_dir=None, seed=None, data_root=".", tape=None, device=0):
         if tape is None:
             f = "%s_%s_34200000_57600000_message_1.csv" % (ticker, date)
-            tape = load_lobster(os.path.join(data_root, "data", "lobster", "LOBSTER_SampleFile_%s_1" % ticker, f), date)
+            tape = load_lobster(os.path.join(data_root, "data", "lobster", "LOBSTER_SampleFile_%s_1" % ticker, f), date,
+                                symbol=ticker)
         self.ticker, self.date, self.log_dir = ticker, date, log_dir
         self.seed = np.random.randint(low=0, high=2 ** 31 - 1) if seed is None else seed  # agents draw nothing
         self._v = VecABIDESEnv(tape, 1, device=device)

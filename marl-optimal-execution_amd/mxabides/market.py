@@ -31,7 +31,7 @@ class VecMarket:
             raise ValueError("unknown config %r (supported: %s)" % (config, sorted(_lib.CONFIG_IDS)))
         self.L = _lib.load()
         self.config = config
-        self.symbol = symbol_of(config, symbol)
+        self.symbol = symbol_of(config, symbol, tape)
         self.book_freq = BOOK_FREQ[config] if book_freq == "config" else book_freq
         self.seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
         self.n_envs = len(self.seeds)

@@ -4,7 +4,7 @@ Envs are independent markets, so a batch shards with no data-path collective: ra
 owns global envs [r*n, (r+1)*n) of every episode batch, and env g always gets seed
 (SEED0 + g) mod 2**32 — results never depend on the world size.  The only
 collective is one all-gather of the per-env episode records
-(events, hash, status, current_time) at episode end: over RCCL/xGMI on the GPU path
+(RECORD_WORDS int64 words: events, hash, status, time, ...) at episode end: over RCCL/xGMI on the GPU path
 (backend "nccl"), over gloo in the CPU tests.
 """
 import numpy as np
@@ -23,7 +23,7 @@ def env_seeds(batch, rank, world, n_per_rank, seed0=SEED0):
 
 
 def gather_records(local, world):
-    """All-gather the [n, RECORD_WORDS] int64 episode records of every rank -> [world * n, 4], rank-major
+    """All-gather the [n, RECORD_WORDS] int64 episode records of every rank -> [world * n, RECORD_WORDS], rank-major
     (= global env order).  One collective per episode batch."""
     if world == 1:
         return local

@@ -8,6 +8,8 @@ SIZE, PRICE (1e-4 $), BUY_SELL_FLAG (1 buy / -1 sell); time = date + 09:30 + (s 
 via pandas Timedelta; PRICE / 100 truncated to int (cents); keep 09:30 <= time < 16:00;
 records grouped by time in file order (`groupby(level=0)`).
 """
+import os
+
 import numpy as np
 
 OPEN = "09:30:00"
@@ -15,9 +17,11 @@ CLOSE = "16:00:00"
 
 
 class Tape:
-    """Time-sorted replay records: t (ns since midnight), oid, price (cents), size, buy."""
+    """Time-sorted replay records: t (ns since midnight), oid, price (cents), size, buy, and the
+    ticker they belong to (`symbol`: the MarketReplayAgent's symbol, config/marketreplay.py -t)."""
 
-    def __init__(self, t, oid, price, size, buy):
+    def __init__(self, t, oid, price, size, buy, symbol=None):
+        self.symbol = symbol
         self.t = np.ascontiguousarray(t, dtype=np.int64)
         self.oid = np.ascontiguousarray(oid, dtype=np.int64)
         self.price = np.ascontiguousarray(price, dtype=np.int64)
@@ -38,15 +42,26 @@ class Tape:
         return len(self.t)
 
     def save(self, path):
-        np.savez_compressed(path, t=self.t, oid=self.oid, price=self.price, size=self.size, buy=self.buy)
+        extra = {"symbol": np.array(self.symbol)} if self.symbol else {}
+        np.savez_compressed(path, t=self.t, oid=self.oid, price=self.price, size=self.size, buy=self.buy, **extra)
 
     @classmethod
-    def load(cls, path):
+    def load(cls, path, symbol=None):
+        """symbol: the ticker; default the one saved with the tape, else the <SYM> of a
+        tape_<SYM>_<date>.npz file name"""
         z = np.load(path, allow_pickle=False)
-        return cls(z["t"], z["oid"], z["price"], z["size"], z["buy"])
+        if symbol is None:
+            if "symbol" in z.files:
+                symbol = str(z["symbol"])
+            else:
+                base = os.path.basename(path)
+                if base.startswith("tape_") and base.count("_") >= 2:
+                    symbol = base.split("_")[1]
+        return cls(z["t"], z["oid"], z["price"], z["size"], z["buy"], symbol=symbol)
 
 
-def load_lobster(path, date):
+def load_lobster(path, date, symbol=None):
+    """symbol: the ticker (default the <SYM> of LOBSTER's <SYM>_<date>_..._message_<k>.csv name)"""
     import pandas as pd
 
     df = pd.read_csv(path, names=["TIMESTAMP", "EVENT_TYPE", "ORDER_ID", "SIZE", "PRICE", "BUY_SELL_FLAG"])
@@ -60,4 +75,6 @@ def load_lobster(path, date):
     price = (df["PRICE"].astype(float) / 100).astype(int).to_numpy().astype(np.int64)[keep]
     buy = (df["BUY_SELL_FLAG"].astype(int) == 1).to_numpy()[keep]
     order = np.argsort(t, kind="stable")
-    return Tape(t[order], oid[order], price[order], size[order], buy[order])
+    if symbol is None:
+        symbol = os.path.basename(path).split("_")[0] or None
+    return Tape(t[order], oid[order], price[order], size[order], buy[order], symbol=symbol)

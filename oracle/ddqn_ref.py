@@ -73,3 +73,20 @@ def rmsprop_step(layers, grads, rms, lr, rho=0.9, eps=1e-7):
 def step_reward(fills, arrival, q0):
     """compute_reward summed over fills [(qty, fill_price)] for a BUY (ddqlearning_execution_agent.py:425-432)"""
     return sum((1 - ((f - arrival) / arrival)) * q / q0 * 10000 for q, f in fills)
+
+
+def train_step(eval_layers, target_layers, rms, counter, batch, lr=0.01, gamma=0.98, replace_target_iter=5):
+    """One whole `train_neural_nets` update (ddqlearning_execution_agent.py:448-515) after the
+    batch is sampled, in the reference's order:
+      1. q_next, q_eval4next from the target net AS IT STANDS, q_eval from eval (:486-505);
+      2. then, if learn_step_counter % replace_target_iter == 0, eval -> target (:508-510);
+      3. then train_on_batch on the eval net (:513): MSE, one RMSprop step;
+      4. epsilon, then learn_step_counter += 1 (:526-530).
+    batch = (s, a, s2, r). Returns (eval', target', rms', counter', loss)."""
+    s, a, s2, r = batch
+    tgt = q_target(eval_layers, target_layers, s, a, s2, r, gamma)
+    if counter % replace_target_iter == 0:
+        target_layers = [(W.copy(), b.copy()) for W, b in eval_layers]
+    loss, grads = mse_grads(eval_layers, s, tgt)
+    eval_layers, rms = rmsprop_step(eval_layers, grads, rms, lr)
+    return eval_layers, target_layers, rms, counter + 1, loss

@@ -68,10 +68,7 @@ def test_dropout_only_in_training():
 
 
 def _learner(**kw):
-    L = ddqn.DDQNLearner(device="cpu", dropout=0.0, seed=3, **kw)
-    L.eval_model.double()
-    L.target_model.double()
-    return L
+    return ddqn.DDQNLearner(device="cpu", dropout=0.0, seed=3, dtype=torch.float64, **kw)
 
 
 def _batch(n=32, seed=5):
@@ -94,24 +91,47 @@ def test_q_target_matches_reference_target():
     np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-9)
 
 
-def test_learn_step_matches_keras_rmsprop_restatement():
+def test_target_and_eval_are_initialised_independently():
+    """EvalModel and TargetModel are separate Keras models (QNets.py:54-60), not a copy"""
     L = _learner()
-    lay = _layers(L.eval_model)
-    rms = [(np.zeros_like(W), np.zeros_like(b)) for W, b in lay]
-    T = lay
-    for it in range(7):
-        s, a, s2, r = _batch(seed=10 + it)
-        if it % 5 == 0:  # replace_target_iter: copy before the update
-            T = [(W.copy(), b.copy()) for W, b in lay]
-        tgt = ddqn_ref.q_target(lay, T, s, a, s2, r, 0.98)
-        loss, grads = ddqn_ref.mse_grads(lay, s, tgt)
-        lay, rms = ddqn_ref.rmsprop_step(lay, grads, rms, 0.01)
-        cost = L.learn_on(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(s2), torch.from_numpy(r))
+    for (W, b), (W2, b2) in zip(_layers(L.eval_model), _layers(L.target_model)):
+        assert not np.array_equal(W, W2)
+
+
+def test_learn_steps_match_reference_train_step():
+    """ddqn_ref.train_step owns the whole update, target copy included (stale target first,
+    then eval -> target every 5th learn step, then RMSprop): 17 updates over 4 target copies
+    from distinct eval/target inits; the test only feeds batches"""
+    L = _learner()
+    ev, tg = _layers(L.eval_model), _layers(L.target_model)
+    rms = [(np.zeros_like(W), np.zeros_like(b)) for W, b in ev]
+    counter = 0
+    for it in range(17):
+        batch = _batch(seed=10 + it)
+        ev, tg, rms, counter, loss = ddqn_ref.train_step(ev, tg, rms, counter, batch)
+        cost = L.learn_on(*(torch.from_numpy(x) for x in batch))
         assert abs(float(cost) - loss) <= 1e-9 * max(1.0, loss), it
-        for (W, b), (W2, b2) in zip(_layers(L.eval_model), lay):
+        for (W, b), (W2, b2) in zip(_layers(L.eval_model), ev):
             np.testing.assert_allclose(W, W2, rtol=1e-9, atol=1e-9)
             np.testing.assert_allclose(b, b2, rtol=1e-9, atol=1e-9)
-    assert L.learn_step_counter == 7
+        for (W, b), (W2, b2) in zip(_layers(L.target_model), tg):
+            np.testing.assert_allclose(W, W2, rtol=1e-9, atol=1e-9)
+            np.testing.assert_allclose(b, b2, rtol=1e-9, atol=1e-9)
+    assert L.learn_step_counter == counter == 17
+
+
+def test_masked_update_is_a_no_op():
+    """learn_on(live=False): no target copy, no RMSprop step or state change, no counter/epsilon
+    advance (the device-side guard run_episode uses once every env is done)"""
+    L = _learner(epsilon_increment=0.1)
+    e0, t0, r0 = L.eflat.clone(), L.tflat.clone(), L.rms.clone()
+    batch = [torch.from_numpy(x) for x in _batch()]
+    L.learn_on(*batch, live=torch.tensor(False))
+    assert torch.equal(L.eflat, e0) and torch.equal(L.tflat, t0) and torch.equal(L.rms, r0)
+    assert L.learn_step_counter == 0 and L.epsilon == 0 and L.cost_hist == []
+    L.learn_on(*batch, live=torch.tensor(True))
+    assert not torch.equal(L.eflat, e0) and torch.equal(L.tflat, e0)  # copied before the update
+    assert L.learn_step_counter == 1 and len(L.cost_hist) == 1
 
 
 def test_epsilon_schedule_overshoots_like_reference():

@@ -6,7 +6,8 @@ divergence and fails these tests.
 
 Workloads (seeds as bench.py draws them, shard.env_seeds(batch, rank 0, world 1, n)):
 * rmsc02 x4096, batches 0-2 (bench: warmup 1 + 2 timed steps), obi_rmsc02 x4096, rmsc01 x4096,
-  random_fund_value / random_fund_diverse x2048 — Kernel.runner configs (Kernel.py:190-292);
+  random_fund_value / random_fund_diverse x2048, sparse_zi_1000 x1024 (rank 0 batch 0 and rank 7
+  of 8 batch 3) — Kernel.runner configs (Kernel.py:190-292);
 * rmsc03 with a SpreadBasedMarketMakerAgent (subscribe / polling) x4096: 899 polling envs end in
   the agent's own UnboundLocalError (oracle -18, device 28);
 * rmsc03_rl x4096 — GymKernel.stepRunner (GymKernel.py:158-306) with a fixed host action stream of
@@ -47,17 +48,24 @@ def _check_batch(s, ev, hs, er):
     assert (s["hash"] == hs).all(), np.nonzero(s["hash"] != hs)[0][:20]
 
 
+# (batch, rank, world) seed sets of shard.env_seeds: batch 0 of rank 0 everywhere; rmsc02's three
+# bench batches; sparse_zi_1000 also the last batch of rank 7 of 8 (bench.py --gpus 8, warmup 1 +
+# steps 3), whose capacities are sized close to the oracle maximum
+B0 = ((0, 0, 1),)
+
+
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("cfg,n,batches", [("rmsc02", 4096, (0, 1, 2)), ("obi_rmsc02", 4096, (0,)),
-                                           ("rmsc01", 4096, (0,)), ("random_fund_value", 2048, (0,)),
-                                           ("random_fund_diverse", 2048, (0,)), ("hist_fund_value", 2048, (0,)),
-                                           ("hist_fund_diverse", 2048, (0,)), ("rmsc03_sbmm", 4096, (0,)),
-                                           ("rmsc03_sbmm_poll", 4096, (0,))])
-def test_gpu_bench_batches_equal_oracle(mx, cfg, n, batches):
+@pytest.mark.parametrize("cfg,n,sets", [("rmsc02", 4096, ((0, 0, 1), (1, 0, 1), (2, 0, 1))), ("obi_rmsc02", 4096, B0),
+                                        ("rmsc01", 4096, B0), ("random_fund_value", 2048, B0),
+                                        ("random_fund_diverse", 2048, B0), ("hist_fund_value", 2048, B0),
+                                        ("hist_fund_diverse", 2048, B0), ("rmsc03_sbmm", 4096, B0),
+                                        ("rmsc03_sbmm_poll", 4096, B0),
+                                        ("sparse_zi_1000", 1024, ((0, 0, 1), (3, 7, 8)))])
+def test_gpu_bench_batches_equal_oracle(mx, cfg, n, sets):
     from golden_util import market_kw
-    m = mx.VecMarket(cfg, shard.env_seeds(batches[0], 0, 1, n), **market_kw(cfg))
-    for b in batches:
-        seeds = shard.env_seeds(b, 0, 1, n)
+    m = mx.VecMarket(cfg, shard.env_seeds(*sets[0], n), **market_kw(cfg))
+    for bset in sets:
+        seeds = shard.env_seeds(*bset, n)
         m.set_seeds(seeds)
         m.reset()
         m.run()

@@ -95,29 +95,37 @@ def _batch(n, seed):
 
 @pytest.mark.parametrize("dtype,rtol,atol", [(torch.float64, 1e-9, 1e-9), (torch.float32, 2e-3, 2e-4)])
 def test_gpu_learner_updates_match_numpy_reference(dtype, rtol, atol):
-    """train_neural_nets on the device (ddqlearning_execution_agent.py:448-515: the target from
-    the target net, MSE, Keras RMSprop with eps outside the sqrt, the target copy every
-    replace_target_iter updates) against oracle/ddqn_ref.py in float64, step by step: exact to
-    1e-9 in float64, within fp32 tolerance for the fp32 learner the bench runs"""
+    """train_neural_nets on the device against oracle/ddqn_ref.train_step, which owns the whole
+    update (ddqlearning_execution_agent.py:448-530: target from the target net as it stands,
+    THEN the eval -> target copy every replace_target_iter steps, then MSE + Keras RMSprop):
+    the test only feeds batches. 18 updates spanning 4 target copies from distinct eval/target
+    inits (QNets.py:54-60); exact to 1e-9 in float64, within fp32 tolerance for the fp32
+    learner the bench runs"""
     import ddqn_ref
-    L = ddqn.DDQNLearner(device="cuda", dropout=0.0, seed=3, batch_size=32)
-    L.eval_model.to(dtype)
-    L.target_model.to(dtype)
-    L.opt = torch.optim.RMSprop(L.eval_model.parameters(), lr=0.01, alpha=0.9, eps=1e-7)
-    lay = _layers(L.eval_model)
-    rms = [(np.zeros_like(W), np.zeros_like(b)) for W, b in lay]
-    T = lay
-    for it in range(12):
+    L = ddqn.DDQNLearner(device="cuda", dropout=0.0, seed=3, batch_size=32, dtype=dtype)
+    ev, tg = _layers(L.eval_model), _layers(L.target_model)
+    assert not np.array_equal(ev[0][0], tg[0][0])
+    rms = [(np.zeros_like(W), np.zeros_like(b)) for W, b in ev]
+    counter = 0
+    dv = lambda x: torch.from_numpy(x).to("cuda", dtype)
+    for it in range(18):
         s, a, s2, r = _batch(32, 100 + it)
-        if it % L.replace_target_iter == 0:
-            T = [(W.copy(), b.copy()) for W, b in lay]
-        tgt = ddqn_ref.q_target(lay, T, s, a, s2, r, 0.98)
-        loss, grads = ddqn_ref.mse_grads(lay, s, tgt)
-        lay, rms = ddqn_ref.rmsprop_step(lay, grads, rms, 0.01)
-        dv = lambda x: torch.from_numpy(x).to("cuda", dtype)
+        ev, tg, rms, counter, loss = ddqn_ref.train_step(ev, tg, rms, counter, (s, a, s2, r))
         cost = L.learn_on(dv(s), torch.from_numpy(a).cuda(), dv(s2), dv(r))
         assert abs(float(cost) - loss) <= max(rtol, 1e-9) * max(1.0, loss) * (1 if dtype == torch.float64 else 10), it
-        for (W, b), (W2, b2) in zip(_layers(L.eval_model), lay):
-            np.testing.assert_allclose(W, W2, rtol=rtol, atol=atol, err_msg="update %d" % it)
-            np.testing.assert_allclose(b, b2, rtol=rtol, atol=atol, err_msg="update %d" % it)
-    assert L.learn_step_counter == 12
+        for net, ref in ((L.eval_model, ev), (L.target_model, tg)):
+            for (W, b), (W2, b2) in zip(_layers(net), ref):
+                np.testing.assert_allclose(W, W2, rtol=rtol, atol=atol, err_msg="update %d" % it)
+                np.testing.assert_allclose(b, b2, rtol=rtol, atol=atol, err_msg="update %d" % it)
+    assert L.learn_step_counter == 18
+
+
+def test_gpu_learner_masked_update_is_a_no_op():
+    """run_episode's device-side guard: an update with live == False changes nothing"""
+    L = ddqn.DDQNLearner(device="cuda", dropout=0.0, seed=3, batch_size=32)
+    e0, t0, r0 = L.eflat.clone(), L.tflat.clone(), L.rms.clone()
+    s, a, s2, r = _batch(32, 7)
+    dv = lambda x: torch.from_numpy(x).to("cuda", torch.float32)
+    L.learn_on(dv(s), torch.from_numpy(a).cuda(), dv(s2), dv(r), live=torch.zeros((), dtype=torch.bool, device="cuda"))
+    assert torch.equal(L.eflat, e0) and torch.equal(L.tflat, t0) and torch.equal(L.rms, r0)
+    assert L.learn_step_counter == 0

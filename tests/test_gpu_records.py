@@ -2,6 +2,9 @@
  agrees with the handle's own readers: summary counters, the env seed, and the
 cash / holdings / mark-to-market gain summed over the trading agents (TradingAgent.markToMarket,
 TradingAgent.py:609-633) or the execution agent's own for a GymKernel handle."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -9,6 +12,7 @@ import torch
 from mxabides import shard
 
 pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def _check(rec, s, seeds):
@@ -21,7 +25,7 @@ def _check(rec, s, seeds):
 
 def test_records_kernel_runner_config():
     import mxabides
-    seeds = [123456789, 7, 1008, 99]
+    seeds = [123456789, 7, 1008, 99]  # the first three are reference fixtures
     m = mxabides.VecMarket("rmsc03", seeds)
     m.run()
     out = torch.zeros((len(seeds), shard.RECORD_WORDS), dtype=torch.int64, device="cuda")
@@ -37,6 +41,15 @@ def test_records_kernel_runner_config():
         assert rec[e, shard.R_HOLD] == sum(a["shares"] for a in ag) == 0  # every trade has two sides
         gain = sum(a["cash"] + (a["last_trade"] * a["shares"] if a["shares"] else 0) - a["starting_cash"] for a in ag)
         assert rec[e, shard.R_GAIN] == gain
+    # the reference's own Kernel.summaryLog of the fixture seeds (tests/golden/rmsc03_<seed>_summary.json):
+    # cash = sum of FINAL_CASH_POSITION, gain = sum of ENDING_CASH - STARTING_CASH (TradingAgent.py:101, 118-123)
+    for e, seed in enumerate(seeds[:3]):
+        with open(os.path.join(GOLD, "rmsc03_%d_summary.json" % seed)) as f:
+            rows = json.load(f)
+        ev = {(r["AgentID"], r["EventType"]): r["Event"] for r in rows}
+        ids = sorted({r["AgentID"] for r in rows})
+        assert rec[e, shard.R_CASH] == sum(ev[(a, "FINAL_CASH_POSITION")] for a in ids), seed
+        assert rec[e, shard.R_GAIN] == sum(ev[(a, "ENDING_CASH")] - ev[(a, "STARTING_CASH")] for a in ids), seed
 
 
 def test_records_gym_handle():
