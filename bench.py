@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU-baseline threads (default: the cores this process may run on, capped by OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample: at least this much wall time")
+    ap.add_argument("--no-latency", action="store_true", help="skip the solo-latency run of the latency bound")
     ap.add_argument("--parity-hash", action="store_true",
                     help="also compute the per-pop parity hash (test instrumentation, off by default: "
                          "tests/test_gpu_hash_switch.py shows every market result is identical either way)")
@@ -57,6 +59,8 @@ def parse():
     return ap.parse_args()
 
 
+# scripts/rmsc03.sh:5-13: the options its sweep passes to config/rmsc03.py (--config rmsc03_sweep)
+SWEEP_OPTIONS = dict(pov=0.05, min_order_size=25, window_size=5, num_ticks=50, wake_up_freq="10S")
 DEFAULT_ENVS = {"marketreplay": 512, "sparse_zi_1000": 1024, "random_fund_value": 2048, "random_fund_diverse": 2048,
                 "hist_fund_value": 2048, "hist_fund_diverse": 2048}
 FUND = os.path.join(ROOT, "tests", "golden", "fund_JPM_20190628.npz")  # hist_fund_*: the JPM mid-price series
@@ -224,12 +228,18 @@ class MarketEngine(Engine):
             self.tname = args.tape or "IBM_2003-01-14"
             kw["tape"] = tape.Tape.load(os.path.join(ROOT, "tests", "golden", "tape_%s.npz" % self.tname))
             self.has_seeds = False  # nothing in these compositions draws
-        self.m = mxabides.VecMarket(args.config, self.seeds(0), device=ctx.local, **kw)
+        cfg = args.config
+        if cfg == "rmsc03_sweep":  # config/rmsc03.py with scripts/rmsc03.sh's --mm-* options in every env
+            from mxabides.configs import mm_params
+            kw["mm_params"] = mm_params(self.n, **SWEEP_OPTIONS)
+            cfg = "rmsc03"
+        self.m = mxabides.VecMarket(cfg, self.seeds(0), device=ctx.local, **kw)
         self.stream = self.torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
         self.torch.cuda.set_stream(self.stream)
         self.m.set_stream(self.stream.cuda_stream)
         self.m.set_parity_hash(args.parity_hash)
-        self.kernel = "mxa_run_kernel<%d> (%s)" % (mxabides.CONFIG_IDS[args.config], args.config)
+        cid = mxabides.CONFIG_IDS[cfg] if args.config != "rmsc03_sweep" else mxabides._lib.MXA_RMSC03_MM
+        self.kernel = "mxa_run_kernel<%d> (%s)" % (cid, args.config)
 
     def step(self, k, timed):
         m = self.m
@@ -257,6 +267,12 @@ class MarketEngine(Engine):
     def describe(self):
         a, n = self.args, self.n
         metric = METRIC if a.config == "rmsc03" else "env-steps/sec, %s x%d envs per GPU" % (a.config, n)
+        if a.config == "rmsc03_sweep":
+            return {"metric": metric, "dtype": "int64", "data": "synthetic (per-env seeds; every input built on the device)",
+                    "workload": "config/rmsc03.py with scripts/rmsc03.sh's options (--mm-pov 0.05 --mm-min-order-size 25 "
+                                "--mm-window-size 5 --mm-num-ticks 50 --mm-wake-up-freq 10S) x%d envs per GPU, full "
+                                "episode per step, seeds %d+global_env" % (n, self.shard.SEED0),
+                    "agents_per_env": self.m.n_agents}
         if self.tname:
             return {"metric": metric + " (%s LOBSTER tape)" % self.tname, "dtype": "int64",
                     "data": "LOBSTER sample tape %s (every env replays it; nothing draws)" % self.tname,
@@ -267,24 +283,63 @@ class MarketEngine(Engine):
                             "session), seeds %d+global_env" % (a.config, n, self.shard.SEED0),
                 "agents_per_env": self.m.n_agents}
 
-    def cpu_baseline(self, threads):
+    def cpu_baseline(self, threads, min_s):
+        """the C oracle on `threads` host threads over whole episodes of this workload's seeds,
+        batch after batch until at least min_s of wall time: (env-steps/s, sample text)"""
         import numpy as np
         import pyoracle
-        if self.tname:  # identical envs: one Kernel.runner episode of the oracle, single-threaded
+        if self.tname:  # identical envs: Kernel.runner episodes of the oracle, single-threaded
             cfg = self.args.config
-            t0 = time.perf_counter()
-            o = pyoracle.OracleReplayRunner(self.m.tape, symbol=self.m.symbol,
-                                            twap=None if cfg == "marketreplay_runner" else cfg.endswith("_e"))
-            o.run()
-            sec = time.perf_counter() - t0
-            return float(o.events) / sec, "1 %s episode on %s, C oracle (oracle/abides_oracle.c), 1 thread, %.1f s " \
-                "wall (reported per thread: every env is the same episode)" % (cfg, self.tname, sec)
-        k = self.args.cpu_envs or max(2 * threads, 2048 if self.args.config in ("rmsc03", "sparse_zi_100", "value_noise")
-                                      else 8 * threads)
-        cseeds = ((self.shard.SEED0 + np.arange(k, dtype=np.int64)) & 0xFFFFFFFF).astype(np.uint32)
-        cev, _, csec = pyoracle.run_batch(self.args.config, cseeds, threads)
-        return float(cev.sum()) / csec, "%d %s envs (seeds %d..), full episodes, C oracle (oracle/abides_oracle.c), " \
-            "%d threads, %.1f s wall" % (k, self.args.config, self.shard.SEED0, threads, csec)
+            ev, sec, k = 0, 0.0, 0
+            while sec < min_s:
+                t0 = time.perf_counter()
+                o = pyoracle.OracleReplayRunner(self.m.tape, symbol=self.m.symbol,
+                                                twap=None if cfg == "marketreplay_runner" else cfg.endswith("_e"))
+                o.run()
+                sec += time.perf_counter() - t0
+                ev += o.events
+                k += 1
+            return float(ev) / sec, "%d %s episodes on %s, C oracle (oracle/abides_oracle.c), 1 thread, %.1f s " \
+                "wall (every env is the same episode)" % (k, cfg, self.tname, sec), 1
+        k = self.args.cpu_envs or max(2 * threads, 256 if self.args.config in ("rmsc03", "sparse_zi_100", "value_noise")
+                                      else 4 * threads)
+        ev, sec, first = 0, 0.0, 0
+        while sec < min_s:
+            cseeds = ((self.shard.SEED0 + first + np.arange(k, dtype=np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+            if self.args.config == "rmsc03_sweep":
+                cev, _, _, csec = pyoracle.run_batch_mm(cseeds, self.m.mm_params[:1].repeat(k), threads)
+            else:
+                cev, _, csec = pyoracle.run_batch(self.args.config, cseeds, threads)
+            ev += int(cev.sum())
+            sec += csec
+            first += k
+        return float(ev) / sec, "%d %s envs (seeds %d..%d), full episodes, C oracle (oracle/abides_oracle.c), " \
+            "%d threads, %.1f s wall" % (first, self.args.config, self.shard.SEED0, self.shard.SEED0 + first - 1, threads,
+                                        sec), threads
+
+    def latency_bound(self):
+        """SURVEY.md §8(d)'s latency bound: resident envs / the per-event latency of one env's
+        serial chain, measured here on one env per CU (256 envs of this workload's seeds, so no
+        wave shares its SIMD): the throughput if every resident wave kept its solo pace"""
+        seeds = self.seeds(0)[:256]
+        kw = {"mm_params": self.m.mm_params[:256]} if getattr(self.m, "mm_params", None) is not None else {}
+        if self.args.config.startswith("hist_fund"):
+            kw["fundamental"] = self.m.fundamental
+        if self.tname:
+            kw["tape"] = self.m.tape
+        s = self.mx.VecMarket(self.args.config, seeds, device=self.ctx.local, **kw)
+        s.set_stream(self.stream.cuda_stream)
+        s.set_parity_hash(self.args.parity_hash)
+        s.run(chunk=self.args.chunk)
+        ms = s.last_kernel_ms
+        ev = s.summary()["events"]
+        s.close()
+        ns = ms * 1e6 / max(1, int(ev.max()))  # the longest env's chain sets the launch's length
+        res = self.m.resident_envs
+        return {"resident_envs": res, "solo_envs": len(seeds), "solo_kernel_ms": ms, "solo_ns_per_event": ns,
+                "bound_env_steps_per_s": res / (ns * 1e-9),
+                "how": "256 envs (one per CU) of this workload's seeds: kernel time / the longest env's events; "
+                       "resident envs = run-kernel occupancy x CUs (mxa_resident_envs)"}
 
 
 class GymEngine(Engine):
@@ -365,22 +420,28 @@ class GymEngine(Engine):
     def gym_steps(self):
         return self.n * self.ctx.world * self.n_steps
 
-    def cpu_baseline(self, threads):
+    def cpu_baseline(self, threads, min_s):
         import numpy as np
         import pyoracle
-        k = self.args.cpu_envs or (64 * threads if self.replay else 128 * threads)
-        rs = np.random.RandomState(0)
-        acts = rs.uniform(0, 1, (self.n_steps, k, 3))
-        acts[:, :, 0] *= 0.01
-        if self.replay:
-            r = pyoracle.gym_batch(acts, threads, tape=self.tp)
-            what = "%d %s episodes" % (k, self.tname)
-        else:
-            sd = ((self.shard.SEED0 + np.arange(k, dtype=np.int64)) & 0xFFFFFFFF).astype(np.uint32)
-            r = pyoracle.gym_batch(acts, threads, seeds=sd)
-            what = "%d rmsc03_rl episodes (seeds %d..)" % (k, self.shard.SEED0)
-        return float(r["events"].sum()) / r["seconds"], "%s, U(0, 0.01) actions, C oracle GymKernel batch " \
-            "(oracle/abides_oracle.c ora_gym_batch), %d threads, %.1f s wall" % (what, threads, r["seconds"])
+        k = self.args.cpu_envs or (4 * threads if self.replay else 16 * threads)
+        ev, sec, first, b = 0, 0.0, 0, 0
+        while sec < min_s:
+            rs = np.random.RandomState(b)
+            acts = rs.uniform(0, 1, (self.n_steps, k, 3))
+            acts[:, :, 0] *= 0.01
+            if self.replay:
+                r = pyoracle.gym_batch(acts, threads, tape=self.tp)
+            else:
+                sd = ((self.shard.SEED0 + first + np.arange(k, dtype=np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+                r = pyoracle.gym_batch(acts, threads, seeds=sd)
+            ev += int(r["events"].sum())
+            sec += r["seconds"]
+            first += k
+            b += 1
+        what = ("%d %s episodes" % (first, self.tname) if self.replay else
+                "%d rmsc03_rl episodes (seeds %d..%d)" % (first, self.shard.SEED0, self.shard.SEED0 + first - 1))
+        return float(ev) / sec, "%s, U(0, 0.01) actions, C oracle GymKernel batch (oracle/abides_oracle.c " \
+            "ora_gym_batch), %d threads, %.1f s wall" % (what, threads, sec), threads
 
 
 class DDQNEngine(Engine):
@@ -443,6 +504,14 @@ class DDQNEngine(Engine):
     def gym_steps(self):
         return int(self.env_steps.item()) * self.ctx.world  # every rank steps its own envs alike
 
+    def cpu_baseline(self, threads, min_s):
+        """the market side on the host: the same rmsc03 + DummyRL GymKernel composition in the C
+        oracle under random actions (no learner on the host side)"""
+        g = GymEngine.__new__(GymEngine)
+        g.args, g.shard, g.replay, g.n_steps = self.args, self.shard, False, 27
+        v, sample, th = GymEngine.cpu_baseline(g, threads, min_s)
+        return v, sample + "; market only, the learner is not part of the CPU figure", th
+
 
 # ----------------------------------------------------------------------------------------------
 def traffic_record(config, envs, parity_hash, tape=None):
@@ -489,7 +558,18 @@ def host_info():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    return {"nproc": os.cpu_count(), "affinity_cpus": avail, "cpu_model": model}
+    phys = set()
+    try:  # distinct (package, core) pairs: the physical cores of the host
+        base = "/sys/devices/system/cpu"
+        for d in os.listdir(base):
+            if d.startswith("cpu") and d[3:].isdigit():
+                t = os.path.join(base, d, "topology")
+                with open(os.path.join(t, "physical_package_id")) as f1, open(os.path.join(t, "core_id")) as f2:
+                    phys.add((f1.read().strip(), f2.read().strip()))
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity_cpus": avail, "cpu_model": model,
+            "physical_cores": len(phys) or os.cpu_count()}
 
 
 def cpu_threads(args, info):
@@ -561,7 +641,8 @@ def main():
             if args.no_count:
                 bpe, bparts, bunits = float(NOMINAL_BYTES_PER_EVENT), None, None
             else:
-                bpe, bparts, bunits = mc.bytes_per_event(eng.count(args.warmup))
+                eng.last_counters = eng.count(args.warmup)
+                bpe, bparts, bunits = mc.bytes_per_event(eng.last_counters)
             achieved = bpe * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
             traffic, tsrc = (traffic_record(args.config, eng.n, bool(args.parity_hash), args.tape)
                              if isinstance(eng, (MarketEngine, GymEngine)) else (None, {"why": "no PMC record for this config"}))
@@ -575,12 +656,34 @@ def main():
                                "nominal_bytes_per_event": NOMINAL_BYTES_PER_EVENT}
             if traffic:
                 out["roofline"]["traffic_per_event"] = traffic / my_ev_per_launch
+            if not args.no_count:
+                strict = mc.strict_bytes_per_event(eng.last_counters)
+                a_strict = strict * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
+                out["roofline"]["strict"] = {
+                    "algo_bytes_per_event": strict, "achieved": a_strict, "frac": a_strict / HBM_PEAK_GBS,
+                    "rule": "SURVEY.md §8(d) read literally: 2 x 64 B agent record on every pop (the counted figure "
+                            "charges it only where an event loads the recipient's state)"}
+            if hasattr(eng, "latency_bound") and not args.no_latency:
+                lb = eng.latency_bound()
+                lb["achieved_env_steps_per_s"] = my_ev_per_launch / (avg_ms * 1e-3)
+                lb["frac"] = lb["achieved_env_steps_per_s"] / lb["bound_env_steps_per_s"]
+                out["roofline"]["latency_bound"] = lb
             if not args.no_cpu and hasattr(eng, "cpu_baseline"):
                 info = host_info()
                 th = cpu_threads(args, info)
-                v, sample = eng.cpu_baseline(th)
-                out["cpu_baseline"] = {"value": v, "unit": "env-steps/s", "cores": th, "kind": "port", "sample": sample,
-                                       "per_core": v / th, **info}
+                v, sample, used = eng.cpu_baseline(th, args.cpu_seconds)
+                v1, sample1, _ = eng.cpu_baseline(1, min(5.0, args.cpu_seconds))
+                phys = info["physical_cores"]
+                out["cpu_baseline"] = {
+                    "value": v, "unit": "env-steps/s", "cores": used, "kind": "port", "sample": sample, "per_core": v / used,
+                    "single_thread": {"value": v1, "sample": sample1},
+                    "physical_cores_extrapolated": {
+                        "value": v1 * phys, "cores": phys,
+                        "how": "single-thread figure x physical cores (SMT siblings not counted); NOT measured: a "
+                               "GPU box grants this process %d CPUs, so the host's other cores are not ours to load; "
+                               "the %d-thread figure / (%d x single-thread) = %.2f is the scaling seen up to that "
+                               "share" % (used, used, used, v / (used * v1))},
+                    **info}
         print(json.dumps(out), flush=True)
     ctx.close()
 

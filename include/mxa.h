@@ -8,6 +8,7 @@
  *
  * Reference interfaces replaced (file:line in yutiansut/marl-optimal-execution):
  *   mxa_create ......... config/{rmsc01,rmsc02,obi_rmsc02,rmsc03,sparse_zi_100,sparse_zi_1000,value_noise}.py module body
+ *   mxa_create_params .. config/rmsc03.py with its --mm-* options (config/rmsc03.py:39-43), per env
  *                        (and rmsc03 with SpreadBasedMarketMakerAgent.py:17-297, MXA_RMSC03_SBMM*)
  *                        (agent/oracle/kernel construction, global-RNG draw order) and
  *                        Kernel.__init__ (Kernel.py:13-46)
@@ -55,7 +56,10 @@ enum { MXA_RMSC03 = 0, MXA_SPARSE_ZI_100 = 1, MXA_SPARSE_ZI_1000 = 2, MXA_MARKET
        /* config/rmsc03.py with agent/market_makers/SpreadBasedMarketMakerAgent.py in the market maker's
         * slot (no reference config uses that agent; composition of tests/golden/gen_fixtures.py):
         * subscribe=True (level-1 MARKET_DATA every 10 s) and the polling mode (QUERY_SPREAD every second) */
-       MXA_RMSC03_SBMM = 15, MXA_RMSC03_SBMM_POLL = 16 };
+       MXA_RMSC03_SBMM = 15, MXA_RMSC03_SBMM_POLL = 16,
+       /* config/rmsc03.py with per-env market-maker options: the handles of mxa_create_params.
+        * mxa_create(MXA_RMSC03_MM, ...) gives every env the script's defaults (mxa_mm_defaults) */
+       MXA_RMSC03_MM = 17 };
 enum {
   MXA_OK = 0, MXA_EINVAL = -1, MXA_EHIP = -2, MXA_ENOMEM = -3, MXA_ERANGE = -4
 };
@@ -99,6 +103,31 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
  * interpolated exactly as getPriceAtTime / getInterpolatedPrice do (ExternalFileOracle.py:52-159). */
 int mxa_create_hist(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t device, int32_t trace_cap,
                     const int64_t* fund_t, const double* fund_v, int32_t n_fund, mxa_handle** out);
+/* config/rmsc03.py's market-maker options (config/rmsc03.py:39-43, 158-177), the parameters its
+ * only driver script sweeps (scripts/rmsc03.sh:5-13, 29-39).  They reach POVMarketMakerAgent.__init__
+ * only (POVMarketMakerAgent.py:19-60) and change no draw. */
+typedef struct {
+  double mm_pov;               /* --mm-pov (default 0.05) */
+  int32_t mm_min_order_size;   /* --mm-min-order-size (20) */
+  int32_t mm_window_size;      /* --mm-window-size (5) */
+  int32_t mm_num_ticks;        /* --mm-num-ticks (20): a ladder of 2 * (num_ticks + 1) orders */
+  int32_t pad;
+  int64_t mm_wake_up_freq_ns;  /* --mm-wake-up-freq as pd.Timedelta(freq).value ("1S": 1e9) */
+} mxa_mm_params;
+mxa_mm_params mxa_mm_defaults(void);
+/* config/rmsc03.py -s seeds[i] --mm-* per_env[i] for every env i: a parameter sweep is one batch.
+ * config must be MXA_RMSC03; the handle's instantiation (MXA_RMSC03_MM) reads the options from the
+ * market maker's record and holds 320 pending events, 192 resting orders and 256 open orders per
+ * agent (scripts/rmsc03.sh's 50 ticks peak at 266 / 122 / 204); beyond that an env stops with a
+ * capacity error, never silently.  MXA_EINVAL for options the script cannot run (negative
+ * window or ticks, wake-up period <= 0). */
+int mxa_create_params(int32_t config, int32_t n_envs, const uint32_t* seeds, const mxa_mm_params* per_env,
+                      int32_t device, int32_t trace_cap, mxa_handle** out);
+/* replace the options the next mxa_reset builds with (handles of mxa_create_params) */
+int mxa_set_mm_params(mxa_handle* h, const mxa_mm_params* per_env);
+/* envs of the handle resident on the device at once (run / step kernel occupancy x CUs, at most
+ * n_envs): the resident waves of the latency bound */
+int mxa_resident_envs(const mxa_handle* h);
 /* rebuild envs from their seeds (env_mask: NULL = all) — runs the config construction.  On a
  * GymKernel handle (mxa_create_replay, MXA_RMSC03_RL) a reset is ABIDESEnv.reset in the same
  * process: Order.order_id / Order._order_ids carry over from the env's previous episode

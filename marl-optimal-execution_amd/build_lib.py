@@ -14,7 +14,7 @@ SRC = os.path.join(HERE, "csrc", "mxa_api.hip")
 INST = os.path.join(HERE, "csrc", "mxa_inst.hip")
 OUT = os.path.join(HERE, "lib", "libmxa.so")
 OBJ = os.path.join(HERE, "build")
-N_CONFIGS = 17  # csrc/mxa_entry.h MXA_N_CONFIGS
+N_CONFIGS = 18  # csrc/mxa_entry.h MXA_N_CONFIGS
 DEPS = ["mxa_api.hip", "mxa_inst.hip", "mxa_entry.h", "mxa_kernels.hip", "mxa_layout.h", "mxa_config.h", "glibc_math.h",
         "glibc_math_tables.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -191,6 +192,10 @@ struct mxa_handle {
   size_t tb_t, tb_oid, tb_dense, tb_price, tb_size, tb_buy, tb_tm, tb_tm0, tb_uid, tb_ufirst;
   bool ext = false;  // ExternalFileOracle configurations: the fundamental series in d_tape
   size_t tb_fs_t = 0, tb_fs_v = 0;
+  // MXA_RMSC03_MM: per-env market-maker options (config/rmsc03.py --mm-*), read by every build
+  std::vector<MmParams> mm;
+  MmParams* d_mmp = nullptr;
+  mxa_occ_fn occ = nullptr;  // resident waves per CU of the handle's measured kernel
 };
 
 static int hip_fail(mxa_handle* h, hipError_t e, const char* what) {
@@ -229,6 +234,7 @@ static bool bind(mxa_handle* h, int cfg) {
   case 14: e = mxa_entry_14(); break;
   case 15: e = mxa_entry_15(); break;
   case 16: e = mxa_entry_16(); break;
+  case 17: e = mxa_entry_17(); break;
 #endif
   default: return false;
   }
@@ -241,6 +247,7 @@ static bool bind(mxa_handle* h, int cfg) {
   h->step = e.step;
   h->step_fast = e.step_fast;
   h->gym = e.step != nullptr;
+  h->occ = e.occ;
   h->lds = mxa_cfg::lds_bytes(cfg);
   return true;
 }
@@ -273,9 +280,19 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
                     (int)MXA_MARKETREPLAY_RUNNER == (int)MXA_CFG_MARKETREPLAY_RUNNER &&
                     (int)MXA_MARKETREPLAY_TWAP == (int)MXA_CFG_MARKETREPLAY_TWAP &&
                     (int)MXA_RMSC03_SBMM == (int)MXA_CFG_RMSC03_SBMM &&
-                    (int)MXA_RMSC03_SBMM_POLL == (int)MXA_CFG_RMSC03_SBMM_POLL,
+                    (int)MXA_RMSC03_SBMM_POLL == (int)MXA_CFG_RMSC03_SBMM_POLL &&
+                    (int)MXA_RMSC03_MM == (int)MXA_CFG_RMSC03_MM,
                 "config ids");
-  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_RMSC03_SBMM_POLL + 1, "one entry per configuration");
+  static_assert(MXA_N_CONFIGS == (int)MXA_CFG_RMSC03_MM + 1, "one entry per configuration");
+  static_assert(sizeof(mxa_mm_params) == sizeof(MmParams) && offsetof(mxa_mm_params, mm_wake_up_freq_ns) ==
+                    offsetof(MmParams, wake_up_freq) && offsetof(mxa_mm_params, mm_num_ticks) == offsetof(MmParams, num_ticks),
+                "mxa_mm_params is MmParams");
+  if (config == MXA_RMSC03_MM) {  // the config script's defaults in every env
+    std::vector<mxa_mm_params> d(n_envs > 0 ? n_envs : 0);
+    for (auto& x : d) x = mxa_mm_defaults();
+    delete h;
+    return mxa_create_params(MXA_RMSC03, n_envs, seeds, d.data(), device, trace_cap, out);
+  }
   // replay handles: mxa_create_replay(_runner); ExternalFileOracle configurations: mxa_create_hist
   if (config == MXA_MARKETREPLAY || config == MXA_MARKETREPLAY_RUNNER || config == MXA_MARKETREPLAY_TWAP ||
       config == MXA_HIST_FUND_VALUE ||
@@ -292,6 +309,68 @@ int mxa_create(int32_t config, int32_t n_envs, const uint32_t* seeds, int32_t de
     h->P.L.env_stride = h->ctx.L.end;
   }
   return create_common(h, n_envs, seeds, device, out);
+}
+
+static int check_mm(const mxa_mm_params* p, int n) {
+  for (int i = 0; i < n; i++) {
+    const mxa_mm_params& x = p[i];
+    // the reference raises nowhere on these, but a negative window / tick count, a
+    // non-positive wake-up period or a size beyond int32 is no option the script can run
+    if (!(x.mm_pov == x.mm_pov) || x.mm_pov < 0 || x.mm_pov > 1e6 || x.mm_min_order_size < 0 || x.mm_window_size < 0 ||
+        x.mm_num_ticks < 0 || x.mm_num_ticks > 100000 || x.mm_wake_up_freq_ns <= 0)
+      return MXA_EINVAL;
+  }
+  return MXA_OK;
+}
+
+mxa_mm_params mxa_mm_defaults(void) {
+  mxa_mm_params p{};
+  const MxaParams P = mxa_cfg::params(MXA_CFG_RMSC03);
+  p.mm_pov = P.mm_pov;
+  p.mm_min_order_size = P.mm_min_size;
+  p.mm_window_size = P.mm_window;
+  p.mm_num_ticks = P.mm_ticks;
+  p.mm_wake_up_freq_ns = P.mm_wake;
+  return p;
+}
+
+// config/rmsc03.py with each env's market-maker options; see include/mxa.h
+int mxa_create_params(int32_t config, int32_t n_envs, const uint32_t* seeds, const mxa_mm_params* per_env,
+                      int32_t device, int32_t trace_cap, mxa_handle** out) {
+  if (!out || n_envs <= 0 || !seeds || !per_env || trace_cap < 0 || config != MXA_RMSC03) return MXA_EINVAL;
+  if (check_mm(per_env, n_envs)) return MXA_EINVAL;
+  mxa_handle* h = new mxa_handle();
+  if (!bind(h, MXA_CFG_RMSC03_MM)) {
+    delete h;
+    return MXA_EINVAL;
+  }
+  h->P = mxa_cfg::params(MXA_CFG_RMSC03_MM);
+  h->P.n_envs = n_envs;
+  h->P.L.trace_cap = trace_cap;
+  h->P.L.env_stride = mxa_cfg::env_stride(MXA_CFG_RMSC03_MM, trace_cap);
+  h->mm.assign((const MmParams*)per_env, (const MmParams*)per_env + n_envs);
+  return create_common(h, n_envs, seeds, device, out);
+}
+
+int mxa_set_mm_params(mxa_handle* h, const mxa_mm_params* per_env) {
+  if (!h || !per_env || !h->d_mmp) return MXA_EINVAL;
+  if (check_mm(per_env, h->P.n_envs)) return MXA_EINVAL;
+  HIPCHK(h, hipSetDevice(h->device));
+  memcpy(h->mm.data(), per_env, sizeof(MmParams) * h->P.n_envs);
+  HIPCHK(h, hipMemcpyAsync(h->d_mmp, h->mm.data(), sizeof(MmParams) * h->P.n_envs, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
+int mxa_resident_envs(const mxa_handle* h) {
+  if (!h || !h->occ) return MXA_EINVAL;
+  int dev = 0, cus = 0;
+  if (hipSetDevice(h->device) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return MXA_EHIP;
+  const int per_cu = h->occ(h->lds);
+  if (per_cu < 0) return MXA_EHIP;
+  return per_cu * cus < h->P.n_envs ? per_cu * cus : h->P.n_envs;
 }
 
 // config/hist_fund_value.py / hist_fund_diverse.py: the ExternalFileOracle's series is the
@@ -362,14 +441,19 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
     h->ctx.fs_t = (const int64_t*)(h->d_tape + h->tb_fs_t);
     h->ctx.fs_v = (const double*)(h->d_tape + h->tb_fs_v);
   }
-  if (h->gym || h->ext || h->replay) {
+  if (!h->mm.empty()) {
+    HIPCHK(h, hipMalloc(&h->d_mmp, sizeof(MmParams) * n_envs));
+    HIPCHK(h, hipMemcpyAsync(h->d_mmp, h->mm.data(), sizeof(MmParams) * n_envs, hipMemcpyHostToDevice, h->stream));
+    h->ctx.mmp = h->d_mmp;
+  }
+  if (h->gym || h->ext || h->replay || !h->mm.empty()) {
     HIPCHK(h, hipMalloc(&h->d_ctx, sizeof(RpCtx)));
     HIPCHK(h, hipMemcpyAsync(h->d_ctx, &h->ctx, sizeof(RpCtx), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMalloc(&h->d_act, sizeof(double) * 3 * n_envs));
     HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 9 * n_envs));
     HIPCHK(h, hipMalloc(&h->d_flags, sizeof(int32_t) * n_envs));
   }
-  if (h->gym || h->ext || h->replay) HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->gym || h->ext || h->replay || !h->mm.empty()) HIPCHK(h, hipStreamSynchronize(h->stream));
   const int rc = mxa_reset(h, nullptr);  // a fresh process: ids from 0
   h->persist_ids = h->gym;               // later resets continue the process (Order.py:8-9)
   return rc;
@@ -940,6 +1024,7 @@ void mxa_destroy(mxa_handle* h) {
   if (h->d_count) hipFree(h->d_count);
   if (h->d_tape) hipFree(h->d_tape);
   if (h->d_ctx) hipFree(h->d_ctx);
+  if (h->d_mmp) hipFree(h->d_mmp);
   if (h->d_act) hipFree(h->d_act);
   if (h->d_obs) hipFree(h->d_obs);
   if (h->d_flags) hipFree(h->d_flags);

@@ -105,6 +105,11 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_RMSC03_SBMM ? Shape{3, 2, true, 4, 8, 0}
        : cfg == MXA_CFG_RMSC03_SBMM_POLL ? Shape{3, 2, true, 4, 6, 0}
        : cfg == MXA_CFG_RMSC03_RL ? Shape{3, 2, true, 4, 8, 2 * MXA_HOT_RECORDS}  // wide spread replies (depth 500)
+       // rmsc03 with per-env market-maker options: scripts/rmsc03.sh's 50 ticks (a 102-order ladder)
+       // peak at 266 pending events and 122 resting orders (oracle, 4,096 seeds of the script's
+       // options and of a mixed grid: pov 0.01-0.2, sizes 10-50, windows 1-10, 5-50 ticks, 1-60 s);
+       // 320 queue slots, 192 book slots; the LDS queue holds the wave count to 3 per SIMD
+       : cfg == MXA_CFG_RMSC03_MM ? Shape{5, 3, true, 3, 6, 0}
        // rmsc01: oracle maxima over seeds 123456789 / 7: 140 pending events, 75 resting orders;
        // wide replies for the market maker's depth-5 spread queries
        : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, MXA_RMSC01_WAVES, 8, 0}
@@ -199,6 +204,18 @@ constexpr void params_rmsc03(MxaParams& P) {
   P.L.open_cap = 128;
   P.L.tx_cap = 256;
   P.L.lat_len = 0;
+}
+
+// config/rmsc03.py with its market-maker options per env (--mm-pov, --mm-min-order-size,
+// --mm-window-size, --mm-num-ticks, --mm-wake-up-freq; config/rmsc03.py:39-43, 158-177): the
+// values here are the defaults, the build kernel writes each env's into the market maker's
+// record.  The market maker's open orders peak at twice its ladder (the cancelled ladder stays
+// in TradingAgent.orders until ORDER_CANCELLED): 204 at 50 ticks, so 256 per agent
+constexpr void params_rmsc03_mm(MxaParams& P) {
+  params_rmsc03(P);
+  P.config = MXA_CFG_RMSC03_MM;
+  P.mm_rt = 1;
+  P.L.open_cap = 256;
 }
 
 // rmsc03 with a SpreadBasedMarketMakerAgent in its market maker's slot (agent 61), built from the
@@ -581,6 +598,7 @@ constexpr void params_value_noise(MxaParams& P) {
 constexpr MxaParams params(int cfg) {
   MxaParams P{};
   if (cfg == MXA_CFG_RMSC03) params_rmsc03(P);
+  else if (cfg == MXA_CFG_RMSC03_MM) params_rmsc03_mm(P);
   else if (cfg == MXA_CFG_RMSC03_SBMM || cfg == MXA_CFG_RMSC03_SBMM_POLL) params_rmsc03_sbmm(P, cfg == MXA_CFG_RMSC03_SBMM);
   else if (cfg == MXA_CFG_RMSC03_RL) params_rmsc03_rl(P);
   else if (cfg == MXA_CFG_MARKETREPLAY) params_marketreplay(P);

@@ -18,12 +18,15 @@ typedef void (*mxa_stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, in
 typedef void (*mxa_step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*,
                             const double*, double*, int32_t*);
 
+typedef int (*mxa_occ_fn)(size_t);  // resident blocks (envs) per CU of the measured kernel at that LDS size
+
 struct MxaEntry {
   mxa_build_fn build;
   mxa_run_fn run, run_log;     // run_log: the book-update-log variant (plain Kernel.runner configs)
   mxa_run_fn run_fast;         // without the parity instrumentation (hash off, no trace ring)
   mxa_stop_fn stop, stop_log;
   mxa_step_fn step, step_fast; // GymKernel configurations (step_fast: without the instrumentation)
+  mxa_occ_fn occ;              // hipOccupancyMaxActiveBlocksPerMultiprocessor of run_fast / step_fast
 };
 
 MxaEntry mxa_entry_0();
@@ -43,4 +46,5 @@ MxaEntry mxa_entry_13();
 MxaEntry mxa_entry_14();
 MxaEntry mxa_entry_15();
 MxaEntry mxa_entry_16();
-#define MXA_N_CONFIGS 17
+MxaEntry mxa_entry_17();
+#define MXA_N_CONFIGS 18

@@ -33,6 +33,15 @@ void launch_step(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t
 }
 #endif
 
+template <int CFG, bool GYM>
+int occupancy(size_t lds) {
+  int n = 0;
+  hipError_t e;
+  if constexpr (GYM) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mxa_step_kernel<CFG, false>, 64, lds);
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mxa_run_kernel<CFG, false, false>, 64, lds);
+  return e == hipSuccess ? n : -1;
+}
+
 template <int CFG>
 MxaEntry make_entry() {
   MxaEntry e{};
@@ -40,6 +49,13 @@ MxaEntry make_entry() {
   e.run = launch_run<CFG, false, true>;
   e.stop = launch_stop<CFG, false>;
   constexpr bool gym = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL;
+#ifndef MXA_NO_FAST
+#ifndef MXA_NO_GYM
+  e.occ = occupancy<CFG, gym>;
+#else
+  if constexpr (!gym) e.occ = occupancy<CFG, false>;
+#endif
+#endif
   if constexpr (!gym) {  // the book-update log: plain Kernel.runner configurations
     e.run_log = launch_run<CFG, true, true>;
     // measured per configuration (one box, hash off, run kernel): without the instrumentation

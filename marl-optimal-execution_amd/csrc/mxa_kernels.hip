@@ -2376,7 +2376,7 @@ struct Eng {
     return (f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE) && !(f & FL_MKT_CLOSED);
   }
   DEV i64 wake_frequency(int type) {
-    if (type == AG_POVMM) return PC.mm_wake;
+    if (type == AG_POVMM) return mm_wake();
     if (type == AG_MOMENTUM) return PC.mom_wake;
     if (type == AG_MKTMAKER) return PC.mk_wake;  // pd.Timedelta(wake_up_freq) (MarketMakerAgent.py:148-149)
     if (type == AG_OBI) return PC.obi_wake;      // pd.Timedelta("1s") (OrderBookImbalanceAgent.py:187-188)
@@ -2712,10 +2712,16 @@ struct Eng {
   }
 
   // ---------------- POVMarketMakerAgent (POVMarketMakerAgent.py:83-206)
+  // its options: the config script's constants, or (MXA_CFG_RMSC03_MM) this env's, from its record
+  DEV double mm_pov() { if constexpr (PC.mm_rt) return rgd(AF_MM_POV); else return PC.mm_pov; }
+  DEV i64 mm_min() { if constexpr (PC.mm_rt) return rgi(AF_MM_MIN); else return PC.mm_min_size; }
+  DEV i64 mm_window() { if constexpr (PC.mm_rt) return rgi(AF_MM_WIN); else return PC.mm_window; }
+  DEV i64 mm_ticks() { if constexpr (PC.mm_rt) return rgi(AF_MM_TICKS); else return PC.mm_ticks; }
+  DEV i64 mm_wake() { if constexpr (PC.mm_rt) return rg64(AF_MM_WAKE); else return PC.mm_wake; }
   DEV void mm_wakeup() {
     if (ta_wakeup()) {
       get_spread(1);
-      get_tv(PC.mm_wake);
+      get_tv(mm_wake());  // lookback_period = wake_up_freq
     }
   }
   DEV void mm_receive(const Msg& m) {
@@ -2723,8 +2729,9 @@ struct Eng {
     i64 mid = rg64(AF_LAST_MID);
     u32 k = m_kind(m);
     if (k == MK_TV && fl(FL_AW_TV)) {
-      i64 qty = py_round(PC.mm_pov * (double)rg64(AF_TV));
-      rs(AF_ORDER_SIZE, (u32)(qty >= PC.mm_min_size ? qty : PC.mm_min_size));
+      i64 qty = py_round(mm_pov() * (double)rg64(AF_TV));
+      const i64 mn = mm_min();
+      rs(AF_ORDER_SIZE, (u32)(qty >= mn ? qty : mn));
       fl_set(FL_AW_TV, false);
     }
     if (k == MK_SPREAD && fl(FL_AW_SPREAD)) {
@@ -2739,46 +2746,79 @@ struct Eng {
     }
     if (!fl(FL_AW_SPREAD) && !fl(FL_AW_TV)) {
       cancel_all();
-      i64 hb = mid - 1, la = mid + PC.mm_window;
-      i64 lb = hb - PC.mm_ticks, ha = la + PC.mm_ticks;
+      const i64 ticks = mm_ticks();
+      i64 hb = mid - 1, la = mid + mm_window();
+      i64 lb = hb - ticks, ha = la + ticks;
       i64 sz = rgi(AF_ORDER_SIZE);
-      constexpr int NL = 2 * (PC.mm_ticks + 1);
-      if (BATCH && NL <= 64 && sz > 0 && rgi(AF_NORD) + NL <= PC.L.open_cap) {
-        mm_place_ladder(sz, lb, la);
+      const int NL = 2 * (int)(ticks + 1);
+      if (BATCH && NL <= MM_LADDER_MAX && sz > 0 && rgi(AF_NORD) + NL <= PC.L.open_cap) {
+        mm_place_ladder(sz, lb, la, (int)ticks + 1);
       } else {
         for (i64 p = lb; p <= hb; p++) place_limit(sz, 1, p);
         for (i64 p = la; p <= ha; p++) place_limit(sz, 0, p);
       }
       fl_set(FL_AW_SPREAD, true);
       fl_set(FL_AW_TV, true);
-      wakeup_at(cur_agent, cur + PC.mm_wake);
+      wakeup_at(cur_agent, cur + mm_wake());
     }
   }
 
-  // the ladder's placeLimitOrder calls in one pass: lane i places bid lb+i (i < ticks+1) or ask
-  // la+i-(ticks+1); ids, open-order list entries and queue seqs in the same order as the loop
-  DEV void mm_place_ladder(i64 sz, i64 lb, i64 la) {
-    constexpr int NB = PC.mm_ticks + 1, NL = 2 * NB;
+  // the ladder's placeLimitOrder calls in batched passes of 64: member i places bid lb+i (i < NB)
+  // or ask la+i-NB; ids, open-order list entries and queue seqs in the same order as the loop.
+  // Each pass is one batched push (one exchange-side LIMIT run); two passes cover 63 ticks
+  static constexpr int MM_LADDER_MAX = PC.mm_rt ? 128 : 64;
+  DEV void mm_place_ladder(i64 sz, i64 lb, i64 la, int NB) {
+    if constexpr (!PC.mm_rt) {  // the script's constant ladder: one pass (the measured rmsc03 code)
+      constexpr int CNB = PC.mm_ticks + 1, CNL = 2 * CNB;
+      i32 u = rgi(AF_NUSED);
+      if (u + CNL > PC.L.open_cap) u = open_compact();
+      const bool act = lane < CNL;
+      const int buy = lane < CNB;
+      const i32 price = (i32)(buy ? lb + lane : la + (lane - CNB));
+      const i32 oid = (i32)(ocnt + lane);
+      ocnt += CNL;
+      if (act) {
+        OpenOrder o;
+        o.oid = oid;
+        o.is_buy = buy;
+        o.qty = (i32)sz;
+        o.price = price;
+        open_ptr(cur_agent)[u + lane] = o;
+      }
+      rs(AF_NUSED, (u32)(u + CNL));
+      rs(AF_NORD, (u32)(rgi(AF_NORD) + CNL));
+      Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, (i32)sz, price, 0);
+      lm.w[0] = (lm.w[0] & 0xFFFFu) | ((u32)cur_agent << 16);
+      q_push_lanes(act, ex_key(), lm);
+      return;
+    }
+    const int NL = 2 * NB;
     i32 u = rgi(AF_NUSED);
     if (u + NL > PC.L.open_cap) u = open_compact();
-    const bool act = lane < NL;
-    const int buy = lane < NB;
-    const i32 price = (i32)(buy ? lb + lane : la + (lane - NB));
-    const i32 oid = (i32)(ocnt + lane);
+    const i64 o0 = ocnt;
     ocnt += NL;
-    if (act) {
-      OpenOrder o;
-      o.oid = oid;
-      o.is_buy = buy;
-      o.qty = (i32)sz;
-      o.price = price;
-      open_ptr(cur_agent)[u + lane] = o;
-    }
     rs(AF_NUSED, (u32)(u + NL));
     rs(AF_NORD, (u32)(rgi(AF_NORD) + NL));
-    Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, (i32)sz, price, 0);
-    lm.w[0] = (lm.w[0] & 0xFFFFu) | ((u32)cur_agent << 16);
-    q_push_lanes(act, ex_key(), lm);
+    const u64 key = ex_key();
+    for (int c = 0; c < MM_LADDER_MAX / 64; c++) {
+      if (c * 64 >= NL) break;
+      const int i = c * 64 + lane;
+      const bool act = i < NL;
+      const int buy = i < NB;
+      const i32 price = (i32)(buy ? lb + i : la + (i - NB));
+      const i32 oid = (i32)(o0 + i);
+      if (act) {
+        OpenOrder o;
+        o.oid = oid;
+        o.is_buy = buy;
+        o.qty = (i32)sz;
+        o.price = price;
+        open_ptr(cur_agent)[u + i] = o;
+      }
+      Msg lm = msg_order(MK_LIMIT, oid, cur_agent, buy, (i32)sz, price, 0);
+      lm.w[0] = (lm.w[0] & 0xFFFFu) | ((u32)cur_agent << 16);
+      q_push_lanes(act, key, lm);
+    }
   }
 
   // ---------------- SpreadBasedMarketMakerAgent (agent/market_makers/SpreadBasedMarketMakerAgent.py)
@@ -4740,6 +4780,7 @@ struct Builder : Eng<CFG, true> {
   typedef Eng<CFG, true> E;
   typedef typename E::RS RS;
   DEV Builder(char* e, char* lds, const RpCtx* ctx = nullptr) : E(e, lds, 0, ctx) {}
+  const MmParams* mmp = nullptr;  // MXA_CFG_RMSC03_MM: this env's market-maker options
 
   DEV u32 g_seed(RS& G) { return (u32)rs_randint(G, 0, 4294967296LL); }
   DEV void set_seed(int stream, u32 s) {
@@ -4920,7 +4961,8 @@ struct Builder : Eng<CFG, true> {
     RS G = this->grs(0);
     int n = P.n_agents;
     u32 tmp;
-    if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_RL || P.config == MXA_CFG_RANDOM_FUND_VALUE ||
+    if (P.config == MXA_CFG_RMSC03 || P.config == MXA_CFG_RMSC03_MM || P.config == MXA_CFG_RMSC03_RL ||
+        P.config == MXA_CFG_RANDOM_FUND_VALUE ||
         P.config == MXA_CFG_RMSC03_SBMM || P.config == MXA_CFG_RMSC03_SBMM_POLL ||
         P.config == MXA_CFG_RANDOM_FUND_DIVERSE || P.config == MXA_CFG_HIST_FUND_VALUE ||
         P.config == MXA_CFG_HIST_FUND_DIVERSE) {
@@ -4957,7 +4999,17 @@ struct Builder : Eng<CFG, true> {
       for (int a = P.first_mm; a < P.first_mm + P.n_mm; a++) {
         set_seed(4 + a, g_seed(G));
         rec_init(a, AG_POVMM);
-        this->rs(AF_ORDER_SIZE, (u32)P.mm_min_size);
+        if constexpr (P.mm_rt) {  // this env's --mm-* options (POVMarketMakerAgent.py:19-60)
+          const MmParams mp = *mmp;
+          this->rsd(AF_MM_POV, mp.pov);
+          this->rs(AF_MM_MIN, (u32)mp.min_order_size);
+          this->rs(AF_MM_WIN, (u32)mp.window_size);
+          this->rs(AF_MM_TICKS, (u32)mp.num_ticks);
+          this->rs64(AF_MM_WAKE, mp.wake_up_freq);
+          this->rs(AF_ORDER_SIZE, (u32)mp.min_order_size);  // order_size = min_order_size
+        } else {
+          this->rs(AF_ORDER_SIZE, (u32)P.mm_min_size);
+        }
         this->rec_store();
       }
       for (int a = P.first_sb; a < P.first_sb + P.n_sb; a++) {  // rmsc03_sbmm*: the market maker's slot and draw
@@ -5220,6 +5272,7 @@ __global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stri
   if (env >= n_envs) return;
   if (mask && !mask[env]) return;
   mxa::Builder<CFG> b(base + (size_t)env * stride, lds, ctx);
+  if constexpr (mxa::Eng<CFG>::PC.mm_rt) b.mmp = ctx->mmp + env;
   b.build(seeds[env], mask && mask[env] == 2);  // 2: a later episode of the same process
 }
 

@@ -25,7 +25,21 @@ enum mxa_config_id { MXA_CFG_RMSC03 = 0, MXA_CFG_SPARSE_ZI_100 = 1, MXA_CFG_SPAR
                      MXA_CFG_MARKETREPLAY_TWAP = 14,
                      // rmsc03 with a SpreadBasedMarketMakerAgent in the market maker's slot: subscribe=True
                      // (the agent's default) and the polling mode
-                     MXA_CFG_RMSC03_SBMM = 15, MXA_CFG_RMSC03_SBMM_POLL = 16 };
+                     MXA_CFG_RMSC03_SBMM = 15, MXA_CFG_RMSC03_SBMM_POLL = 16,
+                     // config/rmsc03.py with per-env market-maker options (--mm-pov ... --mm-wake-up-freq,
+                     // config/rmsc03.py:39-43; the sweep of scripts/rmsc03.sh) and the capacities they need
+                     MXA_CFG_RMSC03_MM = 17 };
+
+// config/rmsc03.py's market-maker options of one env (include/mxa.h mxa_mm_params): read by the
+// build kernel into the POVMarketMakerAgent's record (AF_MM_*)
+typedef struct {
+  double pov;                  // --mm-pov
+  int32_t min_order_size;      // --mm-min-order-size
+  int32_t window_size;         // --mm-window-size
+  int32_t num_ticks;           // --mm-num-ticks
+  int32_t pad;
+  int64_t wake_up_freq;        // --mm-wake-up-freq as pd.Timedelta(...).value (ns)
+} MmParams;
 
 // message kinds (tests/golden/gen_fixtures.py KIND; oracle/abides_oracle.c)
 enum {
@@ -253,6 +267,7 @@ typedef struct {  // device-resident tape (shared by all envs of a handle)
   int32_t fs_n;
   int32_t twap_trade;   // execution_marketreplay.py -e: the TWAP agent trades
   RpLayout L;
+  const MmParams* mmp;  // MXA_CFG_RMSC03_MM: [n_envs] market-maker options (read by the build kernel)
 } RpCtx;
 
 typedef struct {
@@ -277,6 +292,9 @@ enum {
   // current_bids / current_asks as rings of order ids with one head and one length (they always
   // have equal lengths), prices contiguous from the left end's
   AF_SB_N = 39, AF_SB_HEAD = 40, AF_SB_BLO = 41, AF_SB_ALO = 42, AF_SB_CNT = 43, AF_SB_IDS = 46,
+  // POVMarketMakerAgent with per-env options (MXA_CFG_RMSC03_MM): pov, min_order_size, window_size,
+  // num_ticks, wake_up_freq in the ZI / momentum areas it never uses
+  AF_MM_POV = AF_R_T, AF_MM_MIN = 46, AF_MM_WIN = 47, AF_MM_TICKS = 48, AF_MM_WAKE = 50,
   AF_MIDS = 66,       // 50 x int32 (2*mid ring), momentum
   AF_STREAM_N = 66,   // HBL: epochs of the last QUERY_ORDER_STREAM reply (momentum's AF_MIDS area)
   AF_STREAM_HI = 68,  // HBL: absolute history epoch of its first entry (history[1]), int64
@@ -322,7 +340,8 @@ typedef struct {
   int64_t noise_open, noise_close;
   // POVMarketMakerAgent
   double mm_pov;
-  int32_t mm_min_size, mm_window, mm_ticks, pad2;
+  int32_t mm_min_size, mm_window, mm_ticks;
+  int32_t mm_rt;           // 1: the options above are per env, in the market maker's record (AF_MM_*)
   int64_t mm_wake;
   // MomentumAgent
   int32_t mom_min, mom_max;

@@ -21,6 +21,7 @@ MXA_MARKETREPLAY_RUNNER = 13
 MXA_MARKETREPLAY_TWAP = 14
 MXA_RMSC03_SBMM = 15
 MXA_RMSC03_SBMM_POLL = 16
+MXA_RMSC03_MM = 17  # config/rmsc03.py with per-env --mm-* options (mxa_create_params)
 CONFIG_IDS = {"rmsc03": MXA_RMSC03, "sparse_zi_100": MXA_SPARSE_ZI_100, "sparse_zi_1000": MXA_SPARSE_ZI_1000,
               "value_noise": MXA_VALUE_NOISE, "rmsc01": MXA_RMSC01, "rmsc02": MXA_RMSC02,
               "obi_rmsc02": MXA_OBI_RMSC02, "random_fund_value": MXA_RANDOM_FUND_VALUE,
@@ -78,7 +79,8 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_step_device", "mxa_finalize", "mxa_read_final", "mxa_write_rl_state", "mxa_set_parity_hash",
            "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log", "mxa_write_records", "mxa_set_id_persistence",
            "mxa_read_counters", "mxa_create_hist", "mxa_create_replay_runner",
-           "mxa_set_stop_time", "mxa_run_until", "mxa_create_replay_twap"]
+           "mxa_set_stop_time", "mxa_run_until", "mxa_create_replay_twap", "mxa_create_params", "mxa_set_mm_params",
+           "mxa_mm_defaults", "mxa_resident_envs"]
 COUNTER_WORDS = 34  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
@@ -126,7 +128,9 @@ def load():
                        ("mxa_create_hist", [I32, I32, P, I32, I32, P, P, I32, ctypes.POINTER(P)]),
                        ("mxa_create_replay_runner", [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)]),
                        ("mxa_set_stop_time", [P, I64]), ("mxa_run_until", [P, I64, P]),
-                       ("mxa_create_replay_twap", [P, P, P, P, P, I32, I32, I32, I32, I32, ctypes.POINTER(P)])):
+                       ("mxa_create_replay_twap", [P, P, P, P, P, I32, I32, I32, I32, I32, ctypes.POINTER(P)]),
+                       ("mxa_create_params", [I32, I32, P, P, I32, I32, ctypes.POINTER(P)]),
+                       ("mxa_set_mm_params", [P, P]), ("mxa_resident_envs", [P])):
         if hasattr(L, name):  # (older single-configuration A/B builds lack them; libmxa.so has all)
             getattr(L, name).argtypes = args
     L.mxa_write_rl_state.argtypes = [P, P]

@@ -6,6 +6,8 @@ config/rmsc01.py:75-211 and config/rmsc02.py (the same agents), config/obi_rmsc0
 config/random_fund_value.py:113-153, config/random_fund_diverse.py:116-198,
 config/hist_fund_value.py:84-148, config/hist_fund_diverse.py:86-190 (the same agents).
 """
+import numpy as np
+
 ZI_GROUPS = [(0, 250, "1"), (0, 500, "1"), (0, 1000, "0.8"), (0, 1000, "1"), (0, 2000, "0.8"), (250, 500, "0.8"),
              (250, 500, "1")]
 ZI_COUNTS = {"sparse_zi_100": [15, 15, 14, 14, 14, 14, 14], "sparse_zi_1000": [143] * 6 + [142]}
@@ -102,4 +104,36 @@ def agent_type_names(config):
     for g, cnt in enumerate(ZI_COUNTS[config]):
         lo, hi, eta = ZI_GROUPS[g]
         out += ["ZeroIntelligenceAgent Type %d [%d <= R <= %d, eta=%s]" % (g + 1, lo, hi, eta)] * cnt
+    return out
+
+
+# include/mxa.h mxa_mm_params: config/rmsc03.py's market-maker options (config/rmsc03.py:39-43)
+MM_PARAMS_DTYPE = np.dtype([("mm_pov", "<f8"), ("mm_min_order_size", "<i4"), ("mm_window_size", "<i4"),
+                            ("mm_num_ticks", "<i4"), ("pad", "<i4"), ("mm_wake_up_freq_ns", "<i8")])
+MM_DEFAULTS = {"pov": 0.05, "min_order_size": 20, "window_size": 5, "num_ticks": 20, "wake_up_freq": "1S"}
+
+
+def _timedelta_ns(x):
+    """pd.Timedelta(wake_up_freq).value, as getWakeFrequency and the transacted-volume lookback
+    read the option (POVMarketMakerAgent.py:203-206, OrderBook.py:400-436)"""
+    if isinstance(x, str):
+        import pandas as pd
+        return int(pd.Timedelta(x).value)
+    return int(x)
+
+
+def mm_params(n=1, pov=0.05, min_order_size=20, window_size=5, num_ticks=20, wake_up_freq="1S"):
+    """[n] MM_PARAMS_DTYPE records of `python abides.py -c rmsc03 --mm-pov POV --mm-min-order-size
+    MIN_ORDER_SIZE --mm-window-size WINDOW_SIZE --mm-num-ticks NUM_TICKS --mm-wake-up-freq
+    WAKE_UP_FREQ`; each option a scalar or one value per env (a parameter sweep in one batch,
+    scripts/rmsc03.sh).  wake_up_freq: a pandas frequency string ("10S") or ns."""
+    out = np.zeros(n, dtype=MM_PARAMS_DTYPE)
+    out["mm_pov"] = pov
+    out["mm_min_order_size"] = min_order_size
+    out["mm_window_size"] = window_size
+    out["mm_num_ticks"] = num_ticks
+    wf = wake_up_freq if isinstance(wake_up_freq, (list, tuple, np.ndarray)) else [wake_up_freq] * n
+    if len(wf) != n:
+        raise ValueError("wake_up_freq: one value or one per env")
+    out["mm_wake_up_freq_ns"] = [_timedelta_ns(x) for x in wf]
     return out

@@ -63,3 +63,14 @@ def bytes_per_event(c):
              "record_round_trips": float(c[:, C_REC].sum()) / n, "run_members": float(c[:, C_RUN].sum()) / n,
              "heap_sift_model": float((SIFT_BYTES * sift * (c[:, C_POPS] + c[:, C_PUSH])).sum()) / n}
     return total / n, per, units
+
+
+def strict_bytes_per_event(c):
+    """SURVEY.md §8(d) read literally: the 2 x 64 B agent-record round trip charged on EVERY pop
+    (not only where an event loads the recipient's state), the other terms as counted.  Reported
+    beside the counted figure (bytes_per_event), which is the conservative one."""
+    total, pops, parts = algorithmic_bytes(c)
+    c = np.asarray(c, dtype=np.int64)
+    n = max(1, pops)
+    strict = total - parts["agent_records"] + 2 * RECORD_BYTES * int(c[:, C_POPS].sum())
+    return strict / n

@@ -10,14 +10,15 @@ import os
 import numpy as np
 
 from . import _lib
-from .configs import BOOK_FREQ, HIST_CONFIGS, REPLAY_CONFIGS, agent_names, agent_type_names, symbol_of
+from .configs import (BOOK_FREQ, HIST_CONFIGS, MM_PARAMS_DTYPE, REPLAY_CONFIGS, agent_names, agent_type_names,
+                      symbol_of)
 
 CHUNK_DEFAULT = 1 << 20
 
 
 class VecMarket:
     def __init__(self, config, seeds, device=0, trace_cap=0, book_log=0, symbol=None, fundamental=None,
-                 book_freq="config", tape=None):
+                 book_freq="config", tape=None, mm_params=None):
         """book_log: records per env of the book-update log (0 off), the input of the exchange's
         order-book outputs (orderbook_snapshots, exchange_events; include/mxa.h
         mxa_set_book_log).  A limit order takes 2-4 records, a cancellation 1.
@@ -26,7 +27,9 @@ class VecMarket:
         (mxabides.fundamental.FundamentalSeries).  book_freq: the exchange's (default: the config
         script's, configs.BOOK_FREQ), which decides the order-book file write_logs writes.
         tape: the LOBSTER tape (mxabides.tape.Tape) of marketreplay_runner, config/marketreplay.py
-        (the seeds only count the envs there: nothing in that composition draws)."""
+        (the seeds only count the envs there: nothing in that composition draws).
+        mm_params: rmsc03 only: config/rmsc03.py's --mm-* options per env (configs.mm_params, one
+        record or one per env; include/mxa.h mxa_create_params)."""
         if config not in _lib.CONFIG_IDS:
             raise ValueError("unknown config %r (supported: %s)" % (config, sorted(_lib.CONFIG_IDS)))
         self.L = _lib.load()
@@ -58,6 +61,13 @@ class VecMarket:
             rc = self.L.mxa_create_hist(_lib.CONFIG_IDS[config], self.n_envs, self.seeds.ctypes.data, device, trace_cap,
                                         f.t.ctypes.data, f.v.ctypes.data, len(f), ctypes.byref(self._h))
             self._check(rc, "mxa_create_hist")
+        elif mm_params is not None:
+            if config != "rmsc03":
+                raise ValueError("mm_params are config/rmsc03.py's market-maker options")
+            self.mm_params = self._mm_array(mm_params)
+            rc = self.L.mxa_create_params(_lib.MXA_RMSC03, self.n_envs, self.seeds.ctypes.data,
+                                          self.mm_params.ctypes.data, device, trace_cap, ctypes.byref(self._h))
+            self._check(rc, "mxa_create_params")
         else:
             if fundamental is not None:
                 raise ValueError("%s runs the SparseMeanRevertingOracle; a fundamental series is for %s" % (config, HIST_CONFIGS))
@@ -68,6 +78,24 @@ class VecMarket:
         self.book_log_cap = int(book_log)
         if book_log:
             self._check(self.L.mxa_set_book_log(self._h, int(book_log)), "mxa_set_book_log")
+
+    def _mm_array(self, p):
+        p = np.asarray(p, dtype=MM_PARAMS_DTYPE).reshape(-1)
+        if len(p) == 1:
+            p = np.repeat(p, self.n_envs)
+        if len(p) != self.n_envs:
+            raise ValueError("mm_params: one record or one per env")
+        return np.ascontiguousarray(p)
+
+    def set_mm_params(self, mm_params):
+        """the --mm-* options the next reset() builds with (a handle created with mm_params)"""
+        self.mm_params = self._mm_array(mm_params)
+        self._check(self.L.mxa_set_mm_params(self._h, self.mm_params.ctypes.data), "mxa_set_mm_params")
+
+    @property
+    def resident_envs(self):
+        """envs resident on the device at once (occupancy x CUs; include/mxa.h mxa_resident_envs)"""
+        return self._check(self.L.mxa_resident_envs(self._h), "mxa_resident_envs")
 
     def _check(self, rc, what):
         if rc < 0:

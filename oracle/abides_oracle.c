@@ -3235,6 +3235,28 @@ int ora_create(const char* config, uint32_t seed, ora_env** out) {
     return 0;
 }
 
+/* config/rmsc03.py -s SEED --mm-pov ... (config/rmsc03.py:39-43, 158-177): the options only reach
+ * POVMarketMakerAgent.__init__ (pov, min_order_size, window_size, num_ticks, wake_up_freq;
+ * POVMarketMakerAgent.py:19-60, order_size = min_order_size), never a draw, so the build is
+ * rmsc03's with the market maker's fields replaced */
+int ora_create_mm(uint32_t seed, const ora_mm_params* p, ora_env** out) {
+    if (!p || p->mm_window_size < 0 || p->mm_num_ticks < 0 || p->mm_wake_up_freq_ns <= 0) return -1;
+    int rc = ora_create("rmsc03", seed, out);
+    if (rc) return rc;
+    ora_env* e = *out;
+    for (int i = 0; i < e->n; i++) {
+        agent_t* a = &e->ag[i];
+        if (a->type != AG_POVMM) continue;
+        a->pov = p->mm_pov;
+        a->min_size = p->mm_min_order_size;
+        a->window = p->mm_window_size;
+        a->num_ticks = p->mm_num_ticks;
+        a->wake_freq = p->mm_wake_up_freq_ns;
+        a->order_size = p->mm_min_order_size;
+    }
+    return 0;
+}
+
 void ora_destroy(ora_env* e) {
     if (!e) return;
     for (int i = 0; i < e->n; i++) {
@@ -3349,6 +3371,7 @@ typedef struct {
     uint64_t* h;
     int32_t* err; /* optional: the env's oracle error code (0 ok, negative: fail() codes) */
     int64_t* stats; /* optional: [n][4] ora_stats of each env */
+    const ora_mm_params* mm; /* optional: rmsc03 with per-env market-maker options */
     pthread_mutex_t mu;
     int rc;
 } batch_t;
@@ -3361,7 +3384,7 @@ static void* batch_worker(void* p) {
         pthread_mutex_unlock(&b->mu);
         if (i >= b->n) break;
         ora_env* e = NULL;
-        if (ora_create(b->config, b->seeds[i], &e)) {
+        if (b->mm ? ora_create_mm(b->seeds[i], &b->mm[i], &e) : ora_create(b->config, b->seeds[i], &e)) {
             b->rc = -1;
             continue;
         }
@@ -3377,9 +3400,10 @@ static void* batch_worker(void* p) {
 
 static int run_batch_impl(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
                           int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out,
-                          double* seconds_out) {
+                          double* seconds_out, const ora_mm_params* mm) {
     batch_t b;
     memset(&b, 0, sizeof b);
+    b.mm = mm;
     b.err = err_out;
     b.stats = stats_out;
     b.config = config;
@@ -3404,23 +3428,30 @@ static int run_batch_impl(const char* config, const uint32_t* seeds, int n, int 
 
 int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
                   int64_t* events_out, uint64_t* hash_out, double* seconds_out) {
-    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, NULL, NULL, seconds_out);
+    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, NULL, NULL, seconds_out, NULL);
 }
 
 /* the same, with each env's error code (ora_error) in err_out[n] */
 int ora_run_batch_err(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
                       int64_t* events_out, uint64_t* hash_out, int32_t* err_out, double* seconds_out) {
-    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, err_out, NULL, seconds_out);
+    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, err_out, NULL, seconds_out, NULL);
 }
 
 /* capacity statistics (ora_stats) of n envs: stats_out[n][4] */
 int ora_run_batch_stats(const char* config, const uint32_t* seeds, int n, int threads, int64_t* stats_out) {
     int64_t* ev = (int64_t*)calloc(n, sizeof(int64_t));
     uint64_t* h = (uint64_t*)calloc(n, sizeof(uint64_t));
-    int rc = run_batch_impl(config, seeds, n, threads, -1, ev, h, NULL, stats_out, NULL);
+    int rc = run_batch_impl(config, seeds, n, threads, -1, ev, h, NULL, stats_out, NULL, NULL);
     free(ev);
     free(h);
     return rc;
+}
+
+int ora_run_batch_mm(const uint32_t* seeds, const ora_mm_params* params, int n, int threads, int64_t max_pops,
+                     int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out, double* seconds_out) {
+    if (!params) return -1;
+    return run_batch_impl("rmsc03", seeds, n, threads, max_pops, events_out, hash_out, err_out, stats_out, seconds_out,
+                          params);
 }
 
 void ora_set_book_log(ora_env* e, int on) {

@@ -107,6 +107,18 @@ int ora_run_batch_err(const char* config, const uint32_t* seeds, int n, int thre
                       int64_t* events_out, uint64_t* hash_out, int32_t* err_out, double* seconds_out);
 /* capacity statistics of n envs run to completion: stats_out[n][4] = ora_stats */
 int ora_run_batch_stats(const char* config, const uint32_t* seeds, int n, int threads, int64_t* stats_out);
+/* config/rmsc03.py with its market-maker options (config/rmsc03.py:39-43, swept by
+ * scripts/rmsc03.sh): --mm-pov, --mm-min-order-size, --mm-window-size, --mm-num-ticks and
+ * --mm-wake-up-freq (as pd.Timedelta(...).value ns).  Same layout as include/mxa.h mxa_mm_params. */
+typedef struct {
+    double mm_pov;
+    int32_t mm_min_order_size, mm_window_size, mm_num_ticks, pad;
+    int64_t mm_wake_up_freq_ns;
+} ora_mm_params;
+int ora_create_mm(uint32_t seed, const ora_mm_params* p, ora_env** out);
+/* ora_run_batch_err / _stats of rmsc03 envs with per-env market-maker options params[n] */
+int ora_run_batch_mm(const uint32_t* seeds, const ora_mm_params* params, int n, int threads, int64_t max_pops,
+                     int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out, double* seconds_out);
 /* n GymKernel episodes, each stepped with actions[k][i][0..2] until done or error (config
  * "rmsc03_rl" with seeds, or NULL: the replay composition on the tape t/oid/price/size/buy).
  * Per env: pops, hash, error code, steps taken and the last valid observation [n][9]. */

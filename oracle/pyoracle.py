@@ -107,14 +107,27 @@ def _set_arrays(t, v):
     _fund_set = True
 
 
-class OracleEnv:
-    """One reference-semantics simulation (config + seed)."""
+# ora_mm_params (abides_oracle.h): config/rmsc03.py's market-maker options
+MM_DTYPE = np.dtype([("mm_pov", "<f8"), ("mm_min_order_size", "<i4"), ("mm_window_size", "<i4"),
+                     ("mm_num_ticks", "<i4"), ("pad", "<i4"), ("mm_wake_up_freq_ns", "<i8")])
 
-    def __init__(self, config, seed, trace_cap=0):
+
+class OracleEnv:
+    """One reference-semantics simulation (config + seed); config "rmsc03" with `mm` (one
+    MM_DTYPE record) runs config/rmsc03.py with those --mm-* options."""
+
+    def __init__(self, config, seed, trace_cap=0, mm=None):
         L = lib()
         _ensure_fundamental(config)
         self._h = ctypes.c_void_p()
-        rc = L.ora_create(config.encode(), seed & 0xFFFFFFFF, ctypes.byref(self._h))
+        if mm is not None:
+            if config != "rmsc03":
+                raise ValueError("market-maker options are config/rmsc03.py's")
+            self._mm = np.ascontiguousarray(np.asarray(mm, dtype=MM_DTYPE).reshape(1))
+            L.ora_create_mm.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+            rc = L.ora_create_mm(seed & 0xFFFFFFFF, self._mm.ctypes.data, ctypes.byref(self._h))
+        else:
+            rc = L.ora_create(config.encode(), seed & 0xFFFFFFFF, ctypes.byref(self._h))
         if rc:
             raise ValueError("oracle: bad config %r" % config)
         self.trace_buf = None
@@ -284,6 +297,28 @@ def batch_stats(config, seeds, threads):
     if L.ora_run_batch_stats(config.encode(), seeds.ctypes.data, len(seeds), threads, out.ctypes.data):
         raise RuntimeError("oracle batch failed")
     return out
+
+
+def run_batch_mm(seeds, params, threads, max_pops=-1, stats=False):
+    """rmsc03 envs with per-env market-maker options (params: MM_DTYPE [n]): events, hashes, error
+    codes, seconds (and the [n][4] capacity statistics with stats=True)"""
+    L = lib()
+    L.ora_run_batch_mm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64] + \
+        [ctypes.c_void_p] * 4 + [ctypes.POINTER(ctypes.c_double)]
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+    prm = np.ascontiguousarray(np.asarray(params, dtype=MM_DTYPE))
+    if len(prm) != len(seeds):
+        raise ValueError("one parameter record per seed")
+    n = len(seeds)
+    ev = np.zeros(n, dtype=np.int64)
+    hs = np.zeros(n, dtype=np.uint64)
+    er = np.zeros(n, dtype=np.int32)
+    st = np.zeros((n, 4), dtype=np.int64)
+    sec = ctypes.c_double()
+    if L.ora_run_batch_mm(seeds.ctypes.data, prm.ctypes.data, n, threads, max_pops, ev.ctypes.data, hs.ctypes.data,
+                          er.ctypes.data, st.ctypes.data if stats else None, ctypes.byref(sec)):
+        raise RuntimeError("oracle batch failed")
+    return (ev, hs, er, sec.value, st) if stats else (ev, hs, er, sec.value)
 
 
 def gym_batch(actions, threads, seeds=None, tape=None):

@@ -300,6 +300,14 @@ def run_config(cfg, seed, out, full):
         cfg_script = "rmsc03"
     else:
         cfg_script = cfg
+    mm_args = None
+    if cfg.startswith("rmsc03%"):
+        # config/rmsc03.py with its market-maker options (config/rmsc03.py:39-43), the parameters
+        # scripts/rmsc03.sh sweeps: rmsc03%POV,MIN_ORDER_SIZE,WINDOW_SIZE,NUM_TICKS,WAKE_UP_FREQ
+        pov, mos, ws, nt, wf = cfg.split("%", 1)[1].split(",")
+        mm_args = ["--mm-pov", pov, "--mm-min-order-size", mos, "--mm-window-size", ws, "--mm-num-ticks", nt,
+                   "--mm-wake-up-freq", wf]
+        cfg = cfg_script = "rmsc03"
     stop_at = None
     if "@" in cfg:  # CFG@HH:MM:SS: Kernel.runner(stopTime=that time of the day) instead of the script's
         cfg, stop_at = cfg.split("@")
@@ -340,6 +348,8 @@ def run_config(cfg, seed, out, full):
     argv = ["abides.py", "-c", cfg_script, "-s", str(seed)]
     if cfg_script in ("rmsc03", "random_fund_value", "random_fund_diverse"):
         argv += ["-t", "ABM", "-d", "20190628"]
+    if mm_args:
+        argv += mm_args
     if replay:
         argv += ["-t", replay[0], "-d", replay[1]]
     module = "config." + cfg_script
@@ -608,13 +618,16 @@ def main():
             ("rmsc03_sbmm_poll", 123456789, True), ("rmsc03_sbmm_poll", 7, False),
             # a polling seed whose first QUERY_SPREAD finds a side empty before any mid was known:
             # receiveMessage's UnboundLocalError ends the reference's run after 649 pops
-            ("rmsc03_sbmm_poll", 123456798, True)]
+            ("rmsc03_sbmm_poll", 123456798, True),
+            # config/rmsc03.py with the market-maker options of scripts/rmsc03.sh (pov 0.05, min
+            # order size 25, window 5, 50 ticks, wake-up "10S"), on the script's seeds 30-35
+            ] + [("rmsc03%0.05,25,5,50,10S", s, s == 30) for s in range(30, 36)]
     if len(sys.argv) > 2:
         jobs = [j for j in jobs if j[0] == sys.argv[2] or j[0].startswith(sys.argv[2] + ":")]
     procs = []
     for cfg, seed, full in jobs:
         out = os.path.join(HERE, "%s_%d" % (cfg.replace("@", "_stop").replace(":", ""), seed) if "@" in cfg
-                           else "%s_%d" % (cfg.replace(":", "_"), seed))
+                           else "%s_%d" % (cfg.replace(":", "_").replace("%", "_mm_").replace(",", "_"), seed))
         cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out] + (["--full"] if full else []) + extra
         wd = tempfile.mkdtemp(prefix="gf_")
         procs.append((cfg, seed, subprocess.Popen(cmd, cwd=wd, env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))))

@@ -69,3 +69,31 @@ def test_tape_container_validation():
         tape.Tape([1, 2], [1, -2], [5, 5], [1, 1], [1, 0])
     t = tape.Tape([1, 2, 3], [0, 7, 0], [5, 5, 6], [1, 1, 2], [1, 0, 1])
     assert t.n_auto == 2 and len(t) == 3
+
+
+def test_mm_params_abi_layout_and_defaults():
+    """mxa_mm_params (include/mxa.h): the host record, the oracle's ora_mm_params and the library's
+    mxa_mm_defaults() (config/rmsc03.py:39-43 defaults) agree; no GPU call"""
+    import ctypes
+
+    import numpy as np
+
+    import pyoracle
+    from mxabides import configs
+    assert configs.MM_PARAMS_DTYPE.itemsize == 32 and configs.MM_PARAMS_DTYPE == pyoracle.MM_DTYPE
+    p = configs.mm_params(3, pov=[0.05, 0.1, 0.2], num_ticks=50, wake_up_freq=["10S", "1min", 5 * 10 ** 9])
+    assert p["mm_wake_up_freq_ns"].tolist() == [10 ** 10, 6 * 10 ** 10, 5 * 10 ** 9]
+    assert p["mm_num_ticks"].tolist() == [50] * 3 and p["mm_min_order_size"].tolist() == [20] * 3
+    import mxabides
+    L = mxabides.load()
+
+    class MM(ctypes.Structure):
+        _fields_ = [(n, {"<f8": ctypes.c_double, "<i4": ctypes.c_int32, "<i8": ctypes.c_int64}[configs.MM_PARAMS_DTYPE[n].str])
+                    for n in configs.MM_PARAMS_DTYPE.names]
+    L.mxa_mm_defaults.restype = MM
+    d = L.mxa_mm_defaults()
+    ref = configs.mm_params(1)[0]
+    assert (d.mm_pov, d.mm_min_order_size, d.mm_window_size, d.mm_num_ticks, d.mm_wake_up_freq_ns) == \
+        (ref["mm_pov"], ref["mm_min_order_size"], ref["mm_window_size"], ref["mm_num_ticks"], ref["mm_wake_up_freq_ns"])
+    assert (configs.mm_params(1)[["mm_pov", "mm_min_order_size", "mm_window_size", "mm_num_ticks"]].tolist()[0] ==
+            (0.05, 20, 5, 20))
