@@ -327,7 +327,7 @@ class MarketEngine(Engine):
             kw["fundamental"] = self.m.fundamental
         if self.tname:
             kw["tape"] = self.m.tape
-        s = self.mx.VecMarket(self.args.config, seeds, device=self.ctx.local, **kw)
+        s = self.mx.VecMarket(self.m.config, seeds, device=self.ctx.local, **kw)
         s.set_stream(self.stream.cuda_stream)
         s.set_parity_hash(self.args.parity_hash)
         s.run(chunk=self.args.chunk)

@@ -40,11 +40,12 @@ constexpr int lat_lds(int cfg);
 #define MXA_W_RMSC02 2
 #endif
 #ifndef MXA_SO_RMSC02
-#define MXA_SO_RMSC02 8
+#define MXA_SO_RMSC02 10  // 640 book slots: the oracle's maximum over every seed of bench.py --gpus <= 8 is 537 (512 overflowed)
 #endif
 #ifndef MXA_SQ_Z1K
-#define MXA_SQ_Z1K 36  // sparse_zi_1000 queue slots per lane (2,304; the oracle's maximum over the bench seeds is
-                       // 2,004 pending events); r03 s22 run kernel: 48 slots 821 ms, 36 slots 796
+#define MXA_SQ_Z1K 36  // sparse_zi_1000 queue slots per lane (2,304; the oracle's maximum over the 32,768 seeds of
+                       // bench.py --gpus 1-8 is 2,007 pending events, profiles/r04/capacity_sparse_zi_1000.json);
+                       // r03 s22 run kernel: 48 slots 821 ms, 36 slots 796
 #endif
 // configurations whose exchange latency row (the only row Kernel.sendMessage reads with a
 // symmetric matrix) is copied to LDS for each launch (bit = config id)
@@ -52,7 +53,7 @@ constexpr int lat_lds(int cfg);
 #define MXA_LAT_LDS_MASK (1 << MXA_CFG_SPARSE_ZI_1000)  // r03 s22: 796 -> 784 ms (8 KB row, room from the 36-slot queue)
 #endif
 #ifndef MXA_SO_Z1K
-#define MXA_SO_Z1K 13  // sparse_zi_1000 book slots per lane (832; oracle max 734 resting orders over the 4,096 bench seeds); r03 s9 run kernel: 16 slots 1004 ms, 14 952, 13 925
+#define MXA_SO_Z1K 13  // sparse_zi_1000 book slots per lane (832; oracle max 738 resting orders over the 32,768 seeds of bench.py --gpus 1-8); r03 s9 run kernel: 16 slots 1004 ms, 14 952, 13 925
 #endif
 #ifndef MXA_SO_RFD
 #define MXA_SO_RFD 9
@@ -113,11 +114,12 @@ constexpr Shape shape(int cfg) {
        // rmsc01: oracle maxima over seeds 123456789 / 7: 140 pending events, 75 resting orders;
        // wide replies for the market maker's depth-5 spread queries
        : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, MXA_RMSC01_WAVES, 8, 0}
-       // rmsc02: oracle maxima over the 16,384 bench seeds (batches 0-3): 225 pending events, 405
-       // resting orders (320 book slots overflowed in 0.3 % of the bench envs)
+       // rmsc02: oracle maxima over the 131,072 seeds bench.py draws at --gpus 1-8 (batches 0-3 of
+       // ranks 0-7, tools/capacity_sweep.py, profiles/r04/capacity_rmsc02.json): 225 pending
+       // events, 537 resting orders, 59 open orders of one agent
        : cfg == MXA_CFG_RMSC02 ? Shape{6, MXA_SO_RMSC02, true, MXA_W_RMSC02, 8, 0}
-       // obi_rmsc02: oracle maxima over the 16,384 bench seeds: 211 pending events, 127 resting
-       // orders (192 book slots; 128 left one order of room)
+       // obi_rmsc02: oracle maxima over the 131,072 seeds of bench.py --gpus 1-8: 211 pending
+       // events, 149 resting orders (192 book slots; 128 overflowed)
        : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 3, true, MXA_W_OBI, 8, 0}
        : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, MXA_W_Z1, 6, MXA_HOT_RECORDS}
        : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, MXA_W_VN, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
@@ -127,8 +129,9 @@ constexpr Shape shape(int cfg) {
        // the first MXA_RFV_SQL slots per lane (24: 1,536) in LDS for events due within a second,
        // the other 72 per lane an HBM tier for the far wakeups (the two-tier queue, q_push)
        : (cfg == MXA_CFG_RANDOM_FUND_VALUE || cfg == MXA_CFG_HIST_FUND_VALUE) ? Shape{96, 5, false, MXA_RFV_WAVES, 6, 0, MXA_RFV_SQL}
-       // random_fund_diverse: the same queue; 576 book slots (oracle max 484 over the 8,192 bench
-       // seeds: 448 overflowed) and wide replies for the market maker's depth-5 spread queries
+       // random_fund_diverse: the same queue; 576 book slots (oracle max 503 resting orders and 5,153
+       // pending events over the 65,536 seeds of bench.py --gpus 1-8: 448 slots overflowed) and wide
+       // replies for the market maker's depth-5 spread queries
        : (cfg == MXA_CFG_RANDOM_FUND_DIVERSE || cfg == MXA_CFG_HIST_FUND_DIVERSE)
            ? Shape{96, MXA_SO_RFD, false, MXA_RFD_WAVES, 8, 0, MXA_RFD_SQL}
                                        : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay (both): book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)

@@ -1548,7 +1548,15 @@ struct Eng {
     const double pl = V[li], ph = V[ui];
     const i64 tl = U(T[li]), th = U(T[ui]);
     const double slope = pl != ph ? (ph - pl) / td_seconds(th - tl) : 0.0;
-    return pl + td_seconds(t - tl) * slope;
+    const double v = pl + td_seconds(t - tl) * slope;
+    if constexpr (BLOG) efo_log(t, v);  // f_log[symbol].append (:97): the interpolating branch only
+    return v;
+  }
+  // ExternalFileOracle.f_log entry (FundamentalTime, FundamentalValue): two book-log records
+  DEV void efo_log(i64 t, double v) {
+    const u64 b = as_u(v);
+    bl_put(t, BL_FUND_LO, (i32)(u32)b);
+    bl_put(t, BL_FUND_HI, (i32)(u32)(b >> 32));
   }
   // the value agents' r_bar = oracle.fundamentals[symbol].values[0] and sigma_n = r_bar / 10
   // (config/hist_fund_value.py:80-82), else the config's constants
@@ -3559,6 +3567,7 @@ struct Eng {
     i32 agent = m_agent(m);
     int buy = m_buy(m);
     if (qty <= 0) return;
+    if constexpr (BLOG) bl_put(cur, price, buy ? qty : -qty);
     const i32 hep = h.epoch;
     rp_note_entry_epoch(d, hep);
     RpHdr* R = rh();
@@ -3630,6 +3639,7 @@ struct Eng {
     }
     if (best < 0) return;
     i32 q = U(E[best].qty), mt = U(E[best].meta);
+    if constexpr (BLOG) bl_put(cur, -price, side == 0 ? q : -q);
     rp_unlink(side, x, best);
     Msg r = msg_order(MK_CANCELLED, oid, mt >> 1, mt & 1, q, price, 0);
     r.w[5] = (u32)d;
@@ -3668,6 +3678,7 @@ struct Eng {
       E[hd].meta = (agent << 1) | buy;
       lv_qty(side)[x] += (i64)(qty - hq);
     }
+    if constexpr (BLOG) bl_put(cur, -(oprice | BL_MODIFY | (side << 29)), qty - hq);
     // one ORDER_MODIFIED per retained history epoch holding the id (OrderBook.py:352-355)
     const i32* EP = idep() + MXA_ID_EPOCHS * (size_t)d;
     const i32 lo = h.epoch - PC.stream_history;
@@ -4585,6 +4596,9 @@ struct Eng {
     return n;
   }
   DEV void run(i64 max_pops) {
+    if constexpr (BLOG && EXT) {  // f_log's opening entry (kept by the build in o_pt / o_pv)
+      if (pops == 0 && h.blog_n == 0 && h.o_pt >= 0) efo_log(h.o_pt, h.o_pv);
+    }
     for (i64 n = 0; n < max_pops && status == ST_RUNNING; n++) {
       if constexpr (GYM) {
         if (end_step) break;  // GymKernel.stepRunner: `while not end_step and ...`
@@ -5237,8 +5251,14 @@ struct Builder : Eng<CFG, true> {
     // ExternalFileOracle int(round(price at the open)), ExternalFileOracle.py:37-50),
     // kernelStarting (every agent wakes at startTime, in id order)
     if constexpr (E::EXT) {
-      h.last_trade = py_round(this->efo_price(P.mkt_open));
+      const double op = this->efo_price(P.mkt_open);
+      h.last_trade = py_round(op);
       h.last_trade_float = 0;
+      // getDailyOpenPrice's getPriceAtTime logs f_log's first entry when the open lies inside the
+      // series; the build has no book-update log, so the first logged launch writes it (efo_open)
+      const i64 t0 = U(this->rx->fs_t[0]), t1 = U(this->rx->fs_t[U(this->rx->fs_n) - 1]);
+      h.o_pt = (P.mkt_open >= t0 && P.mkt_open <= t1) ? P.mkt_open : -1;
+      h.o_pv = op;
     } else {
       h.last_trade = (i64)P.o_rbar;
       h.last_trade_float = 1;

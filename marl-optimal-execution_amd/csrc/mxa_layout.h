@@ -159,6 +159,14 @@ typedef struct {
   int32_t qty;
 } BlRec;
 enum { BL_FUNDAMENTAL = -2147483647 - 1 };
+// ExternalFileOracle.f_log entries (ExternalFileOracle.py:97): the interpolated value is a double,
+// so it travels as two records at the query time: the low word (price BL_FUND_LO), then the high
+// word (price BL_FUND_HI)
+enum { BL_FUND_LO = -2147483647, BL_FUND_HI = -2147483646 };
+// OrderBook.modifyOrder on the replay ladder (OrderBook.py:341-372): the level HEAD becomes the new
+// order, so the level's volume changes by qty = new quantity - the old head's; price =
+// -(level price | BL_MODIFY | side << 29), side 0 bids (prices < 2^20 on the replay tape)
+#define BL_MODIFY (1 << 30)
 
 // one event slot as saved between launches (and payload as pushed)
 typedef struct {

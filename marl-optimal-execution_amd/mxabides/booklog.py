@@ -29,6 +29,8 @@ import numpy as np
 
 REC_DTYPE = np.dtype([("t", "<i8"), ("price", "<i4"), ("qty", "<i4")])
 BL_FUNDAMENTAL = -(1 << 31)
+BL_FUND_LO, BL_FUND_HI = -(1 << 31) + 1, -(1 << 31) + 2  # ExternalFileOracle f_log value words
+BL_MODIFY = 1 << 30  # modifyOrder on the replay book: price -(p | BL_MODIFY | side << 29), qty the volume change
 R_BAR = 100000.0           # SparseMeanRevertingOracle r_bar of every plain config (a float)
 MKT_OPEN_NS = (9 * 60 + 30) * 60 * 10**9
 SESSION_DATE = "2019-06-28"  # the plain configs' simulated date (abides.py -d / config defaults)
@@ -39,11 +41,16 @@ FORBIDDEN_QUOTES = (0, 19999900)
 def rows_from_records(rec):
     """Replay device records into flat book_log rows (format above)."""
     rec = np.asarray(rec, dtype=REC_DTYPE)
-    rec = rec[rec["price"] != BL_FUNDAMENTAL]
+    rec = rec[rec["price"] > BL_FUND_HI]  # f_log records (either oracle) carry no book change
     vol = ({}, {})       # bids, asks: price -> resting volume
     px = ([], [])        # their prices, ascending
     out = []
     for t, p, q in zip(rec["t"].tolist(), rec["price"].tolist(), rec["qty"].tolist()):
+        if p < 0 and (-p) & BL_MODIFY:  # modifyOrder (replay): the level's head takes the new quantity
+            s = ((-p) >> 29) & 1
+            p = (-p) & ((1 << 29) - 1)
+            vol[s][p] += q
+            continue
         if p < 0:  # cancelOrder: the level loses the cancelled quantity
             s = 0 if q > 0 else 1
             p = -p
@@ -184,20 +191,32 @@ def orderbook_full(flat, date=SESSION_DATE, wide_book=False):
     return out
 
 
-def fundamental_log(rec, mkt_open=MKT_OPEN_NS, r_bar=R_BAR):
-    """SparseMeanRevertingOracle.f_log[symbol]: the opening entry (mkt_open, r_bar) and one
-    (FundamentalTime, FundamentalValue) per computed value, as (times ns, values) arrays"""
+def fundamental_log(rec, mkt_open=MKT_OPEN_NS, r_bar=R_BAR, external=False):
+    """the oracle's f_log[symbol] as (times ns, values) arrays:
+    * SparseMeanRevertingOracle (SMRO:63, 122): the opening entry (mkt_open, r_bar) and one
+      (FundamentalTime, FundamentalValue) per computed value (BL_FUNDAMENTAL records);
+    * ExternalFileOracle (ExternalFileOracle.py:19, 97): one entry per getPriceAtTime inside the
+      series, the opening lookup included (BL_FUND_LO / BL_FUND_HI record pairs: the double)."""
     rec = np.asarray(rec, dtype=REC_DTYPE)
+    lo = rec[rec["price"] == BL_FUND_LO]
+    if external:
+        hi = rec[rec["price"] == BL_FUND_HI]
+        if len(hi) != len(lo) or (hi["t"] != lo["t"]).any():
+            raise ValueError("ExternalFileOracle f_log records must come in (low, high) pairs")
+        bits = (lo["qty"].astype(np.int64) & 0xFFFFFFFF) | ((hi["qty"].astype(np.int64) & 0xFFFFFFFF) << 32)
+        return lo["t"].astype(np.int64), bits.astype(np.uint64).view(np.float64)
     f = rec[rec["price"] == BL_FUNDAMENTAL]
     t = np.concatenate([[mkt_open], f["t"]]).astype(np.int64)
     v = np.concatenate([[r_bar], f["qty"].astype(np.float64)])
     return t, v
 
 
-def fundamental_frame(rec, date=SESSION_DATE, mkt_open=MKT_OPEN_NS, r_bar=R_BAR):
+def fundamental_frame(rec, date=SESSION_DATE, mkt_open=MKT_OPEN_NS, r_bar=R_BAR, external=False):
     """pd.DataFrame(f_log[symbol]).set_index("FundamentalTime") as ExchangeAgent.kernelTerminating
-    writes it (ExchangeAgent.py:111-117): FundamentalValue float64 (the opening r_bar is a float)"""
+    writes it (ExchangeAgent.py:111-117): FundamentalValue float64 (the opening r_bar is a float;
+    the ExternalFileOracle's values are interpolated floats).  Empty for an ExternalFileOracle that
+    was never asked inside its series (the reference then writes no file)."""
     import pandas as pd
-    t, v = fundamental_log(rec, mkt_open, r_bar)
+    t, v = fundamental_log(rec, mkt_open, r_bar, external)
     idx = pd.DatetimeIndex(pd.Timestamp(date) + pd.to_timedelta(t, unit="ns"), name="FundamentalTime")
     return pd.DataFrame({"FundamentalValue": v}, index=idx)

@@ -324,24 +324,35 @@ class VecMarket:
         from .booklog import rows_from_records
         return rows_from_records(self.book_log_records(env))
 
+    @property
+    def date(self):
+        """the simulated date of the outputs' timestamps: the replay tape's, else the configs'"""
+        from .booklog import SESSION_DATE
+        if self.config in REPLAY_CONFIGS and getattr(self.tape, "date", None):
+            return self.tape.date
+        return SESSION_DATE
+
     def exchange_events(self, env):
         """the exchange's BEST_BID / BEST_ASK / LAST_TRADE log rows (OrderBook.py:114-141) as a
         DataFrame indexed by EventTime"""
         from .booklog import exchange_events_frame
-        return exchange_events_frame(self.book_log_rows(env), self.symbol)
+        return exchange_events_frame(self.book_log_rows(env), self.symbol, self.date)
 
     def orderbook_snapshots(self, env, wide_book=False):
         """ExchangeAgent.logOrderBookSnapshots' DataFrame with book_freq 0 (ORDERBOOK_<sym>_FULL)"""
         from .booklog import orderbook_full
-        return orderbook_full(self.book_log_rows(env), wide_book=wide_book)
+        return orderbook_full(self.book_log_rows(env), self.date, wide_book=wide_book)
 
     def fundamental_log(self, env):
-        """SparseMeanRevertingOracle.f_log of env as the DataFrame fundamental_<sym>.bz2 holds,
-        after Kernel.runner's kernelStopping pass (whose oracle observations it includes)"""
+        """the oracle's f_log of env as the DataFrame fundamental_<sym>.bz2 holds, after Kernel.runner's
+        kernelStopping pass (whose oracle observations it includes): the SparseMeanRevertingOracle's,
+        or the ExternalFileOracle's of hist_fund_* (ExternalFileOracle.py:19, 97)"""
         from .booklog import fundamental_frame
+        if self.config in REPLAY_CONFIGS:
+            raise ValueError("config/marketreplay.py runs without an oracle (oracle=None): no f_log")
         if not getattr(self, "_finalized", False):
             self.finalize()
-        return fundamental_frame(self.book_log_records(env))
+        return fundamental_frame(self.book_log_records(env), self.date, external=self.config in HIST_CONFIGS)
 
     def write_logs(self, env, log_dir, wide_book=False):
         """env's run directory as the reference writes it at termination (Kernel.writeLog /
@@ -353,15 +364,14 @@ class VecMarket:
             # and "all" (obi_rmsc02) is no pandas frequency: the reference raises in both
             raise NotImplementedError("book_freq %r: the resampled ORDERBOOK_%s_FREQ_* file is not restated"
                                       % (self.book_freq, self.symbol))
-        if self.config in HIST_CONFIGS:
-            raise NotImplementedError("the ExternalFileOracle's f_log (fundamental_%s) is not restated" % self.symbol)
-        if self.config in REPLAY_CONFIGS:
-            raise NotImplementedError("ORDERBOOK_%s_FULL of the replay's price-ladder book is not restated" % self.symbol)
         os.makedirs(log_dir, exist_ok=True)
         paths = [self.write_summary_log(env, log_dir)]
-        p = os.path.join(log_dir, "fundamental_%s.bz2" % self.symbol)
-        self.fundamental_log(env).to_pickle(p, compression="bz2")
-        paths.append(p)
+        if self.config not in REPLAY_CONFIGS:  # config/marketreplay.py: oracle=None, no f_log
+            f = self.fundamental_log(env)
+            if not f.empty:  # ExchangeAgent.kernelTerminating writes only a non-empty frame
+                p = os.path.join(log_dir, "fundamental_%s.bz2" % self.symbol)
+                f.to_pickle(p, compression="bz2")
+                paths.append(p)
         if self.book_freq == 0:
             paths.append(self.write_orderbook_log(env, log_dir, wide_book))
         return paths

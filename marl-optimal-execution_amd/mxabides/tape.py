@@ -20,8 +20,9 @@ class Tape:
     """Time-sorted replay records: t (ns since midnight), oid, price (cents), size, buy, and the
     ticker they belong to (`symbol`: the MarketReplayAgent's symbol, config/marketreplay.py -t)."""
 
-    def __init__(self, t, oid, price, size, buy, symbol=None):
+    def __init__(self, t, oid, price, size, buy, symbol=None, date=None):
         self.symbol = symbol
+        self.date = date  # the simulated date (YYYY-MM-DD): the outputs' timestamps
         self.t = np.ascontiguousarray(t, dtype=np.int64)
         self.oid = np.ascontiguousarray(oid, dtype=np.int64)
         self.price = np.ascontiguousarray(price, dtype=np.int64)
@@ -43,21 +44,22 @@ class Tape:
 
     def save(self, path):
         extra = {"symbol": np.array(self.symbol)} if self.symbol else {}
+        if self.date:
+            extra["date"] = np.array(self.date)
         np.savez_compressed(path, t=self.t, oid=self.oid, price=self.price, size=self.size, buy=self.buy, **extra)
 
     @classmethod
-    def load(cls, path, symbol=None):
-        """symbol: the ticker; default the one saved with the tape, else the <SYM> of a
-        tape_<SYM>_<date>.npz file name"""
+    def load(cls, path, symbol=None, date=None):
+        """symbol / date: the ticker and the simulated date; default the ones saved with the tape,
+        else those of a tape_<SYM>_<YYYY-MM-DD>.npz file name"""
         z = np.load(path, allow_pickle=False)
+        base = os.path.basename(path)
+        parts = base[:-4].split("_") if base.startswith("tape_") and base.endswith(".npz") else []
         if symbol is None:
-            if "symbol" in z.files:
-                symbol = str(z["symbol"])
-            else:
-                base = os.path.basename(path)
-                if base.startswith("tape_") and base.count("_") >= 2:
-                    symbol = base.split("_")[1]
-        return cls(z["t"], z["oid"], z["price"], z["size"], z["buy"], symbol=symbol)
+            symbol = str(z["symbol"]) if "symbol" in z.files else (parts[1] if len(parts) >= 3 else None)
+        if date is None:
+            date = str(z["date"]) if "date" in z.files else (parts[2] if len(parts) >= 3 else None)
+        return cls(z["t"], z["oid"], z["price"], z["size"], z["buy"], symbol=symbol, date=date)
 
 
 def load_lobster(path, date, symbol=None):
@@ -77,4 +79,5 @@ def load_lobster(path, date, symbol=None):
     order = np.argsort(t, kind="stable")
     if symbol is None:
         symbol = os.path.basename(path).split("_")[0] or None
-    return Tape(t[order], oid[order], price[order], size[order], buy[order], symbol=symbol)
+    return Tape(t[order], oid[order], price[order], size[order], buy[order], symbol=symbol,
+                date=str(day.date()))

@@ -529,6 +529,9 @@ static int64_t next_order_id(ora_env* e) {
 /* --------------------------- oracle (SMRO) -------------------------------- */
 static void blr_push(ora_env* e, int64_t t, int64_t price, int64_t qty);
 #define BL_FUNDAMENTAL (-2147483647 - 1) /* f_log records in the book-record stream */
+#define BL_FUND_LO (-2147483647)           /* ExternalFileOracle f_log: the value's low word */
+#define BL_FUND_HI (-2147483646)           /* ... and its high word */
+#define BL_MODIFY (1 << 30)                /* modifyOrder: -(price | BL_MODIFY | side << 29), volume delta */
 /* compute_fundamental_at_timestamp (SMRO:88-125); f_log append at SMRO:122 */
 static double o_compute(ora_env* e, int64_t ts, double v_adj, int64_t pt, double pv) {
     int64_t d = ts - pt;
@@ -581,7 +584,17 @@ static double td_seconds(int64_t ns) {
     return (double)s + (double)(us - s * 1000000) / 1000000.0;
 }
 /* getPriceAtTime (ExternalFileOracle.py:52-97) + getInterpolatedPrice (:131-159) */
-static double efo_price(int64_t t) {
+static void blr_push(ora_env* e, int64_t t, int64_t price, int64_t qty);
+/* ExternalFileOracle.f_log entry (ExternalFileOracle.py:97) as two book-log records (the value's
+ * low and high words; include/mxa.h, mxa_layout.h BL_FUND_LO / BL_FUND_HI) */
+static void efo_log(ora_env* e, int64_t t, double v) {
+    uint64_t b;
+    memcpy(&b, &v, 8);
+    blr_push(e, t, BL_FUND_LO, (int32_t)(uint32_t)b);
+    blr_push(e, t, BL_FUND_HI, (int32_t)(uint32_t)(b >> 32));
+}
+/* getPriceAtTime (ExternalFileOracle.py:52-97); e (nullable) logs the interpolating branch's value */
+static double efo_price_e(ora_env* e, int64_t t) {
     int n = g_fs_n;
     if (t < g_fs_t[0]) return g_fs_v[0];
     if (t > g_fs_t[n - 1]) return g_fs_v[n - 1];
@@ -595,13 +608,16 @@ static double efo_price(int64_t t) {
     if (li < 0) li += n; /* fundamental_series[-1] */
     double pl = g_fs_v[li], ph = g_fs_v[ui];
     double slope = pl != ph ? (ph - pl) / td_seconds(g_fs_t[ui] - g_fs_t[li]) : 0.0;
-    return pl + td_seconds(t - g_fs_t[li]) * slope;
+    double v = pl + td_seconds(t - g_fs_t[li]) * slope;
+    if (e && e->book_log) efo_log(e, t, v);
+    return v;
 }
+static double efo_price(int64_t t) { return efo_price_e(NULL, t); }
 
 /* observePrice (SMRO:210-227; ExternalFileOracle.py:110-129) */
 static int64_t o_observe(ora_env* e, int64_t t, double sigma_n, ora_rs* rs) {
     if (e->efo) {
-        double tp = efo_price(t);
+        double tp = efo_price_e(e, t);
         if (sigma_n == 0) return py_round(tp);
         return py_round(rs_normal(rs, tp, sqrt(sigma_n)));
     }
@@ -962,8 +978,12 @@ static void modify_order(ora_env* e, const msg_t* req) {
     for (int i = 0; i < book->n; i++) {
         level_t* L = &book->lv[i];
         if (L->o[0].price != req->oprice) continue;
+        const int64_t head_q = L->o[0].qty;
+        int hit = 0;
         for (int j = 0; j < L->n; j++) {
             if (L->o[j].id != req->ooid) continue;
+            if (!hit++ && e->book_log) /* the level's volume changes by new - old head (BL_MODIFY) */
+                blr_push(e, e->cur, -(req->oprice | BL_MODIFY | ((req->obuy ? 0 : 1) << 29)), nw.qty - head_q);
             L->o[0] = nw;
             for (int h = 0; h < e->nhist; h++) {
                 if (!hist_find(&e->hist[h], nw.id)) continue;
@@ -3458,6 +3478,10 @@ void ora_set_book_log(ora_env* e, int on) {
     e->book_log = on;
     e->nblg = 0;
     e->nblr = 0;
+    /* ExternalFileOracle: getDailyOpenPrice at kernelInitializing logged f_log's first entry when
+     * the open lies inside the series (the device writes it at its first logged launch) */
+    if (on && e->efo && e->pops == 0 && e->ex_open >= g_fs_t[0] && e->ex_open <= g_fs_t[g_fs_n - 1])
+        efo_log(e, e->ex_open, efo_price(e->ex_open));
 }
 int64_t ora_book_records(const ora_env* e, int64_t* buf, int64_t cap) {
     if (buf) memcpy(buf, e->blr, sizeof(int64_t) * (size_t)(cap < e->nblr ? cap : e->nblr));

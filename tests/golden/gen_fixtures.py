@@ -200,6 +200,8 @@ def encode(t_rel, recipient, mtype, msg):
 MIDNIGHT = 0
 TRACE = []
 BOOK_LOG = False  # book_freq 0 with a compact OrderBook.book_log (booklog fixtures only)
+FLOG = False      # only the oracle's f_log (flog fixtures: the ExternalFileOracle's)
+DIGEST_ROWS = 2000  # booklog fixtures above this many rows keep these verbatim and the rest as digests
 BOOKLOG_FULL_ROWS = 300  # rows kept verbatim to run the reference's logOrderBookSnapshots on
 
 
@@ -327,7 +329,7 @@ def run_config(cfg, seed, out, full):
     if cfg.startswith("marketreplay:"):  # config/marketreplay.py TICKER DATE (Kernel.runner replay)
         _, ticker, rdate = cfg.split(":")
         replay = (ticker, rdate)
-        cfg = "marketreplay"
+        cfg = cfg_script = "marketreplay"
         # the script's relative paths: the LOBSTER message file under data/lobster/ (linked to the
         # one the reference ships) and an empty processed-orders folder (the processor parses the
         # CSV; the committed pickles are never loaded)
@@ -429,6 +431,15 @@ def run_config(cfg, seed, out, full):
                for r in kern.summaryLog]
     with open(out + "_summary.json", "w") as f:
         json.dump(summary, f, indent=0)
+    if FLOG:  # the oracle's f_log[sym] after kernelStopping (ExchangeAgent.kernelTerminating's frame)
+        fl = ex.oracle.f_log[sym]
+        np.savez_compressed(
+            out + "_flog.npz",
+            fund_time=np.asarray([int(pd.Timestamp(r["FundamentalTime"]).value) - MIDNIGHT for r in fl], dtype=np.int64),
+            fund_value=np.asarray([r["FundamentalValue"] for r in fl], dtype=np.float64),
+            fund_types=np.asarray(sorted({type(r["FundamentalValue"]).__name__ for r in fl})),
+            fund_dtype=np.asarray(str(pd.DataFrame(fl).set_index("FundamentalTime")["FundamentalValue"].dtype)))
+        return
     if BOOK_LOG:
         save_booklog(ex, ob, sym, orig_snapshots, out)
         return
@@ -475,16 +486,24 @@ def save_booklog(ex, ob, sym, orig_snapshots, out):
     logOrderBookSnapshots' DataFrames (book_freq 0; wide_book False and True) over the first
     BOOKLOG_FULL_ROWS rows, as the reference writes them."""
     import pandas as pd
-    flat = []
-    for t, lv in ob.book_log:
+    flat, digests = [], []
+    for k, (t, lv) in enumerate(ob.book_log):
         bids = sorted((p, v) for p, v in lv if v < 0)[::-1]
         asks = sorted((p, v) for p, v in lv if v > 0)
-        flat += [t - MIDNIGHT, len(bids) + len(asks)]
+        row = [t - MIDNIGHT, len(bids) + len(asks)]
         for p, v in bids + asks:
-            flat += [p, v]
+            row += [p, v]
+        digests.append(fnv_words(FNV_OFF, row))  # every row: FNV-1a-64 over its int64 words
+        if k < DIGEST_ROWS:
+            flat += row
     types_ = {"BEST_BID": 0, "BEST_ASK": 1, "LAST_TRADE": 2}
     ev = [(int(r["EventTime"].value) - MIDNIGHT, types_[r["EventType"]], r["Event"]) for r in ex.log
           if r["EventType"] in types_]
+    ev_digest = FNV_OFF
+    for e_t, e_k, e_s in ev:  # every event: time, kind and the Event string's bytes
+        ev_digest = fnv_words(ev_digest, [e_t, e_k] + list(e_s.encode()))
+    rows_complete = len(ob.book_log) <= DIGEST_ROWS
+    ev = ev if rows_complete else ev[:3 * DIGEST_ROWS]
     frames = {}
     full_rows = ob.book_log.full
     for wide in (False, True):
@@ -496,9 +515,15 @@ def save_booklog(ex, ob, sym, orig_snapshots, out):
         df = got["df"]
         frames[wide] = df
     narrow, wide = frames[False], frames[True]
+    has_oracle = getattr(ex, "oracle", None) is not None  # config/marketreplay.py: oracle=None
+    flog = ex.oracle.f_log[sym] if has_oracle else []
     np.savez_compressed(
         out + "_booklog.npz",
         rows=np.asarray(flat, dtype=np.int64),
+        rows_complete=np.asarray(rows_complete),
+        row_digests=np.asarray(digests, dtype=np.uint64),
+        ev_digest=np.asarray(ev_digest, dtype=np.uint64),
+        n_events=np.asarray(len([r for r in ex.log if r["EventType"] in types_])),
         ev_t=np.asarray([e[0] for e in ev], dtype=np.int64),
         ev_type=np.asarray([e[1] for e in ev], dtype=np.int8),
         ev_text=np.asarray([e[2] for e in ev]),
@@ -513,10 +538,11 @@ def save_booklog(ex, ob, sym, orig_snapshots, out):
         wide_dtypes=np.asarray([str(d) for d in wide.dtypes]),
         # SparseMeanRevertingOracle.f_log[sym] after kernelStopping, the frame ExchangeAgent.
         # kernelTerminating writes as fundamental_<sym> (ExchangeAgent.py:111-117)
-        fund_time=np.asarray([int(r["FundamentalTime"].value) - MIDNIGHT for r in ex.oracle.f_log[sym]], dtype=np.int64),
-        fund_value=np.asarray([r["FundamentalValue"] for r in ex.oracle.f_log[sym]], dtype=np.float64),
-        fund_types=np.asarray([type(r["FundamentalValue"]).__name__ for r in ex.oracle.f_log[sym]]),
-        fund_dtype=np.asarray(str(pd.DataFrame(ex.oracle.f_log[sym]).set_index("FundamentalTime")["FundamentalValue"].dtype)),
+        fund_time=np.asarray([int(r["FundamentalTime"].value) - MIDNIGHT for r in flog], dtype=np.int64),
+        fund_value=np.asarray([r["FundamentalValue"] for r in flog], dtype=np.float64),
+        fund_types=np.asarray([type(r["FundamentalValue"]).__name__ for r in flog]),
+        fund_dtype=np.asarray(str(pd.DataFrame(flog).set_index("FundamentalTime")["FundamentalValue"].dtype)
+                              if flog else ""),
         full_rows=np.asarray(BOOKLOG_FULL_ROWS))
 
 
@@ -557,17 +583,25 @@ def rng_kats(path):
 def main():
     global SUMMARY_ONLY
     global BOOK_LOG
+    global FLOG
     if sys.argv[1] == "run":
         SUMMARY_ONLY = "--summary-only" in sys.argv
         BOOK_LOG = "--booklog" in sys.argv
+        FLOG = "--flog" in sys.argv
         run_config(sys.argv[2], int(sys.argv[3]), sys.argv[4], "--full" in sys.argv)
         return
-    if sys.argv[1] == "booklog":  # <cfg>_<seed>_booklog.npz: order-book snapshot outputs
-        jobs = [("rmsc03", 123456789), ("value_noise", 7)]
+    if sys.argv[1] in ("booklog", "flog"):  # <cfg>_<seed>_booklog.npz / _flog.npz
+        if sys.argv[1] == "booklog":  # order-book snapshot outputs (the replays: config/marketreplay.py's book_freq 0)
+            jobs = [("rmsc03", 123456789), ("value_noise", 7), ("marketreplay:IBM:2003-01-14", 1),
+                    ("marketreplay:GOOG:2012-06-21", 1)]
+        else:  # the ExternalFileOracle's f_log (fundamental_JPM)
+            jobs = [("hist_fund_value", 7), ("hist_fund_diverse", 7)]
+        if len(sys.argv) > 2:
+            jobs = [j for j in jobs if j[0].startswith(sys.argv[2])]
         procs = []
         for cfg, seed in jobs:
-            out = os.path.join(HERE, "%s_%d" % (cfg, seed))
-            cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out, "--booklog"]
+            out = os.path.join(HERE, "%s_%d" % (cfg.replace(":", "_"), seed))
+            cmd = [sys.executable, os.path.abspath(__file__), "run", cfg, str(seed), out, "--" + sys.argv[1]]
             procs.append(subprocess.Popen(cmd, cwd=tempfile.mkdtemp(prefix="gf_"),
                                           env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1")))
         for (cfg, seed), p in zip(jobs, procs):

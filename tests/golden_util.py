@@ -71,3 +71,31 @@ def load_named(name):
         summ = json.load(f)
     tr = np.load(os.path.join(GOLDEN, name + ".npz"))["trace"]
     return d, tr, summ
+
+
+FNV_OFF, FNV_PRIME, M64 = 0xCBF29CE484222325, 0x100000001B3, (1 << 64) - 1
+
+
+def fnv_words(h, words):
+    """gen_fixtures.fnv_words: FNV-1a-64 over int64 words"""
+    for w in words:
+        h = ((h ^ (int(w) & M64)) * FNV_PRIME) & M64
+    return h
+
+
+def book_row_digests(flat):
+    """per book_log row: FNV-1a-64 over (t, n, price, volume, ...) without the executed-quantity
+    words, the digest gen_fixtures.save_booklog stores for every row"""
+    from mxabides import booklog as bl
+    return [fnv_words(FNV_OFF, [t, len(p)] + np.stack([p, v], axis=1).ravel().tolist())
+            for t, _, _, p, v in bl.iter_rows(flat)]
+
+
+def event_digest(events):
+    """gen_fixtures.save_booklog's digest of the exchange's BEST_BID / BEST_ASK / LAST_TRADE rows
+    (time, kind 0/1/2, Event bytes)"""
+    kinds = {"BEST_BID": 0, "BEST_ASK": 1, "LAST_TRADE": 2}
+    h = FNV_OFF
+    for t, k, s in events:
+        h = fnv_words(h, [t, kinds[k]] + list(s.encode()))
+    return h

@@ -163,3 +163,54 @@ def test_duplicate_timestamps_keep_last_row(tmp_path):
     d.to_pickle(p, compression="bz2")
     back = pd.read_pickle(p, compression="bz2")
     assert back.equals(d)
+
+
+# ---- config/marketreplay.py (book_freq 0: ORDERBOOK_<sym>_FULL of the replay's book) and the
+# ExternalFileOracle's f_log (fundamental_JPM of hist_fund_*), pinned by reference runs
+# (gen_fixtures.py booklog marketreplay / flog): every book_log row and the exchange's events as
+# digests, the first rows verbatim
+REPLAY_TAPES = ["IBM_2003-01-14", "GOOG_2012-06-21"]
+
+
+def _recs(rows3):
+    r = np.zeros(len(rows3), dtype=bl.REC_DTYPE)
+    r["t"], r["price"], r["qty"] = rows3[:, 0], rows3[:, 1], rows3[:, 2]
+    return r
+
+
+@pytest.mark.parametrize("tname", REPLAY_TAPES)
+def test_oracle_replay_book_log_equals_reference(tname):
+    """the oracle's replay rows equal the reference's (all rows by digest, the first ones word by
+    word); its book-update records (limit, cancel and the modifyOrder head-replace as a volume
+    change) replay on the host to exactly those rows"""
+    import golden_util as gu
+    from mxabides import tape
+    z = np.load(os.path.join(GOLDEN, "marketreplay_%s_1_booklog.npz" % tname))
+    tp = tape.Tape.load(os.path.join(GOLDEN, "tape_%s.npz" % tname))
+    o = pyoracle.OracleReplayRunner(tp, symbol=tp.symbol)
+    o.set_book_log()
+    o.run()
+    flat = o.book_log()
+    assert np.array_equal(np.asarray(gu.book_row_digests(flat), dtype=np.uint64), z["row_digests"])
+    head = bl.strip_executions(flat)[:len(z["rows"])]
+    assert np.array_equal(head, z["rows"])
+    ev = bl.exchange_events(flat, tp.symbol)
+    assert len(ev) == int(z["n_events"]) and gu.event_digest(ev) == int(z["ev_digest"])
+    rec = _recs(o.book_records())
+    assert (rec["price"] < 0).sum() > 1000  # the replay's modifies / cancels are in the stream
+    assert np.array_equal(bl.rows_from_records(rec), flat)
+
+
+@pytest.mark.parametrize("cfg", ["hist_fund_value", "hist_fund_diverse"])
+def test_oracle_external_file_oracle_f_log_equals_reference(cfg):
+    """ExternalFileOracle.f_log (ExternalFileOracle.py:19, 97) after kernelStopping: one entry per
+    getPriceAtTime inside the series, as (low, high) word record pairs of the interpolated double"""
+    z = np.load(os.path.join(GOLDEN, "%s_7_flog.npz" % cfg))
+    o = pyoracle.OracleEnv(cfg, 7)
+    o.set_book_log()
+    o.run()
+    o.finish()
+    t, v = bl.fundamental_log(_recs(o.book_records()), external=True)
+    assert np.array_equal(t, z["fund_time"]) and np.array_equal(v, z["fund_value"])
+    f = bl.fundamental_frame(_recs(o.book_records()), external=True)
+    assert str(f["FundamentalValue"].dtype) == str(z["fund_dtype"]) and len(f) == len(t)

@@ -133,7 +133,8 @@ def test_gpu_fundamental_records_equal_oracle(mx):
 def test_gpu_write_logs_follows_the_config_book_freq(mx, tmp_path):
     """ExchangeAgent.kernelTerminating (ExchangeAgent.py:106-126): with book_freq None
     (random_fund_value, value_noise's default) no order-book file; the ticker names the files;
-    a resampling frequency (rmsc01 "M", obi_rmsc02 "all") is not restated and says so"""
+    a resampling frequency (rmsc01 "M", obi_rmsc02 "all") is not restated and says so (the
+    reference's own pd.date_range(..., closed=) fails under pandas 2)"""
     import pandas as pd
     m = mx.VecMarket("value_noise", [7], book_log=CAP)
     m.run()
@@ -147,3 +148,51 @@ def test_gpu_write_logs_follows_the_config_book_freq(mx, tmp_path):
     q = mx.VecMarket("rmsc01", [7], book_log=CAP)
     with pytest.raises(NotImplementedError):
         q.write_logs(0, str(tmp_path / "r1"))
+
+
+@pytest.mark.parametrize("tname", ["IBM_2003-01-14", "GOOG_2012-06-21"])
+def test_gpu_replay_book_log_equals_reference(mx, tname, tmp_path):
+    """config/marketreplay.py (book_freq 0) on the device's price ladder: the host replay of its
+    book-update records (limit orders, cancellations, modifyOrder's head-replace) gives the
+    reference's every book_log row and exchange event (digests; the first rows verbatim), and
+    write_logs writes summary_log + ORDERBOOK_<sym>_FULL, with no fundamental file (oracle=None)"""
+    import golden_util as gu
+    import pandas as pd
+    from mxabides import tape
+    z = np.load(os.path.join(GOLDEN, "marketreplay_%s_1_booklog.npz" % tname))
+    tp = tape.Tape.load(os.path.join(GOLDEN, "tape_%s.npz" % tname))
+    m = mx.VecMarket("marketreplay_runner", [0, 0], tape=tp, book_log=CAP)
+    m.run()
+    s = m.summary()
+    assert (s["status"] == 1).all(), s["err"]
+    for e in range(2):
+        rows = m.book_log_rows(e)
+        assert np.array_equal(np.asarray(gu.book_row_digests(rows), dtype=np.uint64), z["row_digests"])
+        assert np.array_equal(bl.strip_executions(rows)[:len(z["rows"])], z["rows"])
+    ev = m.exchange_events(0)
+    assert len(ev) == int(z["n_events"])
+    mid = pd.Timestamp(tp.date).value
+    assert gu.event_digest(zip((ev.index.asi8 - mid).tolist(), ev["EventType"], ev["Event"])) == int(z["ev_digest"])
+    if tname.startswith("IBM"):  # the narrow frame of GOOG is 47 M cells: the same code, not rerun here
+        paths = m.write_logs(0, str(tmp_path))
+        assert sorted(os.path.basename(p) for p in paths) == ["ORDERBOOK_IBM_FULL.bz2", "summary_log.bz2"]
+        back = pd.read_pickle(os.path.join(str(tmp_path), "ORDERBOOK_IBM_FULL.bz2"), compression="bz2")
+        assert back.index.names == ["time", "quote"]
+        assert back.index.get_level_values(0).nunique() == len({t for t, _, _, _, _ in bl.iter_rows(m.book_log_rows(0))})
+
+
+@pytest.mark.parametrize("cfg", ["hist_fund_value", "hist_fund_diverse"])
+def test_gpu_external_file_oracle_f_log_equals_reference(mx, cfg, tmp_path):
+    """the ExternalFileOracle's f_log from the device (the value agents' observations, the
+    kernelStopping pass) equals the reference's; write_logs writes fundamental_JPM"""
+    import pandas as pd
+    from golden_util import market_kw
+    z = np.load(os.path.join(GOLDEN, "%s_7_flog.npz" % cfg))
+    m = mx.VecMarket(cfg, [7], book_log=1 << 20, **market_kw(cfg))
+    m.run()
+    df = m.fundamental_log(0)
+    assert np.array_equal(df.index.asi8 - pd.Timestamp(bl.SESSION_DATE).value, z["fund_time"])
+    assert np.array_equal(df["FundamentalValue"].to_numpy(), z["fund_value"])
+    paths = m.write_logs(0, str(tmp_path))
+    assert sorted(os.path.basename(p) for p in paths) == ["fundamental_JPM.bz2", "summary_log.bz2"]
+    assert pd.read_pickle(os.path.join(str(tmp_path), "fundamental_JPM.bz2"), compression="bz2").equals(df)
