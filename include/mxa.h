@@ -265,7 +265,10 @@ typedef struct {
  * fundamental value (price MXA_BL_FUNDAMENTAL, qty the value), including the oracle
  * observations of the last mxa_finalize, the series written as fundamental_<sym>.bz2 */
 #define MXA_BL_FUNDAMENTAL (-2147483647 - 1)
-/* plain Kernel.runner configs: `cap` records per env (0 = off); resets every env's record
+/* Kernel.runner configs (the replay of mxa_create_replay_runner / _twap included: its records add
+ * modifyOrder's head-replace as a level-volume change, price -(p | 1 << 30 | side << 29); the
+ * ExternalFileOracle's f_log travels as (low, high) word pairs of the double, prices -2^31 + 1 and
+ * -2^31 + 2): `cap` records per env (0 = off); resets every env's record
  * count, so enable it after mxa_create / mxa_reset and before the first launch.  An env that
  * fills its log stops with error ERR_BOOK_LOG_FULL (20).  The exchange's event runs (batched
  * LIMIT/CANCEL handling) are off while logging. */

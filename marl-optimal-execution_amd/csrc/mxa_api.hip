@@ -748,8 +748,8 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
 // book-update log (OrderBook.book_log / the exchange's BEST_BID, BEST_ASK, LAST_TRADE events):
 // `cap` records per env in one device buffer; every env's record count restarts at 0
 int mxa_set_book_log(mxa_handle* h, int32_t cap) {
-  // (the replay book is a price ladder the log does not follow: not for replay handles)
-  if (!h || h->gym || h->replay || !h->run_log || cap < 0) return MXA_EINVAL;
+  // Kernel.runner handles, the replay's (config/marketreplay.py) included; not GymKernel handles
+  if (!h || h->gym || !h->run_log || cap < 0) return MXA_EINVAL;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->d_blog) HIPCHK(h, hipFree(h->d_blog));

@@ -3563,6 +3563,7 @@ struct Eng {
   }
   // handleLimitOrder / executeOrder (OrderBook.py:38-254) on the ladder
   DEV void rp_handle_limit(const Msg& m) {
+    PROF_SCOPE(84);
     i32 oid = (i32)m.w[1], qty = (i32)m.w[2], price = (i32)m.w[3], d = (i32)m.w[5];
     i32 agent = m_agent(m);
     int buy = m_buy(m);
@@ -3621,6 +3622,7 @@ struct Eng {
   }
   // cancelOrder (OrderBook.py:284-339): first live entry of the id at the request's level
   DEV void rp_cancel(const Msg& m) {
+    PROF_SCOPE(86);
     i32 oid = (i32)m.w[1], price = (i32)m.w[3], d = (i32)m.w[5];
     const int side = m_buy(m) ? 0 : 1;
     i32 x = price - U(rx->L.pmin);
@@ -3648,6 +3650,7 @@ struct Eng {
   // modifyOrder (OrderBook.py:341-372): each entry of the id at the level replaces the level
   // HEAD with the new order; one ORDER_MODIFIED per match per history epoch holding the id
   DEV void rp_modify(const Msg& m) {
+    PROF_SCOPE(85);
     if (m.w[0] & MF_NOT_SAME) return;  // isSameOrder(order, new_order) is False
     i32 oid = (i32)m.w[1], qty = (i32)m.w[2], price = (i32)m.w[3], oprice = (i32)m.w[4], d = (i32)m.w[5];
     const int buy = m_buy(m), side = buy ? 0 : 1;
@@ -3725,6 +3728,7 @@ struct Eng {
   // placing or modifying builds LimitOrder(order_id=0), which takes the next auto id
   // (Order.py:26), so a modify then fails isSameOrder at the exchange (OrderBook.py:343-344)
   DEV void mr_place_record(i32 r) {
+    PROF_SCOPE(91);
     const i32 oid = U(rx->oid[r]), price = U(rx->price[r]), size = U(rx->size[r]);
     const i32 d = oid == 0 ? zero_dense() : U(rx->dense[r]);
     const int buy = (int)U((i32)rx->buy[r]);
@@ -3769,6 +3773,7 @@ struct Eng {
     }
   }
   DEV void mr_wakeup() {
+    PROF_SCOPE(87);
     ta_wakeup();
     u32 f = flags();
     if (!((f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE))) return;
@@ -3802,7 +3807,10 @@ struct Eng {
     const i32 r1 = U(rx->tm0[g + 1]);
     for (i32 r = U(rx->tm0[g]); r < r1; r++) mr_place_record(r);
   }
-  DEV void mr_receive(const Msg& m) { ta_receive(m, AG_REPLAY); }
+  DEV void mr_receive(const Msg& m) {
+    PROF_SCOPE(88);
+    ta_receive(m, AG_REPLAY);
+  }
 
   // ---------------- DummyRLExecutionAgent (dummy_rl_execution_agent.py) + GymKernel hooks
   DEV void kcancel_at(i64 t) {  // GymKernel.setCancelOrder(sender, t - Timedelta(0.5) = t)
@@ -3863,6 +3871,7 @@ struct Eng {
     }
   }
   DEV void rl_receive(const Msg& m) {
+    PROF_SCOPE(89);
     ta_receive(m, AG_DUMMYRL);
     RpHdr* R = rh();
     const u32 k = m_kind(m);
@@ -3967,6 +3976,7 @@ struct Eng {
   }
   // DummyRL.process_action + place_orders (dummy_rl:138-179), called by the step kernel
   DEV void rl_place_orders(const double* act) {
+    PROF_SCOPE(90);
     RpHdr* R = rh();
     rec_load(PC.first_rl);
     const double q0 = (double)PC.rl_quantity, q = q0;  // metrics.rem_quantity is never updated
@@ -4768,6 +4778,13 @@ struct Eng {
         pb = kk == MK_SPREAD_REQ ? 48 : kk == MK_TV_REQ ? 49 : kk == MK_LIMIT ? 50 : kk == MK_CANCEL ? 51 : 52;
         pc = pb + 8;
       }
+      if constexpr (RP) {  // replay: 92 / 93 MarketReplayAgent message / wakeup, 94 / 95 the RL agent's (counts +32)
+        const int at = rgi(AF_TYPE);
+        if (at == AG_REPLAY || at == AG_DUMMYRL) {
+          pb = 92 + 2 * (at == AG_DUMMYRL) + (type == MT_WAKEUP);
+          pc = pb + 32;
+        }
+      }
       if (type == MT_MESSAGE && rgi(AF_TYPE) == AG_ZI) {  // ZI messages: 80 SPREAD, 81 ACCEPTED, 82 EXECUTED, 83 other
         const u32 kk = m_kind(m);
         pb = kk == MK_SPREAD ? 80 : kk == MK_ACCEPTED ? 81 : kk == MK_EXECUTED ? 82 : 83;
@@ -5359,6 +5376,10 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
     if (g.status == ST_DONE) g.rp_terminate();
   }
   g.save();
+#ifdef MXA_PROF
+  atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
+  atomicAdd(&mxa::g_mxa_prof[64 + g.lane], (unsigned long long)g.prof[64 + g.lane]);
+#endif
   RpHdr* R = g.rh();
   if (g.lane < 9) obs[9 * (size_t)env + g.lane] = R->obs[g.lane];
   u64 key;
