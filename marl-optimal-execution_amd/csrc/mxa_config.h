@@ -94,6 +94,9 @@ constexpr int lat_lds(int cfg);
 #ifndef MXA_RFV_SQL
 #define MXA_RFV_SQL 24  // LDS-resident queue slots per lane (96 = no HBM tier); rfv x2048 run kernel: 12 -> 1220 ms, 24 -> 840, 36 -> 1237 (fewer waves fit)
 #endif
+#ifndef MXA_RP_HOT
+#define MXA_RP_HOT 2  // replay configurations: the exchange's and the MarketReplayAgent's records in LDS
+#endif
 #ifndef MXA_HOT_RECORDS
 #define MXA_HOT_RECORDS 0  // measured (r01 s3i): exchange + MM records in LDS were 3 % slower than L1/L2-served loads
 #endif
@@ -134,14 +137,20 @@ constexpr Shape shape(int cfg) {
        // replies for the market maker's depth-5 spread queries
        : (cfg == MXA_CFG_RANDOM_FUND_DIVERSE || cfg == MXA_CFG_HIST_FUND_DIVERSE)
            ? Shape{96, MXA_SO_RFD, false, MXA_RFD_WAVES, 8, 0, MXA_RFD_SQL}
-                                       : Shape{4, 1, true, 2, 8, MXA_HOT_RECORDS};  // marketreplay (both): book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
+                                       : Shape{4, 1, true, 2, 8, MXA_RP_HOT};  // marketreplay (both): book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
+// configurations with the replay / gym header (RpHdr) in LDS for a launch
+constexpr bool is_rp(int cfg) {
+  return cfg == MXA_CFG_MARKETREPLAY || cfg == MXA_CFG_MARKETREPLAY_RUNNER || cfg == MXA_CFG_MARKETREPLAY_TWAP ||
+         cfg == MXA_CFG_RMSC03_RL;
+}
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)sq_lds(cfg) * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
          + 1024                                                                               // RNG stream windows
          + (size_t)lat_lds(cfg) * 8                                                           // exchange latency row
+         + (is_rp(cfg) ? 256 : 0)                                                             // RpHdr (replay / gym)
 #ifdef MXA_QREG
          + 768  // batched-push scratch: slot table + staged keys
 #else

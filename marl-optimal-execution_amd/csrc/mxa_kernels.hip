@@ -778,7 +778,8 @@ struct Eng {
 #ifdef MXA_PROF
   LDSP u64* prof;
 #endif
-  LDSP u64* hotrec;  // [HOT][64]: the exchange's (and the market maker's) agent record
+  LDSP u64* hotrec;  // [HOT][64]: the exchange's (and the market maker's or replay agent's) agent record
+  LDSP RpHdr* rhl;   // RP: the replay header for the launch (rh())
   // the exchange's latency row in LDS for the launch (MXA_LAT_LDS_MASK): every send reads one
   // entry, which from HBM is a dependent memory round trip on the event chain
   static constexpr int LATL = BUILD ? 0 : mxa_cfg::lat_lds(CFG);
@@ -823,6 +824,7 @@ struct Eng {
     hotrec = (LDSP u64*)(lds + LDS_Q + 512);
 #endif
     latl = (LDSP double*)(hotrec + mxa_cfg::shape(CFG).hot * 64);
+    rhl = (LDSP RpHdr*)(latl + mxa_cfg::lat_lds(CFG));
   }
 
   // ---------------- env block accessors
@@ -846,9 +848,12 @@ struct Eng {
   // ---------------- agent record
   // the exchange and the market maker take ~95 % of rmsc03's events: their records live in
   // LDS for the launch (load()/save() move them), every other agent's comes from HBM
+  // second hot record: the market maker (rmsc03) or the MarketReplayAgent (the replay configs,
+  // whose every other event is its wakeup or an execution report)
+  static constexpr int HOT1 = PC.n_mm > 0 ? PC.first_mm : PC.n_replay > 0 ? PC.first_replay : -1;
   DEV int hot_slot(int a) {
     if (HOT > 0 && a == 0) return 0;
-    if (HOT > 1 && PC.n_mm > 0 && a == PC.first_mm) return 1;
+    if (HOT > 1 && HOT1 >= 0 && a == HOT1) return 1;
     return -1;
   }
   DEV void rec_load(int a) {
@@ -882,7 +887,7 @@ struct Eng {
       else agent_ptr(a)[lane] = (u64)t;
     }
   }
-  DEV int hot_agent(int hs) { return hs == 0 ? 0 : PC.first_mm; }
+  DEV int hot_agent(int hs) { return hs == 0 ? 0 : HOT1; }
   DEV u32 rg(int f) { return (f & 1) ? rdl(rhi, f >> 1) : rdl(rlo, f >> 1); }
   DEV i32 rgi(int f) { return (i32)rg(f); }
   DEV i64 rg64(int f) { return (i64)(((u64)rdl(rhi, f >> 1) << 32) | rdl(rlo, f >> 1)); }
@@ -3384,7 +3389,14 @@ struct Eng {
   // (count, head, tail, total qty); entries come from a per-env pool; the live entries of one
   // order id are chained so cancel/modify find them without walking a level.
   // =====================================================================================
-  DEV RpHdr* rh() { return (RpHdr*)(env + rx->L.off_rh); }
+  DEV RpHdr* rh_g() { return (RpHdr*)(env + rx->L.off_rh); }
+  // the replay / gym header (best levels, free-stack top, replay cursor, RL state) lives in LDS
+  // for a launch of the engine (load() / save() move it): every handler reads it on its
+  // dependent chain.  The builder writes the env block directly
+  DEV auto rh() {
+    if constexpr (BUILD) return rh_g();
+    else return rhl;
+  }
   DEV i32* lv_cnt(int s) { return (i32*)(env + rx->L.off_lvc) + (size_t)s * U(rx->L.P); }
   DEV i32* lv_head(int s) { return (i32*)(env + rx->L.off_lvh) + (size_t)s * U(rx->L.P); }
   DEV i32* lv_tail(int s) { return (i32*)(env + rx->L.off_lvt) + (size_t)s * U(rx->L.P); }
@@ -3412,7 +3424,7 @@ struct Eng {
   // SIZE > 0 record has been handled, in an earlier episode of the process or this one
   DEV i64 rp_skip_used(i64 c) {
     const i32 n = U(rx->nuid);
-    const RpHdr* R = rh();
+    auto R = rh();
     const i32 hi = max(U(R->tape_hi), U(R->mr_done));
     for (;;) {
       i32 lo = 0, h2 = n - 1, f = -1;
@@ -3471,7 +3483,7 @@ struct Eng {
   }
   // enterOrder (OrderBook.py:256-282): append to the level FIFO
   DEV void rp_enter(i32 oid, i32 d, i32 agent, int buy, i32 qty, i32 price) {
-    RpHdr* R = rh();
+    auto R = rh();
     const int side = buy ? 0 : 1;
     i32 x = lvl_index(price);
     if (x < 0) return;
@@ -3520,7 +3532,7 @@ struct Eng {
   }
   // remove entry e (level x of `side`) from the book
   DEV void rp_unlink(int side, i32 x, i32 e) {
-    RpHdr* R = rh();
+    auto R = rh();
     RpEntry* E = pool();
     i32 p = U(E[e].prev), n = U(E[e].next), q = U(E[e].qty), d = U(E[e].dense);
     i32 cnt = U(lv_cnt(side)[x]);
@@ -3571,7 +3583,7 @@ struct Eng {
     if constexpr (BLOG) bl_put(cur, price, buy ? qty : -qty);
     const i32 hep = h.epoch;
     rp_note_entry_epoch(d, hep);
-    RpHdr* R = rh();
+    auto R = rh();
     RpEntry* E = pool();
     const i32 pmin = U(rx->L.pmin);
     i64 ex_q = 0, ex_pq = 0;
@@ -3695,7 +3707,7 @@ struct Eng {
   // QUERY_SPREAD reply with `depth` levels (ExchangeAgent.py:215-245): level-1 price/qty,
   // level-2 prices and the level counts (w6/w7 = price2 | count << 20)
   DEV void rp_spread(const Msg& m, bool closed) {
-    RpHdr* R = rh();
+    auto R = rh();
     const i32 pmin = U(rx->L.pmin);
     i32 depth = (i32)m.w[1];
     i32 nb = U(R->nlev[0]), na = U(R->nlev[1]);
@@ -3777,11 +3789,19 @@ struct Eng {
     ta_wakeup();
     u32 f = flags();
     if (!((f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE))) return;
-    RpHdr* R = rh();
+    auto R = rh();
     i32 wi = U(R->mr_wi);
     const i32 ntm = U(rx->L.ntm);
     if (wi >= ntm) return;  // IndexError: every order submitted (the last group never is)
-    const i64 tn = U(rx->tm[wi]);
+    // one round trip for the tape words this wakeup reads in the common case: lane 0 tm[wi],
+    // lane 1 tm[wi - 1], lanes 2-4 tm0[wi - 1 .. wi + 1] (tm0 has ntm + 1 entries)
+    i64 tv = 0;
+    {
+      const i32 ix = lane == 0 ? wi : lane == 1 ? wi - 1 : wi - 3 + lane;
+      if (lane < 2 && ix >= 0) tv = rx->tm[ix];
+      else if (lane >= 2 && lane < 5 && ix >= 0 && ix <= ntm) tv = (i64)rx->tm0[ix];
+    }
+    const i64 tn = (i64)rdl64((u64)tv, 0);
     wakeup_at(cur_agent, tn);
     R->mr_wi = wi + 1;
     // orders[currentTime]: tm is strictly increasing (sorted tape), so the match is unique. A
@@ -3789,7 +3809,12 @@ struct Eng {
     // one); anything else (a delayed wakeup) takes the binary search
     i32 lo = 0, hi = ntm - 1, g = -1;
     if (tn == cur) g = wi, lo = hi + 1;
-    else if (wi > 0 && U(rx->tm[wi - 1]) == cur) g = wi - 1, lo = hi + 1;
+    else if (wi > 0 && (i64)rdl64((u64)tv, 1) == cur) g = wi - 1, lo = hi + 1;
+    if (g >= 0) {  // the group's record range from the batch
+      const i32 r0 = (i32)rdl64((u64)tv, g == wi ? 3 : 2), r1 = (i32)rdl64((u64)tv, g == wi ? 4 : 3);
+      for (i32 r = r0; r < r1; r++) mr_place_record(r);
+      return;
+    }
     while (lo <= hi) {
       i32 mid = (lo + hi) >> 1;
       i64 tv = U(rx->tm[mid]);
@@ -3824,7 +3849,7 @@ struct Eng {
   }
   DEV void rl_wakeup() {
     if (!ta_wakeup()) return;
-    RpHdr* R = rh();
+    auto R = rh();
     // first horizon time strictly after now
     i32 k = cur < PC.rl_h0 ? 0 : (i32)((cur - PC.rl_h0) / PC.rl_hstep) + 1;
     i32 trade = U(R->rl_trade);
@@ -3842,7 +3867,7 @@ struct Eng {
   }
   // ABIDESEnvMetrics.addLOB: deque(maxlen=100), newest first
   DEV void rl_add_lob(const Msg& m) {
-    RpHdr* R = rh();
+    auto R = rh();
     const i32 nb = (i32)(m.w[6] >> 20), na = (i32)(m.w[7] >> 20);
     const int dnone = !m_hasdata(m);
     i32 ph = U(R->ph_n), cnt = U(R->m_cnt), hd = U(R->m_head);
@@ -3873,7 +3898,7 @@ struct Eng {
   DEV void rl_receive(const Msg& m) {
     PROF_SCOPE(89);
     ta_receive(m, AG_DUMMYRL);
-    RpHdr* R = rh();
+    auto R = rh();
     const u32 k = m_kind(m);
     if (k == MK_EXECUTED) {  // ExecutionAgent.handleOrderExecution (the DummyRL override is misspelt)
       i64 ex = U(R->rl_exec) + (i32)m.w[2];
@@ -3894,31 +3919,34 @@ struct Eng {
     }
   }
   // numpy pairwise summation (n <= 128) and np.std
-  DEV static double np_pairwise(const double* a, int n) {
+  // numpy's pairwise sum (pairwise_sum, numpy/core/src/umath/loops_utils.h: 8 accumulators below
+  // 128 elements) over a[i] = lane i % 64 of v0 (i < 64) / v1 (i >= 64), in numpy's order
+  DEV double np_pairwise_lanes(double v0, double v1, int n) {
+    auto at = [&](int i) -> double { return i < 64 ? rdl_d(v0, i) : rdl_d(v1, i - 64); };
     if (n < 8) {
       double r = 0.;
-      for (int i = 0; i < n; i++) r += a[i];
+      for (int i = 0; i < n; i++) r += at(i);
       return r;
     }
-    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    double r0 = at(0), r1 = at(1), r2 = at(2), r3 = at(3), r4 = at(4), r5 = at(5), r6 = at(6), r7 = at(7);
     int i;
     for (i = 8; i < n - (n % 8); i += 8) {
-      r0 += a[i];
-      r1 += a[i + 1];
-      r2 += a[i + 2];
-      r3 += a[i + 3];
-      r4 += a[i + 4];
-      r5 += a[i + 5];
-      r6 += a[i + 6];
-      r7 += a[i + 7];
+      r0 += at(i);
+      r1 += at(i + 1);
+      r2 += at(i + 2);
+      r3 += at(i + 3);
+      r4 += at(i + 4);
+      r5 += at(i + 5);
+      r6 += at(i + 6);
+      r7 += at(i + 7);
     }
     double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    for (; i < n; i++) res += a[i];
+    for (; i < n; i++) res += at(i);
     return res;
   }
   // DummyRL.get_observation (dummy_rl:291-312): float64[9] into the replay header
   DEV void rl_observe() {
-    RpHdr* R = rh();
+    auto R = rh();
     const i64 fl = (cur / PC.rl_hstep) * PC.rl_hstep;  // currentTime.floor("30S")
     i32 rem = PC.rl_nh;
     if (fl >= PC.rl_h0 && (fl - PC.rl_h0) / PC.rl_hstep < PC.rl_nh) rem = PC.rl_nh - 1 - (i32)((fl - PC.rl_h0) / PC.rl_hstep);
@@ -3938,26 +3966,34 @@ struct Eng {
     }
     const i64 p0 = U(R->p0), pt = U(L[hd].data);
     const i64 bid = U(L[hd].bid), ask = U(L[hd].ask), bv = U(R->m_bq), av = U(R->m_aq);
-    double lm[100];
-    for (int i = 0; i < cnt; i++) {
-      const RpLob li = L[(hd + i) % 100];
-      if ((U(li.flags) & 3) != 3) {
-        fail(ERR_RP_OBS);
-        return;
+    // the deque's log mid returns, lane-parallel: entry i in lane i % 64, register i / 64 (at
+    // most 100 entries); one coalesced load and one log evaluation per register
+    double lv[2];
+    bool bad = false;
+    for (int c = 0; c < 2; c++) {
+      const int i = c * 64 + lane;
+      double x = 1.0;
+      if (i < cnt) {
+        const RpLob li = L[(hd + i) % 100];
+        bad |= (li.flags & 3) != 3;
+        x = (double)((i64)li.bid + li.ask) / 2 / (double)p0;
       }
-      double mid = (double)((i64)U(li.bid) + U(li.ask)) / 2;
-      lm[i] = gm_log(mid / (double)p0);
+      lv[c] = gm_log(x);
+    }
+    if (bal(bad)) {  // the reference raises at the first LOB with a missing side
+      fail(ERR_RP_OBS);
+      return;
     }
     o[2] = gm_log((double)pt / (double)p0);
     o[3] = (double)(ask - bid);
     o[4] = (double)(bv - av) / (double)(bv + av);
     o[5] = tanh((double)ask / (double)av - (double)bid / (double)bv);
-    double mean = np_pairwise(lm, cnt) / cnt;
-    for (int i = 0; i < cnt; i++) {
-      double dd = lm[i] - mean;
-      lm[i] = dd * dd;
+    const double mean = np_pairwise_lanes(lv[0], lv[1], cnt) / cnt;
+    for (int c = 0; c < 2; c++) {
+      const double dd = lv[c] - mean;
+      lv[c] = dd * dd;
     }
-    o[6] = __builtin_sqrt(np_pairwise(lm, cnt) / cnt);
+    o[6] = __builtin_sqrt(np_pairwise_lanes(lv[0], lv[1], cnt) / cnt);
     const double mt = (double)(bid + ask) / 2;
     int dir;
     if ((double)pt > mt) dir = 1;
@@ -3977,7 +4013,7 @@ struct Eng {
   // DummyRL.process_action + place_orders (dummy_rl:138-179), called by the step kernel
   DEV void rl_place_orders(const double* act) {
     PROF_SCOPE(90);
-    RpHdr* R = rh();
+    auto R = rh();
     rec_load(PC.first_rl);
     const double q0 = (double)PC.rl_quantity, q = q0;  // metrics.rem_quantity is never updated
     const double x = act[0], sum = 0.0 + act[1] + act[2];
@@ -4000,7 +4036,7 @@ struct Eng {
   }
   // GymKernel CANCEL_ORDER branch (GymKernel.py:244-249): get_reward (None), cancelAllOrders
   DEV void rl_kernel_cancel() {
-    RpHdr* R = rh();
+    auto R = rh();
     if (U(R->m_cnt) == 0 || U(R->ph_none)) {
       fail(ERR_RP_OBS);
       return;
@@ -4011,7 +4047,7 @@ struct Eng {
   }
   // GymKernel.terminateRunner -> ExecutionAgent.kernelStopping (execution_agent.py:45-58)
   DEV void rp_terminate() {
-    RpHdr* R = rh();
+    auto R = rh();
     if (U(R->finished)) return;
     R->finished = 1;
     if (U(R->rl_trade)) fail(ERR_RP_STOPPING);
@@ -4232,8 +4268,14 @@ struct Eng {
     u64* dst = (u64*)hdr();
     if (lane < (int)(sizeof(EnvHdr) / 8)) dst[lane] = src[lane];
   }
+  static constexpr int RPW = (int)(sizeof(RpHdr) / 8);
+  static_assert(sizeof(RpHdr) % 8 == 0 && RPW <= 64, "RpHdr: one u64 per lane");
   DEV void load() {
     hdr_from_global();
+    if constexpr (RP || GYM) {
+      if (lane < RPW) ((LDSP u64*)rhl)[lane] = ((const u64*)rh_g())[lane];
+      wfence();
+    }
     for (int hs = 0; hs < HOT; hs++) hotrec[hs * 64 + lane] = agent_ptr(hot_agent(hs))[lane];
     for (int i = lane; i < LATL; i += 64) latl[i] = lat()[i];
     SavedEvent* sq = (SavedEvent*)(env + PC.L.off_q);
@@ -4287,6 +4329,10 @@ struct Eng {
       so[j * 64 + lane] = o;
     }
     for (int hs = 0; hs < HOT; hs++) agent_ptr(hot_agent(hs))[lane] = hotrec[hs * 64 + lane];
+    if constexpr (RP || GYM) {
+      wfence();
+      if (lane < RPW) ((u64*)rh_g())[lane] = ((const LDSP u64*)rhl)[lane];
+    }
     hdr_to_global();
   }
 
@@ -5380,7 +5426,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
   atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
   atomicAdd(&mxa::g_mxa_prof[64 + g.lane], (unsigned long long)g.prof[64 + g.lane]);
 #endif
-  RpHdr* R = g.rh();
+  auto R = g.rh();
   if (g.lane < 9) obs[9 * (size_t)env + g.lane] = R->obs[g.lane];
   u64 key;
   u32 sq;

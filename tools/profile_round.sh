@@ -13,7 +13,7 @@ ENVS=${3:-4096}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp
-B="$R/bench.py --config $CFG --envs $ENVS --no-cpu --no-count"
+B="$R/bench.py --config $CFG --envs $ENVS --no-cpu --no-count --no-latency"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 $B > $OUT/trace.log 2>&1 || { echo "trace pass failed"; tail $OUT/trace.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o pmc -- \
