@@ -536,6 +536,21 @@ struct ProfScope {
 #define PROF_ADD(b, v)
 #define PROF_CNT(b)
 #endif
+// diagnostics build (-DMXA_RP_CHECK): the replay book's computed indices are range-checked before
+// the global access they address; a bad one prints and ends the env with ERR_BAD_CONFIG
+// instead of faulting the device
+#ifdef MXA_RP_CHECK
+#define RPCHK(c, what, v)                                                                     \
+  do {                                                                                        \
+    if (!(c)) {                                                                               \
+      if (lane == 0) printf("RPCHK %s = %lld at pop %lld\n", what, (long long)(v), (long long)pops); \
+      fail(ERR_BAD_CONFIG);                                                                   \
+      return;                                                                                 \
+    }                                                                                         \
+  } while (0)
+#else
+#define RPCHK(c, what, v)
+#endif
 template <int CFG, bool BUILD = false, bool LOG = false, bool INSTR = true>
 struct Eng {
   // every configuration constant is an immediate (mxa_config.h)
@@ -2435,6 +2450,7 @@ struct Eng {
       rs64(AF_CASH, rg64(AF_CASH) - q * (i64)(i32)m.w[4]);
       if constexpr (RP) {
         if (type == AG_REPLAY) {  // MarketReplayAgent.orders: dense-indexed table
+          RPCHK((i32)m.w[5] >= 0 && (i32)m.w[5] < U(rx->L.D), "ta_receive EXECUTED dense", (i32)m.w[5]);
           RpOrder* o = mro() + (i32)m.w[5];
           if (U(o->present)) {  // all lanes store the same value
             if ((i32)m.w[2] >= U(o->qty)) o->present = 0;
@@ -2454,6 +2470,7 @@ struct Eng {
     case MK_CANCELLED: {
       if constexpr (RP) {
         if (type == AG_REPLAY) {
+          RPCHK((i32)m.w[5] >= 0 && (i32)m.w[5] < U(rx->L.D), "ta_receive CANCELLED dense", (i32)m.w[5]);
           mro()[(i32)m.w[5]].present = 0;
           break;
         }
@@ -3492,10 +3509,14 @@ struct Eng {
       fail(ERR_RP_POOL);
       return;
     }
+    RPCHK(top <= U(rx->L.C), "rp_enter free_top", top);
     i32 e = U(freel()[top - 1]);
+    RPCHK(e >= 0 && e < U(rx->L.C), "rp_enter entry", e);
+    RPCHK(d >= 0 && d < U(rx->L.D), "rp_enter dense", d);
     u32 arr = h.arrival++;
     i32 tl = U(lv_tail(side)[x]);
     i32 cnt = U(lv_cnt(side)[x]);
+    RPCHK(tl >= -1 && tl < U(rx->L.C), "rp_enter tail", tl);
     RpEntry* E = pool();
     {  // every lane stores the same (uniform) value
       R->free_top = top - 1;
@@ -3534,9 +3555,12 @@ struct Eng {
   DEV void rp_unlink(int side, i32 x, i32 e) {
     auto R = rh();
     RpEntry* E = pool();
+    RPCHK(e >= 0 && e < U(rx->L.C) && x >= 0 && x < U(rx->L.P), "rp_unlink entry/level", (i64)e * 100000 + x);
     i32 p = U(E[e].prev), n = U(E[e].next), q = U(E[e].qty), d = U(E[e].dense);
     i32 cnt = U(lv_cnt(side)[x]);
     i32 top = U(R->free_top);
+    RPCHK(p >= -1 && p < U(rx->L.C) && n >= -1 && n < U(rx->L.C) && d >= 0 && d < U(rx->L.D) && top >= 0 && top < U(rx->L.C),
+          "rp_unlink links", (i64)p * 1000000 + n);
     {  // every lane stores the same (uniform) value
       if (p >= 0) E[p].next = n;
       else lv_head(side)[x] = n;
@@ -3580,6 +3604,7 @@ struct Eng {
     i32 agent = m_agent(m);
     int buy = m_buy(m);
     if (qty <= 0) return;
+    RPCHK(d >= 0 && d < U(rx->L.D), "rp_handle_limit dense", d);
     if constexpr (BLOG) bl_put(cur, price, buy ? qty : -qty);
     const i32 hep = h.epoch;
     rp_note_entry_epoch(d, hep);
@@ -3600,7 +3625,9 @@ struct Eng {
         ex_notify(agent, ma);
         break;
       }
+      RPCHK(b < U(rx->L.P), "rp_handle_limit best", b);
       i32 e = U(lv_head(opp)[b]);
+      RPCHK(e >= 0 && e < U(rx->L.C), "rp_handle_limit head", e);
       i32 hq = U(E[e].qty), ho = U(E[e].oid), hd = U(E[e].dense), hm = U(E[e].meta), hp = U(E[e].price);
       i32 mq;
       if (qty >= hq) {
@@ -3639,6 +3666,7 @@ struct Eng {
     const int side = m_buy(m) ? 0 : 1;
     i32 x = price - U(rx->L.pmin);
     if (x < 0 || x >= U(rx->L.P)) return;
+    RPCHK(d >= 0 && d < U(rx->L.D), "rp_cancel dense", d);
     RpEntry* E = pool();
     i32 best = -1;
     u32 ba = 0xFFFFFFFFu;
@@ -3674,6 +3702,7 @@ struct Eng {
       fail(ERR_RP_MODIFY);
       return;
     }
+    RPCHK(d >= 0 && d < U(rx->L.D), "rp_modify dense", d);
     RpEntry* E = pool();
     int matches = 0;
     i32 guard = 0;
@@ -3681,6 +3710,7 @@ struct Eng {
       if (U(E[e].price) == oprice && (U(E[e].meta) & 1) == buy && U(E[e].oid) == oid) matches++;
     if (matches == 0) return;
     i32 hd = U(lv_head(side)[x]);
+    RPCHK(hd >= 0 && hd < U(rx->L.C), "rp_modify head", hd);
     i32 hq = U(E[hd].qty), hdense = U(E[hd].dense);
     if (hdense != d) {
       id_unlink(hdense, hd);
@@ -3742,7 +3772,9 @@ struct Eng {
   DEV void mr_place_record(i32 r) {
     PROF_SCOPE(91);
     const i32 oid = U(rx->oid[r]), price = U(rx->price[r]), size = U(rx->size[r]);
+    RPCHK(r >= 0 && r < U(rx->L.nrec), "mr_place_record record", r);
     const i32 d = oid == 0 ? zero_dense() : U(rx->dense[r]);
+    RPCHK(d >= 0 && d < U(rx->L.D), "mr_place_record dense", d);
     const int buy = (int)U((i32)rx->buy[r]);
     mr_place_record_as(r, oid, d, price, size, buy);
     rh()->mr_done = r + 1;  // record r's explicit id (if SIZE > 0) is in Order._order_ids now
@@ -3812,6 +3844,7 @@ struct Eng {
     else if (wi > 0 && (i64)rdl64((u64)tv, 1) == cur) g = wi - 1, lo = hi + 1;
     if (g >= 0) {  // the group's record range from the batch
       const i32 r0 = (i32)rdl64((u64)tv, g == wi ? 3 : 2), r1 = (i32)rdl64((u64)tv, g == wi ? 4 : 3);
+      RPCHK(r0 >= 0 && r0 <= r1 && r1 <= U(rx->L.nrec), "mr_wakeup group", (i64)r0 * 1000000 + r1);
       for (i32 r = r0; r < r1; r++) mr_place_record(r);
       return;
     }
@@ -3871,6 +3904,7 @@ struct Eng {
     const i32 nb = (i32)(m.w[6] >> 20), na = (i32)(m.w[7] >> 20);
     const int dnone = !m_hasdata(m);
     i32 ph = U(R->ph_n), cnt = U(R->m_cnt), hd = U(R->m_head);
+    RPCHK(cnt >= 0 && cnt <= 100 && hd >= 0 && hd < 100, "rl_add_lob ring", (i64)cnt * 1000 + hd);
     hd = (hd + 99) % 100;
     {  // every lane stores the same (uniform) value
       if (ph == 0) {
@@ -3951,6 +3985,7 @@ struct Eng {
     i32 rem = PC.rl_nh;
     if (fl >= PC.rl_h0 && (fl - PC.rl_h0) / PC.rl_hstep < PC.rl_nh) rem = PC.rl_nh - 1 - (i32)((fl - PC.rl_h0) / PC.rl_hstep);
     const i32 cnt = U(R->m_cnt), hd = U(R->m_head);
+    RPCHK(cnt >= 0 && cnt <= 100 && hd >= 0 && hd < 100, "rl_observe ring", (i64)cnt * 1000 + hd);
     double o[9];
     o[0] = (double)rem;
     o[1] = (double)U(R->rl_rem);
@@ -5422,10 +5457,6 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
     if (g.status == ST_DONE) g.rp_terminate();
   }
   g.save();
-#ifdef MXA_PROF
-  atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
-  atomicAdd(&mxa::g_mxa_prof[64 + g.lane], (unsigned long long)g.prof[64 + g.lane]);
-#endif
   auto R = g.rh();
   if (g.lane < 9) obs[9 * (size_t)env + g.lane] = R->obs[g.lane];
   u64 key;
