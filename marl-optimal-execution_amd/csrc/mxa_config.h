@@ -140,17 +140,11 @@ constexpr Shape shape(int cfg) {
                                        : Shape{4, 1, true, 2, 8, MXA_RP_HOT};  // marketreplay (both): book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
-// configurations with the replay / gym header (RpHdr) in LDS for a launch
-constexpr bool is_rp(int cfg) {
-  return cfg == MXA_CFG_MARKETREPLAY || cfg == MXA_CFG_MARKETREPLAY_RUNNER || cfg == MXA_CFG_MARKETREPLAY_TWAP ||
-         cfg == MXA_CFG_RMSC03_RL;
-}
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)sq_lds(cfg) * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
          + 1024                                                                               // RNG stream windows
          + (size_t)lat_lds(cfg) * 8                                                           // exchange latency row
-         + (is_rp(cfg) ? 256 : 0)                                                             // RpHdr (replay / gym)
 #ifdef MXA_QREG
          + 768  // batched-push scratch: slot table + staged keys
 #else

@@ -794,7 +794,6 @@ struct Eng {
   LDSP u64* prof;
 #endif
   LDSP u64* hotrec;  // [HOT][64]: the exchange's (and the market maker's or replay agent's) agent record
-  LDSP RpHdr* rhl;   // RP: the replay header for the launch (rh())
   // the exchange's latency row in LDS for the launch (MXA_LAT_LDS_MASK): every send reads one
   // entry, which from HBM is a dependent memory round trip on the event chain
   static constexpr int LATL = BUILD ? 0 : mxa_cfg::lat_lds(CFG);
@@ -839,7 +838,6 @@ struct Eng {
     hotrec = (LDSP u64*)(lds + LDS_Q + 512);
 #endif
     latl = (LDSP double*)(hotrec + mxa_cfg::shape(CFG).hot * 64);
-    rhl = (LDSP RpHdr*)(latl + mxa_cfg::lat_lds(CFG));
   }
 
   // ---------------- env block accessors
@@ -3406,18 +3404,11 @@ struct Eng {
   // (count, head, tail, total qty); entries come from a per-env pool; the live entries of one
   // order id are chained so cancel/modify find them without walking a level.
   // =====================================================================================
-  DEV RpHdr* rh_g() { return (RpHdr*)(env + rx->L.off_rh); }
-  // the replay / gym header (best levels, free-stack top, replay cursor, RL state) lives in LDS
-  // for a launch of the engine (load() / save() move it): every handler reads it on its
-  // dependent chain.  The builder writes the env block directly
-  DEV auto rh() {
-#ifdef MXA_RPHDR_GLOBAL
-    return rh_g();
-#else
-    if constexpr (BUILD) return rh_g();
-    else return rhl;
-#endif
-  }
+  // the replay / gym header (best levels, free-stack top, replay cursor, RL state) in the env
+  // block.  (Round 4 moved it to LDS for the launch, load() / save() copying it: the replay step
+  // kernel then faulted on its first step while the same source with the header in HBM passed,
+  // a cause not found from the code; reverted)
+  DEV RpHdr* rh() { return (RpHdr*)(env + rx->L.off_rh); }
   DEV i32* lv_cnt(int s) { return (i32*)(env + rx->L.off_lvc) + (size_t)s * U(rx->L.P); }
   DEV i32* lv_head(int s) { return (i32*)(env + rx->L.off_lvh) + (size_t)s * U(rx->L.P); }
   DEV i32* lv_tail(int s) { return (i32*)(env + rx->L.off_lvt) + (size_t)s * U(rx->L.P); }
@@ -3445,7 +3436,7 @@ struct Eng {
   // SIZE > 0 record has been handled, in an earlier episode of the process or this one
   DEV i64 rp_skip_used(i64 c) {
     const i32 n = U(rx->nuid);
-    auto R = rh();
+    RpHdr* R = rh();
     const i32 hi = max(U(R->tape_hi), U(R->mr_done));
     for (;;) {
       i32 lo = 0, h2 = n - 1, f = -1;
@@ -3504,7 +3495,7 @@ struct Eng {
   }
   // enterOrder (OrderBook.py:256-282): append to the level FIFO
   DEV void rp_enter(i32 oid, i32 d, i32 agent, int buy, i32 qty, i32 price) {
-    auto R = rh();
+    RpHdr* R = rh();
     const int side = buy ? 0 : 1;
     i32 x = lvl_index(price);
     if (x < 0) return;
@@ -3557,7 +3548,7 @@ struct Eng {
   }
   // remove entry e (level x of `side`) from the book
   DEV void rp_unlink(int side, i32 x, i32 e) {
-    auto R = rh();
+    RpHdr* R = rh();
     RpEntry* E = pool();
     RPCHK(e >= 0 && e < U(rx->L.C) && x >= 0 && x < U(rx->L.P), "rp_unlink entry/level", (i64)e * 100000 + x);
     i32 p = U(E[e].prev), n = U(E[e].next), q = U(E[e].qty), d = U(E[e].dense);
@@ -3612,7 +3603,7 @@ struct Eng {
     if constexpr (BLOG) bl_put(cur, price, buy ? qty : -qty);
     const i32 hep = h.epoch;
     rp_note_entry_epoch(d, hep);
-    auto R = rh();
+    RpHdr* R = rh();
     RpEntry* E = pool();
     const i32 pmin = U(rx->L.pmin);
     i64 ex_q = 0, ex_pq = 0;
@@ -3741,7 +3732,7 @@ struct Eng {
   // QUERY_SPREAD reply with `depth` levels (ExchangeAgent.py:215-245): level-1 price/qty,
   // level-2 prices and the level counts (w6/w7 = price2 | count << 20)
   DEV void rp_spread(const Msg& m, bool closed) {
-    auto R = rh();
+    RpHdr* R = rh();
     const i32 pmin = U(rx->L.pmin);
     i32 depth = (i32)m.w[1];
     i32 nb = U(R->nlev[0]), na = U(R->nlev[1]);
@@ -3825,7 +3816,7 @@ struct Eng {
     ta_wakeup();
     u32 f = flags();
     if (!((f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE))) return;
-    auto R = rh();
+    RpHdr* R = rh();
     i32 wi = U(R->mr_wi);
     const i32 ntm = U(rx->L.ntm);
     if (wi >= ntm) return;  // IndexError: every order submitted (the last group never is)
@@ -3895,7 +3886,7 @@ struct Eng {
   }
   DEV void rl_wakeup() {
     if (!ta_wakeup()) return;
-    auto R = rh();
+    RpHdr* R = rh();
     // first horizon time strictly after now
     i32 k = cur < PC.rl_h0 ? 0 : (i32)((cur - PC.rl_h0) / PC.rl_hstep) + 1;
     i32 trade = U(R->rl_trade);
@@ -3913,7 +3904,7 @@ struct Eng {
   }
   // ABIDESEnvMetrics.addLOB: deque(maxlen=100), newest first
   DEV void rl_add_lob(const Msg& m) {
-    auto R = rh();
+    RpHdr* R = rh();
     const i32 nb = (i32)(m.w[6] >> 20), na = (i32)(m.w[7] >> 20);
     const int dnone = !m_hasdata(m);
     i32 ph = U(R->ph_n), cnt = U(R->m_cnt), hd = U(R->m_head);
@@ -3945,7 +3936,7 @@ struct Eng {
   DEV void rl_receive(const Msg& m) {
     PROF_SCOPE(89);
     ta_receive(m, AG_DUMMYRL);
-    auto R = rh();
+    RpHdr* R = rh();
     const u32 k = m_kind(m);
     if (k == MK_EXECUTED) {  // ExecutionAgent.handleOrderExecution (the DummyRL override is misspelt)
       i64 ex = U(R->rl_exec) + (i32)m.w[2];
@@ -3993,7 +3984,7 @@ struct Eng {
   }
   // DummyRL.get_observation (dummy_rl:291-312): float64[9] into the replay header
   DEV void rl_observe() {
-    auto R = rh();
+    RpHdr* R = rh();
     const i64 fl = (cur / PC.rl_hstep) * PC.rl_hstep;  // currentTime.floor("30S")
     i32 rem = PC.rl_nh;
     if (fl >= PC.rl_h0 && (fl - PC.rl_h0) / PC.rl_hstep < PC.rl_nh) rem = PC.rl_nh - 1 - (i32)((fl - PC.rl_h0) / PC.rl_hstep);
@@ -4102,7 +4093,7 @@ struct Eng {
   // DummyRL.process_action + place_orders (dummy_rl:138-179), called by the step kernel
   DEV void rl_place_orders(const double* act) {
     PROF_SCOPE(90);
-    auto R = rh();
+    RpHdr* R = rh();
     rec_load(PC.first_rl);
     const double q0 = (double)PC.rl_quantity, q = q0;  // metrics.rem_quantity is never updated
     const double x = act[0], sum = 0.0 + act[1] + act[2];
@@ -4125,7 +4116,7 @@ struct Eng {
   }
   // GymKernel CANCEL_ORDER branch (GymKernel.py:244-249): get_reward (None), cancelAllOrders
   DEV void rl_kernel_cancel() {
-    auto R = rh();
+    RpHdr* R = rh();
     if (U(R->m_cnt) == 0 || U(R->ph_none)) {
       fail(ERR_RP_OBS);
       return;
@@ -4136,7 +4127,7 @@ struct Eng {
   }
   // GymKernel.terminateRunner -> ExecutionAgent.kernelStopping (execution_agent.py:45-58)
   DEV void rp_terminate() {
-    auto R = rh();
+    RpHdr* R = rh();
     if (U(R->finished)) return;
     R->finished = 1;
     if (U(R->rl_trade)) fail(ERR_RP_STOPPING);
@@ -4357,16 +4348,8 @@ struct Eng {
     u64* dst = (u64*)hdr();
     if (lane < (int)(sizeof(EnvHdr) / 8)) dst[lane] = src[lane];
   }
-  static constexpr int RPW = (int)(sizeof(RpHdr) / 8);
-  static_assert(sizeof(RpHdr) % 8 == 0 && RPW <= 64, "RpHdr: one u64 per lane");
   DEV void load() {
     hdr_from_global();
-#ifndef MXA_RPHDR_GLOBAL
-    if constexpr (RP || GYM) {
-      if (lane < RPW) ((LDSP u64*)rhl)[lane] = ((const u64*)rh_g())[lane];
-      wfence();
-    }
-#endif
     for (int hs = 0; hs < HOT; hs++) hotrec[hs * 64 + lane] = agent_ptr(hot_agent(hs))[lane];
     for (int i = lane; i < LATL; i += 64) latl[i] = lat()[i];
     SavedEvent* sq = (SavedEvent*)(env + PC.L.off_q);
@@ -4420,12 +4403,6 @@ struct Eng {
       so[j * 64 + lane] = o;
     }
     for (int hs = 0; hs < HOT; hs++) agent_ptr(hot_agent(hs))[lane] = hotrec[hs * 64 + lane];
-#ifndef MXA_RPHDR_GLOBAL
-    if constexpr (RP || GYM) {
-      wfence();
-      if (lane < RPW) ((u64*)rh_g())[lane] = ((const LDSP u64*)rhl)[lane];
-    }
-#endif
     hdr_to_global();
   }
 
@@ -5515,7 +5492,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
     if (g.status == ST_DONE) g.rp_terminate();
   }
   g.save();
-  auto R = g.rh();
+  RpHdr* R = g.rh();
   if (g.lane < 9) obs[9 * (size_t)env + g.lane] = R->obs[g.lane];
   u64 key;
   u32 sq;
