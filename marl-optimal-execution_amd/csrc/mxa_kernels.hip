@@ -3820,14 +3820,6 @@ struct Eng {
     i32 wi = U(R->mr_wi);
     const i32 ntm = U(rx->L.ntm);
     if (wi >= ntm) return;  // IndexError: every order submitted (the last group never is)
-#ifdef MXA_OLD_WAKEUP
-    const i64 tn = U(rx->tm[wi]);
-    wakeup_at(cur_agent, tn);
-    R->mr_wi = wi + 1;
-    i32 lo = 0, hi = ntm - 1, g = -1;
-    if (tn == cur) g = wi, lo = hi + 1;
-    else if (wi > 0 && U(rx->tm[wi - 1]) == cur) g = wi - 1, lo = hi + 1;
-#else
     // one round trip for the tape words this wakeup reads in the common case: lane 0 tm[wi],
     // lane 1 tm[wi - 1], lanes 2-4 tm0[wi - 1 .. wi + 1] (tm0 has ntm + 1 entries)
     i64 tv = 0;
@@ -3851,7 +3843,6 @@ struct Eng {
       for (i32 r = r0; r < r1; r++) mr_place_record(r);
       return;
     }
-#endif
     while (lo <= hi) {
       i32 mid = (lo + hi) >> 1;
       i64 tv = U(rx->tm[mid]);
@@ -4005,46 +3996,6 @@ struct Eng {
     }
     const i64 p0 = U(R->p0), pt = U(L[hd].data);
     const i64 bid = U(L[hd].bid), ask = U(L[hd].ask), bv = U(R->m_bq), av = U(R->m_aq);
-#ifdef MXA_OLD_OBSERVE
-    double lm[100];
-    for (int i = 0; i < cnt; i++) {
-      const RpLob li = L[(hd + i) % 100];
-      if ((U(li.flags) & 3) != 3) {
-        fail(ERR_RP_OBS);
-        return;
-      }
-      double mid = (double)((i64)U(li.bid) + U(li.ask)) / 2;
-      lm[i] = gm_log(mid / (double)p0);
-    }
-    o[2] = gm_log((double)pt / (double)p0);
-    o[3] = (double)(ask - bid);
-    o[4] = (double)(bv - av) / (double)(bv + av);
-    o[5] = tanh((double)ask / (double)av - (double)bid / (double)bv);
-    double lv[2] = {0, 0};
-    (void)lv;
-    auto pw = [](const double* a, int n) {
-      if (n < 8) {
-        double r = 0.;
-        for (int i = 0; i < n; i++) r += a[i];
-        return r;
-      }
-      double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
-      int i;
-      for (i = 8; i < n - (n % 8); i += 8) {
-        r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
-        r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
-      }
-      double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-      for (; i < n; i++) res += a[i];
-      return res;
-    };
-    double mean = pw(lm, cnt) / cnt;
-    for (int i = 0; i < cnt; i++) {
-      double dd = lm[i] - mean;
-      lm[i] = dd * dd;
-    }
-    o[6] = __builtin_sqrt(pw(lm, cnt) / cnt);
-#else
     // the deque's log mid returns, lane-parallel: entry i in lane i % 64, register i / 64 (at
     // most 100 entries); one coalesced load and one log evaluation per register
     double lv[2];
@@ -4073,7 +4024,6 @@ struct Eng {
       lv[c] = dd * dd;
     }
     o[6] = __builtin_sqrt(np_pairwise_lanes(lv[0], lv[1], cnt) / cnt);
-#endif
     const double mt = (double)(bid + ask) / 2;
     int dir;
     if ((double)pt > mt) dir = 1;
