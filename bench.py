@@ -154,6 +154,7 @@ class Engine:
         self.gathered = None
         self.last_batch = None
         self.errs = torch.zeros((), dtype=torch.int64, device=ctx.device)  # envs in error, every timed batch
+        self.errs_warm = torch.zeros((), dtype=torch.int64, device=ctx.device)
 
     def seeds(self, k):
         return self.shard.env_seeds(k, self.ctx.rank, self.ctx.world, self.n)
@@ -161,8 +162,12 @@ class Engine:
     def gather(self, k, timed=False):
         self.last_batch = k
         self.gathered = self.shard.gather_records(self.records, self.ctx.world)
+        # the same torch kernels in warmup and timed steps (their first launch loads code objects)
+        e = (self.records[:, self.shard.R_STATUS] == 2).sum()
         if timed:
-            self.errs += (self.records[:, self.shard.R_STATUS] == 2).sum()
+            self.errs += e
+        else:
+            self.errs_warm += e
         return self.records[:, self.shard.R_EVENTS].sum()
 
     def check_gathered(self):
@@ -521,7 +526,8 @@ def traffic_record(config, envs, parity_hash, tape=None):
     of the kernel sources and flags), config, env count and parity-hash setting all match the
     running bench; otherwise traffic is null and traffic_record says why."""
     import mxabides
-    prof = os.path.join(ROOT, "profiles", "hbm_traffic_%s.json" % config)
+    name = config if tape in (None, "IBM_2003-01-14") else "%s_%s" % (config, tape)  # a replay tape's own record
+    prof = os.path.join(ROOT, "profiles", "hbm_traffic_%s.json" % name)
     if not os.path.exists(prof):
         return None, {"file": None, "match": False, "why": "no PMC record for this config"}
     with open(prof) as f:

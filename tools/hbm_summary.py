@@ -61,9 +61,12 @@ if "--record" in sys.argv:
     assert len(res) == 1, "expected exactly one run- or step-kernel instantiation, got %s" % list(res)
     (k, r), = res.items()
     rec = {"config": cfg, "envs": envs, "kernel": k, "build_id": mxabides.build_id(), "parity_hash": ph}
+    tape = os.environ.get("MXA_PROF_TAPE")  # marketreplay on another tape than IBM_2003-01-14
+    if tape:
+        rec["tape"] = tape
     rec.update({x: r[x] for x in ("bytes_per_launch", "read_bytes_corrected", "write_bytes", "fetch_size_kib",
                                   "write_size_kib", "launches")})
     rec["source"] = source
-    with open(os.path.join(out, "hbm_traffic_%s.json" % cfg), "w") as f:
+    with open(os.path.join(out, "hbm_traffic_%s.json" % (cfg + ("_" + tape if tape else ""))), "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec, indent=1))
