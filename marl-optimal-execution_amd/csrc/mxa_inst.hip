@@ -37,8 +37,11 @@ template <int CFG, bool GYM>
 int occupancy(size_t lds) {
   int n = 0;
   hipError_t e;
+#ifndef MXA_NO_GYM
   if constexpr (GYM) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mxa_step_kernel<CFG, false>, 64, lds);
-  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mxa_run_kernel<CFG, false, false>, 64, lds);
+  else
+#endif
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mxa_run_kernel<CFG, false, false>, 64, lds);
   return e == hipSuccess ? n : -1;
 }
 

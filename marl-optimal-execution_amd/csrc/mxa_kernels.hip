@@ -53,6 +53,14 @@ namespace mxa {
 DEV int laneid() { return (int)__lane_id(); }
 DEV u32 rdl(u32 v, int l) { return (u32)__builtin_amdgcn_readlane((int)v, l); }
 DEV i32 rdli(i32 v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// one memory round trip for a wave of independent words: each lane's address is selected with
+// VALU ops and ONE load is issued (lanes with ok false load nothing).  A chain of per-lane
+// `if (lane == k) v = A[..]; else if ...` arms instead became one load and one wait per arm
+DEV i32 gather1(const i32* a, bool ok) {
+  i32 v = 0;
+  if (ok) v = *a;
+  return v;
+}
 DEV u64 rdl64(u64 v, int l) {
   return ((u64)rdl((u32)(v >> 32), l) << 32) | rdl((u32)v, l);
 }
@@ -283,8 +291,85 @@ DEV i64 rs_randint(RSt<B>& r, i64 lo, i64 hi) {
   } while (v > (u32)rng);
   return lo + (i64)v;
 }
+DEV u32 mt_temper(u32 y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+// legacy_gauss's polar rejection loop with its candidates evaluated across the wave (run kernel,
+// wave-uniform call sites): lane j loads the stream's word p + j in one round trip (the LDS
+// window or the MT block in HBM), lane i < 16 forms candidate i from words 4i .. 4i + 3, and the
+// first accepted candidate is the one the serial loop would stop at, so p, the cached second
+// normal and both values are the serial loop's.  A stream with fewer than 4 materialized words
+// left (the look-ahead overrun) finishes in the serial loop, which flags it.
+template <bool B>
+DEV double rs_gauss_serial(RSt<B>& r);
+template <bool B>
+DEV double rs_gauss_wave(RSt<B>& r) {
+  const int lane = laneid();
+  for (;;) {
+    u32 w = 0;
+    int navail;
+    if (r.lw) {
+      u32 off = (u32)(r.p - r.lw0);
+      if (off >= (u32)r.lwn) {
+        rs_fill(r);
+        off = 0;
+      }
+      navail = r.lwn - (int)off;
+      if (lane < navail) w = r.lw[off + lane];
+    } else {
+      const int q = r.p + lane, b = q / MXA_MT_N;
+      const bool ok = b <= r.m && b >= r.m - 1;
+      if (ok) w = r.key[(b & 1) * MXA_MT_N + (q - b * MXA_MT_N)];
+      const u64 okb = __ballot(ok);
+      navail = ~okb == 0 ? 64 : __ffsll((unsigned long long)~okb) - 1;
+    }
+    const int nc = navail >> 2;  // whole candidates available (at most 16)
+    if (nc == 0) return rs_gauss_serial(r);
+    w = mt_temper(w);
+    const int i4 = (lane & 15) * 4;
+    const u32 w0 = (u32)__shfl((int)w, i4, 64), w1 = (u32)__shfl((int)w, i4 + 1, 64);
+    const u32 w2 = (u32)__shfl((int)w, i4 + 2, 64), w3 = (u32)__shfl((int)w, i4 + 3, 64);
+    const double d1 = ((double)(i32)(w0 >> 5) * 67108864.0 + (double)(i32)(w1 >> 6)) / 9007199254740992.0;
+    const double d2 = ((double)(i32)(w2 >> 5) * 67108864.0 + (double)(i32)(w3 >> 6)) / 9007199254740992.0;
+    const double x1 = 2.0 * d1 - 1.0, x2 = 2.0 * d2 - 1.0;
+    const double r2 = x1 * x1 + x2 * x2;
+    const u64 acc = __ballot(lane < nc && !(r2 >= 1.0 || r2 == 0.0));
+    if (acc) {
+      const int L = __ffsll((unsigned long long)acc) - 1;
+      r.p += 4 * (L + 1);
+      const double X1 = rdl_d(x1, L), X2 = rdl_d(x2, L), R2 = rdl_d(r2, L);
+      const double f = __builtin_sqrt(-2.0 * gm_log(R2) / R2);
+      r.gauss = f * X1;
+      r.hasg |= 1;
+      return f * X2;
+    }
+    r.p += 4 * nc;  // every available candidate rejected
+  }
+}
+#ifdef MXA_SERIAL_GAUSS
+#define MXA_WAVE_GAUSS 0
+#else
+#define MXA_WAVE_GAUSS 1
+#endif
 template <bool B>
 DEV double rs_gauss(RSt<B>& r) {
+  if constexpr (!B && MXA_WAVE_GAUSS) {
+    if (r.hasg & 1) {
+      double t = r.gauss;
+      r.hasg &= ~1;
+      r.gauss = 0.0;
+      return t;
+    }
+    return rs_gauss_wave(r);
+  }
+  return rs_gauss_serial(r);
+}
+template <bool B>
+DEV double rs_gauss_serial(RSt<B>& r) {
   if (r.hasg & 1) {
     double t = r.gauss;
     r.hasg &= ~1;
@@ -575,6 +660,7 @@ struct Eng {
 #define MXA_QHIER_MIN 9
 #endif
   static constexpr int QG = SQ >= 16 ? MXA_QG : SQ / 2;
+  static constexpr bool TIER_CFG = mxa_cfg::sq_lds(CFG) < SQ;  // (TIER below)
 #ifdef MXA_QREG
   static constexpr bool QHIER = false;
 #else
@@ -583,7 +669,17 @@ struct Eng {
   // to the flat scan (a -DMXA_QG sweep must measure what it names)
   static_assert(!QHIER || SQ % QG == 0, "queue groups must tile the lane's slots (MXA_QG)");
 #endif
-  static constexpr int NG = QHIER ? SQ / QG : 1;
+  // the two-tier queue keeps the LDS tier's groups and ONE entry for the lane's whole HBM tier
+  // (its SQH far slots): a push there is a select on that entry, and only a pop or rekey of an
+  // HBM-tier slot rescans it, in the owner lane alone (HQ_AGG; a twelfth of the pops in
+  // random_fund_value).  One VGPR entry instead of six per-group entries, which the run kernel
+  // spilled on every push (880 scratch instructions at q_gupd, r04 isa_lines)
+#ifdef MXA_HQ_GROUPS
+  static constexpr bool HQ_AGG = false;
+#else
+  static constexpr bool HQ_AGG = true;
+#endif
+  static constexpr int NG = QHIER ? ((TIER_CFG && HQ_AGG) ? mxa_cfg::sq_lds(CFG) / QG + 1 : SQ / QG) : 1;
   // group rescans as one batch of loads and a select tree (q_scan): groups of 4 and more slots.
   // r03 s20, same per-env results: sparse_zi_1000 916 -> 826 ms, random_fund_value 778 -> 575,
   // sparse_zi_100 132.5 -> 125.7, value_noise 22.0 -> 21.2; rmsc02 (groups of 3) 1053 -> 1086, so
@@ -646,25 +742,40 @@ struct Eng {
   // HBM tier (TIER): keys and sequence numbers of slots QCL .. QCAP - 1.  Global address space
   // spelled out: a generic pointer next to the LDS arrays let the optimizer merge the two tiers
   // into flat accesses (273 flat loads, 1,949 scratch reloads, 2x slower)
+  // Lane-major: a lane's SQH tier slots are contiguous, so the owner lane's group rescan reads
+  // 96 + 48 contiguous bytes instead of the 64-lane block of the group (r03: 29.5x the counted
+  // bytes were these rescans)
   static constexpr size_t OFF_HQ = PC.L.off_q + sizeof(SavedEvent) * QCAP + (PL_LDS ? 0 : (size_t)QCAP * 4 * PW);
+  static constexpr int SQH = SQ - SQL;
+#ifdef MXA_HQ_SLOT_MAJOR  // the round-3 layout: slot j of every lane together
+  static constexpr bool HQ_LM = false;
+#else
+  static constexpr bool HQ_LM = true;
+#endif
+#ifdef MXA_HQ_ALL_LANES  // the round-3 rescans: every lane rescans an HBM-tier group
+  static constexpr bool HQ_OWNER = false;
+#else
+  static constexpr bool HQ_OWNER = true;
+#endif
+  static DEV int hidx(int slot) { return HQ_LM ? (slot & 63) * SQH + ((slot >> 6) - SQL) : slot - QCL; }
   DEV GLBP u64* hqk() { return (GLBP u64*)(env + OFF_HQ); }
   DEV GLBP u32* hqs() { return (GLBP u32*)(env + OFF_HQ + (size_t)(QCAP - QCL) * 8); }
   DEV u64 qk_get(int slot) {
     if constexpr (TIER) {
-      if (slot >= QCL) return hqk()[slot - QCL];
+      if (slot >= QCL) return hqk()[hidx(slot)];
     }
     return qk[slot];
   }
   DEV u32 qs_get(int slot) {
     if constexpr (TIER) {
-      if (slot >= QCL) return hqs()[slot - QCL];
+      if (slot >= QCL) return hqs()[hidx(slot)];
     }
     return qs[slot];
   }
   DEV void qk_put(int slot, u64 v) {
     if constexpr (TIER) {
       if (slot >= QCL) {
-        hqk()[slot - QCL] = v;
+        hqk()[hidx(slot)] = v;
         return;
       }
     }
@@ -673,7 +784,7 @@ struct Eng {
   DEV void qs_put(int slot, u32 v) {
     if constexpr (TIER) {
       if (slot >= QCL) {
-        hqs()[slot - QCL] = v;
+        hqs()[hidx(slot)] = v;
         return;
       }
     }
@@ -1069,12 +1180,14 @@ struct Eng {
       u32 s[QG];
       i32 j[QG];
       if (TIER && j0 >= SQL) {
-        const GLBP u64* K = hqk() + (j0 - SQL) * 64 + lane;
-        const GLBP u32* S = hqs() + (j0 - SQL) * 64 + lane;
+        constexpr int ST = HQ_LM ? 1 : 64;  // word stride between a lane's consecutive slots
+        const int b0 = HQ_LM ? lane * SQH + (j0 - SQL) : (j0 - SQL) * 64 + lane;
+        const GLBP u64* K = hqk() + b0;
+        const GLBP u32* S = hqs() + b0;
 #pragma unroll
         for (int i = 0; i < QG; i++) {
-          k[i] = K[i * 64];
-          s[i] = S[i * 64];
+          k[i] = K[i * ST];
+          s[i] = S[i * ST];
         }
       } else {
 #pragma unroll
@@ -1100,11 +1213,13 @@ struct Eng {
     bj = -1;
     if constexpr (TIER) {
       if (j0 >= SQL) {  // a whole group of the HBM tier (groups never straddle the tiers)
-        const GLBP u64* K = hqk() + (j0 - SQL) * 64 + lane;
-        const GLBP u32* S = hqs() + (j0 - SQL) * 64 + lane;
+        constexpr int ST = HQ_LM ? 1 : 64;
+        const int b0 = HQ_LM ? lane * SQH + (j0 - SQL) : (j0 - SQL) * 64 + lane;
+        const GLBP u64* K = hqk() + b0;
+        const GLBP u32* S = hqs() + b0;
         for (int j = 0; j < n; j++) {
-          const u64 k = K[j * 64];
-          const u32 s = S[j * 64];
+          const u64 k = K[j * ST];
+          const u32 s = S[j * ST];
           if (k < bk || (k == bk && s < bs)) {
             bk = k;
             bs = s;
@@ -1145,9 +1260,53 @@ struct Eng {
     ms = bs;
     mj = bj;
   }
-  // QHIER: rescan group g (wave-uniform) in every lane, then the lane mins; lanes whose group g
-  // did not change recompute the same values
-  DEV void q_regroup(int g) {
+  // HQ_AGG: min (key, seq, slot) over this lane's HBM-tier slots, QG at a time
+  DEV void q_scan_hbm(u64& bk, u32& bs, i32& bj) {
+    q_scan(SQL, QG, bk, bs, bj);
+#pragma unroll 1
+    for (int j0 = SQL + QG; j0 < SQ; j0 += QG) {
+      u64 k;
+      u32 s;
+      i32 j;
+      q_scan(j0, QG, k, s, j);
+      q_min2(bk, bs, bj, k, s, j);
+    }
+    if (bk == KEY_EMPTY && bs == 0xFFFFFFFFu) bj = -1;
+  }
+  // QHIER: the slot's group changed.  An LDS-tier group is rescanned in every lane (the group
+  // index is wave-uniform; lanes whose group did not change recompute the same values), then the
+  // lane mins.  An HBM-tier slot: its owner lane alone rescans (HQ_OWNER: that group; HQ_AGG:
+  // the whole tier), the other lanes' entries are unchanged and their rescans were HBM traffic
+  DEV void q_regroup(int slot) {
+    const int g = (slot >> 6) / QG, owner = slot & 63;
+    if constexpr (TIER && HQ_AGG) {
+      if ((slot >> 6) >= SQL) {
+        if (lane == owner) {
+          q_scan_hbm(gk[NG - 1], gs[NG - 1], gj[NG - 1]);
+          q_lanemin();
+        }
+        return;
+      }
+    } else if constexpr (TIER && HQ_OWNER) {
+      if (g * QG >= SQL) {
+        if (lane == owner) {
+          u64 k;
+          u32 s;
+          i32 j;
+          q_scan(g * QG, QG, k, s, j);
+#pragma unroll
+          for (int gg = SQL / QG; gg < NG; gg++) {
+            if (gg == g) {
+              gk[gg] = k;
+              gs[gg] = s;
+              gj[gg] = j;
+            }
+          }
+          q_lanemin();
+        }
+        return;
+      }
+    }
     u64 k;
     u32 s;
     i32 j;
@@ -1163,7 +1322,7 @@ struct Eng {
     q_lanemin();
   }
   DEV void q_gupd(int j, u64 k, u32 s) {  // QHIER: slot j of this lane now holds (k, s)
-    const int g = j / QG;
+    const int g = (TIER && HQ_AGG && j >= SQL) ? NG - 1 : j / QG;
     if constexpr (QTREE) {
 #pragma unroll
       for (int gg = 0; gg < NG; gg++) {  // selects: g differs between lanes
@@ -1184,7 +1343,11 @@ struct Eng {
   }
   DEV void q_rescan() {  // recompute this lane's min over its own slots
     if constexpr (QHIER) {
-      if constexpr (TIER) {  // unrolled: a rolled loop indexes gk/gs/gj dynamically (scratch)
+      if constexpr (TIER && HQ_AGG) {
+#pragma unroll
+        for (int g = 0; g < NG - 1; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
+        q_scan_hbm(gk[NG - 1], gs[NG - 1], gj[NG - 1]);
+      } else if constexpr (TIER) {  // unrolled: a rolled loop indexes gk/gs/gj dynamically (scratch)
 #pragma unroll
         for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
       } else {  // (unrolled here too: the same time for sparse_zi_1000, +0.5-2 % for sparse_zi_100 and value_noise, r03 s9)
@@ -1438,7 +1601,7 @@ struct Eng {
     qset(slot >> 6, KEY_EMPTY, 0xFFFFFFFFu, lane == (slot & 63));
     qfree |= (lane == (slot & 63)) ? qm_bit(slot >> 6) : (QM)0;
     if constexpr (QHIER) {
-      q_regroup((slot >> 6) / QG);
+      q_regroup(slot);
       qcount--;
       return;
     }
@@ -1455,7 +1618,7 @@ struct Eng {
   DEV void q_rekey(int slot, u64 key) {
     qsetk(slot >> 6, key, lane == (slot & 63));
     if constexpr (QHIER) {
-      q_regroup((slot >> 6) / QG);
+      q_regroup(slot);
       return;
     }
     u64 k0 = mk;
@@ -2450,9 +2613,10 @@ struct Eng {
         if (type == AG_REPLAY) {  // MarketReplayAgent.orders: dense-indexed table
           RPCHK((i32)m.w[5] >= 0 && (i32)m.w[5] < U(rx->L.D), "ta_receive EXECUTED dense", (i32)m.w[5]);
           RpOrder* o = mro() + (i32)m.w[5];
-          if (U(o->present)) {  // all lanes store the same value
-            if ((i32)m.w[2] >= U(o->qty)) o->present = 0;
-            else o->qty = U(o->qty) - (i32)m.w[2];
+          const RpOrder ov = *o;  // one 16-byte load: present and qty in the same round trip
+          if (U(ov.present)) {  // all lanes store the same value
+            if ((i32)m.w[2] >= U(ov.qty)) o->present = 0;
+            else o->qty = U(ov.qty) - (i32)m.w[2];
           }
           break;
         }
@@ -3497,9 +3661,22 @@ struct Eng {
   DEV void rp_enter(i32 oid, i32 d, i32 agent, int buy, i32 qty, i32 price) {
     RpHdr* R = rh();
     const int side = buy ? 0 : 1;
-    i32 x = lvl_index(price);
-    if (x < 0) return;
-    i32 top = U(R->free_top);
+    const i32 x = price - U(rx->L.pmin);
+    const bool xin = x >= 0 && x < U(rx->L.P);
+    rp_enter_pf(oid, d, agent, buy, qty, price, x, U(R->free_top), xin ? U(lv_tail(side)[x]) : -1,
+                xin ? U(lv_cnt(side)[x]) : 0, U(R->nlev[side]), U(R->best[side]), U(idh()[d]));
+  }
+  // rp_enter with the words it reads already loaded (rp_handle_limit gathers them in one round
+  // trip): the free-stack top, the level's tail and count, the side's level count and best,
+  // and the id's live-entry chain head
+  DEV void rp_enter_pf(i32 oid, i32 d, i32 agent, int buy, i32 qty, i32 price, i32 x, i32 top, i32 tl, i32 cnt,
+                       i32 nl, i32 bs, i32 hd) {
+    RpHdr* R = rh();
+    const int side = buy ? 0 : 1;
+    if (x < 0 || x >= U(rx->L.P)) {
+      fail(ERR_RP_PRICE);
+      return;
+    }
     if (top <= 0) {
       fail(ERR_RP_POOL);
       return;
@@ -3509,8 +3686,6 @@ struct Eng {
     RPCHK(e >= 0 && e < U(rx->L.C), "rp_enter entry", e);
     RPCHK(d >= 0 && d < U(rx->L.D), "rp_enter dense", d);
     u32 arr = h.arrival++;
-    i32 tl = U(lv_tail(side)[x]);
-    i32 cnt = U(lv_cnt(side)[x]);
     RPCHK(tl >= -1 && tl < U(rx->L.C), "rp_enter tail", tl);
     RpEntry* E = pool();
     {  // every lane stores the same (uniform) value
@@ -3525,7 +3700,7 @@ struct Eng {
       n.prev = tl;
       n.next = -1;
       n.idprev = -1;
-      n.idnext = -1;
+      n.idnext = hd;  // id_link: the entry heads the id's live-entry chain
       n.pad[0] = n.pad[1] = 0;
       E[e] = n;
       if (tl >= 0) E[tl].next = e;
@@ -3533,27 +3708,36 @@ struct Eng {
       lv_tail(side)[x] = e;
       lv_cnt(side)[x] = cnt + 1;
       lv_qty(side)[x] += qty;
+      if (hd >= 0) E[hd].idprev = e;
+      idh()[d] = e;
     }
     if (cnt == 0) {
-      i32 nl = U(R->nlev[side]);
-      i32 b = U(R->best[side]);
       {  // every lane stores the same (uniform) value
         R->nlev[side] = nl + 1;
-        if (b < 0 || (side == 0 ? x > b : x < b)) R->best[side] = x;
+        if (bs < 0 || (side == 0 ? x > bs : x < bs)) R->best[side] = x;
       }
     }
-    id_link(d, e);
     h.b_count++;
     if (h.b_count > h.max_book) h.max_book = h.b_count;
   }
-  // remove entry e (level x of `side`) from the book
-  DEV void rp_unlink(int side, i32 x, i32 e) {
+  // every word rp_unlink reads, in one round trip: lanes 0-9 the entry's words (RpEntry order:
+  // price qty oid dense meta arrival prev next idprev idnext), 12 the level's count, 13
+  // free_top, 14/15 the side's level count and best
+  DEV i32 rp_gather(int side, i32 x, i32 e) {
+    RPCHK(e >= 0 && e < U(rx->L.C) && x >= 0 && x < U(rx->L.P), "rp_unlink entry/level", (i64)e * 100000 + x);
+    RpHdr* R = rh();
+    const i32* W = (const i32*)(pool() + e);
+    const i32* a = lane < 10 ? W + lane : lane == 12 ? lv_cnt(side) + x : lane == 13 ? &R->free_top
+                   : lane == 14 ? &R->nlev[side] : &R->best[side];
+    return gather1(a, lane < 10 || (lane >= 12 && lane < 16));
+  }
+  // remove entry e (level x of `side`, its words gathered in g) from the book; returns the
+  // side's best level after the removal
+  DEV i32 rp_unlink(int side, i32 x, i32 e, i32 g) {
     RpHdr* R = rh();
     RpEntry* E = pool();
-    RPCHK(e >= 0 && e < U(rx->L.C) && x >= 0 && x < U(rx->L.P), "rp_unlink entry/level", (i64)e * 100000 + x);
-    i32 p = U(E[e].prev), n = U(E[e].next), q = U(E[e].qty), d = U(E[e].dense);
-    i32 cnt = U(lv_cnt(side)[x]);
-    i32 top = U(R->free_top);
+    const i32 q = rdli(g, 1), d = rdli(g, 3), p = rdli(g, 6), n = rdli(g, 7), ip = rdli(g, 8), in = rdli(g, 9);
+    const i32 cnt = rdli(g, 12), top = rdli(g, 13), nl = rdli(g, 14), b = rdli(g, 15);
     RPCHK(p >= -1 && p < U(rx->L.C) && n >= -1 && n < U(rx->L.C) && d >= 0 && d < U(rx->L.D) && top >= 0 && top < U(rx->L.C),
           "rp_unlink links", (i64)p * 1000000 + n);
     {  // every lane stores the same (uniform) value
@@ -3565,32 +3749,23 @@ struct Eng {
       lv_qty(side)[x] -= q;
       freel()[top] = e;
       R->free_top = top + 1;
+      // the id's live-entry chain
+      if (ip >= 0) E[ip].idnext = in;
+      else idh()[d] = in;
+      if (in >= 0) E[in].idprev = ip;
     }
-    id_unlink(d, e);
     h.b_count--;
-    if (cnt == 1) {
-      i32 nl = U(R->nlev[side]);
-      i32 b = U(R->best[side]);
-      i32 nb = b;
-      if (b == x) {
-        __threadfence_block();
-        nb = lvl_next(side, side == 0 ? x - 1 : x + 1);
-      }
-      {  // every lane stores the same (uniform) value
-        R->nlev[side] = nl - 1;
-        R->best[side] = nb;
-      }
+    if (cnt != 1) return b;
+    i32 nb = b;
+    if (b == x) {
+      __threadfence_block();
+      nb = lvl_next(side, side == 0 ? x - 1 : x + 1);
     }
-  }
-  // history[0][order_id] = ... (OrderBook.py:51-60): the id's distinct entry epochs, newest
-  // first, one per lane (lanes < MXA_ID_EPOCHS)
-  DEV void rp_note_entry_epoch(i32 d, i32 ep) {
-    static_assert(MXA_ID_EPOCHS > PC.stream_history, "the id's entry epochs must cover the history window");
-    i32* E = idep() + MXA_ID_EPOCHS * (size_t)d;
-    if (U(E[0]) == ep) return;
-    i32 v = 0;
-    if (lane < MXA_ID_EPOCHS) v = lane == 0 ? ep : E[lane - 1];
-    if (lane < MXA_ID_EPOCHS) E[lane] = v;  // every lane's load completed before the stores
+    {  // every lane stores the same (uniform) value
+      R->nlev[side] = nl - 1;
+      R->best[side] = nb;
+    }
+    return nb;
   }
   // handleLimitOrder / executeOrder (OrderBook.py:38-254) on the ladder
   DEV void rp_handle_limit(const Msg& m) {
@@ -3602,19 +3777,48 @@ struct Eng {
     RPCHK(d >= 0 && d < U(rx->L.D), "rp_handle_limit dense", d);
     if constexpr (BLOG) bl_put(cur, price, buy ? qty : -qty);
     const i32 hep = h.epoch;
-    rp_note_entry_epoch(d, hep);
     RpHdr* R = rh();
     RpEntry* E = pool();
     const i32 pmin = U(rx->L.pmin);
+    const int side = buy ? 0 : 1;
+    const i32 x = price - pmin;
+    const bool xin = x >= 0 && x < U(rx->L.P);
+    // every word the first pass reads whose address is known now, in one round trip: lanes
+    // 0-11 the id's entry epochs, 16/17 best[bids/asks], 18/19 nlev, 20 free_top, 21 the id's
+    // live-entry head, 22/23 the own level's count and tail (a dependent chain of six before)
+    i32 pf;
+    {
+      static_assert(offsetof(RpHdr, nlev) == 8 && offsetof(RpHdr, free_top) == 16, "RpHdr: best, nlev, free_top");
+      i32* EP = idep() + MXA_ID_EPOCHS * (size_t)d;
+      const i32* a = lane < MXA_ID_EPOCHS ? EP + lane
+                     : lane < 21          ? (const i32*)R + (lane - 16)
+                     : lane == 21         ? idh() + d
+                     : lane == 22         ? lv_cnt(side) + x
+                                          : lv_tail(side) + x;
+      pf = gather1(a, lane < MXA_ID_EPOCHS || (lane >= 16 && lane < 22) || (xin && (lane == 22 || lane == 23)));
+      // history[0][order_id] = ... (OrderBook.py:51-60): the id's distinct entry epochs, newest
+      // first, one per lane (lanes < MXA_ID_EPOCHS)
+      static_assert(MXA_ID_EPOCHS > PC.stream_history, "the id's entry epochs must cover the history window");
+      if (rdli(pf, 0) != hep) {
+        const i32 up = __shfl_up(pf, 1, 64);
+        if (lane < MXA_ID_EPOCHS) EP[lane] = lane == 0 ? hep : up;
+      }
+    }
     i64 ex_q = 0, ex_pq = 0;
     bool executed = false;
+    i32 nb_opp = -1;
     for (;;) {
       const int opp = buy ? 1 : 0;
       __threadfence_block();
-      i32 b = U(R->best[opp]);
+      // the opposite side's best: gathered, then tracked through the fills
+      i32 b = executed ? nb_opp : rdli(pf, 16 + opp);
       bool match = b >= 0 && (buy ? price >= pmin + b : price <= pmin + b);
       if (!match) {
-        rp_enter(oid, d, agent, buy, qty, price);
+        if (!executed)  // no fill changed the gathered words
+          rp_enter_pf(oid, d, agent, buy, qty, price, x, rdli(pf, 20), xin ? rdli(pf, 23) : -1,
+                      xin ? rdli(pf, 22) : 0, rdli(pf, 18 + side), rdli(pf, 16 + side), rdli(pf, 21));
+        else
+          rp_enter(oid, d, agent, buy, qty, price);
         Msg ma = msg_order(MK_ACCEPTED, oid, agent, buy, qty, price, 0);
         ma.w[5] = (u32)d;
         ex_notify(agent, ma);
@@ -3623,11 +3827,12 @@ struct Eng {
       RPCHK(b < U(rx->L.P), "rp_handle_limit best", b);
       i32 e = U(lv_head(opp)[b]);
       RPCHK(e >= 0 && e < U(rx->L.C), "rp_handle_limit head", e);
-      i32 hq = U(E[e].qty), ho = U(E[e].oid), hd = U(E[e].dense), hm = U(E[e].meta), hp = U(E[e].price);
+      const i32 g = rp_gather(opp, b, e);
+      i32 hq = rdli(g, 1), ho = rdli(g, 2), hd = rdli(g, 3), hm = rdli(g, 4), hp = rdli(g, 0);
       i32 mq;
       if (qty >= hq) {
         mq = hq;
-        rp_unlink(opp, b, e);
+        nb_opp = rp_unlink(opp, b, e, g);
       } else {
         mq = qty;
         {  // every lane stores the same (uniform) value
@@ -3677,7 +3882,7 @@ struct Eng {
     if (best < 0) return;
     i32 q = U(E[best].qty), mt = U(E[best].meta);
     if constexpr (BLOG) bl_put(cur, -price, side == 0 ? q : -q);
-    rp_unlink(side, x, best);
+    rp_unlink(side, x, best, rp_gather(side, x, best));
     Msg r = msg_order(MK_CANCELLED, oid, mt >> 1, mt & 1, q, price, 0);
     r.w[5] = (u32)d;
     ex_notify(m_agent(m), r);
@@ -3692,24 +3897,47 @@ struct Eng {
     i32 agent = m_agent(m);
     i32 x = oprice - U(rx->L.pmin);
     if (x < 0 || x >= U(rx->L.P)) return;
-    if (U(lv_cnt(side)[x]) == 0) return;
+    RPCHK(d >= 0 && d < U(rx->L.D), "rp_modify dense", d);
+    // the words known now, in one round trip: lanes 0-11 the id's entry epochs, 12/13 the
+    // level's count and head, 14 the id's live-entry head
+    const i32* EP = idep() + MXA_ID_EPOCHS * (size_t)d;
+    const i32 g = gather1(lane < MXA_ID_EPOCHS ? EP + lane : lane == 12 ? lv_cnt(side) + x : lane == 13 ? lv_head(side) + x : idh() + d,
+                          lane < 15);
+    if (rdli(g, 12) == 0) return;
     if (price != oprice) {
       fail(ERR_RP_MODIFY);
       return;
     }
-    RPCHK(d >= 0 && d < U(rx->L.D), "rp_modify dense", d);
     RpEntry* E = pool();
+    const i32 hd = rdli(g, 13);
+    RPCHK(hd >= 0 && hd < U(rx->L.C), "rp_modify head", hd);
+    // one round trip: lanes 0-9 the id chain's first entry, 16-25 the level head's entry
+    const i32 e0 = rdli(g, 14);
+    const i32 g2 = gather1(lane < 10 ? (const i32*)(E + (e0 >= 0 ? e0 : 0)) + lane : (const i32*)(E + hd) + (lane - 16),
+                           (lane < 10 && e0 >= 0) || (lane >= 16 && lane < 26));
     int matches = 0;
-    i32 guard = 0;
-    for (i32 e = U(idh()[d]); e >= 0 && guard < (1 << 16); e = U(E[e].idnext), guard++)
+    i32 guard = 0, e = e0;
+    if (e >= 0) {
+      if (rdli(g2, 0) == oprice && (rdli(g2, 4) & 1) == buy && rdli(g2, 2) == oid) matches++;
+      e = rdli(g2, 9);
+      guard = 1;
+    }
+    for (; e >= 0 && guard < (1 << 16); e = U(E[e].idnext), guard++)
       if (U(E[e].price) == oprice && (U(E[e].meta) & 1) == buy && U(E[e].oid) == oid) matches++;
     if (matches == 0) return;
-    i32 hd = U(lv_head(side)[x]);
-    RPCHK(hd >= 0 && hd < U(rx->L.C), "rp_modify head", hd);
-    i32 hq = U(E[hd].qty), hdense = U(E[hd].dense);
-    if (hdense != d) {
-      id_unlink(hdense, hd);
-      id_link(d, hd);
+    i32 hq = rdli(g2, 17), hdense = rdli(g2, 19);
+    if (hdense != d) {  // the head moves from its id's live-entry chain to the new id's
+      const i32 p = rdli(g2, 24), n = rdli(g2, 25);
+      {  // every lane stores the same (uniform) value
+        if (p >= 0) E[p].idnext = n;
+        else idh()[hdense] = n;
+        if (n >= 0) E[n].idprev = p;
+        // (the chain of d is untouched by that: its head is still e0)
+        E[hd].idprev = -1;
+        E[hd].idnext = e0;
+        if (e0 >= 0) E[e0].idprev = hd;
+        idh()[d] = hd;
+      }
     }
     {  // every lane stores the same (uniform) value
       E[hd].oid = oid;
@@ -3720,9 +3948,8 @@ struct Eng {
     }
     if constexpr (BLOG) bl_put(cur, -(oprice | BL_MODIFY | (side << 29)), qty - hq);
     // one ORDER_MODIFIED per retained history epoch holding the id (OrderBook.py:352-355)
-    const i32* EP = idep() + MXA_ID_EPOCHS * (size_t)d;
     const i32 lo = h.epoch - PC.stream_history;
-    const int neps = __popcll(bal(lane < MXA_ID_EPOCHS && EP[lane < MXA_ID_EPOCHS ? lane : 0] >= lo));
+    const int neps = __popcll(bal(lane < MXA_ID_EPOCHS && g >= lo));
     for (int k = 0; k < matches * neps; k++) {
       Msg r = msg_order(MK_MODIFIED, oid, agent, buy, qty, price, 0);
       r.w[5] = (u32)d;
@@ -3766,17 +3993,21 @@ struct Eng {
   // (Order.py:26), so a modify then fails isSameOrder at the exchange (OrderBook.py:343-344)
   DEV void mr_place_record(i32 r) {
     PROF_SCOPE(91);
-    const i32 oid = U(rx->oid[r]), price = U(rx->price[r]), size = U(rx->size[r]);
+    mr_place_record_v(r, U(rx->oid[r]), U(rx->price[r]), U(rx->size[r]), U(rx->dense[r]), (i32)rx->buy[r]);
+  }
+  // record r with its tape words already loaded (mr_wakeup gathers the next record's with the
+  // group times)
+  DEV void mr_place_record_v(i32 r, i32 oid, i32 price, i32 size, i32 dense, i32 buy) {
     RPCHK(r >= 0 && r < U(rx->L.nrec), "mr_place_record record", r);
-    const i32 d = oid == 0 ? zero_dense() : U(rx->dense[r]);
+    const i32 d = oid == 0 ? zero_dense() : dense;
     RPCHK(d >= 0 && d < U(rx->L.D), "mr_place_record dense", d);
-    const int buy = (int)U((i32)rx->buy[r]);
-    mr_place_record_as(r, oid, d, price, size, buy);
+    mr_place_record_as(r, oid, d, price, size, U(buy));
     rh()->mr_done = r + 1;  // record r's explicit id (if SIZE > 0) is in Order._order_ids now
+    rs(AF_MR_DONE, (u32)(r + 1));
   }
   DEV void mr_place_record_as(i32 r, i32 oid, i32 d, i32 price, i32 size, int buy) {
-    RpOrder* O = mro() + d;
-    const i32 present = U(O->present);
+    const RpOrder O = mro()[d];  // one 16-byte load: every field the three branches read
+    const i32 present = U(O.present);
     if (!present && size > 0) {  // placeLimitOrder(..., order_id=ORDER_ID)
       i32 id = oid, dd = d;
       if (oid == 0) {
@@ -3795,17 +4026,17 @@ struct Eng {
       lm.w[5] = (u32)dd;
       send_ex(lm);
     } else if (present && size == 0) {  // cancelOrder(existing_order)
-      Msg cm = msg_order(MK_CANCEL, oid, cur_agent, U(O->is_buy), U(O->qty), U(O->price), 0);
+      Msg cm = msg_order(MK_CANCEL, oid, cur_agent, U(O.is_buy), U(O.qty), U(O.price), 0);
       cm.w[5] = (u32)d;
       send_ex(cm);
     } else if (present) {  // modifyOrder(existing_order, LimitOrder(..., order_id))
       i32 id = oid;
       if (oid == 0) id = (i32)next_order_id();
-      else if (buy != U(O->is_buy)) {
+      else if (buy != U(O.is_buy)) {
         fail(ERR_RP_MODIFY);
         return;
       }
-      Msg mm = msg_order(MK_MODIFY, id, cur_agent, buy, size, price, U(O->price));
+      Msg mm = msg_order(MK_MODIFY, id, cur_agent, buy, size, price, U(O.price));
       mm.w[5] = (u32)d;
       if (id != oid) mm.w[0] |= MF_NOT_SAME;
       send_ex(mm);
@@ -3816,31 +4047,51 @@ struct Eng {
     ta_wakeup();
     u32 f = flags();
     if (!((f & FL_HAS_OPEN) && (f & FL_HAS_CLOSE))) return;
-    RpHdr* R = rh();
-    i32 wi = U(R->mr_wi);
+    const i32 wi = rgi(AF_MR_WI);
     const i32 ntm = U(rx->L.ntm);
     if (wi >= ntm) return;  // IndexError: every order submitted (the last group never is)
     // one round trip for the tape words this wakeup reads in the common case: lane 0 tm[wi],
-    // lane 1 tm[wi - 1], lanes 2-4 tm0[wi - 1 .. wi + 1] (tm0 has ntm + 1 entries)
-    i64 tv = 0;
+    // lane 1 tm[wi - 1], lanes 2-4 tm0[wi - 1 .. wi + 1] (tm0 has ntm + 1 entries), and lanes
+    // 8-12 the words of record rn, the next one in tape order (a group's first on time)
+    const i32 rn = rgi(AF_MR_DONE);
+    const bool rn_ok = rn < U(rx->L.nrec);
+    // 32-bit words: lanes 0/1 tm[wi] (lo, hi), 2/3 tm[wi - 1], 4-6 tm0[wi - 1 .. wi + 1], 8-11 the
+    // record's oid / price / size / dense, 12 the aligned word holding its int8 side
+    i32 tw;
     {
-      const i32 ix = lane == 0 ? wi : lane == 1 ? wi - 1 : wi - 3 + lane;
-      if (lane < 2 && ix >= 0) tv = rx->tm[ix];
-      else if (lane >= 2 && lane < 5 && ix >= 0 && ix <= ntm) tv = (i64)rx->tm0[ix];
+      const i32* tm = (const i32*)rx->tm;
+      const i32* a = lane < 2 ? tm + 2 * wi + lane
+                     : lane < 4 ? tm + 2 * (wi - 1) + (lane - 2)
+                     : lane < 8 ? rx->tm0 + (wi - 5 + lane)
+                     : lane == 8 ? rx->oid + rn
+                     : lane == 9 ? rx->price + rn
+                     : lane == 10 ? rx->size + rn
+                     : lane == 11 ? rx->dense + rn
+                                  : (const i32*)((uintptr_t)(rx->buy + rn) & ~(uintptr_t)3);
+      const bool ok = lane < 2 || ((lane == 2 || lane == 3 || lane == 4) && wi > 0) || lane == 5 || lane == 6 ||
+                      (lane >= 8 && lane < 13 && rn_ok);
+      tw = gather1(a, ok);
     }
-    const i64 tn = (i64)rdl64((u64)tv, 0);
+    const i64 tn = (i64)(((u64)(u32)rdli(tw, 1) << 32) | (u32)rdli(tw, 0));
+    const i64 tprev = (i64)(((u64)(u32)rdli(tw, 3) << 32) | (u32)rdli(tw, 2));
+    const i32 rbuy = (i32)(int8_t)(rdli(tw, 12) >> (8 * (rn & 3)));
     wakeup_at(cur_agent, tn);
-    R->mr_wi = wi + 1;
+    rs(AF_MR_WI, (u32)(wi + 1));
     // orders[currentTime]: tm is strictly increasing (sorted tape), so the match is unique. A
     // wakeup on time is at the group just scheduled before (wi - 1) or at wi itself (the first
     // one); anything else (a delayed wakeup) takes the binary search
     i32 lo = 0, hi = ntm - 1, g = -1;
     if (tn == cur) g = wi, lo = hi + 1;
-    else if (wi > 0 && (i64)rdl64((u64)tv, 1) == cur) g = wi - 1, lo = hi + 1;
+    else if (wi > 0 && tprev == cur) g = wi - 1, lo = hi + 1;
     if (g >= 0) {  // the group's record range from the batch
-      const i32 r0 = (i32)rdl64((u64)tv, g == wi ? 3 : 2), r1 = (i32)rdl64((u64)tv, g == wi ? 4 : 3);
+      const i32 r0 = rdli(tw, g == wi ? 5 : 4), r1 = rdli(tw, g == wi ? 6 : 5);
       RPCHK(r0 >= 0 && r0 <= r1 && r1 <= U(rx->L.nrec), "mr_wakeup group", (i64)r0 * 1000000 + r1);
-      for (i32 r = r0; r < r1; r++) mr_place_record(r);
+      for (i32 r = r0; r < r1; r++) {
+        if (r == rn && rn_ok)
+          mr_place_record_v(r, rdli(tw, 8), rdli(tw, 9), rdli(tw, 10), rdli(tw, 11), rbuy);
+        else
+          mr_place_record(r);
+      }
       return;
     }
     while (lo <= hi) {
@@ -5481,6 +5732,29 @@ __global__ __launch_bounds__(64) void mxa_rng_probe_kernel(uint32_t seed, int mo
     }
     if (__lane_id() == 0) out[i] = v;
   }
+}
+// the run kernel's normal draws (rs_gauss_wave): mode 0 from the MT block in HBM (agent
+// streams), mode 1 through a 64-word LDS window (global streams); blocks are materialized as
+// the run kernel's event boundary does (rs_maint), so the sequence must equal mode 3 above
+__global__ __launch_bounds__(64) void mxa_rng_probe_wave_kernel(uint32_t seed, int mode, double a, double b, int n, double* out,
+                                                                uint32_t* scratch) {
+  __shared__ uint32_t win[64];
+  mxa::mt_seed(scratch, seed);
+  mxa::RSt<false> r;
+  r.key = scratch;
+  r.p = MXA_MT_N;
+  r.m = 0;
+  r.hasg = 0;
+  r.gauss = 0;
+  r.lw = mode == 1 ? (LDSP uint32_t*)win : nullptr;
+  r.lw0 = r.p;
+  r.lwn = 0;
+  for (int i = 0; i < n; i++) {
+    mxa::rs_maint(r);
+    const double v = mxa::rs_normal(r, a, b);
+    if (__lane_id() == 0) out[i] = v;
+  }
+  if (__lane_id() == 0) out[n] = (double)(r.hasg & 2);  // a look-ahead overrun would be a probe bug
 }
 
 __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y, double* out, int64_t n) {

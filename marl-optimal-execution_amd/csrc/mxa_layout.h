@@ -303,6 +303,9 @@ enum {
   // POVMarketMakerAgent with per-env options (MXA_CFG_RMSC03_MM): pov, min_order_size, window_size,
   // num_ticks, wake_up_freq in the ZI / momentum areas it never uses
   AF_MM_POV = AF_R_T, AF_MM_MIN = 46, AF_MM_WIN = 47, AF_MM_TICKS = 48, AF_MM_WAKE = 50,
+  // MarketReplayAgent: the next wakeup group (the reference's wakeup index) and the tape records
+  // handled, in its LDS-resident record (RpHdr::mr_done stays the copy other agents read)
+  AF_MR_WI = 46, AF_MR_DONE = 47,
   AF_MIDS = 66,       // 50 x int32 (2*mid ring), momentum
   AF_STREAM_N = 66,   // HBL: epochs of the last QUERY_ORDER_STREAM reply (momentum's AF_MIDS area)
   AF_STREAM_HI = 68,  // HBL: absolute history epoch of its first entry (history[1]), int64
