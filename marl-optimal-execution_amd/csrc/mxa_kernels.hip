@@ -893,7 +893,11 @@ struct Eng {
   i64* trace;
   i32 trace_cap;
   bool hash_on;  // per-pop parity hash (kernel argument trace_cap < 0: off, and no trace ring)
-  const RpCtx* rx;  // marketreplay: tape + runtime layout (nullptr otherwise)
+  // marketreplay / hist_fund: tape + runtime layout (nullptr otherwise).  Read through the
+  // constant address space: the context never changes during a launch, so its fields (the
+  // layout offsets every replay handler starts from) come from scalar loads, not from a vector
+  // load round trip at the head of each handler's chain
+  const __attribute__((address_space(4))) RpCtx* rx;
   i32 end_step;     // GymKernel: the RL agent's spread reply ends a step
   u32 run_skip;     // event runs: members below this seq are popped one by one (a LIMIT run that crosses)
   // book-update log of this env: a kernel variant of its own (LOG), so the event loop of the
@@ -915,7 +919,7 @@ struct Eng {
   static constexpr size_t LDS_Q = (size_t)QCL * (12 + (PL_LDS ? 4 * PW : 0));
   DEV Eng(char* e, char* lds, i32 tcap, const RpCtx* ctx = nullptr, BlRec* bl = nullptr, i32 bl_cap = 0)
       : env((EnvPtr)e), h(*(LDSP EnvHdr*)(lds + LDS_Q)) {
-    rx = ctx;
+    rx = (const __attribute__((address_space(4))) RpCtx*)ctx;
     blog = bl;
     blog_cap = bl_cap;
     end_step = 0;
@@ -5195,7 +5199,7 @@ struct Builder : Eng<CFG, true> {
   // No RNG stream is ever drawn in this composition.
   DEV void build_replay(i32 id_base, i32 tape_hi) {
     const MxaParams& P = E::PC;
-    const RpLayout& L = this->rx->L;
+    const __attribute__((address_space(4))) RpLayout& L = this->rx->L;
     const i32 Pn = U(L.P), C = U(L.C), D = U(L.D);
     for (int s = 0; s < 2; s++) {
       i32 *c = this->lv_cnt(s), *hd = this->lv_head(s), *tl = this->lv_tail(s);
