@@ -61,6 +61,8 @@ DEV i32 gather1(const i32* a, bool ok) {
   if (ok) v = *a;
   return v;
 }
+// the i64 whose lo / hi words a gather put in lanes l / l + 1
+DEV i64 rdl64g(i32 g, int l) { return (i64)(((u64)(u32)__builtin_amdgcn_readlane(g, l + 1) << 32) | (u32)__builtin_amdgcn_readlane(g, l)); }
 DEV u64 rdl64(u64 v, int l) {
   return ((u64)rdl((u32)(v >> 32), l) << 32) | rdl((u32)v, l);
 }
@@ -3668,13 +3670,15 @@ struct Eng {
     const i32 x = price - U(rx->L.pmin);
     const bool xin = x >= 0 && x < U(rx->L.P);
     rp_enter_pf(oid, d, agent, buy, qty, price, x, U(R->free_top), xin ? U(lv_tail(side)[x]) : -1,
-                xin ? U(lv_cnt(side)[x]) : 0, U(R->nlev[side]), U(R->best[side]), U(idh()[d]));
+                xin ? U(lv_cnt(side)[x]) : 0, U(R->nlev[side]), U(R->best[side]), U(idh()[d]),
+                xin ? U(lv_qty(side)[x]) : (i64)0);
   }
   // rp_enter with the words it reads already loaded (rp_handle_limit gathers them in one round
-  // trip): the free-stack top, the level's tail and count, the side's level count and best,
-  // and the id's live-entry chain head
+  // trip): the free-stack top, the level's tail, count and quantity, the side's level count and
+  // best, and the id's live-entry chain head.  No load follows its stores (a load issued after a
+  // store waits for the store as well)
   DEV void rp_enter_pf(i32 oid, i32 d, i32 agent, int buy, i32 qty, i32 price, i32 x, i32 top, i32 tl, i32 cnt,
-                       i32 nl, i32 bs, i32 hd) {
+                       i32 nl, i32 bs, i32 hd, i64 lq) {
     RpHdr* R = rh();
     const int side = buy ? 0 : 1;
     if (x < 0 || x >= U(rx->L.P)) {
@@ -3711,7 +3715,7 @@ struct Eng {
       else lv_head(side)[x] = e;
       lv_tail(side)[x] = e;
       lv_cnt(side)[x] = cnt + 1;
-      lv_qty(side)[x] += qty;
+      lv_qty(side)[x] = lq + qty;
       if (hd >= 0) E[hd].idprev = e;
       idh()[d] = e;
     }
@@ -3725,15 +3729,18 @@ struct Eng {
     if (h.b_count > h.max_book) h.max_book = h.b_count;
   }
   // every word rp_unlink reads, in one round trip: lanes 0-9 the entry's words (RpEntry order:
-  // price qty oid dense meta arrival prev next idprev idnext), 12 the level's count, 13
-  // free_top, 14/15 the side's level count and best
+  // price qty oid dense meta arrival prev next idprev idnext), 10/11 the level's quantity (lo,
+  // hi), 12 the level's count, 13 free_top, 14/15 the side's level count and best
   DEV i32 rp_gather(int side, i32 x, i32 e) {
     RPCHK(e >= 0 && e < U(rx->L.C) && x >= 0 && x < U(rx->L.P), "rp_unlink entry/level", (i64)e * 100000 + x);
-    RpHdr* R = rh();
-    const i32* W = (const i32*)(pool() + e);
-    const i32* a = lane < 10 ? W + lane : lane == 12 ? lv_cnt(side) + x : lane == 13 ? &R->free_top
-                   : lane == 14 ? &R->nlev[side] : &R->best[side];
-    return gather1(a, lane < 10 || (lane >= 12 && lane < 16));
+    const u64 sx = (u64)side * (u32)rx->L.P + (u32)x;
+    const u64 o_w = rx->L.off_pool + (u64)e * sizeof(RpEntry), o_c = rx->L.off_lvc + 4 * sx, o_q = rx->L.off_lvq + 8 * sx,
+              o_rh = rx->L.off_rh;
+    asm volatile("" ::"s"(o_w), "s"(o_c), "s"(o_q), "s"(o_rh));
+    const u64 ob = lane < 10 ? o_w + 4 * lane : lane < 12 ? o_q + 4 * (lane - 10) : lane == 12 ? o_c
+                   : lane == 13 ? o_rh + offsetof(RpHdr, free_top) : lane == 14 ? o_rh + offsetof(RpHdr, nlev) + 4 * side
+                                : o_rh + 4 * side;
+    return gather1((const i32*)(env + ob), lane < 16);
   }
   // remove entry e (level x of `side`, its words gathered in g) from the book; returns the
   // side's best level after the removal
@@ -3750,7 +3757,7 @@ struct Eng {
       if (n >= 0) E[n].prev = p;
       else lv_tail(side)[x] = p;
       lv_cnt(side)[x] = cnt - 1;
-      lv_qty(side)[x] -= q;
+      lv_qty(side)[x] = rdl64g(g, 10) - q;
       freel()[top] = e;
       R->free_top = top + 1;
       // the id's live-entry chain
@@ -3789,25 +3796,34 @@ struct Eng {
     const bool xin = x >= 0 && x < U(rx->L.P);
     // every word the first pass reads whose address is known now, in one round trip: lanes
     // 0-11 the id's entry epochs, 16/17 best[bids/asks], 18/19 nlev, 20 free_top, 21 the id's
-    // live-entry head, 22/23 the own level's count and tail (a dependent chain of six before)
+    // live-entry head, 22/23 the own level's count and tail, 24/25 its quantity (lo, hi)
+    PROF_IN(pt_g);
     i32 pf;
     {
       static_assert(offsetof(RpHdr, nlev) == 8 && offsetof(RpHdr, free_top) == 16, "RpHdr: best, nlev, free_top");
-      i32* EP = idep() + MXA_ID_EPOCHS * (size_t)d;
-      const i32* a = lane < MXA_ID_EPOCHS ? EP + lane
-                     : lane < 21          ? (const i32*)R + (lane - 16)
-                     : lane == 21         ? idh() + d
-                     : lane == 22         ? lv_cnt(side) + x
-                                          : lv_tail(side) + x;
-      pf = gather1(a, lane < MXA_ID_EPOCHS || (lane >= 16 && lane < 22) || (xin && (lane == 22 || lane == 23)));
-      // history[0][order_id] = ... (OrderBook.py:51-60): the id's distinct entry epochs, newest
-      // first, one per lane (lanes < MXA_ID_EPOCHS)
-      static_assert(MXA_ID_EPOCHS > PC.stream_history, "the id's entry epochs must cover the history window");
-      if (rdli(pf, 0) != hep) {
-        const i32 up = __shfl_up(pf, 1, 64);
-        if (lane < MXA_ID_EPOCHS) EP[lane] = lane == 0 ? hep : up;
-      }
+      // the layout words first, in one batch of scalar loads (selected per lane below: loads in
+      // the arms of the select became one scalar-cache wait per arm)
+      const u64 o_ep = rx->L.off_idep, o_idh = rx->L.off_idh, o_c = rx->L.off_lvc, o_t = rx->L.off_lvt, o_rh = rx->L.off_rh,
+                o_q = rx->L.off_lvq;
+      const u64 px = 4 * ((u64)side * (u32)rx->L.P + (u32)x);
+      asm volatile("" ::"s"(o_ep), "s"(o_idh), "s"(o_c), "s"(o_t), "s"(o_rh), "s"(o_q), "s"(px));
+      const u64 ob = lane < MXA_ID_EPOCHS ? o_ep + 4 * ((u64)MXA_ID_EPOCHS * d + lane)
+                     : lane < 21          ? o_rh + 4 * (lane - 16)
+                     : lane == 21         ? o_idh + 4 * (u64)d
+                     : lane == 22         ? o_c + px
+                     : lane == 23         ? o_t + px
+                                          : o_q + 2 * px + 4 * (lane - 24);
+      pf = gather1((const i32*)(env + ob),
+                   lane < MXA_ID_EPOCHS || (lane >= 16 && lane < 22) || (xin && lane >= 22 && lane < 26));
     }
+    // history[0][order_id] = ... (OrderBook.py:51-60): the id's distinct entry epochs, newest
+    // first, one per lane (lanes < MXA_ID_EPOCHS).  Stored after the handler's loads (below):
+    // a load issued after a store waits for that store too (one in-order vmcnt on gfx9-class
+    // parts), and nothing in the handler reads these words
+    static_assert(MXA_ID_EPOCHS > PC.stream_history, "the id's entry epochs must cover the history window");
+    const bool ep_new = rdli(pf, 0) != hep;
+    PROF_OUT(76, pt_g);  // (the gather's wait lands here: rdli uses it)
+    const i32 ep_up = __shfl_up(pf, 1, 64);
     i64 ex_q = 0, ex_pq = 0;
     bool executed = false;
     i32 nb_opp = -1;
@@ -3818,14 +3834,18 @@ struct Eng {
       i32 b = executed ? nb_opp : rdli(pf, 16 + opp);
       bool match = b >= 0 && (buy ? price >= pmin + b : price <= pmin + b);
       if (!match) {
+        PROF_IN(pt_e);
         if (!executed)  // no fill changed the gathered words
           rp_enter_pf(oid, d, agent, buy, qty, price, x, rdli(pf, 20), xin ? rdli(pf, 23) : -1,
-                      xin ? rdli(pf, 22) : 0, rdli(pf, 18 + side), rdli(pf, 16 + side), rdli(pf, 21));
+                      xin ? rdli(pf, 22) : 0, rdli(pf, 18 + side), rdli(pf, 16 + side), rdli(pf, 21), rdl64g(pf, 24));
         else
           rp_enter(oid, d, agent, buy, qty, price);
+        PROF_OUT(79, pt_e);
+        PROF_IN(pt_n);
         Msg ma = msg_order(MK_ACCEPTED, oid, agent, buy, qty, price, 0);
         ma.w[5] = (u32)d;
         ex_notify(agent, ma);
+        PROF_OUT(80, pt_n);
         break;
       }
       RPCHK(b < U(rx->L.P), "rp_handle_limit best", b);
@@ -3841,7 +3861,7 @@ struct Eng {
         mq = qty;
         {  // every lane stores the same (uniform) value
           E[e].qty = hq - qty;
-          lv_qty(opp)[b] -= qty;
+          lv_qty(opp)[b] = rdl64g(g, 10) - qty;
         }
       }
       qty -= mq;
@@ -3862,6 +3882,7 @@ struct Eng {
       h.epoch = hep + 1;
       R->ex_has_last = 1;
     }
+    if (ep_new && lane < MXA_ID_EPOCHS) idep()[MXA_ID_EPOCHS * (size_t)d + lane] = lane == 0 ? hep : ep_up;
   }
   // cancelOrder (OrderBook.py:284-339): first live entry of the id at the request's level
   DEV void rp_cancel(const Msg& m) {
@@ -3905,8 +3926,18 @@ struct Eng {
     // the words known now, in one round trip: lanes 0-11 the id's entry epochs, 12/13 the
     // level's count and head, 14 the id's live-entry head
     const i32* EP = idep() + MXA_ID_EPOCHS * (size_t)d;
-    const i32 g = gather1(lane < MXA_ID_EPOCHS ? EP + lane : lane == 12 ? lv_cnt(side) + x : lane == 13 ? lv_head(side) + x : idh() + d,
-                          lane < 15);
+    i32 g;
+    {
+      const u64 px = 4 * ((u64)side * (u32)rx->L.P + (u32)x);
+      const u64 o_ep = rx->L.off_idep + 4 * (u64)MXA_ID_EPOCHS * d, o_c = rx->L.off_lvc + px, o_h = rx->L.off_lvh + px,
+                o_idh = rx->L.off_idh + 4 * (u64)d, o_q = rx->L.off_lvq + 2 * px;
+      asm volatile("" ::"s"(o_ep), "s"(o_c), "s"(o_h), "s"(o_idh), "s"(o_q));
+      // lanes 0-11 the id's epochs, 12/13 the level's count and head, 14 the id's chain head,
+      // 15/16 the level's quantity (lo, hi)
+      const u64 ob = lane < MXA_ID_EPOCHS ? o_ep + 4 * lane : lane == 12 ? o_c : lane == 13 ? o_h : lane == 14 ? o_idh
+                                                                                     : o_q + 4 * (lane - 15);
+      g = gather1((const i32*)(env + ob), lane < 17);
+    }
     if (rdli(g, 12) == 0) return;
     if (price != oprice) {
       fail(ERR_RP_MODIFY);
@@ -3948,7 +3979,7 @@ struct Eng {
       E[hd].dense = d;
       E[hd].qty = qty;
       E[hd].meta = (agent << 1) | buy;
-      lv_qty(side)[x] += (i64)(qty - hq);
+      lv_qty(side)[x] = rdl64g(g, 15) + (i64)(qty - hq);
     }
     if constexpr (BLOG) bl_put(cur, -(oprice | BL_MODIFY | (side << 29)), qty - hq);
     // one ORDER_MODIFIED per retained history epoch holding the id (OrderBook.py:352-355)
@@ -4057,30 +4088,37 @@ struct Eng {
     // one round trip for the tape words this wakeup reads in the common case: lane 0 tm[wi],
     // lane 1 tm[wi - 1], lanes 2-4 tm0[wi - 1 .. wi + 1] (tm0 has ntm + 1 entries), and lanes
     // 8-12 the words of record rn, the next one in tape order (a group's first on time)
+    PROF_IN(pt_w);
     const i32 rn = rgi(AF_MR_DONE);
     const bool rn_ok = rn < U(rx->L.nrec);
     // 32-bit words: lanes 0/1 tm[wi] (lo, hi), 2/3 tm[wi - 1], 4-6 tm0[wi - 1 .. wi + 1], 8-11 the
     // record's oid / price / size / dense, 12 the aligned word holding its int8 side
     i32 tw;
     {
-      const i32* tm = (const i32*)rx->tm;
-      const i32* a = lane < 2 ? tm + 2 * wi + lane
-                     : lane < 4 ? tm + 2 * (wi - 1) + (lane - 2)
-                     : lane < 8 ? rx->tm0 + (wi - 5 + lane)
-                     : lane == 8 ? rx->oid + rn
-                     : lane == 9 ? rx->price + rn
-                     : lane == 10 ? rx->size + rn
-                     : lane == 11 ? rx->dense + rn
-                                  : (const i32*)((uintptr_t)(rx->buy + rn) & ~(uintptr_t)3);
+      // the tape's array addresses first, in one batch of scalar loads, then one select per lane
+      const u64 a_tm = (u64)rx->tm, a_tm0 = (u64)rx->tm0, a_oid = (u64)rx->oid, a_pr = (u64)rx->price,
+                a_sz = (u64)rx->size, a_dn = (u64)rx->dense, a_buy = (u64)rx->buy;
+      asm volatile("" ::"s"(a_tm), "s"(a_tm0), "s"(a_oid), "s"(a_pr), "s"(a_sz), "s"(a_dn), "s"(a_buy));
+      const u64 a = lane < 2    ? a_tm + 8 * (i64)wi + 4 * lane
+                    : lane < 4  ? a_tm + 8 * (i64)(wi - 1) + 4 * (lane - 2)
+                    : lane < 8  ? a_tm0 + 4 * (i64)(wi - 5 + lane)
+                    : lane == 8 ? a_oid + 4 * (i64)rn
+                    : lane == 9 ? a_pr + 4 * (i64)rn
+                    : lane == 10 ? a_sz + 4 * (i64)rn
+                    : lane == 11 ? a_dn + 4 * (i64)rn
+                                 : ((a_buy + (u64)rn) & ~(u64)3);
       const bool ok = lane < 2 || ((lane == 2 || lane == 3 || lane == 4) && wi > 0) || lane == 5 || lane == 6 ||
                       (lane >= 8 && lane < 13 && rn_ok);
-      tw = gather1(a, ok);
+      tw = gather1((const i32*)a, ok);
     }
     const i64 tn = (i64)(((u64)(u32)rdli(tw, 1) << 32) | (u32)rdli(tw, 0));
     const i64 tprev = (i64)(((u64)(u32)rdli(tw, 3) << 32) | (u32)rdli(tw, 2));
     const i32 rbuy = (i32)(int8_t)(rdli(tw, 12) >> (8 * (rn & 3)));
+    PROF_OUT(81, pt_w);
+    PROF_IN(pt_k);
     wakeup_at(cur_agent, tn);
     rs(AF_MR_WI, (u32)(wi + 1));
+    PROF_OUT(82, pt_k);
     // orders[currentTime]: tm is strictly increasing (sorted tape), so the match is unique. A
     // wakeup on time is at the group just scheduled before (wi - 1) or at wi itself (the first
     // one); anything else (a delayed wakeup) takes the binary search
@@ -4091,8 +4129,11 @@ struct Eng {
       const i32 r0 = rdli(tw, g == wi ? 5 : 4), r1 = rdli(tw, g == wi ? 6 : 5);
       RPCHK(r0 >= 0 && r0 <= r1 && r1 <= U(rx->L.nrec), "mr_wakeup group", (i64)r0 * 1000000 + r1);
       for (i32 r = r0; r < r1; r++) {
-        if (r == rn && rn_ok)
+        if (r == rn && rn_ok) {
+          PROF_IN(pt_p);
           mr_place_record_v(r, rdli(tw, 8), rdli(tw, 9), rdli(tw, 10), rdli(tw, 11), rbuy);
+          PROF_OUT(83, pt_p);
+        }
         else
           mr_place_record(r);
       }

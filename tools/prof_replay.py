@@ -40,7 +40,9 @@ for b, nm, c in phases:
 print("inclusive function timers (cycles per call, calls per event)")
 for b, nm in [(84, "rp_handle_limit"), (85, "rp_modify"), (86, "rp_cancel"), (87, "mr_wakeup"), (91, "mr_place_record"),
               (88, "mr_receive"), (89, "rl_receive"), (90, "rl_place_orders"), (64, "send"), (65, "q_push"),
-              (73, "ex_receive"), (74, "ta_receive"), (75, "ta_wakeup"), (77, "rec_load")]:
+              (73, "ex_receive"), (74, "ta_receive"), (75, "ta_wakeup"), (77, "rec_load"),
+              (76, " limit: gather"), (79, " limit: enter"), (80, " limit: notify"),
+              (81, " wakeup: gather"), (82, " wakeup: setWakeup"), (83, " wakeup: place record")]:
     c = p[b + 32]
     if c:
         print("  %-22s %8.0f cyc/call %6.3f calls/event %8.0f cyc/event" % (nm, p[b] / c, c / ev, p[b] / ev))
