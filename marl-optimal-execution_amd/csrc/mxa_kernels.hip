@@ -5051,7 +5051,10 @@ struct Eng {
           PROF_ADD(31, t0);
           continue;
         }
-        if (type == MT_MESSAGE && m_kind(m) == MK_ACCEPTED && rcp > 0 && rcp < ACK_LIMIT) {
+        // ORDER_ACCEPTED, and ORDER_MODIFIED, which no agent of the reference handles (only
+        // util/OrderBook.py sends it; TradingAgent.receiveMessage has no branch for it): the
+        // whole effect is agentCurrentTimes[a] = t
+        if (type == MT_MESSAGE && (m_kind(m) == MK_ACCEPTED || m_kind(m) == MK_MODIFIED) && rcp > 0 && rcp < ACK_LIMIT) {
           PROF_ADD(0, t0);
           account_pop(t, key, m);
           PROF_ADD(32, t0);
