@@ -646,6 +646,11 @@ struct Eng {
   static constexpr int SO = mxa_cfg::shape(CFG).so;
   static constexpr bool PL_LDS = mxa_cfg::shape(CFG).pl;
   static constexpr int PW = mxa_cfg::shape(CFG).pw;           // payload words queued
+#ifdef MXA_NO_EARLY_REC
+  static constexpr bool EARLY_REC = false;
+#else
+  static constexpr bool EARLY_REC = !BUILD && !PL_LDS;  // (event loop: record beside the HBM payload)
+#endif
   // grouped lane-min cache for deep queues (sparse_zi_1000: 48 slots per lane): a lane's slots
   // in groups of QG, each group's min (key, seq, slot) kept in VGPRs, so a remove or requeue
   // rescans one group of QG slots instead of all SQ
@@ -986,12 +991,14 @@ struct Eng {
     if (HOT > 1 && HOT1 >= 0 && a == HOT1) return 1;
     return -1;
   }
-  DEV void rec_load(int a) {
-    PROF_SCOPE(77);
+  DEV u64 rec_fetch(int a) {
     const int hs = hot_slot(a);
-    u64 v;
-    if (hs >= 0) v = hotrec[hs * 64 + lane];
-    else v = agent_ptr(a)[lane];
+    if (hs >= 0) return hotrec[hs * 64 + lane];
+    return agent_ptr(a)[lane];
+  }
+  DEV void rec_load(int a) { rec_set(a, rec_fetch(a)); }
+  DEV void rec_set(int a, u64 v) {
+    PROF_SCOPE(77);
     rlo = (u32)v;
     rhi = (u32)(v >> 32);
     cur_agent = a;
@@ -1279,6 +1286,42 @@ struct Eng {
     }
     if (bk == KEY_EMPTY && bs == 0xFFFFFFFFu) bj = -1;
   }
+  // HQ_AGG, a pop or rekey in the HBM tier: the owner lane's SQH far slots in ONE round trip,
+  // spread over the wave (lane i holds slots SQL + i and SQL + 64 + i), then a wave-wide
+  // lexicographic min (as q_peek).  Results are wave-uniform.  The owner-lane scan took SQH / QG
+  // dependent round trips (34 % of random_fund_value's cycles in q_remove, r04 s12)
+  DEV void q_scan_hbm_wave(int owner, u64& bk, u32& bs, i32& bj) {
+    static_assert(SQH <= 128, "two far slots per lane");
+    u64 k0 = KEY_EMPTY, k1 = KEY_EMPTY;
+    u32 s0 = 0xFFFFFFFFu, s1 = 0xFFFFFFFFu;
+    i32 j0 = SQL + lane, j1 = SQL + 64 + lane;
+    if (lane < SQH) {
+      const int h = hidx(j0 * 64 + owner);
+      k0 = hqk()[h];
+      s0 = hqs()[h];
+    }
+    if (64 + lane < SQH) {
+      const int h = hidx(j1 * 64 + owner);
+      k1 = hqk()[h];
+      s1 = hqs()[h];
+    }
+    q_min2(k0, s0, j0, k1, s1, j1);
+    const u32 kh = (u32)(k0 >> 32), kl = (u32)k0;
+    const u32 m1 = wmin_u32(kh);
+    u64 b = bal(kh == m1);
+    if (__popcll(b) > 1) {
+      const u32 m2 = wmin_u32(kh == m1 ? kl : 0xFFFFFFFFu);
+      b = bal(kh == m1 && kl == m2);
+      if (__popcll(b) > 1) {
+        const u32 m3 = wmin_u32((kh == m1 && kl == m2) ? s0 : 0xFFFFFFFFu);
+        b = bal(kh == m1 && kl == m2 && s0 == m3);
+      }
+    }
+    const int L = ffs64(b);
+    bk = ((u64)m1 << 32) | rdl(kl, L);
+    bs = rdl(s0, L);
+    bj = (bk == KEY_EMPTY && bs == 0xFFFFFFFFu) ? -1 : rdli(j0, L);
+  }
   // QHIER: the slot's group changed.  An LDS-tier group is rescanned in every lane (the group
   // index is wave-uniform; lanes whose group did not change recompute the same values), then the
   // lane mins.  An HBM-tier slot: its owner lane alone rescans (HQ_OWNER: that group; HQ_AGG:
@@ -1287,8 +1330,14 @@ struct Eng {
     const int g = (slot >> 6) / QG, owner = slot & 63;
     if constexpr (TIER && HQ_AGG) {
       if ((slot >> 6) >= SQL) {
+        u64 k;
+        u32 s;
+        i32 j;
+        q_scan_hbm_wave(owner, k, s, j);
         if (lane == owner) {
-          q_scan_hbm(gk[NG - 1], gs[NG - 1], gj[NG - 1]);
+          gk[NG - 1] = k;
+          gs[NG - 1] = s;
+          gj[NG - 1] = j;
           q_lanemin();
         }
         return;
@@ -4997,10 +5046,18 @@ struct Eng {
         status = ST_DONE;
         break;
       }
-      Msg m = pl_read(slot);
       i64 t = (i64)(key >> KSH);
       int rcp = (int)((key >> 2) & KRCP);
       int type = (int)(key & 3);
+      // payload in HBM: the recipient's record is loaded beside it, one round trip for both
+      // instead of payload -> fast-path test -> record (the record of an acknowledgement that
+      // takes a fast path is loaded for nothing: 512 B, no latency)
+      u64 rv_early = 0;
+      if constexpr (EARLY_REC) {
+        if (rcp != 0) rv_early = rec_fetch(rcp);
+      }
+      Msg m = pl_read(slot);
+      if constexpr (EARLY_REC) asm volatile("" ::"v"(rv_early));
       if constexpr (RUNS) {
         // a run past stopTime is not batched: the loop stops after its first member
         if (type == MT_MESSAGE && (m.w[0] & MF_RUN) && t <= stop_t && eseq >= run_skip) {
@@ -5068,7 +5125,8 @@ struct Eng {
         if (ACK_FAST && type == MT_MESSAGE && m_kind(m) == MK_CANCELLED && rcp > 0 && rcp < ACK_LIMIT) {
           // TradingAgent.orderCancelled (TradingAgent.py:464-480): del self.orders[id]. The
           // open-order chunks are loaded with the record, not after it (one latency, not two)
-          rec_load(rcp);
+          if constexpr (EARLY_REC) rec_set(rcp, rv_early);
+          else rec_load(rcp);
           OpenOrder my[OC];
           {
             const OpenOrder* oo = open_ptr(rcp);
@@ -5099,7 +5157,8 @@ struct Eng {
       }
 #endif
       PROF_ADD(0, t0);
-      rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
+      if constexpr (EARLY_REC) rec_set(rcp, rv_early);
+      else rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
       cur = t;
       if (INSTR && (hash_on || trace)) {
         if (lane == 0) h.kc[pop_class(key, m)]++;
