@@ -40,7 +40,10 @@ constexpr int lat_lds(int cfg);
 #define MXA_W_RMSC02 2
 #endif
 #ifndef MXA_SO_RMSC02
-#define MXA_SO_RMSC02 10  // 640 book slots: the oracle's maximum over every seed of bench.py --gpus <= 8 is 537 (512 overflowed)
+// 576 book slots: the oracle's maximum over every seed of bench.py --gpus <= 8 is 537 (512
+// overflowed).  The book lives in VGPRs: 640 slots measured 1319 ms against 1054 ms for 576
+// (rmsc02 x4096 run kernel, same digest; 848 vs 535 static scratch instructions)
+#define MXA_SO_RMSC02 9
 #endif
 #ifndef MXA_SQ_Z1K
 #define MXA_SQ_Z1K 36  // sparse_zi_1000 queue slots per lane (2,304; the oracle's maximum over the 32,768 seeds of
@@ -119,7 +122,7 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, MXA_RMSC01_WAVES, 8, 0}
        // rmsc02: oracle maxima over the 131,072 seeds bench.py draws at --gpus 1-8 (batches 0-3 of
        // ranks 0-7, tools/capacity_sweep.py, profiles/r04/capacity_rmsc02.json): 225 pending
-       // events, 537 resting orders, 59 open orders of one agent
+       // events, 537 resting orders, 59 open orders of one agent (576 book slots)
        : cfg == MXA_CFG_RMSC02 ? Shape{6, MXA_SO_RMSC02, true, MXA_W_RMSC02, 8, 0}
        // obi_rmsc02: oracle maxima over the 131,072 seeds of bench.py --gpus 1-8: 211 pending
        // events, 149 resting orders (192 book slots; 128 overflowed)

@@ -352,10 +352,13 @@ DEV double rs_gauss_wave(RSt<B>& r) {
     r.p += 4 * nc;  // every available candidate rejected
   }
 }
-#ifdef MXA_SERIAL_GAUSS
+// the run kernel's normal draws: serial (default) or wave-parallel (-DMXA_WAVE_GAUSS=1).  The
+// wave form was neutral on sparse_zi_1000 (721.9 vs 722.x ms) and grew rmsc02's run kernel
+// (62.1 k vs 54.4 k instructions, 1,129 vs 848 scratch instructions: it is inlined at every
+// normal draw of a kernel already at 256 VGPRs), so it is opt-in; the parity probe
+// (mxa_rng_probe modes 6 / 7) runs it either way
+#ifndef MXA_WAVE_GAUSS
 #define MXA_WAVE_GAUSS 0
-#else
-#define MXA_WAVE_GAUSS 1
 #endif
 template <bool B>
 DEV double rs_gauss(RSt<B>& r) {
@@ -649,7 +652,10 @@ struct Eng {
 #ifdef MXA_NO_EARLY_REC
   static constexpr bool EARLY_REC = false;
 #else
-  static constexpr bool EARLY_REC = !BUILD && !PL_LDS;  // (event loop: record beside the HBM payload)
+  // (event loop: record beside the HBM payload).  Not on the two-tier queue configurations:
+  // there it measured neutral (393.1 vs 393.7 ms) and loads the records of the acknowledgements
+  // that take a fast path, +46 B/event of HBM traffic
+  static constexpr bool EARLY_REC = !BUILD && !PL_LDS && !(mxa_cfg::sq_lds(CFG) < mxa_cfg::shape(CFG).sq);
 #endif
   // grouped lane-min cache for deep queues (sparse_zi_1000: 48 slots per lane): a lane's slots
   // in groups of QG, each group's min (key, seq, slot) kept in VGPRs, so a remove or requeue
@@ -5858,7 +5864,15 @@ __global__ __launch_bounds__(64) void mxa_rng_probe_wave_kernel(uint32_t seed, i
   r.lwn = 0;
   for (int i = 0; i < n; i++) {
     mxa::rs_maint(r);
-    const double v = mxa::rs_normal(r, a, b);
+    double g;
+    if (r.hasg & 1) {  // legacy_gauss's cached second value
+      g = r.gauss;
+      r.hasg &= ~1;
+      r.gauss = 0.0;
+    } else {
+      g = mxa::rs_gauss_wave(r);
+    }
+    const double v = a + b * g;
     if (__lane_id() == 0) out[i] = v;
   }
   if (__lane_id() == 0) out[n] = (double)(r.hasg & 2);  // a look-ahead overrun would be a probe bug
