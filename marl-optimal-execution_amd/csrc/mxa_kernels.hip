@@ -5163,8 +5163,13 @@ struct Eng {
       }
 #endif
       PROF_ADD(0, t0);
-      if constexpr (EARLY_REC) rec_set(rcp, rv_early);
-      else rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
+      // (the exchange's record is not fetched early: its messages take the fast path)
+      if constexpr (EARLY_REC) {
+        if (rcp != 0) rec_set(rcp, rv_early);
+        else rec_load(rcp);
+      } else {
+        rec_load(rcp);  // issued before the trace encode/hash so its latency overlaps them
+      }
       cur = t;
       if (INSTR && (hash_on || trace)) {
         if (lane == 0) h.kc[pop_class(key, m)]++;

@@ -71,7 +71,8 @@ def test_records_gym_handle():
         assert rec[e, shard.R_CASH] == cash and rec[e, shard.R_HOLD] == shares
 
 
-@pytest.mark.parametrize("cfg,seed", [("rmsc03", 123456789), ("sparse_zi_100", 123456789), ("value_noise", 7)])
+@pytest.mark.parametrize("cfg,seed", [("rmsc03", 123456789), ("sparse_zi_100", 123456789), ("value_noise", 7),
+                                      ("sparse_zi_1000", 123456789), ("random_fund_value", 7)])
 def test_counters_agree_with_the_trace(cfg, seed):
     """the event-class counters of an instrumented run (mxa_read_counters, the algorithmic-byte
     count of bench.py) equal the per-kind histogram of the env's full parity trace, whose records
@@ -90,6 +91,9 @@ def test_counters_agree_with_the_trace(cfg, seed):
     assert c[mc.C_PUSH] + m.n_agents >= c[mc.C_POPS] - c[mc.C_REQUEUE] and c[mc.C_RNG] > 0
     bpe, parts, units = mc.bytes_per_event(m.counters())
     assert 100 < bpe < 600 and 0 < units["record_round_trips"] <= 1
+    # every agent record's stream position is a real one: an event that ran on a record it never
+    # loaded (the round-4 early record fetch once did, for the exchange) stores a zeroed position
+    assert 0 <= units["rng_words"] < 50, units
 
 
 def test_counters_off_without_instrumentation():
