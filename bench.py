@@ -650,8 +650,8 @@ def main():
                 eng.last_counters = eng.count(args.warmup)
                 bpe, bparts, bunits = mc.bytes_per_event(eng.last_counters)
             achieved = bpe * my_ev_per_launch / (avg_ms * 1e-3) / 1e9
-            traffic, tsrc = (traffic_record(args.config, eng.n, bool(args.parity_hash), args.tape)
-                             if isinstance(eng, (MarketEngine, GymEngine)) else (None, {"why": "no PMC record for this config"}))
+            # (the DDQN line's record is a PMC pass of the same bench command: its step kernel)
+            traffic, tsrc = traffic_record(args.config, eng.n, bool(args.parity_hash), args.tape)
             out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_record": tsrc,
                                "kernel": eng.kernel, "avg_launch_ms": avg_ms, "launches": eng.launches,
