@@ -9,7 +9,7 @@ TAG=$1; CFG=$2; ENVS=$3
 OUT=$R/gpurun_out/sq_$TAG
 mkdir -p $OUT
 cd /tmp
-B="$R/bench.py --config $CFG --envs $ENVS --steps 1 --warmup 0 --no-cpu --no-count"
+B="$R/bench.py --config $CFG --envs $ENVS --steps 1 --warmup 0 --no-cpu --no-count --no-latency"
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_LDS"
 P2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_FLAT"
 P3="SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_WAIT_INST_LDS SQ_ACTIVE_INST_FLAT SQ_ACTIVE_INST_MISC SQ_INSTS_SALU"
