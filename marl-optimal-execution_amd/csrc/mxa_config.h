@@ -143,11 +143,19 @@ constexpr Shape shape(int cfg) {
                                        : Shape{4, 1, true, 2, 8, MXA_RP_HOT};  // marketreplay (both): book in HBM; 256 queue slots (GOOG 2012-06-21 peaks at 113)
 }
 constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(cfg).sq; }
+// configurations whose replay / gym header (RpHdr: best levels, free-stack top, replay cursor, RL
+// state) is LDS-resident for a launch of the run / step kernel: the replay ladder's handlers read
+// and update it on every event (IBM x512 step 0.369 -> 0.363 ms).  Not rmsc03_rl, whose header
+// only DummyRL's events touch: there it cost the step kernel 1.88 -> 2.05 ms (r05 s1)
+constexpr bool rp_hdr_lds(int cfg) {
+  return cfg == MXA_CFG_MARKETREPLAY || cfg == MXA_CFG_MARKETREPLAY_RUNNER || cfg == MXA_CFG_MARKETREPLAY_TWAP;
+}
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)sq_lds(cfg) * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
          + 1024                                                                               // RNG stream windows
          + (size_t)lat_lds(cfg) * 8                                                           // exchange latency row
+         + (rp_hdr_lds(cfg) ? 256 : 0)                                                        // RpHdr (replay / gym)
 #ifdef MXA_QREG
          + 768  // batched-push scratch: slot table + staged keys
 #else

@@ -926,6 +926,11 @@ struct Eng {
   // entry, which from HBM is a dependent memory round trip on the event chain
   static constexpr int LATL = BUILD ? 0 : mxa_cfg::lat_lds(CFG);
   LDSP double* latl;
+  // the replay / gym header (RpHdr) for a launch of the run / step kernel (RPH): every replay
+  // handler reads and updates it on its dependent chain.  load() copies it in and save() out;
+  // the builder (BUILD) writes the env block's copy directly and never touches this one
+  static constexpr bool RPH = !BUILD && mxa_cfg::rp_hdr_lds(CFG);
+  LDSP RpHdr* rhl;
   LDSP i32* scr;     // [64] rank -> queue slot, then [64] u64 staged keys (MXA_QREG)
   LDSP u32* rwin;    // [4][64] output windows of the global RNG streams (RSt::lw)
 
@@ -966,6 +971,7 @@ struct Eng {
     hotrec = (LDSP u64*)(lds + LDS_Q + 512);
 #endif
     latl = (LDSP double*)(hotrec + mxa_cfg::shape(CFG).hot * 64);
+    rhl = (LDSP RpHdr*)(latl + mxa_cfg::lat_lds(CFG));
   }
 
   // ---------------- env block accessors
@@ -3629,11 +3635,16 @@ struct Eng {
   // (count, head, tail, total qty); entries come from a per-env pool; the live entries of one
   // order id are chained so cancel/modify find them without walking a level.
   // =====================================================================================
-  // the replay / gym header (best levels, free-stack top, replay cursor, RL state) in the env
-  // block.  (Round 4 moved it to LDS for the launch, load() / save() copying it: the replay step
-  // kernel then faulted on its first step while the same source with the header in HBM passed,
-  // a cause not found from the code; reverted)
-  DEV RpHdr* rh() { return (RpHdr*)(env + rx->L.off_rh); }
+  // the replay / gym header (best levels, free-stack top, replay cursor, RL state): the env
+  // block's copy (rh_g) is the one between launches and the builder's; a run / step launch works
+  // on the LDS copy (rhl, RPH).  Round 4's first LDS version faulted because the builder's save()
+  // copied the LDS header -- never loaded in a build launch, so whatever an earlier kernel left
+  // there -- over the header it had just written to the env block
+  DEV RpHdr* rh_g() { return (RpHdr*)(env + rx->L.off_rh); }
+  DEV auto rh() {
+    if constexpr (RPH) return rhl;
+    else return rh_g();
+  }
   DEV i32* lv_cnt(int s) { return (i32*)(env + rx->L.off_lvc) + (size_t)s * U(rx->L.P); }
   DEV i32* lv_head(int s) { return (i32*)(env + rx->L.off_lvh) + (size_t)s * U(rx->L.P); }
   DEV i32* lv_tail(int s) { return (i32*)(env + rx->L.off_lvt) + (size_t)s * U(rx->L.P); }
@@ -3661,7 +3672,7 @@ struct Eng {
   // SIZE > 0 record has been handled, in an earlier episode of the process or this one
   DEV i64 rp_skip_used(i64 c) {
     const i32 n = U(rx->nuid);
-    RpHdr* R = rh();
+    auto R = rh();
     const i32 hi = max(U(R->tape_hi), U(R->mr_done));
     for (;;) {
       i32 lo = 0, h2 = n - 1, f = -1;
@@ -3720,7 +3731,7 @@ struct Eng {
   }
   // enterOrder (OrderBook.py:256-282): append to the level FIFO
   DEV void rp_enter(i32 oid, i32 d, i32 agent, int buy, i32 qty, i32 price) {
-    RpHdr* R = rh();
+    auto R = rh();
     const int side = buy ? 0 : 1;
     const i32 x = price - U(rx->L.pmin);
     const bool xin = x >= 0 && x < U(rx->L.P);
@@ -3734,7 +3745,7 @@ struct Eng {
   // store waits for the store as well)
   DEV void rp_enter_pf(i32 oid, i32 d, i32 agent, int buy, i32 qty, i32 price, i32 x, i32 top, i32 tl, i32 cnt,
                        i32 nl, i32 bs, i32 hd, i64 lq) {
-    RpHdr* R = rh();
+    auto R = rh();
     const int side = buy ? 0 : 1;
     if (x < 0 || x >= U(rx->L.P)) {
       fail(ERR_RP_PRICE);
@@ -3795,12 +3806,19 @@ struct Eng {
     const u64 ob = lane < 10 ? o_w + 4 * lane : lane < 12 ? o_q + 4 * (lane - 10) : lane == 12 ? o_c
                    : lane == 13 ? o_rh + offsetof(RpHdr, free_top) : lane == 14 ? o_rh + offsetof(RpHdr, nlev) + 4 * side
                                 : o_rh + 4 * side;
-    return gather1((const i32*)(env + ob), lane < 16);
+    if constexpr (RPH) {  // the header words from its LDS copy, beside the gathered load
+      i32 v = gather1((const i32*)(env + ob), lane < 13);
+      const int hw = lane == 13 ? (int)(offsetof(RpHdr, free_top) / 4) : lane == 14 ? 2 + side : side;
+      const i32 hv = ((const LDSP i32*)rhl)[hw];
+      return lane >= 13 && lane < 16 ? hv : v;
+    } else {
+      return gather1((const i32*)(env + ob), lane < 16);
+    }
   }
   // remove entry e (level x of `side`, its words gathered in g) from the book; returns the
   // side's best level after the removal
   DEV i32 rp_unlink(int side, i32 x, i32 e, i32 g) {
-    RpHdr* R = rh();
+    auto R = rh();
     RpEntry* E = pool();
     const i32 q = rdli(g, 1), d = rdli(g, 3), p = rdli(g, 6), n = rdli(g, 7), ip = rdli(g, 8), in = rdli(g, 9);
     const i32 cnt = rdli(g, 12), top = rdli(g, 13), nl = rdli(g, 14), b = rdli(g, 15);
@@ -3843,7 +3861,7 @@ struct Eng {
     RPCHK(d >= 0 && d < U(rx->L.D), "rp_handle_limit dense", d);
     if constexpr (BLOG) bl_put(cur, price, buy ? qty : -qty);
     const i32 hep = h.epoch;
-    RpHdr* R = rh();
+    auto R = rh();
     RpEntry* E = pool();
     const i32 pmin = U(rx->L.pmin);
     const int side = buy ? 0 : 1;
@@ -3868,8 +3886,14 @@ struct Eng {
                      : lane == 22         ? o_c + px
                      : lane == 23         ? o_t + px
                                           : o_q + 2 * px + 4 * (lane - 24);
-      pf = gather1((const i32*)(env + ob),
-                   lane < MXA_ID_EPOCHS || (lane >= 16 && lane < 22) || (xin && lane >= 22 && lane < 26));
+      if constexpr (RPH) {  // lanes 16-20 from the header's LDS copy (best, nlev, free_top)
+        pf = gather1((const i32*)(env + ob), lane < MXA_ID_EPOCHS || lane == 21 || (xin && lane >= 22 && lane < 26));
+        const i32 hv = ((const LDSP i32*)rhl)[lane >= 16 && lane < 21 ? lane - 16 : 0];
+        if (lane >= 16 && lane < 21) pf = hv;
+      } else {
+        pf = gather1((const i32*)(env + ob),
+                     lane < MXA_ID_EPOCHS || (lane >= 16 && lane < 22) || (xin && lane >= 22 && lane < 26));
+      }
     }
     // history[0][order_id] = ... (OrderBook.py:51-60): the id's distinct entry epochs, newest
     // first, one per lane (lanes < MXA_ID_EPOCHS).  Stored after the handler's loads (below):
@@ -4049,7 +4073,7 @@ struct Eng {
   // QUERY_SPREAD reply with `depth` levels (ExchangeAgent.py:215-245): level-1 price/qty,
   // level-2 prices and the level counts (w6/w7 = price2 | count << 20)
   DEV void rp_spread(const Msg& m, bool closed) {
-    RpHdr* R = rh();
+    auto R = rh();
     const i32 pmin = U(rx->L.pmin);
     i32 depth = (i32)m.w[1];
     i32 nb = U(R->nlev[0]), na = U(R->nlev[1]);
@@ -4228,7 +4252,7 @@ struct Eng {
   }
   DEV void rl_wakeup() {
     if (!ta_wakeup()) return;
-    RpHdr* R = rh();
+    auto R = rh();
     // first horizon time strictly after now
     i32 k = cur < PC.rl_h0 ? 0 : (i32)((cur - PC.rl_h0) / PC.rl_hstep) + 1;
     i32 trade = U(R->rl_trade);
@@ -4246,7 +4270,7 @@ struct Eng {
   }
   // ABIDESEnvMetrics.addLOB: deque(maxlen=100), newest first
   DEV void rl_add_lob(const Msg& m) {
-    RpHdr* R = rh();
+    auto R = rh();
     const i32 nb = (i32)(m.w[6] >> 20), na = (i32)(m.w[7] >> 20);
     const int dnone = !m_hasdata(m);
     i32 ph = U(R->ph_n), cnt = U(R->m_cnt), hd = U(R->m_head);
@@ -4278,7 +4302,7 @@ struct Eng {
   DEV void rl_receive(const Msg& m) {
     PROF_SCOPE(89);
     ta_receive(m, AG_DUMMYRL);
-    RpHdr* R = rh();
+    auto R = rh();
     const u32 k = m_kind(m);
     if (k == MK_EXECUTED) {  // ExecutionAgent.handleOrderExecution (the DummyRL override is misspelt)
       i64 ex = U(R->rl_exec) + (i32)m.w[2];
@@ -4326,7 +4350,7 @@ struct Eng {
   }
   // DummyRL.get_observation (dummy_rl:291-312): float64[9] into the replay header
   DEV void rl_observe() {
-    RpHdr* R = rh();
+    auto R = rh();
     const i64 fl = (cur / PC.rl_hstep) * PC.rl_hstep;  // currentTime.floor("30S")
     i32 rem = PC.rl_nh;
     if (fl >= PC.rl_h0 && (fl - PC.rl_h0) / PC.rl_hstep < PC.rl_nh) rem = PC.rl_nh - 1 - (i32)((fl - PC.rl_h0) / PC.rl_hstep);
@@ -4394,7 +4418,7 @@ struct Eng {
   // DummyRL.process_action + place_orders (dummy_rl:138-179), called by the step kernel
   DEV void rl_place_orders(const double* act) {
     PROF_SCOPE(90);
-    RpHdr* R = rh();
+    auto R = rh();
     rec_load(PC.first_rl);
     const double q0 = (double)PC.rl_quantity, q = q0;  // metrics.rem_quantity is never updated
     const double x = act[0], sum = 0.0 + act[1] + act[2];
@@ -4417,7 +4441,7 @@ struct Eng {
   }
   // GymKernel CANCEL_ORDER branch (GymKernel.py:244-249): get_reward (None), cancelAllOrders
   DEV void rl_kernel_cancel() {
-    RpHdr* R = rh();
+    auto R = rh();
     if (U(R->m_cnt) == 0 || U(R->ph_none)) {
       fail(ERR_RP_OBS);
       return;
@@ -4428,7 +4452,7 @@ struct Eng {
   }
   // GymKernel.terminateRunner -> ExecutionAgent.kernelStopping (execution_agent.py:45-58)
   DEV void rp_terminate() {
-    RpHdr* R = rh();
+    auto R = rh();
     if (U(R->finished)) return;
     R->finished = 1;
     if (U(R->rl_trade)) fail(ERR_RP_STOPPING);
@@ -4649,8 +4673,13 @@ struct Eng {
     u64* dst = (u64*)hdr();
     if (lane < (int)(sizeof(EnvHdr) / 8)) dst[lane] = src[lane];
   }
+  static constexpr int RPW = (int)(sizeof(RpHdr) / 8);
+  static_assert(sizeof(RpHdr) % 8 == 0 && RPW <= 32, "RpHdr: one u64 per lane, 256 LDS bytes");
+  static_assert(!RPH || RP || GYM, "an LDS replay header needs the replay / gym context");
   DEV void load() {
     hdr_from_global();
+    if constexpr (RPH)
+      if (lane < RPW) ((LDSP u64*)rhl)[lane] = ((const u64*)rh_g())[lane];
     for (int hs = 0; hs < HOT; hs++) hotrec[hs * 64 + lane] = agent_ptr(hot_agent(hs))[lane];
     for (int i = lane; i < LATL; i += 64) latl[i] = lat()[i];
     SavedEvent* sq = (SavedEvent*)(env + PC.L.off_q);
@@ -4704,6 +4733,10 @@ struct Eng {
       so[j * 64 + lane] = o;
     }
     for (int hs = 0; hs < HOT; hs++) agent_ptr(hot_agent(hs))[lane] = hotrec[hs * 64 + lane];
+    if constexpr (RPH) {
+      wfence();
+      if (lane < RPW) ((u64*)rh_g())[lane] = ((const LDSP u64*)rhl)[lane];
+    }
     hdr_to_global();
   }
 
@@ -5811,7 +5844,7 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
     if (g.status == ST_DONE) g.rp_terminate();
   }
   g.save();
-  RpHdr* R = g.rh();
+  auto R = g.rh();
   if (g.lane < 9) obs[9 * (size_t)env + g.lane] = R->obs[g.lane];
   u64 key;
   u32 sq;
