@@ -273,6 +273,25 @@ typedef struct {
  * fills its log stops with error ERR_BOOK_LOG_FULL (20).  The exchange's event runs (batched
  * LIMIT/CANCEL handling) are off while logging. */
 int mxa_set_book_log(mxa_handle* h, int32_t cap);
+/* the exchange's own log, ExchangeAgent.log (agent/ExchangeAgent.py:39 log_events=True), which
+ * Agent.kernelTerminating writes as EXCHANGE_AGENT.bz2 (agent/Agent.py:86-95), rides in the same
+ * stream when on != 0 (kept across mxa_reset; needs mxa_set_book_log first).  Codes, price = code +
+ * message kind (MK_* = the trace kinds):
+ *   MXA_BL_EV_RX    a message the exchange logs on receipt (ExchangeAgent.py:162-167): qty = sender;
+ *                   LIMIT_ORDER / CANCEL_ORDER only when the config's exchange has log_orders
+ *   MXA_BL_EV_NT    ORDER_ACCEPTED / ORDER_CANCELLED / ORDER_EXECUTED sent, with log_orders
+ *                   (ExchangeAgent.py:477-482): qty = recipient
+ *   MXA_BL_EV_PLACE an order created (LimitOrder.time_placed), with log_orders: t, qty = order id
+ * An RX record of LIMIT_ORDER / CANCEL_ORDER and every NT record is followed by its order:
+ * t = fill_price << 32 | (uint32)order_id (fill_price INT32_MIN: None), price = limit price,
+ * qty = quantity (> 0 buy, < 0 sell).  The BEST_BID / BEST_ASK / LAST_TRADE rows follow from the
+ * limit-order records (mxabides.booklog.exchange_log rebuilds the frame).  Replaces the
+ * reference's in-process log list (Agent.logEvent, Agent.py:97-110). */
+#define MXA_BL_EV_RX (-2147483647 - 1 + 256)
+#define MXA_BL_EV_NT (MXA_BL_EV_RX + 256)
+#define MXA_BL_EV_PLACE (MXA_BL_EV_RX + 512)
+#define MXA_BL_EV_END (MXA_BL_EV_RX + 768)
+int mxa_set_exchange_log(mxa_handle* h, int32_t on);
 /* env's records: min(total, cap, log capacity) are written to out, the total to *n (above the
  * log capacity: the log overflowed) */
 int mxa_read_book_log(mxa_handle* h, int32_t env, mxa_book_rec* out, int64_t cap, int64_t* n);

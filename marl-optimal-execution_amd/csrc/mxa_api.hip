@@ -33,6 +33,11 @@ __global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int 
 }
 
 // Kernel.runner's stopTime of every env (EnvHdr::t_stop; 0 = the config's own)
+// the exchange-log switch of every env (EnvHdr::exlog)
+__global__ void mxa_set_exlog_kernel(char* base, uint64_t stride, int n, int32_t on) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ((EnvHdr*)(base + (size_t)i * stride))->exlog = on;
+}
 __global__ void mxa_set_stop_kernel(char* base, uint64_t stride, int n, int64_t t_stop) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) ((EnvHdr*)(base + (size_t)i * stride))->t_stop = t_stop;
@@ -180,6 +185,7 @@ struct mxa_handle {
   // GymKernel handles: mxa_reset continues Order.order_id / Order._order_ids of the previous
   // episode (one process running consecutive ABIDESEnv episodes)
   bool persist_ids = false;
+  int32_t exlog = 0;   // mxa_set_exchange_log: the exchange's own log rides in the book-update log
   int64_t t_stop = 0;  // mxa_set_stop_time: Kernel.runner's stopTime override (0: the config's)
   int32_t tcap_arg() const { return (parity_hash || P.L.trace_cap > 0) ? P.L.trace_cap : -1; }
   // the run kernel of the current settings: the log variant, the instrumented one, or (hash off,
@@ -657,6 +663,12 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
   h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_seeds, dm,
            h->d_ctx);
   HIPCHK(h, hipGetLastError());
+  if (h->exlog) {  // the build cleared the header: the switch outlives resets
+    const int n = h->P.n_envs;
+    hipLaunchKernelGGL(mxa_set_exlog_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env,
+                       h->P.L.env_stride, n, h->exlog);
+    HIPCHK(h, hipGetLastError());
+  }
   if (h->t_stop > 0) {  // the build cleared the header: the override outlives resets
     const int n = h->P.n_envs;
     hipLaunchKernelGGL(mxa_set_stop_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env,
@@ -767,11 +779,29 @@ int mxa_set_book_log(mxa_handle* h, int32_t cap) {
   return MXA_OK;
 }
 
+// the exchange's own log (ExchangeAgent.log -> EXCHANGE_AGENT.bz2) in the book-update log: the
+// log-variant kernels write its records (mxa_layout.h BL_EV_*) while EnvHdr::exlog is set
+int mxa_set_exchange_log(mxa_handle* h, int32_t on) {
+  if (!h || h->gym || !h->run_log || on < 0 || on > 1) return MXA_EINVAL;
+  if (on && !h->d_blog) return MXA_EINVAL;  // it rides in the book-update log: mxa_set_book_log first
+  HIPCHK(h, hipSetDevice(h->device));
+  h->exlog = on;
+  const int n = h->P.n_envs;
+  hipLaunchKernelGGL(mxa_set_exlog_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env, h->P.L.env_stride,
+                     n, on);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return MXA_OK;
+}
+
 int mxa_read_book_log(mxa_handle* h, int32_t env, mxa_book_rec* out, int64_t cap, int64_t* n) {
   if (!h || env < 0 || env >= h->P.n_envs || !n || cap < 0 || (cap > 0 && !out)) return MXA_EINVAL;
   static_assert(sizeof(mxa_book_rec) == sizeof(BlRec) && offsetof(mxa_book_rec, qty) == offsetof(BlRec, qty),
                 "mxa_book_rec mirrors BlRec");
   static_assert((int)MXA_BL_FUNDAMENTAL == (int)BL_FUNDAMENTAL, "f_log record tag");
+  static_assert((int)MXA_BL_EV_RX == (int)BL_EV_RX && (int)MXA_BL_EV_NT == (int)BL_EV_NT &&
+                    (int)MXA_BL_EV_PLACE == (int)BL_EV_PLACE && (int)MXA_BL_EV_END == (int)BL_EV_END,
+                "exchange-log record codes");
   HIPCHK(h, hipSetDevice(h->device));
   EnvHdr hd;
   HIPCHK(h, hipMemcpyAsync(&hd, h->d_env + (size_t)env * h->P.L.env_stride, sizeof(hd), hipMemcpyDeviceToHost,

@@ -185,6 +185,7 @@ constexpr void base_params(MxaParams& P) {
 constexpr void params_rmsc03(MxaParams& P) {
   base_params(P);
   P.config = MXA_CFG_RMSC03;
+  P.ex_log_orders = 1;  // config/rmsc03.py:102
   P.mkt_close = 9 * HOUR + 45 * MIN;
   P.start = P.mkt_open;
   P.stop = P.mkt_close + MIN;
@@ -316,6 +317,7 @@ constexpr void params_hist_fund(MxaParams& P, bool diverse) {
 constexpr void params_sparse_zi(MxaParams& P, bool big) {
   base_params(P);
   P.config = big ? MXA_CFG_SPARSE_ZI_1000 : MXA_CFG_SPARSE_ZI_100;
+  P.ex_log_orders = big ? 0 : 1;  // sparse_zi_100.py:187 log_orders=True; sparse_zi_1000.py:183 the -o option (off)
   P.mkt_close = 16 * HOUR;
   P.start = 0;
   P.stop = 17 * HOUR;
@@ -369,6 +371,7 @@ constexpr void params_sparse_zi(MxaParams& P, bool big) {
 constexpr void params_marketreplay(MxaParams& P) {
   base_params(P);
   P.config = MXA_CFG_MARKETREPLAY;
+  P.ex_log_orders = 1;  // config/marketreplay.py:77, agent_config.py:54
   P.mkt_close = 16 * HOUR;
   P.start = 0;
   P.stop = 16 * HOUR + 10 * MIN;
@@ -450,6 +453,7 @@ constexpr void params_rmsc03_rl(MxaParams& P) {
 constexpr void params_rmsc01(MxaParams& P) {
   base_params(P);
   P.config = MXA_CFG_RMSC01;
+  P.ex_log_orders = 0;  // config/rmsc01.py:84
   P.mkt_close = 16 * HOUR;
   P.start = P.mkt_open;
   P.stop = 16 * HOUR + MIN;
@@ -500,6 +504,7 @@ constexpr void params_rmsc01(MxaParams& P) {
 constexpr void params_rmsc02(MxaParams& P) {
   params_rmsc01(P);
   P.config = MXA_CFG_RMSC02;
+  P.ex_log_orders = 1;  // config/rmsc02.py:84
   P.start = 0;
   P.stop = 17 * HOUR;
   P.lat_mode = 1;
@@ -520,6 +525,7 @@ constexpr void params_rmsc02(MxaParams& P) {
 constexpr void params_obi_rmsc02(MxaParams& P) {
   params_rmsc02(P);
   P.config = MXA_CFG_OBI_RMSC02;
+  P.ex_log_orders = 0;  // config/obi_rmsc02.py:86
   P.zi_group_count[0] = 89;
   P.n_zi = 89;
   P.first_hbl = 0;
@@ -586,6 +592,7 @@ constexpr void layout(MxaParams& P, int cfg) {
 constexpr void params_value_noise(MxaParams& P) {
   base_params(P);
   P.config = MXA_CFG_VALUE_NOISE;
+  P.ex_log_orders = 0;  // config/value_noise.py:177 the -o option (off)
   P.mkt_close = 10 * HOUR + 30 * MIN;
   P.start = 0;
   P.stop = 17 * HOUR;

@@ -1540,6 +1540,9 @@ struct Eng {
   // slot table goes through LDS, each message lane writes its own slot, and every lane rescans
   // its slots once for the whole batch instead of a wave-serial push per message.
   DEV void q_push_lanes(bool act, u64 key, const Msg& m) {
+    if constexpr (BLOG && PC.ex_log_orders) {  // a batch of new orders: their time_placed (send_ex)
+      if (h.exlog && m_kind(m) == MK_LIMIT) bl_put_lanes(act, cur, BL_EV_PLACE, (i32)m.w[1]);
+    }
     const u64 ab = bal(act);
     const int n = __popcll(ab);
     if (n == 0) return;
@@ -2120,6 +2123,12 @@ struct Eng {
     // ExchangeAgent.sendMessage: ORDER_* notifications carry the pipeline delay
     u32 k = m_kind(m);
     i64 d = (k == MK_ACCEPTED || k == MK_CANCELLED || k == MK_EXECUTED) ? PC.ex_pipeline : 0;
+    // ... and, with log_orders, are logged with their order (ExchangeAgent.py:477-482)
+    if constexpr (BLOG && PC.ex_log_orders)
+      if (h.exlog && (k == MK_ACCEPTED || k == MK_CANCELLED || k == MK_EXECUTED)) {
+        bl_put(cur, BL_EV_NT + (i32)k, recipient);
+        exl_order(m, k == MK_EXECUTED ? (i32)m.w[4] : (i32)BL_FILL_NONE);
+      }
     send(recipient, m, d);
   }
   // ---------------- OrderBook.history as a ring of per-order records (HBL configurations)
@@ -2158,6 +2167,28 @@ struct Eng {
     }
     h.blog_n = n + 1;
     if (n >= blog_cap) fail(ERR_BOOK_LOG_FULL);
+  }
+  // one record per active lane, in lane order (a batched push of orders)
+  DEV void bl_put_lanes(bool act, i64 t, i32 price, i32 qty) {
+    const u64 ab = bal(act);
+    const i32 n = h.blog_n, c = __popcll(ab);
+    if (c == 0) return;
+    const i32 r = (i32)__builtin_amdgcn_mbcnt_hi((u32)(ab >> 32), __builtin_amdgcn_mbcnt_lo((u32)ab, 0u));
+    if (act && n + r < blog_cap) {
+      BlRec x;
+      x.t = t;
+      x.price = price;
+      x.qty = qty;
+      blog[n + r] = x;
+    }
+    h.blog_n = n + c;
+    if (n + c > blog_cap) fail(ERR_BOOK_LOG_FULL);
+  }
+  // the exchange's own log (ExchangeAgent.log, EXCHANGE_AGENT.bz2; mxa_set_exchange_log): the order
+  // record that follows a LIMIT_ORDER / CANCEL_ORDER or an ORDER_* notification row (mxa_layout.h)
+  DEV void exl_order(const Msg& m, i32 fill) {
+    const i32 q = (i32)m.w[2];
+    bl_put((i64)(((u64)(u32)fill << 32) | (u64)m.w[1]), (i32)m.w[3], m_buy(m) ? q : -q);
   }
   DEV void handle_limit(i32 oid, i32 agent, int is_buy, i32 qty, i32 price) {
     PROF_SCOPE(66);
@@ -2375,6 +2406,17 @@ struct Eng {
         return;
       }
     }
+    // the exchange's log (ExchangeAgent.py:162-167): order messages with their order, and only
+    // with log_orders; every other message with its sender
+    if constexpr (BLOG) {
+      if (h.exlog) {
+        const bool ord = k == MK_LIMIT || k == MK_CANCEL;
+        if (!ord || PC.ex_log_orders) {
+          bl_put(cur, BL_EV_RX + (i32)k, sender);
+          if (ord) exl_order(m, (i32)BL_FILL_NONE);
+        }
+      }
+    }
     if constexpr (RP) {
       if (k == MK_LIMIT) return rp_handle_limit(m);
       if (k == MK_CANCEL) return rp_cancel(m);
@@ -2479,6 +2521,10 @@ struct Eng {
   // ---------------- TradingAgent (TradingAgent.py)
   DEV void send_ex(Msg m) {
     m.w[0] = (m.w[0] & 0xFFFFu) | ((u32)cur_agent << 16);
+    if constexpr (BLOG && PC.ex_log_orders) {  // an order created now: its time_placed (LimitOrder(...))
+      const u32 k = m_kind(m);
+      if (h.exlog && (k == MK_LIMIT || k == MK_MODIFY)) bl_put(cur, BL_EV_PLACE, (i32)m.w[1]);
+    }
     send(0, m, 0);
   }
   DEV void get_spread(int depth) {

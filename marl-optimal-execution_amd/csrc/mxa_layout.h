@@ -123,7 +123,8 @@ typedef struct {
   int64_t ex_comp_delay;         // exchange's current computation delay
   int32_t max_q, max_book;       // capacity high-water marks (diagnostics)
   double o_th2;                  // oracle fund_vol ** 2 (glibc pow, evaluated at build)
-  int32_t blog_fin, pad3;        // book-update log: records after the last kernelStopping pass
+  int32_t blog_fin;              // book-update log: records after the last kernelStopping pass
+  int32_t exlog;                 // the exchange's own log rides in the book-update log (mxa_set_exchange_log)
   int64_t ob_last_update;        // OrderBook.last_update_ts (market-data configs)
   int32_t nsub, has_last_update; // ExchangeAgent.subscription_dict entries; last_update_ts not None
   uint32_t md_seq;               // MARKET_DATA messages sent (their snapshot-slot tags)
@@ -167,6 +168,17 @@ enum { BL_FUND_LO = -2147483647, BL_FUND_HI = -2147483646 };
 // order, so the level's volume changes by qty = new quantity - the old head's; price =
 // -(level price | BL_MODIFY | side << 29), side 0 bids (prices < 2^20 on the replay tape)
 #define BL_MODIFY (1 << 30)
+// the exchange's own log (ExchangeAgent.log, written as EXCHANGE_AGENT.bz2 by Agent.kernelTerminating,
+// agent/Agent.py:86-95) in the same stream, with mxa_set_exchange_log; price = code + message kind:
+//  BL_EV_RX    a message the exchange logs as it receives it (ExchangeAgent.py:162-167): qty = sender
+//  BL_EV_NT    an ORDER_ACCEPTED / _CANCELLED / _EXECUTED it sends with log_orders (:477-482): qty = recipient
+//  BL_EV_PLACE an order created (LimitOrder(...), its time_placed): t = currentTime, qty = order id
+// An RX record of LIMIT_ORDER / CANCEL_ORDER (written only with log_orders) and every NT record is
+// followed by its order: t = fill_price << 32 | (u32)order_id (fill_price INT32_MIN: None), price =
+// limit price, qty = quantity (> 0 buy, < 0 sell).  Codes lie below every modifyOrder record while
+// prices stay below 2^29 - 768
+enum { BL_EV_RX = -2147483647 - 1 + 256, BL_EV_NT = BL_EV_RX + 256, BL_EV_PLACE = BL_EV_RX + 512, BL_EV_END = BL_EV_RX + 768 };
+#define BL_FILL_NONE (-2147483647 - 1)
 
 // one event slot as saved between launches (and payload as pushed)
 typedef struct {
@@ -334,7 +346,8 @@ typedef struct {
   int32_t lat_mode, noise_len;   // 0 zero, 1 matrix (+uniform noise index), 2 cubic model
   double jitter, clip, unit;
   int64_t ex_pipeline, ex_comp;
-  int32_t stream_history, pad0;
+  int32_t stream_history;
+  int32_t ex_log_orders;  // ExchangeAgent(log_orders=...) of the config script (ExchangeAgent.py:163-165, 481-482)
   double o_rbar, o_kappa, o_fundvol, o_lambda, o_msmean, o_msvar;
   int64_t starting_cash;
   int32_t first_zi, n_zi, first_noise, n_noise, first_value, n_value, first_mm, n_mm, first_mom, n_mom;

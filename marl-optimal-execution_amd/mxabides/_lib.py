@@ -80,7 +80,7 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log", "mxa_write_records", "mxa_set_id_persistence",
            "mxa_read_counters", "mxa_create_hist", "mxa_create_replay_runner",
            "mxa_set_stop_time", "mxa_run_until", "mxa_create_replay_twap", "mxa_create_params", "mxa_set_mm_params",
-           "mxa_mm_defaults", "mxa_resident_envs"]
+           "mxa_mm_defaults", "mxa_resident_envs", "mxa_set_exchange_log"]
 COUNTER_WORDS = 34  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
@@ -130,7 +130,8 @@ def load():
                        ("mxa_set_stop_time", [P, I64]), ("mxa_run_until", [P, I64, P]),
                        ("mxa_create_replay_twap", [P, P, P, P, P, I32, I32, I32, I32, I32, ctypes.POINTER(P)]),
                        ("mxa_create_params", [I32, I32, P, P, I32, I32, ctypes.POINTER(P)]),
-                       ("mxa_set_mm_params", [P, P]), ("mxa_resident_envs", [P])):
+                       ("mxa_set_mm_params", [P, P]), ("mxa_resident_envs", [P]),
+                       ("mxa_set_exchange_log", [P, I32])):
         if hasattr(L, name):  # (older single-configuration A/B builds lack them; libmxa.so has all)
             getattr(L, name).argtypes = args
     L.mxa_write_rl_state.argtypes = [P, P]

@@ -19,6 +19,12 @@ The same stream carries SparseMeanRevertingOracle.f_log (util/oracle/SparseMeanR
 63, 122): one record per fundamental value computed (price BL_FUNDAMENTAL, qty the value), the
 series ExchangeAgent.kernelTerminating writes as fundamental_<symbol>.bz2 (ExchangeAgent.py:111-117).
 
+With mxa_set_exchange_log the stream also carries the exchange's own log, ExchangeAgent.log
+(agent/Agent.py:97-110), written by Agent.kernelTerminating as EXCHANGE_AGENT.bz2 (Agent.py:86-95):
+a record per message the exchange logs on receipt (ExchangeAgent.py:162-167), per ORDER_*
+notification it sends with log_orders (:477-482), and per order created (its time_placed);
+exchange_log rebuilds the rows with the BEST_BID / BEST_ASK / LAST_TRADE rows in their place.
+
 Rows are kept in one flat int64 array, the format the CPU oracle writes too:
     t, n, executed quantity, average trade price (0 without an execution),
     then n (price, volume) pairs: bids best-first (negative volumes), then asks best-first.
@@ -31,6 +37,18 @@ REC_DTYPE = np.dtype([("t", "<i8"), ("price", "<i4"), ("qty", "<i4")])
 BL_FUNDAMENTAL = -(1 << 31)
 BL_FUND_LO, BL_FUND_HI = -(1 << 31) + 1, -(1 << 31) + 2  # ExternalFileOracle f_log value words
 BL_MODIFY = 1 << 30  # modifyOrder on the replay book: price -(p | BL_MODIFY | side << 29), qty the volume change
+# the exchange's own log (include/mxa.h MXA_BL_EV_*): price = code + message kind
+BL_EV_RX = -(1 << 31) + 256
+BL_EV_NT = BL_EV_RX + 256
+BL_EV_PLACE = BL_EV_RX + 512
+BL_EV_END = BL_EV_RX + 768
+FILL_NONE = -(1 << 31)
+# message kinds (the trace's, tests/golden/gen_fixtures.py KIND) by the msg names the log holds
+KIND_NAMES = {1: "WHEN_MKT_OPEN", 2: "WHEN_MKT_CLOSE", 5: "QUERY_SPREAD", 7: "QUERY_LAST_TRADE",
+              9: "QUERY_TRANSACTED_VOLUME", 11: "LIMIT_ORDER", 12: "CANCEL_ORDER", 13: "MODIFY_ORDER",
+              14: "ORDER_ACCEPTED", 15: "ORDER_EXECUTED", 16: "ORDER_CANCELLED", 21: "QUERY_ORDER_STREAM",
+              23: "MARKET_DATA_SUBSCRIPTION_REQUEST", 24: "MARKET_DATA_SUBSCRIPTION_CANCELLATION"}
+K_LIMIT, K_CANCEL = 11, 12
 R_BAR = 100000.0           # SparseMeanRevertingOracle r_bar of every plain config (a float)
 MKT_OPEN_NS = (9 * 60 + 30) * 60 * 10**9
 SESSION_DATE = "2019-06-28"  # the plain configs' simulated date (abides.py -d / config defaults)
@@ -38,10 +56,21 @@ SESSION_DATE = "2019-06-28"  # the plain configs' simulated date (abides.py -d /
 FORBIDDEN_QUOTES = (0, 19999900)
 
 
+def book_mask(rec):
+    """the records that change the book (limit orders, cancellations, modifyOrder): not f_log
+    records, not the exchange log's records nor the order records that follow them"""
+    p = np.asarray(rec, dtype=REC_DTYPE)["price"].astype(np.int64)
+    tagged = (p >= -(1 << 31)) & (p < BL_EV_END)  # f_log and exchange-log codes
+    has_order = ((p >= BL_EV_RX + K_LIMIT) & (p <= BL_EV_RX + K_CANCEL)) | ((p >= BL_EV_NT) & (p < BL_EV_PLACE))
+    follows = np.zeros(len(p), dtype=bool)
+    follows[1:] = has_order[:-1]
+    return ~tagged & ~follows
+
+
 def rows_from_records(rec):
     """Replay device records into flat book_log rows (format above)."""
     rec = np.asarray(rec, dtype=REC_DTYPE)
-    rec = rec[rec["price"] > BL_FUND_HI]  # f_log records (either oracle) carry no book change
+    rec = rec[book_mask(rec)]  # f_log and exchange-log records carry no book change
     vol = ({}, {})       # bids, asks: price -> resting volume
     px = ([], [])        # their prices, ascending
     out = []
@@ -126,6 +155,99 @@ def exchange_events(flat, symbol):
         if xq:
             ev.append((t, "LAST_TRADE", "{},${:0.4f}".format(xq, avg)))
     return ev
+
+
+def _order(r, agent, placed, symbol, date):
+    """the order a log row carries, as the jsons.dump stub of the fixtures sees it (vars(order):
+    util/order/LimitOrder.py:14-19, Order.py:11-33): time_placed in ns since midnight here"""
+    t, p, q = int(r["t"]), int(r["price"]), int(r["qty"])
+    oid = t & 0xFFFFFFFF
+    oid = oid - (1 << 32) if oid >= 1 << 31 else oid
+    fill = t >> 32
+    if oid not in placed:
+        raise ValueError("order %d of the exchange log was never placed in this log" % oid)
+    return {"agent_id": agent, "time_placed": placed[oid], "symbol": symbol, "quantity": abs(q),
+            "is_buy_order": q > 0, "order_id": oid, "fill_price": None if fill == FILL_NONE else fill,
+            "limit_price": p}
+
+
+def exchange_log(rec, symbol, agent_type="ExchangeAgent"):
+    """ExchangeAgent.log (Agent.logEvent rows, Agent.py:97-110) from a book-update stream written
+    with the exchange log on: [(EventTime ns since midnight or None, EventType, Event)].
+
+    Row order is the reference's: AGENT_TYPE (Agent.__init__, currentTime None); per received
+    message its row (ExchangeAgent.py:162-167: the sender, or with log_orders the order of a
+    LIMIT_ORDER / CANCEL_ORDER); within handleLimitOrder the ORDER_EXECUTED pairs and the
+    ORDER_ACCEPTED rows (sendMessage, :477-482) and then BEST_BID / BEST_ASK / LAST_TRADE
+    (OrderBook.py:112-141); cancelOrder's ORDER_CANCELLED.  Order Events are dicts in
+    vars(order) key order with time_placed in ns (jsons_dump_order serializes them)."""
+    rec = np.asarray(rec, dtype=REC_DTYPE)
+    p = rec["price"].astype(np.int64)
+    bm = book_mask(rec)
+    per_limit = [[]]
+    for t, xq, avg, pr, v in iter_rows(rows_from_records(rec)):
+        ev = []
+        bid = np.flatnonzero(v < 0)
+        ask = np.flatnonzero(v > 0)
+        if len(bid):
+            ev.append((t, "BEST_BID", "%s,%d,%d" % (symbol, pr[bid[0]], -v[bid[0]])))
+        if len(ask):
+            ev.append((t, "BEST_ASK", "%s,%d,%d" % (symbol, pr[ask[0]], v[ask[0]])))
+        if xq:
+            ev.append((t, "LAST_TRADE", "{},${:0.4f}".format(xq, avg)))
+        per_limit.append(ev)
+    per_limit = per_limit[1:]
+    rows = [(None, "AGENT_TYPE", agent_type)]
+    placed, pending, li, i, n = {}, [], 0, 0, len(rec)
+    while i < n:
+        pi, ti, qi = int(p[i]), int(rec["t"][i]), int(rec["qty"][i])
+        if BL_EV_NT <= pi < BL_EV_PLACE:  # a notification of the order being handled
+            rows.append((ti, KIND_NAMES[pi - BL_EV_NT], _order(rec[i + 1], qi, placed, symbol, None)))
+            i += 2
+            continue
+        rows += pending  # anything else: the last limit order's handling is over
+        pending = []
+        if BL_EV_RX <= pi < BL_EV_NT:
+            k = pi - BL_EV_RX
+            if k in (K_LIMIT, K_CANCEL):
+                rows.append((ti, KIND_NAMES[k], _order(rec[i + 1], qi, placed, symbol, None)))
+                i += 2
+                continue
+            rows.append((ti, KIND_NAMES[k], qi))
+        elif pi == BL_EV_PLACE:
+            placed[qi] = ti
+        elif bm[i] and pi > 0:  # a limit order: its BEST rows follow its notifications
+            pending = per_limit[li]
+            li += 1
+        i += 1
+    return rows + pending
+
+
+def jsons_dump_order(d, date=SESSION_DATE):
+    """js.dump(order, strip_privates=True) of jsons 0.8.8 (requirements.txt), restated from its
+    published serializers: the object's public attributes in __dict__ order, ints and bools as
+    they are, None kept, and time_placed (a pandas Timestamp, a datetime) as RFC 3339
+    '%Y-%m-%dT%H:%M:%S' with '.%f' when it has microseconds and the local UTC offset of a naive
+    datetime ('Z' on a UTC host).  PARITY UNPINNED: jsons is not importable here, so only the
+    fields (exchange_log's dicts) are checked against the reference, not this string form."""
+    import pandas as pd
+    out = dict(d)
+    ts = pd.Timestamp(date) + pd.Timedelta(int(d["time_placed"]), unit="ns")
+    pat = "%Y-%m-%dT%H:%M:%S" + (".%f" if ts.microsecond else "")
+    out["time_placed"] = ts.strftime(pat) + "Z"
+    return out
+
+
+def exchange_log_frame(rows, date=SESSION_DATE):
+    """pd.DataFrame(ExchangeAgent.log).set_index("EventTime") as Agent.kernelTerminating writes it
+    to EXCHANGE_AGENT.bz2 (Agent.py:86-95): EventTime NaT for AGENT_TYPE, order Events through
+    jsons_dump_order"""
+    import pandas as pd
+    base = pd.Timestamp(date)
+    ev = [jsons_dump_order(e, date) if isinstance(e, dict) else e for _, _, e in rows]
+    df = pd.DataFrame({"EventTime": [None if t is None else base + pd.Timedelta(t, unit="ns") for t, _, _ in rows],
+                       "EventType": [r[1] for r in rows], "Event": ev})
+    return df.set_index("EventTime")
 
 
 def exchange_events_frame(flat, symbol, date=SESSION_DATE):

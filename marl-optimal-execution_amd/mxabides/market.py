@@ -18,7 +18,7 @@ CHUNK_DEFAULT = 1 << 20
 
 class VecMarket:
     def __init__(self, config, seeds, device=0, trace_cap=0, book_log=0, symbol=None, fundamental=None,
-                 book_freq="config", tape=None, mm_params=None):
+                 book_freq="config", tape=None, mm_params=None, exchange_log=False):
         """book_log: records per env of the book-update log (0 off), the input of the exchange's
         order-book outputs (orderbook_snapshots, exchange_events; include/mxa.h
         mxa_set_book_log).  A limit order takes 2-4 records, a cancellation 1.
@@ -29,12 +29,17 @@ class VecMarket:
         tape: the LOBSTER tape (mxabides.tape.Tape) of marketreplay_runner, config/marketreplay.py
         (the seeds only count the envs there: nothing in that composition draws).
         mm_params: rmsc03 only: config/rmsc03.py's --mm-* options per env (configs.mm_params, one
-        record or one per env; include/mxa.h mxa_create_params)."""
+        record or one per env; include/mxa.h mxa_create_params).
+        exchange_log: the exchange's own log (ExchangeAgent.log, EXCHANGE_AGENT.bz2) rides in the
+        book-update log (include/mxa.h mxa_set_exchange_log; needs book_log)."""
         if config not in _lib.CONFIG_IDS:
             raise ValueError("unknown config %r (supported: %s)" % (config, sorted(_lib.CONFIG_IDS)))
         self.L = _lib.load()
         self.config = config
-        self.symbol = symbol_of(config, symbol, tape)
+        if symbol is not None:
+            symbol_of(config, symbol, tape)  # a fixed-symbol config refuses -t now, not at output time
+        self._symbol = symbol
+        self.tape = tape
         self.book_freq = BOOK_FREQ[config] if book_freq == "config" else book_freq
         self.seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
         self.n_envs = len(self.seeds)
@@ -78,6 +83,15 @@ class VecMarket:
         self.book_log_cap = int(book_log)
         if book_log:
             self._check(self.L.mxa_set_book_log(self._h, int(book_log)), "mxa_set_book_log")
+        self.exchange_log_on = False
+        if exchange_log:
+            self.set_exchange_log(True)
+
+    @property
+    def symbol(self):
+        """the outputs' ticker, resolved when an output needs it (a replay tape built in memory
+        may carry none; configs.symbol_of)"""
+        return symbol_of(self.config, self._symbol, self.tape)
 
     def _mm_array(self, p):
         p = np.asarray(p, dtype=MM_PARAMS_DTYPE).reshape(-1)
@@ -116,6 +130,14 @@ class VecMarket:
         restarts empty, so set it before the first launch of an episode."""
         self._check(self.L.mxa_set_book_log(self._h, int(cap)), "mxa_set_book_log")
         self.book_log_cap = int(cap)
+
+    def set_exchange_log(self, on=True):
+        """the exchange's own log (ExchangeAgent.log) in the book-update log, kept across resets
+        (include/mxa.h mxa_set_exchange_log); a handle with book_log only"""
+        if on and not self.book_log_cap:
+            raise ValueError("the exchange log rides in the book-update log: create with book_log")
+        self._check(self.L.mxa_set_exchange_log(self._h, 1 if on else 0), "mxa_set_exchange_log")
+        self.exchange_log_on = bool(on)
 
     def set_seeds(self, seeds):
         self.seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
@@ -338,6 +360,27 @@ class VecMarket:
         from .booklog import exchange_events_frame
         return exchange_events_frame(self.book_log_rows(env), self.symbol, self.date)
 
+    def exchange_log(self, env):
+        """ExchangeAgent.log of env (Agent.logEvent rows, Agent.py:97-110): [(EventTime ns since
+        midnight or None, EventType, Event)], order Events as dicts (mxabides.booklog.exchange_log)"""
+        from .booklog import exchange_log
+        if not self.exchange_log_on:
+            raise ValueError("created without exchange_log")
+        return exchange_log(self.book_log_records(env), self.symbol, agent_type_names(self.config)[0])
+
+    def exchange_log_frame(self, env):
+        """the DataFrame Agent.kernelTerminating writes to EXCHANGE_AGENT.bz2 (Agent.py:86-95)"""
+        from .booklog import exchange_log_frame
+        return exchange_log_frame(self.exchange_log(env), self.date)
+
+    def write_exchange_log(self, env, log_dir):
+        """log_dir/<exchange name without spaces>.bz2 as Kernel.writeLog pickles it
+        (Kernel.py:520-547): EXCHANGE_AGENT.bz2, or ExchangeAgent0.bz2 for an "Exchange Agent 0"."""
+        os.makedirs(log_dir, exist_ok=True)
+        path = os.path.join(log_dir, "%s.bz2" % agent_names(self.config)[0].replace(" ", ""))
+        self.exchange_log_frame(env).to_pickle(path, compression="bz2")
+        return path
+
     def orderbook_snapshots(self, env, wide_book=False):
         """ExchangeAgent.logOrderBookSnapshots' DataFrame with book_freq 0 (ORDERBOOK_<sym>_FULL)"""
         from .booklog import orderbook_full
@@ -357,8 +400,10 @@ class VecMarket:
     def write_logs(self, env, log_dir, wide_book=False):
         """env's run directory as the reference writes it at termination (Kernel.writeLog /
         writeSummaryLog, Kernel.py:520-565; ExchangeAgent.kernelTerminating, ExchangeAgent.py:106-126):
-        summary_log.bz2, fundamental_<sym>.bz2 and, with book_freq 0, ORDERBOOK_<sym>_FULL.bz2, each
-        a bz2-pickled DataFrame; with book_freq None no order-book file.  Returns the paths."""
+        summary_log.bz2, fundamental_<sym>.bz2, with book_freq 0 ORDERBOOK_<sym>_FULL.bz2 (with book_freq
+        None no order-book file) and, on a handle with the exchange log, the exchange's own log
+        (EXCHANGE_AGENT.bz2; Agent.kernelTerminating, Agent.py:86-95), each a bz2-pickled DataFrame.
+        Returns the paths."""
         if self.book_freq is not None and self.book_freq != 0:
             # "M" (rmsc01) goes through pd.date_range(..., closed="right"), which pandas 2 rejects,
             # and "all" (obi_rmsc02) is no pandas frequency: the reference raises in both
@@ -372,6 +417,8 @@ class VecMarket:
                 p = os.path.join(log_dir, "fundamental_%s.bz2" % self.symbol)
                 f.to_pickle(p, compression="bz2")
                 paths.append(p)
+        if self.exchange_log_on:
+            paths.append(self.write_exchange_log(env, log_dir))
         if self.book_freq == 0:
             paths.append(self.write_orderbook_log(env, log_dir, wide_book))
         return paths

@@ -337,6 +337,9 @@ struct ora_env {
     int64_t *blg, nblg, capblg;
     /* the device's record stream for the same run (mxa_book_rec: t, price, qty) */
     int64_t *blr, nblr, capblr;
+    /* the exchange's own log (ExchangeAgent.log, EXCHANGE_AGENT.bz2) in that stream
+     * (ora_set_exchange_log; include/mxa.h MXA_BL_EV_*), and the config's log_orders */
+    int exlog, ex_log_orders;
     int done, err;
     char errstr[160];
     int64_t order_counter;
@@ -532,6 +535,10 @@ static void blr_push(ora_env* e, int64_t t, int64_t price, int64_t qty);
 #define BL_FUND_LO (-2147483647)           /* ExternalFileOracle f_log: the value's low word */
 #define BL_FUND_HI (-2147483646)           /* ... and its high word */
 #define BL_MODIFY (1 << 30)                /* modifyOrder: -(price | BL_MODIFY | side << 29), volume delta */
+#define BL_EV_RX (-2147483647 - 1 + 256)    /* the exchange's log: a message it logs on receipt, qty = sender */
+#define BL_EV_NT (BL_EV_RX + 256)           /* ... an ORDER_* notification it sends (log_orders), qty = recipient */
+#define BL_EV_PLACE (BL_EV_RX + 512)        /* ... an order created (time_placed), qty = order id */
+#define BL_FILL_NONE (-2147483647 - 1)      /* an order record's fill_price None */
 /* compute_fundamental_at_timestamp (SMRO:88-125); f_log append at SMRO:122 */
 static double o_compute(ora_env* e, int64_t ts, double v_adj, int64_t pt, double pv) {
     int64_t d = ts - pt;
@@ -794,9 +801,22 @@ static void hist_shift(ora_env* e) {
     e->epoch_abs++;
 }
 
+/* the order a LIMIT_ORDER / CANCEL_ORDER row or an ORDER_* notification row of the exchange's log
+ * carries (js.dump(order, strip_privates=True)): t = fill_price << 32 | order id, price = limit
+ * price, qty = quantity signed by side (include/mxa.h MXA_BL_EV_*) */
+static void exl_order(ora_env* e, const msg_t* m, int64_t fill) {
+    blr_push(e, (int64_t)(((uint64_t)(uint32_t)(int32_t)fill << 32) | (uint32_t)(int32_t)m->oid), m->price,
+             m->is_buy ? m->qty : -m->qty);
+}
 static void ex_send(ora_env* e, int recipient, msg_t* m) {
-    /* ExchangeAgent.sendMessage: order-book notifications carry the pipeline delay */
-    int64_t d = (m->kind == K_ACCEPTED || m->kind == K_CANCELLED || m->kind == K_EXECUTED) ? e->ex_pipeline : 0;
+    /* ExchangeAgent.sendMessage: order-book notifications carry the pipeline delay, and with
+     * log_orders are logged with their order (ExchangeAgent.py:477-482) */
+    int note = m->kind == K_ACCEPTED || m->kind == K_CANCELLED || m->kind == K_EXECUTED;
+    int64_t d = note ? e->ex_pipeline : 0;
+    if (note && e->exlog && e->ex_log_orders) {
+        blr_push(e, e->cur, BL_EV_NT + m->kind, recipient);
+        exl_order(e, m, m->kind == K_EXECUTED ? m->fill : BL_FILL_NONE);
+    }
     k_send(e, 0, recipient, m, d);
 }
 
@@ -1125,6 +1145,15 @@ static void ex_receive(ora_env* e, const msg_t* m) {
             return;
         }
     }
+    /* Log order messages only with log_orders, every other message with its sender
+     * (ExchangeAgent.py:162-167) */
+    if (e->exlog) {
+        int ord = m->kind == K_LIMIT || m->kind == K_CANCEL;
+        if (!ord || e->ex_log_orders) {
+            blr_push(e, e->cur, BL_EV_RX + m->kind, m->sender);
+            if (ord) exl_order(e, m, BL_FILL_NONE);
+        }
+    }
     if (m->kind == K_MD_SUB_REQ || m->kind == K_MD_SUB_CANCEL) update_subscription(e, m);
     switch (m->kind) {
     case K_WHEN_OPEN_REQ:
@@ -1214,6 +1243,10 @@ static void ex_receive(ora_env* e, const msg_t* m) {
 /* --------------------------- TradingAgent --------------------------------- */
 static void ta_send_ex(ora_env* e, agent_t* a, msg_t* m) {
     m->sender = a->id;
+    /* an order created now (LimitOrder(agent, currentTime, ...)): its time_placed, for the
+     * exchange's log rows that carry it */
+    if (e->exlog && e->ex_log_orders && (m->kind == K_LIMIT || m->kind == K_MODIFY))
+        blr_push(e, e->cur, BL_EV_PLACE, m->oid);
     k_send(e, a->id, 0, m, 0);
 }
 static void get_spread(ora_env* e, agent_t* a, int depth) {
@@ -3482,6 +3515,17 @@ void ora_set_book_log(ora_env* e, int on) {
      * the open lies inside the series (the device writes it at its first logged launch) */
     if (on && e->efo && e->pops == 0 && e->ex_open >= g_fs_t[0] && e->ex_open <= g_fs_t[g_fs_n - 1])
         efo_log(e, e->ex_open, efo_price(e->ex_open));
+}
+/* the exchange's own log in the record stream (include/mxa.h mxa_set_exchange_log); log_orders is
+ * the config script's ExchangeAgent(log_orders=...) */
+void ora_set_exchange_log(ora_env* e, int on) {
+    static const char* lo[] = {"rmsc03", "sparse_zi_100", "rmsc02", "random_fund_value", "random_fund_diverse",
+                               "hist_fund_value", "hist_fund_diverse", "marketreplay", "marketreplay_runner",
+                               "marketreplay_twap", "rmsc03_sbmm", "rmsc03_sbmm_poll", NULL};
+    e->exlog = on;
+    e->ex_log_orders = 0;
+    for (int i = 0; lo[i]; i++)
+        if (strcmp(e->config, lo[i]) == 0) e->ex_log_orders = 1;
 }
 int64_t ora_book_records(const ora_env* e, int64_t* buf, int64_t cap) {
     if (buf) memcpy(buf, e->blr, sizeof(int64_t) * (size_t)(cap < e->nblr ? cap : e->nblr));

@@ -64,6 +64,8 @@ int64_t ora_book_log(const ora_env* e, int64_t* buf, int64_t cap);
 /* the same run as device book-update records (include/mxa.h mxa_book_rec) as int64 triples
  * (t, price, qty); returns the record count */
 int64_t ora_book_records(const ora_env* e, int64_t* buf, int64_t cap);
+/* the exchange's own log (ExchangeAgent.log) in those records (include/mxa.h MXA_BL_EV_*) */
+void ora_set_exchange_log(ora_env* e, int on);
 int ora_n_agents(const ora_env* e);
 /* per agent: cash, shares, number of open orders */
 int ora_agent_state(const ora_env* e, int id, int64_t* cash, int64_t* shares, int64_t* n_open);

@@ -174,6 +174,12 @@ class OracleEnv:
         L.ora_set_book_log.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.ora_set_book_log(self._h, 1 if on else 0)
 
+    def set_exchange_log(self, on=True):
+        """the exchange's own log in the book records (ora_set_exchange_log); call before run()"""
+        L = lib()
+        L.ora_set_exchange_log.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.ora_set_exchange_log(self._h, 1 if on else 0)
+
     def book_log(self):
         """the rows as flat int64 (mxabides.booklog format: t, n, executed qty, average price,
         n (price, volume) pairs, bids best-first then asks best-first)"""

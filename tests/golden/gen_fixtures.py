@@ -26,6 +26,7 @@ bz2 log writers are no-ops.  None of them touches the simulated arithmetic.
 Usage:  python tests/golden/gen_fixtures.py all          (writes tests/golden/*.npz/json)
         python tests/golden/gen_fixtures.py summaries    (only the *_summary.json summary logs)
         python tests/golden/gen_fixtures.py booklog      (*_booklog.npz: book snapshot outputs)
+        python tests/golden/gen_fixtures.py exlog        (*_exlog.npz: the exchange's agent log)
         python tests/golden/gen_fixtures.py run CFG SEED OUT [--full] [--booklog]
 """
 import importlib
@@ -201,6 +202,8 @@ MIDNIGHT = 0
 TRACE = []
 BOOK_LOG = False  # book_freq 0 with a compact OrderBook.book_log (booklog fixtures only)
 FLOG = False      # only the oracle's f_log (flog fixtures: the ExternalFileOracle's)
+EXLOG = False     # only the exchange's own log (ExchangeAgent.log: EXCHANGE_AGENT.bz2)
+EXLOG_ROWS = 40000  # exlog fixtures keep this many rows verbatim and every row as a digest
 DIGEST_ROWS = 2000  # booklog fixtures above this many rows keep these verbatim and the rest as digests
 BOOKLOG_FULL_ROWS = 300  # rows kept verbatim to run the reference's logOrderBookSnapshots on
 
@@ -443,6 +446,9 @@ def run_config(cfg, seed, out, full):
     if BOOK_LOG:
         save_booklog(ex, ob, sym, orig_snapshots, out)
         return
+    if EXLOG:
+        save_exlog(ex, sym, out)
+        return
     if SUMMARY_ONLY:
         return
     with open(out + ".json", "w") as f:
@@ -546,6 +552,54 @@ def save_booklog(ex, ob, sym, orig_snapshots, out):
         full_rows=np.asarray(BOOKLOG_FULL_ROWS))
 
 
+def save_exlog(ex, sym, out):
+    """<out>_exlog.npz: ExchangeAgent.log, the frame Agent.kernelTerminating writes as
+    EXCHANGE_AGENT.bz2 (agent/Agent.py:86-95; log_events=True, ExchangeAgent.py:39).  One row per
+    logEvent call (Agent.py:97-110): EventTime (ns since midnight, -1 for AGENT_TYPE's None),
+    EventType, and the Event as the log holds it -- an int (the sender of a non-order message,
+    ExchangeAgent.py:167), a string (AGENT_TYPE, BEST_BID / BEST_ASK / LAST_TRADE,
+    util/OrderBook.py:112-141) or, with log_orders, the order's attribute dict (the jsons.dump
+    stub returns vars(order); ExchangeAgent.py:163-165, 477-482).  The first EXLOG_ROWS rows
+    verbatim, every row in an FNV-1a digest (tests/golden_util.exlog_row_words)."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    from golden_util import exlog_row_words
+    rows = []
+    keys = set()
+    for r in ex.log:
+        t = -1 if r["EventTime"] is None else int(r["EventTime"].value) - MIDNIGHT
+        ev = r["Event"]
+        if isinstance(ev, dict):
+            keys.add(",".join(ev))
+            if ev["symbol"] != sym:
+                raise ValueError("order of another symbol in the exchange log")
+            fill = ev["fill_price"]
+            rows.append((t, r["EventType"], 2, 0, "", (
+                int(ev["agent_id"]), int(ev["time_placed"].value) - MIDNIGHT, int(ev["quantity"]),
+                1 if ev["is_buy_order"] else 0, _oid(ev["order_id"]), -(1 << 63) if fill is None else _price(fill),
+                _price(ev["limit_price"]))))
+        elif isinstance(ev, str):
+            rows.append((t, r["EventType"], 1, 0, ev, (0,) * 7))
+        else:
+            rows.append((t, r["EventType"], 0, int(ev), "", (0,) * 7))
+    digest = FNV_OFF
+    for row in rows:
+        digest = fnv_words(digest, exlog_row_words(*row))
+    keep = rows[:EXLOG_ROWS]
+    types_ = sorted({r[1] for r in rows})
+    o = np.asarray([r[5] for r in keep], dtype=np.int64).reshape(-1, 7)
+    np.savez_compressed(
+        out + "_exlog.npz",
+        n_rows=np.asarray(len(rows)), digest=np.asarray(digest, dtype=np.uint64),
+        t=np.asarray([r[0] for r in keep], dtype=np.int64),
+        types=np.asarray(types_), type_idx=np.asarray([types_.index(r[1]) for r in keep], dtype=np.int16),
+        ekind=np.asarray([r[2] for r in keep], dtype=np.int8),
+        eint=np.asarray([r[3] for r in keep], dtype=np.int64),
+        estr=np.asarray([r[4] for r in keep]),
+        order=o,  # agent_id, time_placed, quantity, is_buy_order, order_id, fill_price, limit_price
+        order_keys=np.asarray(sorted(keys)), symbol=np.asarray(sym),
+        name=np.asarray(ex.name), log_orders=np.asarray(bool(ex.log_orders)))
+
+
 def rng_kats(path):
     """numpy legacy RandomState known answers (MT19937 + legacy distributions)."""
     out = {}
@@ -584,14 +638,19 @@ def main():
     global SUMMARY_ONLY
     global BOOK_LOG
     global FLOG
+    global EXLOG
     if sys.argv[1] == "run":
         SUMMARY_ONLY = "--summary-only" in sys.argv
         BOOK_LOG = "--booklog" in sys.argv
         FLOG = "--flog" in sys.argv
+        EXLOG = "--exlog" in sys.argv
         run_config(sys.argv[2], int(sys.argv[3]), sys.argv[4], "--full" in sys.argv)
         return
-    if sys.argv[1] in ("booklog", "flog"):  # <cfg>_<seed>_booklog.npz / _flog.npz
-        if sys.argv[1] == "booklog":  # order-book snapshot outputs (the replays: config/marketreplay.py's book_freq 0)
+    if sys.argv[1] in ("booklog", "flog", "exlog"):  # <cfg>_<seed>_booklog.npz / _flog.npz / _exlog.npz
+        if sys.argv[1] == "exlog":  # the exchange's agent log, EXCHANGE_AGENT.bz2 (log_orders on / off)
+            jobs = [("sparse_zi_100", 123456789), ("sparse_zi_1000", 123456789), ("rmsc03", 123456789),
+                    ("value_noise", 7), ("marketreplay:IBM:2003-01-14", 1)]
+        elif sys.argv[1] == "booklog":  # order-book snapshot outputs (the replays: config/marketreplay.py's book_freq 0)
             jobs = [("rmsc03", 123456789), ("value_noise", 7), ("marketreplay:IBM:2003-01-14", 1),
                     ("marketreplay:GOOG:2012-06-21", 1)]
         else:  # the ExternalFileOracle's f_log (fundamental_JPM)

@@ -99,3 +99,50 @@ def event_digest(events):
     for t, k, s in events:
         h = fnv_words(h, [t, kinds[k]] + list(s.encode()))
     return h
+
+
+# ExchangeAgent.log rows (gen_fixtures.py save_exlog, mxabides.booklog.exchange_log): the words
+# of one row's digest -- time, Event kind (0 int, 1 str, 2 order dict), the EventType's bytes
+# (length-prefixed), then the int, the string's bytes, or the order's seven fields
+def exlog_row_words(t, etype, ekind, eint, estr, order):
+    b = etype.encode()
+    w = [t, ekind, len(b)] + list(b)
+    if ekind == 0:
+        return w + [eint]
+    if ekind == 1:
+        s = estr.encode()
+        return w + [len(s)] + list(s)
+    return w + list(order)
+
+
+def exlog_row_tuple(row):
+    """one mxabides.booklog.exchange_log row as the fixture's (t, EventType, kind, int, str, order)"""
+    t, et, ev = row
+    t = -1 if t is None else int(t)
+    if isinstance(ev, dict):
+        f = ev["fill_price"]
+        return (t, et, 2, 0, "", (int(ev["agent_id"]), int(ev["time_placed"]), int(ev["quantity"]),
+                                  int(ev["is_buy_order"]), int(ev["order_id"]), -(1 << 63) if f is None else int(f),
+                                  int(ev["limit_price"])))
+    if isinstance(ev, str):
+        return (t, et, 1, 0, ev, (0,) * 7)
+    return (t, et, 0, int(ev), "", (0,) * 7)
+
+
+def exlog_fixture(name):
+    """tests/golden/<name>_exlog.npz (gen_fixtures.py exlog): (row count, digest, verbatim rows as
+    exlog_row_tuple tuples, the npz)"""
+    z = np.load(os.path.join(GOLDEN, "%s_exlog.npz" % name))
+    types = [str(x) for x in z["types"]]
+    rows = [(int(t), types[int(k)], int(ek), int(ei), str(es), tuple(int(x) for x in o))
+            for t, k, ek, ei, es, o in zip(z["t"], z["type_idx"], z["ekind"], z["eint"], z["estr"], z["order"])]
+    return int(z["n_rows"]), int(z["digest"]), rows, z
+
+
+def exlog_digest(rows):
+    """FNV-1a-64 over every row's exlog_row_words (the fixture's digest)"""
+    h = 0xCBF29CE484222325
+    for row in rows:
+        for w in exlog_row_words(*exlog_row_tuple(row)):
+            h = ((h ^ (int(w) & 0xFFFFFFFFFFFFFFFF)) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
