@@ -465,7 +465,10 @@ class DDQNEngine(Engine):
         torch.cuda.set_stream(self.stream)
         self.v.set_stream(self.stream.cuda_stream)
         self.v.set_parity_hash(args.parity_hash)
-        self.learner = ddqn.DDQNLearner(device="cuda", seed=1000 + ctx.rank, batch_size=args.ddqn_batch)
+        # one policy for the node: synchronous data parallelism over the ranks (gradient all-reduce
+        # per update, rank 0's initialisation; mxabides.ddqn module docstring)
+        group = ctx.dist.group.WORLD if ctx.world > 1 else None
+        self.learner = ddqn.DDQNLearner(device="cuda", seed=1000 + ctx.rank, batch_size=args.ddqn_batch, group=group)
         self.task = ddqn.ExecutionTask(device="cuda")
         self.timing = []
         self.env_steps = torch.zeros((), dtype=torch.int64, device="cuda")
@@ -490,9 +493,14 @@ class DDQNEngine(Engine):
         self.launches, self.kernel_ms = len(kms), sum(kms)
 
     def count(self, k):
-        """one more learner-driven episode (batch k's seeds) with the instrumentation on"""
+        """one more learner-driven episode (batch k's seeds) with the instrumentation on (rank 0
+        only, after the timed region: its updates stay local, no collective)"""
         self.v.set_parity_hash(True)
-        self.ddqn.run_episode(self.v, self.learner, self.task, seeds=self.seeds(k))
+        world, self.learner.world = self.learner.world, 1
+        try:
+            self.ddqn.run_episode(self.v, self.learner, self.task, seeds=self.seeds(k))
+        finally:
+            self.learner.world = world
         self.ctx.sync()
         c = self.v.counters()
         self.v.set_parity_hash(self.args.parity_hash)

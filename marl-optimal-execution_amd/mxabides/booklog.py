@@ -56,15 +56,22 @@ SESSION_DATE = "2019-06-28"  # the plain configs' simulated date (abides.py -d /
 FORBIDDEN_QUOTES = (0, 19999900)
 
 
+def exlog_mask(rec):
+    """the exchange log's records (include/mxa.h MXA_BL_EV_*) and the order records after them"""
+    p = np.asarray(rec, dtype=REC_DTYPE)["price"].astype(np.int64)
+    code = (p >= BL_EV_RX) & (p < BL_EV_END)
+    has_order = ((p >= BL_EV_RX + K_LIMIT) & (p <= BL_EV_RX + K_CANCEL)) | ((p >= BL_EV_NT) & (p < BL_EV_PLACE))
+    follows = np.zeros(len(p), dtype=bool)
+    follows[1:] = has_order[:-1]
+    return code | follows
+
+
 def book_mask(rec):
     """the records that change the book (limit orders, cancellations, modifyOrder): not f_log
     records, not the exchange log's records nor the order records that follow them"""
     p = np.asarray(rec, dtype=REC_DTYPE)["price"].astype(np.int64)
-    tagged = (p >= -(1 << 31)) & (p < BL_EV_END)  # f_log and exchange-log codes
-    has_order = ((p >= BL_EV_RX + K_LIMIT) & (p <= BL_EV_RX + K_CANCEL)) | ((p >= BL_EV_NT) & (p < BL_EV_PLACE))
-    follows = np.zeros(len(p), dtype=bool)
-    follows[1:] = has_order[:-1]
-    return ~tagged & ~follows
+    f_log = (p >= -(1 << 31)) & (p <= BL_FUND_HI)
+    return ~f_log & ~exlog_mask(rec)
 
 
 def rows_from_records(rec):

@@ -37,6 +37,20 @@ and never under ABIDESEnv. What the composition changes, and why:
 * one learner serves every env (shared replay, one policy); `batch_size`, `train_every` and
   `updates_per_train` default to the reference's 32, 5 and 1.
 
+Across GPUs (bench.py --gpus N, BASELINE configs[3]) the learner is synchronous data-parallel:
+with `group` (a torch.distributed process group over RCCL) the eval and target nets start from
+rank 0's initialisation (broadcast), every update all-reduces the gradient (mean over ranks) and
+the live flag (any rank), and every rank applies the same RMSprop step, so ONE policy serves the
+whole node. Each rank samples its batch from its own envs' replay; the update equals one learner's
+on the union of the ranks' batches (batch_size x world, tests/test_ddqn_multirank.py). The market
+results of a given action sequence are world-size invariant (envs shard by global index,
+mxabides.shard); the policy trajectory depends on the world size through that batch union.
+
+Random streams: `gen` draws choose_action's exploration, `gen_sample` the batch indices and
+`gen_drop` the dropout masks (Keras Dropout 0.1 in train_on_batch). A masked update (learn with
+live false) still draws its batch and masks, so those two streams advance on it; the exploration
+stream does not.
+
 Everything runs on the device stream the env steps on; the only host read is the stored-transition
 count, when the replay ring's host-side bounds cannot decide the batch-size test.
 """
@@ -97,11 +111,20 @@ class QNet(nn.Module):
                 lin.weight.uniform_(-lim, lim, generator=generator)
                 lin.bias.zero_()
 
-    def forward(self, x):
+    def dropout_widths(self):
+        """the widths of the Dropout layers (after hidden layers 2..n, QNets.py:22-26)"""
+        return [lin.out_features for lin in list(self.hidden)[1:]]
+
+    def forward(self, x, masks=None):
+        """masks: the keep masks (0/1, [batch, width]) of the dropout layers in training mode;
+        kept units are scaled by 1 / (1 - rate) as Keras' Dropout does (TF 2.1 nn.dropout)"""
         for i, lin in enumerate(self.hidden):
             x = torch.relu(lin(x))
-            if i >= 1 and self.p > 0:  # dropout after layers 2..n (QNets.py:22-26)
-                x = nn.functional.dropout(x, self.p, self.training)
+            if i >= 1 and self.p > 0 and self.training:  # dropout after layers 2..n (QNets.py:22-26)
+                if masks is None:
+                    x = nn.functional.dropout(x, self.p, True)
+                else:
+                    x = x * masks[i - 1].to(x.dtype) / (1.0 - self.p)
         return self.logits(x)
 
 
@@ -174,11 +197,15 @@ class DDQNLearner:
 
     def __init__(self, n_state=2, n_actions=N_ACTIONS, replace_target_iter=5, batch_size=32, learning_rate=0.01,
                  epsilon_increment=None, epsilon_max=0.9, reward_decay=0.98, mode="train", model="NNModel_1",
-                 dropout=0.1, capacity=1 << 20, device="cuda", seed=0, dtype=torch.float32):
+                 dropout=0.1, capacity=1 << 20, device="cuda", seed=0, dtype=torch.float32, group=None):
         self.device = torch.device(device)
         self.dtype = dtype
-        self.gen = torch.Generator(device=self.device)
+        self.gen = torch.Generator(device=self.device)  # choose_action's exploration
         self.gen.manual_seed(seed)
+        self.gen_sample = torch.Generator(device=self.device)  # train_neural_nets' batch indices
+        self.gen_sample.manual_seed(seed + (1 << 20))
+        self.gen_drop = torch.Generator(device=self.device)  # train_on_batch's dropout masks
+        self.gen_drop.manual_seed(seed + (2 << 20))
         cpu = torch.Generator()
         cpu.manual_seed(seed)
         # EvalModel and TargetModel are two separately initialised Keras models (QNets.py:54-60):
@@ -196,11 +223,23 @@ class DDQNLearner:
         self.reward_decay = reward_decay
         self.mode = mode
         self._counter = torch.zeros((), dtype=torch.int64, device=self.device)
-        self._costs = []  # (loss, live) device scalars per learn() call
+        # per learn() call: the loss and whether the update ran (device buffers, grown on the host
+        # side: the call count is known without reading the device)
+        self._cost = torch.zeros(256, dtype=torch.float64, device=self.device)
+        self._cost_live = torch.zeros(256, dtype=torch.bool, device=self.device)
+        self._ncost = 0
         # Keras RMSprop (TF 2.1 optimizer_v2, momentum 0, not centered): rho 0.9, epsilon 1e-7
         self.rho, self.rms_eps = 0.9, 1e-7
         self.rms = torch.zeros_like(self.eflat)
         self.memory = ReplayRing(capacity, n_state, self.device)
+        # synchronous data parallelism over the ranks of `group` (module docstring)
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group) if group is not None else 1
+        if self.world > 1:
+            src = dist.get_global_rank(group, 0) if group is not dist.group.WORLD else 0
+            dist.broadcast(self.eflat, src, group=group)
+            dist.broadcast(self.tflat, src, group=group)
 
     def _flat(self, net):
         net = net.to(self.device, self.dtype)
@@ -223,8 +262,26 @@ class DDQNLearner:
 
     @property
     def cost_hist(self):
-        """the losses of the updates that ran (host read; not on the step path)"""
-        return [c for c, live in self._costs if bool(live)]
+        """the losses of the updates that ran (one host read; not on the step path)"""
+        n = self._ncost
+        c, live = self._cost[:n].cpu(), self._cost_live[:n].cpu()
+        return [float(x) for x, ok in zip(c.tolist(), live.tolist()) if ok]
+
+    def _record_cost(self, loss, live):
+        if self._ncost == len(self._cost):
+            self._cost = torch.cat([self._cost, torch.zeros_like(self._cost)])
+            self._cost_live = torch.cat([self._cost_live, torch.zeros_like(self._cost_live)])
+        self._cost[self._ncost] = loss.to(torch.float64)
+        self._cost_live[self._ncost] = live
+        self._ncost += 1
+
+    def dropout_masks(self, n):
+        """train_on_batch's dropout keep masks for a batch of n (Keras: keep where U >= rate)"""
+        p = self.eval_model.p
+        if p <= 0:
+            return None
+        return [torch.rand((n, w), generator=self.gen_drop, device=self.device, dtype=torch.float64) >= p
+                for w in self.eval_model.dropout_widths()]
 
     # ---- acting (choose_action, :333-362)
     def q_values(self, s):
@@ -259,13 +316,22 @@ class DDQNLearner:
             tgt[idx, a] = r + self.reward_decay * q_next[idx, best]
         return tgt
 
-    def learn_on(self, s, a, s2, r, live=None):
+    def learn_on(self, s, a, s2, r, live=None, masks=None):
         """one train_neural_nets update on a given batch, in the reference's order: the target
         from the target net as it stands (:486-505), THEN the eval -> target copy when
         learn_step_counter % replace_target_iter == 0 (:508-510), then train_on_batch (:513).
-        `live` (device bool, default true) masks the whole update. Returns the loss."""
+        `live` (device bool, default true) masks the whole update; `masks` are the dropout keep
+        masks (default: drawn from gen_drop). With a process group the gradient is the mean over
+        ranks and the update runs when any rank is live. Returns the (local) loss."""
         if live is None:
             live = torch.ones((), dtype=torch.bool, device=self.device)
+        if self.world > 1:
+            import torch.distributed as dist
+            lv = live.to(torch.int32).reshape(1).clone()
+            dist.all_reduce(lv, op=dist.ReduceOp.MAX, group=self.group)
+            live = lv[0] > 0
+        if masks is None:
+            masks = self.dropout_masks(s.shape[0])
         tgt = self.q_target(s, a, s2, r)
         with torch.no_grad():
             do_copy = live & (self._counter % self.replace_target_iter == 0)
@@ -273,10 +339,14 @@ class DDQNLearner:
         self.eval_model.train()  # train_on_batch: training=True (dropout active)
         for p in self.eval_model.parameters():
             p.grad = None
-        loss = torch.mean((self.eval_model(s.to(self.dtype)) - tgt) ** 2)
+        loss = torch.mean((self.eval_model(s.to(self.dtype), masks) - tgt) ** 2)
         loss.backward()
         with torch.no_grad():
             g = torch.cat([p.grad.reshape(-1) for p in self.eval_model.parameters()])
+            if self.world > 1:  # one policy for the node: the mean gradient over the ranks
+                import torch.distributed as dist
+                dist.all_reduce(g, group=self.group)
+                g /= self.world
             rms = self.rho * self.rms + (1 - self.rho) * g * g
             self.rms.copy_(torch.where(live, rms, self.rms))
             step = self.learning_rate * g / (torch.sqrt(self.rms) + self.rms_eps)
@@ -289,7 +359,7 @@ class DDQNLearner:
         for p in self.eval_model.parameters():
             p.grad = None
         loss = loss.detach()
-        self._costs.append((loss, live))
+        self._record_cost(loss, live)
         return loss
 
     def learn(self, live=None):
@@ -298,7 +368,7 @@ class DDQNLearner:
         if not m.more_than(self.batch_size):
             return None
         size = torch.clamp(m.n_dev, max=m.cap).to(torch.float64)  # the current size, on the device
-        u = torch.rand(self.batch_size, generator=self.gen, device=self.device, dtype=torch.float64)
+        u = torch.rand(self.batch_size, generator=self.gen_sample, device=self.device, dtype=torch.float64)
         idx = torch.clamp((u * size).to(torch.int64), max=m.cap - 1)
         return self.learn_on(m.s[idx], m.a[idx], m.s2[idx], m.r[idx], live=live)
 

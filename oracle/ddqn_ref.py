@@ -24,12 +24,20 @@ def action_table(size_allocation, size_scale):
     return acts
 
 
-def forward(layers, x):
-    """layers: [(W [in,out], b)], ReLU on all but the last (QNets.py:19-27, no dropout: predict)."""
+def forward(layers, x, masks=None, rate=0.1):
+    """layers: [(W [in,out], b)], ReLU on all but the last (QNets.py:19-27).  masks: the keep
+    masks of the Dropout(rate) layers after hidden layers 2..n in training mode (QNets.py:22-26;
+    Keras scales kept units by 1 / (1 - rate)); None = predict(), no dropout."""
     acts = [x]
     for i, (W, b) in enumerate(layers):
         z = acts[-1] @ W + b
-        acts.append(z if i == len(layers) - 1 else np.maximum(z, 0.0))
+        if i == len(layers) - 1:
+            acts.append(z)
+            continue
+        h = np.maximum(z, 0.0)
+        if masks is not None and i >= 1:
+            h = h * masks[i - 1] / (1.0 - rate)
+        acts.append(h)
     return acts
 
 
@@ -44,9 +52,10 @@ def q_target(eval_layers, target_layers, s, a, s2, r, gamma):
     return tgt
 
 
-def mse_grads(layers, x, tgt):
-    """loss = mean((f(x) - tgt)^2) and d loss / d (W, b) for every layer."""
-    acts = forward(layers, x)
+def mse_grads(layers, x, tgt, masks=None, rate=0.1):
+    """loss = mean((f(x) - tgt)^2) and d loss / d (W, b) for every layer (train_on_batch: the
+    dropout masks of training mode, if given)."""
+    acts = forward(layers, x, masks, rate)
     out = acts[-1]
     loss = np.mean((out - tgt) ** 2)
     d = 2.0 * (out - tgt) / out.size
@@ -55,7 +64,10 @@ def mse_grads(layers, x, tgt):
         W, _ = layers[i]
         grads[i] = (acts[i].T @ d, d.sum(0))
         if i:
-            d = (d @ W.T) * (acts[i] > 0)
+            # acts[i] = relu(z) (* mask / (1 - rate) after a dropout layer): > 0 exactly where
+            # both the ReLU and the mask pass
+            scale = 1.0 / (1.0 - rate) if (masks is not None and i - 1 >= 1) else 1.0
+            d = (d @ W.T) * (acts[i] > 0) * scale
     return loss, grads
 
 
@@ -75,18 +87,20 @@ def step_reward(fills, arrival, q0):
     return sum((1 - ((f - arrival) / arrival)) * q / q0 * 10000 for q, f in fills)
 
 
-def train_step(eval_layers, target_layers, rms, counter, batch, lr=0.01, gamma=0.98, replace_target_iter=5):
+def train_step(eval_layers, target_layers, rms, counter, batch, lr=0.01, gamma=0.98, replace_target_iter=5, masks=None,
+               rate=0.1):
     """One whole `train_neural_nets` update (ddqlearning_execution_agent.py:448-515) after the
     batch is sampled, in the reference's order:
       1. q_next, q_eval4next from the target net AS IT STANDS, q_eval from eval (:486-505);
       2. then, if learn_step_counter % replace_target_iter == 0, eval -> target (:508-510);
       3. then train_on_batch on the eval net (:513): MSE, one RMSprop step;
       4. epsilon, then learn_step_counter += 1 (:526-530).
-    batch = (s, a, s2, r). Returns (eval', target', rms', counter', loss)."""
+    batch = (s, a, s2, r); masks: train_on_batch's dropout keep masks (None: dropout off).
+    Returns (eval', target', rms', counter', loss)."""
     s, a, s2, r = batch
     tgt = q_target(eval_layers, target_layers, s, a, s2, r, gamma)
     if counter % replace_target_iter == 0:
         target_layers = [(W.copy(), b.copy()) for W, b in eval_layers]
-    loss, grads = mse_grads(eval_layers, s, tgt)
+    loss, grads = mse_grads(eval_layers, s, tgt, masks, rate)
     eval_layers, rms = rmsprop_step(eval_layers, grads, rms, lr)
     return eval_layers, target_layers, rms, counter + 1, loss

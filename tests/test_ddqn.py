@@ -193,3 +193,48 @@ def test_actions_and_reward_mapping():
     got = float(task.reward(prev, cur, torch.tensor([10002.5], dtype=torch.float64), 100000.0)[0])
     assert got == pytest.approx(ddqn_ref.step_reward(fills, 10002.5, 100000.0), rel=1e-12)
     assert float(task.reward(prev, prev, torch.tensor([1.0], dtype=torch.float64), 1e5)[0]) == 0.0
+
+
+def test_dropout_on_learn_steps_match_reference_with_the_same_masks():
+    """train_on_batch in training mode (Dropout 0.1 after layers 2-6, QNets.py:22-26; Keras scales
+    kept units by 1 / (1 - rate)): the learner's update with its own drawn masks equals
+    ddqn_ref.train_step fed the same masks, over 12 updates and 2 target copies"""
+    L = ddqn.DDQNLearner(device="cpu", dropout=0.1, seed=4, dtype=torch.float64)
+    ev, tg = _layers(L.eval_model), _layers(L.target_model)
+    rms = [(np.zeros_like(W), np.zeros_like(b)) for W, b in ev]
+    counter = 0
+    dropped = 0
+    for it in range(12):
+        batch = _batch(seed=40 + it)
+        masks = L.dropout_masks(32)
+        dropped += sum(int((~m).sum()) for m in masks)
+        ev, tg, rms, counter, loss = ddqn_ref.train_step(ev, tg, rms, counter, batch,
+                                                         masks=[m.numpy().astype(np.float64) for m in masks])
+        cost = L.learn_on(*(torch.from_numpy(x) for x in batch), masks=masks)
+        assert abs(float(cost) - loss) <= 1e-9 * max(1.0, loss), it
+        for (W, b), (W2, b2) in zip(_layers(L.eval_model), ev):
+            np.testing.assert_allclose(W, W2, rtol=1e-9, atol=1e-9)
+            np.testing.assert_allclose(b, b2, rtol=1e-9, atol=1e-9)
+    assert dropped > 0.05 * 12 * 32 * (64 + 128 + 128 + 64 + 32)  # about 10 % of the units dropped
+    # the masks change the update: the same batches without dropout end elsewhere
+    L0 = ddqn.DDQNLearner(device="cpu", dropout=0.0, seed=4, dtype=torch.float64)
+    for it in range(12):
+        L0.learn_on(*(torch.from_numpy(x) for x in _batch(seed=40 + it)))
+    assert not torch.allclose(L0.eflat, L.eflat)
+
+
+def test_exploration_stream_is_independent_of_masked_updates():
+    """choose_action draws from its own stream: masked (no-op) updates between two acting steps
+    do not change the actions; the masked updates' losses stay out of cost_hist"""
+    s = torch.from_numpy(_batch(n=256)[0])
+    acts = []
+    for n_masked in (0, 3):
+        L = _learner()
+        L.memory.add(s, torch.zeros(256, dtype=torch.int64), s, torch.zeros(256, dtype=torch.float64),
+                     torch.ones(256, dtype=torch.bool))
+        a0 = L.choose_action(s)
+        for _ in range(n_masked):
+            L.learn(live=torch.tensor(False))
+        acts.append((a0, L.choose_action(s)))
+        assert L.cost_hist == []
+    assert torch.equal(acts[0][1], acts[1][1])

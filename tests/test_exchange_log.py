@@ -63,6 +63,7 @@ def test_exchange_log_records_leave_the_book_rows_unchanged(cfg, seed):
     assert np.array_equal(bl.rows_from_records(r0), o.book_log())
     assert len(r) > len(r0)
     assert np.array_equal(r[bl.book_mask(r)], r0[bl.book_mask(r0)])
+    assert np.array_equal(r[~bl.exlog_mask(r)], r0)
 
 
 def test_replay_exchange_log_equals_reference_but_duplicate_id_times():
