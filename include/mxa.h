@@ -297,9 +297,8 @@ int mxa_set_exchange_log(mxa_handle* h, int32_t on);
 int mxa_read_book_log(mxa_handle* h, int32_t env, mxa_book_rec* out, int64_t cap, int64_t* n);
 
 /* parity probes: device numpy-legacy RNG (mode 0 u32, 1 double, 2 randint(a,b),
- * 3 normal(a,b), 4 exponential(a), 5 uniform(a,b); 6 / 7 normal(a,b) as the run kernel draws
- * it, wave-parallel, from an agent stream in HBM / a global stream's LDS window: out holds n + 1
- * doubles, the last the look-ahead overrun flag) and device glibc math (mode 0 log, 1 exp, 2 pow) */
+ * 3 normal(a,b), 4 exponential(a), 5 uniform(a,b)) and device glibc math (mode 0 log, 1 exp,
+ * 2 pow) */
 int mxa_rng_probe(int32_t device, uint32_t seed, int32_t mode, double a, double b, int32_t n, double* out);
 int mxa_math_probe(int32_t device, int32_t mode, const double* x, const double* y, double* out, int64_t n);
 

@@ -18,11 +18,7 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define GM_FN __host__ __device__ __forceinline__ static
-#ifdef MXA_NOINLINE_MATH
-#define GM_BIG __host__ __device__ __attribute__((noinline)) static
-#else
 #define GM_BIG __host__ __device__ __forceinline__ static
-#endif
 #define GM_TABLE_QUAL static __device__ __constant__ const
 #else
 #define GM_FN static inline

@@ -1071,15 +1071,11 @@ int mxa_rng_probe(int32_t device, uint32_t seed, int32_t mode, double a, double 
   if (hipSetDevice(device) != hipSuccess) return MXA_EHIP;
   double* d_out = nullptr;
   uint32_t* d_s = nullptr;
-  if (mode < 0 || mode > 7) return MXA_EINVAL;
-  const int wave = mode >= 6;  // the run kernel's normal draws: n values + the overrun flag
-  if (hipMalloc(&d_out, sizeof(double) * (n + wave)) != hipSuccess) return MXA_ENOMEM;
+  if (mode < 0 || mode > 5) return MXA_EINVAL;
+  if (hipMalloc(&d_out, sizeof(double) * n) != hipSuccess) return MXA_ENOMEM;
   if (hipMalloc(&d_s, MXA_RNG_WORDS * 4) != hipSuccess) return MXA_ENOMEM;
-  if (wave)
-    hipLaunchKernelGGL(mxa_rng_probe_wave_kernel, dim3(1), dim3(64), 0, 0, seed, mode - 6, a, b, n, d_out, d_s);
-  else
-    hipLaunchKernelGGL(mxa_rng_probe_kernel, dim3(1), dim3(64), 0, 0, seed, mode, a, b, n, d_out, d_s);
-  hipError_t e = hipMemcpy(out, d_out, sizeof(double) * (n + wave), hipMemcpyDeviceToHost);
+  hipLaunchKernelGGL(mxa_rng_probe_kernel, dim3(1), dim3(64), 0, 0, seed, mode, a, b, n, d_out, d_s);
+  hipError_t e = hipMemcpy(out, d_out, sizeof(double) * n, hipMemcpyDeviceToHost);
   hipFree(d_out);
   hipFree(d_s);
   return e == hipSuccess ? MXA_OK : MXA_EHIP;

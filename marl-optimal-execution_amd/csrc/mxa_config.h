@@ -100,18 +100,15 @@ constexpr int lat_lds(int cfg);
 #ifndef MXA_RP_HOT
 #define MXA_RP_HOT 2  // replay configurations: the exchange's and the MarketReplayAgent's records in LDS
 #endif
-#ifndef MXA_HOT_RECORDS
-#define MXA_HOT_RECORDS 0  // measured (r01 s3i): exchange + MM records in LDS were 3 % slower than L1/L2-served loads
-#endif
 constexpr Shape shape(int cfg) {
   // rmsc03: 192 queue slots (the oracle's maximum over the 4096 bench seeds is 146, over 1024
   // rmsc03_rl episodes 146), so 16 waves per CU fit the queue, the header and the exchange and
   // market-maker records in LDS
-  return cfg == MXA_CFG_RMSC03 ? Shape{3, 2, true, MXA_RMSC03_WAVES, 6, 2 * MXA_HOT_RECORDS}
+  return cfg == MXA_CFG_RMSC03 ? Shape{3, 2, true, MXA_RMSC03_WAVES, 6, 0}
        // rmsc03 + SpreadBasedMarketMakerAgent: MARKET_DATA carries level counts (8 payload words)
        : cfg == MXA_CFG_RMSC03_SBMM ? Shape{3, 2, true, 4, 8, 0}
        : cfg == MXA_CFG_RMSC03_SBMM_POLL ? Shape{3, 2, true, 4, 6, 0}
-       : cfg == MXA_CFG_RMSC03_RL ? Shape{3, 2, true, 4, 8, 2 * MXA_HOT_RECORDS}  // wide spread replies (depth 500)
+       : cfg == MXA_CFG_RMSC03_RL ? Shape{3, 2, true, 4, 8, 0}  // wide spread replies (depth 500)
        // rmsc03 with per-env market-maker options: scripts/rmsc03.sh's 50 ticks (a 102-order ladder)
        // peak at 266 pending events and 122 resting orders (oracle, 4,096 seeds of the script's
        // options and of a mixed grid: pov 0.01-0.2, sizes 10-50, windows 1-10, 5-50 ticks, 1-60 s);
@@ -127,9 +124,9 @@ constexpr Shape shape(int cfg) {
        // obi_rmsc02: oracle maxima over the 131,072 seeds of bench.py --gpus 1-8: 211 pending
        // events, 149 resting orders (192 book slots; 128 overflowed)
        : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 3, true, MXA_W_OBI, 8, 0}
-       : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, MXA_W_Z1, 6, MXA_HOT_RECORDS}
-       : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, MXA_W_VN, 6, MXA_HOT_RECORDS}  // 384 slots: oracle max 301 (2048 seeds)
-       : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{MXA_SQ_Z1K, MXA_SO_Z1K, false, 1, 6, MXA_HOT_RECORDS}
+       : cfg == MXA_CFG_SPARSE_ZI_100 ? Shape{8, 2, true, MXA_W_Z1, 6, 0}
+       : cfg == MXA_CFG_VALUE_NOISE ? Shape{6, 2, true, MXA_W_VN, 6, 0}  // 384 slots: oracle max 301 (2048 seeds)
+       : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{MXA_SQ_Z1K, MXA_SO_Z1K, false, 1, 6, 0}
        // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
        // maximum over the 8,192 bench seeds is 5,125 events), payload in HBM; 320 book slots (max 279)
        // the first MXA_RFV_SQL slots per lane (24: 1,536) in LDS for events due within a second,
@@ -156,11 +153,7 @@ constexpr size_t lds_bytes(int cfg) {
          + 1024                                                                               // RNG stream windows
          + (size_t)lat_lds(cfg) * 8                                                           // exchange latency row
          + (rp_hdr_lds(cfg) ? 256 : 0)                                                        // RpHdr (replay / gym)
-#ifdef MXA_QREG
-         + 768  // batched-push scratch: slot table + staged keys
-#else
          + 256  // batched-push scratch: slot table
-#endif
 #ifdef MXA_PROF
          + 1024  // phase counters and inclusive function timers (128 x u64)
 #endif

@@ -52,12 +52,10 @@ MxaEntry make_entry() {
   e.run = launch_run<CFG, false, true>;
   e.stop = launch_stop<CFG, false>;
   constexpr bool gym = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_RMSC03_RL;
-#ifndef MXA_NO_FAST
 #ifndef MXA_NO_GYM
   e.occ = occupancy<CFG, gym>;
 #else
   if constexpr (!gym) e.occ = occupancy<CFG, false>;
-#endif
 #endif
   if constexpr (!gym) {  // the book-update log: plain Kernel.runner configurations
     e.run_log = launch_run<CFG, true, true>;
@@ -67,17 +65,13 @@ MxaEntry make_entry() {
     // 986 vs 976), but with the event-class counters in the instrumented kernel (round 3, s10)
     // the plain one wins there too: rmsc01 1047 vs 1082 ms, sparse_zi_1000 916 vs 920
     constexpr bool fast = true;
-#ifndef MXA_NO_FAST
     if constexpr (fast) e.run_fast = launch_run<CFG, false, false>;
-#endif
     e.stop_log = launch_stop<CFG, true>;
   }
 #ifndef MXA_NO_GYM
   if constexpr (gym) {
     e.step = launch_step<CFG, true>;
-#ifndef MXA_NO_FAST
     e.step_fast = launch_step<CFG, false>;
-#endif
   }
 #endif
   return e;

@@ -293,84 +293,12 @@ DEV i64 rs_randint(RSt<B>& r, i64 lo, i64 hi) {
   } while (v > (u32)rng);
   return lo + (i64)v;
 }
-DEV u32 mt_temper(u32 y) {
-  y ^= (y >> 11);
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
-  y ^= (y >> 18);
-  return y;
-}
-// legacy_gauss's polar rejection loop with its candidates evaluated across the wave (run kernel,
-// wave-uniform call sites): lane j loads the stream's word p + j in one round trip (the LDS
-// window or the MT block in HBM), lane i < 16 forms candidate i from words 4i .. 4i + 3, and the
-// first accepted candidate is the one the serial loop would stop at, so p, the cached second
-// normal and both values are the serial loop's.  A stream with fewer than 4 materialized words
-// left (the look-ahead overrun) finishes in the serial loop, which flags it.
-template <bool B>
-DEV double rs_gauss_serial(RSt<B>& r);
-template <bool B>
-DEV double rs_gauss_wave(RSt<B>& r) {
-  const int lane = laneid();
-  for (;;) {
-    u32 w = 0;
-    int navail;
-    if (r.lw) {
-      u32 off = (u32)(r.p - r.lw0);
-      if (off >= (u32)r.lwn) {
-        rs_fill(r);
-        off = 0;
-      }
-      navail = r.lwn - (int)off;
-      if (lane < navail) w = r.lw[off + lane];
-    } else {
-      const int q = r.p + lane, b = q / MXA_MT_N;
-      const bool ok = b <= r.m && b >= r.m - 1;
-      if (ok) w = r.key[(b & 1) * MXA_MT_N + (q - b * MXA_MT_N)];
-      const u64 okb = __ballot(ok);
-      navail = ~okb == 0 ? 64 : __ffsll((unsigned long long)~okb) - 1;
-    }
-    const int nc = navail >> 2;  // whole candidates available (at most 16)
-    if (nc == 0) return rs_gauss_serial(r);
-    w = mt_temper(w);
-    const int i4 = (lane & 15) * 4;
-    const u32 w0 = (u32)__shfl((int)w, i4, 64), w1 = (u32)__shfl((int)w, i4 + 1, 64);
-    const u32 w2 = (u32)__shfl((int)w, i4 + 2, 64), w3 = (u32)__shfl((int)w, i4 + 3, 64);
-    const double d1 = ((double)(i32)(w0 >> 5) * 67108864.0 + (double)(i32)(w1 >> 6)) / 9007199254740992.0;
-    const double d2 = ((double)(i32)(w2 >> 5) * 67108864.0 + (double)(i32)(w3 >> 6)) / 9007199254740992.0;
-    const double x1 = 2.0 * d1 - 1.0, x2 = 2.0 * d2 - 1.0;
-    const double r2 = x1 * x1 + x2 * x2;
-    const u64 acc = __ballot(lane < nc && !(r2 >= 1.0 || r2 == 0.0));
-    if (acc) {
-      const int L = __ffsll((unsigned long long)acc) - 1;
-      r.p += 4 * (L + 1);
-      const double X1 = rdl_d(x1, L), X2 = rdl_d(x2, L), R2 = rdl_d(r2, L);
-      const double f = __builtin_sqrt(-2.0 * gm_log(R2) / R2);
-      r.gauss = f * X1;
-      r.hasg |= 1;
-      return f * X2;
-    }
-    r.p += 4 * nc;  // every available candidate rejected
-  }
-}
-// the run kernel's normal draws: serial (default) or wave-parallel (-DMXA_WAVE_GAUSS=1).  The
-// wave form was neutral on sparse_zi_1000 (721.9 vs 722.x ms) and grew rmsc02's run kernel
-// (62.1 k vs 54.4 k instructions, 1,129 vs 848 scratch instructions: it is inlined at every
-// normal draw of a kernel already at 256 VGPRs), so it is opt-in; the parity probe
-// (mxa_rng_probe modes 6 / 7) runs it either way
-#ifndef MXA_WAVE_GAUSS
-#define MXA_WAVE_GAUSS 0
-#endif
+// the run kernel's normal draws (numpy legacy_gauss).  A wave-parallel form (16 polar
+// candidates across the wave in one load round trip) was built, checked bit-exact and measured in
+// round 4: neutral on sparse_zi_1000 (721.9 vs 722 ms) and rmsc02's run kernel grew (62.1 k vs
+// 54.4 k instructions); removed in round 5
 template <bool B>
 DEV double rs_gauss(RSt<B>& r) {
-  if constexpr (!B && MXA_WAVE_GAUSS) {
-    if (r.hasg & 1) {
-      double t = r.gauss;
-      r.hasg &= ~1;
-      r.gauss = 0.0;
-      return t;
-    }
-    return rs_gauss_wave(r);
-  }
   return rs_gauss_serial(r);
 }
 template <bool B>
@@ -649,14 +577,10 @@ struct Eng {
   static constexpr int SO = mxa_cfg::shape(CFG).so;
   static constexpr bool PL_LDS = mxa_cfg::shape(CFG).pl;
   static constexpr int PW = mxa_cfg::shape(CFG).pw;           // payload words queued
-#ifdef MXA_NO_EARLY_REC
-  static constexpr bool EARLY_REC = false;
-#else
   // (event loop: record beside the HBM payload).  Not on the two-tier queue configurations:
   // there it measured neutral (393.1 vs 393.7 ms) and loads the records of the acknowledgements
   // that take a fast path, +46 B/event of HBM traffic
   static constexpr bool EARLY_REC = !BUILD && !PL_LDS && !(mxa_cfg::sq_lds(CFG) < mxa_cfg::shape(CFG).sq);
-#endif
   // grouped lane-min cache for deep queues (sparse_zi_1000: 48 slots per lane): a lane's slots
   // in groups of QG, each group's min (key, seq, slot) kept in VGPRs, so a remove or requeue
   // rescans one group of QG slots instead of all SQ
@@ -674,38 +598,21 @@ struct Eng {
 #endif
   static constexpr int QG = SQ >= 16 ? MXA_QG : SQ / 2;
   static constexpr bool TIER_CFG = mxa_cfg::sq_lds(CFG) < SQ;  // (TIER below)
-#ifdef MXA_QREG
-  static constexpr bool QHIER = false;
-#else
   static constexpr bool QHIER = SQ >= MXA_QHIER_MIN && SQ > QG;
   // a group size that does not tile the deep queues is a build error, never a silent fall-back
   // to the flat scan (a -DMXA_QG sweep must measure what it names)
   static_assert(!QHIER || SQ % QG == 0, "queue groups must tile the lane's slots (MXA_QG)");
-#endif
   // the two-tier queue keeps the LDS tier's groups and ONE entry for the lane's whole HBM tier
   // (its SQH far slots): a push there is a select on that entry, and only a pop or rekey of an
-  // HBM-tier slot rescans it, in the owner lane alone (HQ_AGG; a twelfth of the pops in
+  // HBM-tier slot rescans it, in the owner lane alone (a twelfth of the pops in
   // random_fund_value).  One VGPR entry instead of six per-group entries, which the run kernel
   // spilled on every push (880 scratch instructions at q_gupd, r04 isa_lines)
-#ifdef MXA_HQ_GROUPS
-  static constexpr bool HQ_AGG = false;
-#else
-  static constexpr bool HQ_AGG = true;
-#endif
-  static constexpr int NG = QHIER ? ((TIER_CFG && HQ_AGG) ? mxa_cfg::sq_lds(CFG) / QG + 1 : SQ / QG) : 1;
+  static constexpr int NG = QHIER ? (TIER_CFG ? mxa_cfg::sq_lds(CFG) / QG + 1 : SQ / QG) : 1;
   // group rescans as one batch of loads and a select tree (q_scan): groups of 4 and more slots.
   // r03 s20, same per-env results: sparse_zi_1000 916 -> 826 ms, random_fund_value 778 -> 575,
   // sparse_zi_100 132.5 -> 125.7, value_noise 22.0 -> 21.2; rmsc02 (groups of 3) 1053 -> 1086, so
   // it keeps the serial scan
-#ifdef MXA_SERIAL_QSCAN
-  static constexpr bool QTREE = false;
-#else
-#ifdef MXA_QTREE_ALL
-  static constexpr bool QTREE = QHIER;
-#else
   static constexpr bool QTREE = QHIER && QG >= 4;
-#endif
-#endif
   static constexpr int HOT = BUILD ? 0 : mxa_cfg::shape(CFG).hot;  // LDS-resident agent records
   // the replay book + tape (ABIDESEnv's composition, or config/marketreplay.py under Kernel.runner)
   static constexpr bool RP = CFG == MXA_CFG_MARKETREPLAY || CFG == MXA_CFG_MARKETREPLAY_RUNNER ||
@@ -760,17 +667,7 @@ struct Eng {
   // bytes were these rescans)
   static constexpr size_t OFF_HQ = PC.L.off_q + sizeof(SavedEvent) * QCAP + (PL_LDS ? 0 : (size_t)QCAP * 4 * PW);
   static constexpr int SQH = SQ - SQL;
-#ifdef MXA_HQ_SLOT_MAJOR  // the round-3 layout: slot j of every lane together
-  static constexpr bool HQ_LM = false;
-#else
-  static constexpr bool HQ_LM = true;
-#endif
-#ifdef MXA_HQ_ALL_LANES  // the round-3 rescans: every lane rescans an HBM-tier group
-  static constexpr bool HQ_OWNER = false;
-#else
-  static constexpr bool HQ_OWNER = true;
-#endif
-  static DEV int hidx(int slot) { return HQ_LM ? (slot & 63) * SQH + ((slot >> 6) - SQL) : slot - QCL; }
+  static DEV int hidx(int slot) { return (slot & 63) * SQH + ((slot >> 6) - SQL); }
   DEV GLBP u64* hqk() { return (GLBP u64*)(env + OFF_HQ); }
   DEV GLBP u32* hqs() { return (GLBP u32*)(env + OFF_HQ + (size_t)(QCAP - QCL) * 8); }
   DEV u64 qk_get(int slot) {
@@ -803,39 +700,16 @@ struct Eng {
     }
     qs[slot] = v;
   }
-#ifdef MXA_QREG
-  u64 rk[SQ];  // this lane's queue slots (j, lane) in VGPRs: keys and seqs
-  u32 rq[SQ];
-#endif
   // this lane's slot j (every use of the key/seq arrays is the owning lane's own slot)
   DEV u64 qkey(int j) {
-#ifdef MXA_QREG
-    u64 v = rk[0];
-    for (int jj = 1; jj < SQ; jj++) v = jj == j ? rk[jj] : v;
-    return v;
-#else
     if constexpr (TIER) return qk_get(j * 64 + lane);
     else return qk[j * 64 + lane];
-#endif
   }
   DEV u32 qseq(int j) {
-#ifdef MXA_QREG
-    u32 v = rq[0];
-    for (int jj = 1; jj < SQ; jj++) v = jj == j ? rq[jj] : v;
-    return v;
-#else
     if constexpr (TIER) return qs_get(j * 64 + lane);
     else return qs[j * 64 + lane];
-#endif
   }
   DEV void qset(int j, u64 k, u32 s, bool me) {
-#ifdef MXA_QREG
-    for (int jj = 0; jj < SQ; jj++) {
-      const bool w = me && jj == j;
-      rk[jj] = w ? k : rk[jj];
-      rq[jj] = w ? s : rq[jj];
-    }
-#else
     if (me) {
       if constexpr (TIER) {
         qk_put(j * 64 + lane, k);
@@ -845,17 +719,12 @@ struct Eng {
         qs[j * 64 + lane] = s;
       }
     }
-#endif
   }
   DEV void qsetk(int j, u64 k, bool me) {
-#ifdef MXA_QREG
-    for (int jj = 0; jj < SQ; jj++) rk[jj] = (me && jj == j) ? k : rk[jj];
-#else
     if (me) {
       if constexpr (TIER) qk_put(j * 64 + lane, k);
       else qk[j * 64 + lane] = k;
     }
-#endif
   }
   PlPtr qpl;
   u64 mk;
@@ -944,7 +813,6 @@ struct Eng {
     add_delay = 0;
     run_skip = 0;
     rdirty = 0;
-    bok = 0;
     lane = laneid();
     qk = (LDSP u64*)lds;
     qs = (LDSP u32*)(lds + 8 * QCL);
@@ -959,11 +827,7 @@ struct Eng {
     prof[64 + lane] = 0;
 #endif
     trace = tcap > 0 ? (i64*)(env + PC.L.off_trace) : nullptr;
-#ifdef MXA_QREG
-    scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 768);
-#else
     scr = (LDSP i32*)(lds + mxa_cfg::lds_bytes(CFG) - 256);
-#endif
     rwin = (LDSP u32*)((LDSP char*)scr - 1024);
 #ifdef MXA_PROF
     hotrec = (LDSP u64*)(lds + LDS_Q + 512 + 1024);
@@ -1044,16 +908,9 @@ struct Eng {
   // record writes are lane selects (v_cndmask), not divergent branches
   DEV void rs(int f, u32 v) {
     rdirty |= 1u << (f >> 5);  // the record quarter (dwords 32q .. 32q + 31) of field f
-#ifdef MXA_DIVERGENT_RS
-    if (lane == (f >> 1)) {
-      if (f & 1) rhi = v;
-      else rlo = v;
-    }
-#else
     bool me = lane == (f >> 1);
     if (f & 1) rhi = me ? v : rhi;
     else rlo = me ? v : rlo;
-#endif
   }
   DEV void rs64(int f, i64 v) {
     rdirty |= 1u << (f >> 5);
@@ -1092,13 +949,8 @@ struct Eng {
   // no materialized block after the one holding position p.  Decided where the state is put
   // (registers) instead of re-read from the header and the record at the event's end
   DEV bool rs_needs_maint(const RS& r) {
-#ifdef MXA_MAINT_AT_END
-    (void)r;
-    return true;
-#else
     if constexpr (BUILD) return true;
     return (r.hasg & 2) || r.m < r.p / MXA_MT_N + 1;
-#endif
   }
   // global streams: 0 = G (np.random), 1 = O (oracle symbol), 2 = K (kernel), 3 = L (latency)
   DEV RS grs(int s) {
@@ -1205,8 +1057,8 @@ struct Eng {
       u32 s[QG];
       i32 j[QG];
       if (TIER && j0 >= SQL) {
-        constexpr int ST = HQ_LM ? 1 : 64;  // word stride between a lane's consecutive slots
-        const int b0 = HQ_LM ? lane * SQH + (j0 - SQL) : (j0 - SQL) * 64 + lane;
+        constexpr int ST = 1;  // word stride between a lane's consecutive slots (lane-major)
+        const int b0 = lane * SQH + (j0 - SQL);
         const GLBP u64* K = hqk() + b0;
         const GLBP u32* S = hqs() + b0;
 #pragma unroll
@@ -1238,8 +1090,8 @@ struct Eng {
     bj = -1;
     if constexpr (TIER) {
       if (j0 >= SQL) {  // a whole group of the HBM tier (groups never straddle the tiers)
-        constexpr int ST = HQ_LM ? 1 : 64;
-        const int b0 = HQ_LM ? lane * SQH + (j0 - SQL) : (j0 - SQL) * 64 + lane;
+        constexpr int ST = 1;
+        const int b0 = lane * SQH + (j0 - SQL);
         const GLBP u64* K = hqk() + b0;
         const GLBP u32* S = hqs() + b0;
         for (int j = 0; j < n; j++) {
@@ -1285,7 +1137,7 @@ struct Eng {
     ms = bs;
     mj = bj;
   }
-  // HQ_AGG: min (key, seq, slot) over this lane's HBM-tier slots, QG at a time
+  // min (key, seq, slot) over this lane's HBM-tier slots, QG at a time
   DEV void q_scan_hbm(u64& bk, u32& bs, i32& bj) {
     q_scan(SQL, QG, bk, bs, bj);
 #pragma unroll 1
@@ -1298,7 +1150,7 @@ struct Eng {
     }
     if (bk == KEY_EMPTY && bs == 0xFFFFFFFFu) bj = -1;
   }
-  // HQ_AGG, a pop or rekey in the HBM tier: the owner lane's SQH far slots in ONE round trip,
+  // a pop or rekey in the HBM tier: the owner lane's SQH far slots in ONE round trip,
   // spread over the wave (lane i holds slots SQL + i and SQL + 64 + i), then a wave-wide
   // lexicographic min (as q_peek).  Results are wave-uniform.  The owner-lane scan took SQH / QG
   // dependent round trips (34 % of random_fund_value's cycles in q_remove, r04 s12)
@@ -1336,11 +1188,11 @@ struct Eng {
   }
   // QHIER: the slot's group changed.  An LDS-tier group is rescanned in every lane (the group
   // index is wave-uniform; lanes whose group did not change recompute the same values), then the
-  // lane mins.  An HBM-tier slot: its owner lane alone rescans (HQ_OWNER: that group; HQ_AGG:
-  // the whole tier), the other lanes' entries are unchanged and their rescans were HBM traffic
+  // lane mins.  An HBM-tier slot: its owner lane alone rescans the whole tier (one aggregate
+  // entry), the other lanes' entries are unchanged and their rescans were HBM traffic
   DEV void q_regroup(int slot) {
     const int g = (slot >> 6) / QG, owner = slot & 63;
-    if constexpr (TIER && HQ_AGG) {
+    if constexpr (TIER) {
       if ((slot >> 6) >= SQL) {
         u64 k;
         u32 s;
@@ -1350,25 +1202,6 @@ struct Eng {
           gk[NG - 1] = k;
           gs[NG - 1] = s;
           gj[NG - 1] = j;
-          q_lanemin();
-        }
-        return;
-      }
-    } else if constexpr (TIER && HQ_OWNER) {
-      if (g * QG >= SQL) {
-        if (lane == owner) {
-          u64 k;
-          u32 s;
-          i32 j;
-          q_scan(g * QG, QG, k, s, j);
-#pragma unroll
-          for (int gg = SQL / QG; gg < NG; gg++) {
-            if (gg == g) {
-              gk[gg] = k;
-              gs[gg] = s;
-              gj[gg] = j;
-            }
-          }
           q_lanemin();
         }
         return;
@@ -1389,7 +1222,7 @@ struct Eng {
     q_lanemin();
   }
   DEV void q_gupd(int j, u64 k, u32 s) {  // QHIER: slot j of this lane now holds (k, s)
-    const int g = (TIER && HQ_AGG && j >= SQL) ? NG - 1 : j / QG;
+    const int g = (TIER && j >= SQL) ? NG - 1 : j / QG;
     if constexpr (QTREE) {
 #pragma unroll
       for (int gg = 0; gg < NG; gg++) {  // selects: g differs between lanes
@@ -1410,20 +1243,16 @@ struct Eng {
   }
   DEV void q_rescan() {  // recompute this lane's min over its own slots
     if constexpr (QHIER) {
-      if constexpr (TIER && HQ_AGG) {
+      if constexpr (TIER) {  // unrolled: a rolled loop indexes gk/gs/gj dynamically (scratch)
 #pragma unroll
         for (int g = 0; g < NG - 1; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
         q_scan_hbm(gk[NG - 1], gs[NG - 1], gj[NG - 1]);
-      } else if constexpr (TIER) {  // unrolled: a rolled loop indexes gk/gs/gj dynamically (scratch)
-#pragma unroll
-        for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
       } else {  // (unrolled here too: the same time for sparse_zi_1000, +0.5-2 % for sparse_zi_100 and value_noise, r03 s9)
         for (int g = 0; g < NG; g++) q_scan(g * QG, QG, gk[g], gs[g], gj[g]);
       }
       q_lanemin();
       return;
     }
-#if !defined(MXA_SERIAL_FLAT) && !defined(MXA_QREG)
     // every slot's load first, then a select tree (as q_scan).  r03 s24, same per-env results:
     // rmsc03 43.8 -> 41.4 ms, rmsc01 1073 -> 963, obi_rmsc02 386 -> 373
     if constexpr (!TIER) {
@@ -1446,19 +1275,13 @@ struct Eng {
       mj = (k[0] == KEY_EMPTY && s[0] == 0xFFFFFFFFu) ? -1 : j[0];
       return;
     }
-#endif
     u64 bk = KEY_EMPTY;
     u32 bs = 0xFFFFFFFFu;
     i32 bj = -1;
     for (int j = 0; j < SQ; j++) {
-#ifdef MXA_QREG
-      u64 k = rk[j];
-      u32 s = rq[j];
-#else
       int slot = j * 64 + lane;
       u64 k = qk[slot];
       u32 s = qs[slot];
-#endif
       if (k < bk || (k == bk && s < bs)) {
         bk = k;
         bs = s;
@@ -1487,11 +1310,7 @@ struct Eng {
 #define MXA_MAXQ_REG_MASK ((1 << MXA_CFG_SPARSE_ZI_1000) | (1 << MXA_CFG_RMSC02) | (1 << MXA_CFG_RANDOM_FUND_VALUE) | \
                            (1 << MXA_CFG_RANDOM_FUND_DIVERSE) | (1 << MXA_CFG_HIST_FUND_VALUE) | (1 << MXA_CFG_HIST_FUND_DIVERSE))
 #endif
-#ifdef MXA_MAXQ_LDS
-  static constexpr bool MAXQ_REG = false;
-#else
   static constexpr bool MAXQ_REG = !BUILD && (((MXA_MAXQ_REG_MASK) >> CFG) & 1);
-#endif
   i32 maxq;
   DEV void note_max_q() {
     if constexpr (MAXQ_REG) maxq = qcount > maxq ? qcount : maxq;
@@ -1573,9 +1392,6 @@ struct Eng {
     __threadfence_block();
     if (act) {
       const int slot = scr[r];
-#ifdef MXA_QREG
-      ((LDSP u64*)(scr + 64))[r] = key;  // staged for the slot's owner lane
-#else
       if constexpr (TIER) {
         qk_put(slot, key);
         qs_put(slot, seq + (u32)r);
@@ -1583,7 +1399,6 @@ struct Eng {
         qk[slot] = key;
         qs[slot] = seq + (u32)r;
       }
-#endif
       Msg mw = m;
       if (r < n - 1) mw.w[0] |= MF_RUN;
       if constexpr (PL_LDS) pl_write(slot, mw);
@@ -1591,13 +1406,6 @@ struct Eng {
         for (int i = 0; i < PW; i++) qpl[slot * PW + i] = mw.w[i];
     }
     __threadfence_block();
-#ifdef MXA_QREG
-    for (int t = 0; t < SQ; t++) {
-      const bool mine = tj[t] >= 0;
-      const u64 k = mine ? ((LDSP u64*)(scr + 64))[base + t] : KEY_EMPTY;
-      qset(tj[t], k, seq + (u32)(base + t), mine);
-    }
-#endif
     if constexpr (QHIER) {  // only the new slots changed: fold them into the group mins
       for (int t = 0; t < SQ; t++) {
         if (tj[t] < 0) break;
@@ -1614,20 +1422,6 @@ struct Eng {
     note_max_q();
   }
   // lexicographic wave-min of the per-lane cached (key, seq); returns winning slot or -1
-#ifdef MXA_KEY96
-  DEV int q_peek(u64& key, u32& seq) {
-    u64 k = mk;
-    u32 s = ms;
-    wmin_key(k, s);
-    key = k;
-    seq = s;
-    if (k == KEY_EMPTY) return -1;
-    u64 b = bal(mk == k && ms == s);
-    int L = ffs64(b);
-    int j = rdli(mj, L);
-    return j * 64 + L;
-  }
-#else
   // three 32-bit wave-mins (key high word, key low word, seq), each only while the previous
   // word still ties across lanes: (key, seq) pairs are unique, so a single candidate lane
   // after any phase is the winner
@@ -1649,24 +1443,6 @@ struct Eng {
     seq = rdl(ms, L);
     return rdli(mj, L) * 64 + L;
   }
-#endif
-#ifdef MXA_DIVERGENT_Q
-  DEV void q_remove(int slot) {
-    if (lane == (slot & 63)) {
-      qk_put(slot, KEY_EMPTY);
-      qs_put(slot, 0xFFFFFFFFu);
-      qfree |= qm_bit(slot >> 6);
-      q_rescan();
-    }
-    qcount--;
-  }
-  DEV void q_rekey(int slot, u64 key) {
-    if (lane == (slot & 63)) {
-      qk_put(slot, key);
-      q_rescan();
-    }
-  }
-#else
   DEV void q_remove(int slot) {
     qset(slot >> 6, KEY_EMPTY, 0xFFFFFFFFu, lane == (slot & 63));
     qfree |= (lane == (slot & 63)) ? qm_bit(slot >> 6) : (QM)0;
@@ -1700,7 +1476,6 @@ struct Eng {
     ms = me ? ms : s0;
     mj = me ? mj : j0;
   }
-#endif
 
   // ---------------- kernel services
   // Kernel.sendMessage (Kernel.py:347-425)
@@ -1878,42 +1653,17 @@ struct Eng {
   }
 
   // ---------------- order book pool (VGPR resident)
-  // best-price cache (BEST_CACHE): side s's best price while bok bit s is set.  A new order
-  // can only improve it; removing an order AT the cached price clears the bit (the level may
-  // have emptied); bulk book writes (launch load, event runs) clear both.  b_best rescans the
-  // pool only when the bit is clear
-#ifdef MXA_BEST_CACHE
-  static constexpr bool BEST_CACHE = true;
-#else
-  static constexpr bool BEST_CACHE = false;
-#endif
-  i32 bbest[2];
-  u32 bok;
-  DEV void b_inval() { bok = 0; }
+  // (a best-price cache, invalidated when an order at the cached price leaves, measured slower in
+  // round 3: rmsc03 40.6 -> 44.8 ms, sparse_zi_1000 unchanged)
   DEV i32 b_best(int buy_side) {  // best bid (max) or best ask (min); INT_MIN/INT_MAX if empty
     PROF_SCOPE(68);
-    if constexpr (BEST_CACHE) {
-      if ((bok >> buy_side) & 1) return buy_side ? bbest[1] : bbest[0];
-    }
     i32 v = buy_side ? INT32_MIN : INT32_MAX;
     for (int j = 0; j < SO; j++) {
       bool m = bm[j] >= 0 && (bm[j] & 1) == buy_side;
       if (m) v = buy_side ? (bp[j] > v ? bp[j] : v) : (bp[j] < v ? bp[j] : v);
     }
     v = buy_side ? wmax_i32(v) : wmin_i32(v);
-    if constexpr (BEST_CACHE) {
-      if (buy_side) bbest[1] = v;
-      else bbest[0] = v;
-      bok |= 1u << buy_side;
-    }
     return v;
-  }
-  // an order of side `buy` at `price` left the pool
-  DEV void b_gone(int buy, i32 price) {
-    if constexpr (BEST_CACHE) {
-      const i32 c = buy ? bbest[1] : bbest[0];
-      if (c == price) bok &= ~(1u << buy);
-    }
   }
   DEV i64 b_level_qty(int buy_side, i32 price) {
     i64 s = 0;
@@ -1995,10 +1745,6 @@ struct Eng {
       }
     h.b_count++;
     if (h.b_count > h.max_book) h.max_book = h.b_count;
-    if constexpr (BEST_CACHE) {
-      if (is_buy) bbest[1] = price > bbest[1] ? price : bbest[1];
-      else bbest[0] = price < bbest[0] ? price : bbest[0];
-    }
   }
   DEV void b_free(int s) {
     b_set(bm, s, -1);
@@ -2039,7 +1785,6 @@ struct Eng {
     i64 start = cur - lookback;
     i64 vol = 0;
     int live_total = 0;
-#ifndef MXA_TV_FULLSCAN
     // Newest records first, 64 per chunk (lane L = record lo + L, chronological).  Records are
     // appended in time order, so once a chunk's oldest record is before `start` every older
     // record is too, and the window is usually inside the newest chunk.  Whether ANY live
@@ -2089,7 +1834,6 @@ struct Eng {
     }
     if (!any) *perr = 1;  // pandas raises when no transaction records exist
     return vol;
-#endif
     for (int b = 0; b < n; b += 64) {
       int k = b + lane;  // k-th record in chronological order
       bool live = false, dup = false, inwin = false;
@@ -2214,7 +1958,6 @@ struct Eng {
         if (qty >= hq) {
           mq = hq;
           b_free(s);
-          b_gone(opp, best);
         } else {
           mq = qty;
           b_set(bq, s, hq - qty);
@@ -2262,7 +2005,6 @@ struct Eng {
     if (s < 0) return;
     i32 q = b_get(bq, s), o = b_get(bo, s), mm = b_get(bm, s), p = b_get(bp, s);
     b_free(s);
-    b_gone(buy, p);
     if constexpr (BLOG) bl_put(cur, -p, buy ? q : -q);
     Msg r = msg_order(MK_CANCELLED, o, mm >> 1, mm & 1, q, p, 0);
     ex_notify(m_agent(m), r);
@@ -4819,11 +4561,7 @@ struct Eng {
   // Handled: CANCEL_ORDER and non-crossing LIMIT_ORDER runs at the exchange, ORDER_ACCEPTED and
   // ORDER_CANCELLED runs at a background TradingAgent.  About 95 % of rmsc03's pops are such
   // members (the market maker's cancel / re-quote cycle every second).
-#if defined(MXA_NO_RUNS) || defined(MXA_QREG)
-  static constexpr bool RUNS = false;
-#else
   static constexpr bool RUNS = ACK_FAST && BATCH && PL_LDS;
-#endif
   // members of the run that starts at (key, s0): lane i gets member i's queue slot (-1 past
   // the run); returns the run length (consecutive seqs from s0 that carry `key`)
   DEV int run_collect(u64 key, u32 s0, int& mslot) {
@@ -4913,7 +4651,6 @@ struct Eng {
       found = s >= 0;
       for (int j = 0; j < SO; j++) bm[j] = hit[j] >= 0 ? -1 : bm[j];  // b_free
       h.b_count -= nfreed;
-      b_inval();
     } else {
       for (int i = 0; i < n; i++) {
         const u32 w0 = rdl(mm.w[0], i);
@@ -4921,7 +4658,6 @@ struct Eng {
         if (s >= 0) {
           const i32 q = b_get(bq, s), mt = b_get(bm, s);
           b_free(s);
-          b_inval();
           const bool me = lane == i;
           found = me || found;
           nq = me ? q : nq;
@@ -4997,7 +4733,6 @@ struct Eng {
         }
         base += __popcll(fb);
       }
-      b_inval();
       h.arrival = arr0 + (u32)m;
       h.b_count += m;
       if (h.b_count > h.max_book) h.max_book = h.b_count;
@@ -5109,7 +4844,6 @@ struct Eng {
       if constexpr (GYM) {
         if (end_step) break;  // GymKernel.stepRunner: `while not end_step and ...`
       }
-#ifndef MXA_NO_LAUNDER_ENV
       {  // opaque per event: env-derived addresses are recomputed, not pinned in SGPRs by LICM
          // (without this the event loop hoists ~1000 SGPRs of addresses and spills them)
         u64 pv = (u64)env;
@@ -5117,12 +4851,9 @@ struct Eng {
         u32 phi = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(pv >> 32));
         asm volatile("" : "+s"(plo), "+s"(phi));
         env = (EnvPtr)(GLBP char*)(((u64)phi << 32) | plo);
-#ifndef MXA_NO_LAUNDER_LANE
         // lane-derived masks (lane == field/2 ...) are rebuilt per use, not hoisted
         asm volatile("" : "+v"(lane));
-#endif
       }
-#endif
       PROF_T(t0);
       u64 key;
       u32 eseq;
@@ -5166,7 +4897,6 @@ struct Eng {
           }
         }
       }
-#ifndef MXA_NO_ACK_FAST
       if constexpr (ACK_FAST || RP_FAST) {
         if (type == MT_MESSAGE && rcp == 0) {
           // ExchangeAgent.receiveMessage reads nothing from its agent record but the
@@ -5240,7 +4970,6 @@ struct Eng {
           continue;
         }
       }
-#endif
       PROF_ADD(0, t0);
       // (the exchange's record is not fetched early: its messages take the fast path)
       if constexpr (EARLY_REC) {
@@ -5930,38 +5659,6 @@ __global__ __launch_bounds__(64) void mxa_rng_probe_kernel(uint32_t seed, int mo
     if (__lane_id() == 0) out[i] = v;
   }
 }
-// the run kernel's normal draws (rs_gauss_wave): mode 0 from the MT block in HBM (agent
-// streams), mode 1 through a 64-word LDS window (global streams); blocks are materialized as
-// the run kernel's event boundary does (rs_maint), so the sequence must equal mode 3 above
-__global__ __launch_bounds__(64) void mxa_rng_probe_wave_kernel(uint32_t seed, int mode, double a, double b, int n, double* out,
-                                                                uint32_t* scratch) {
-  __shared__ uint32_t win[64];
-  mxa::mt_seed(scratch, seed);
-  mxa::RSt<false> r;
-  r.key = scratch;
-  r.p = MXA_MT_N;
-  r.m = 0;
-  r.hasg = 0;
-  r.gauss = 0;
-  r.lw = mode == 1 ? (LDSP uint32_t*)win : nullptr;
-  r.lw0 = r.p;
-  r.lwn = 0;
-  for (int i = 0; i < n; i++) {
-    mxa::rs_maint(r);
-    double g;
-    if (r.hasg & 1) {  // legacy_gauss's cached second value
-      g = r.gauss;
-      r.hasg &= ~1;
-      r.gauss = 0.0;
-    } else {
-      g = mxa::rs_gauss_wave(r);
-    }
-    const double v = a + b * g;
-    if (__lane_id() == 0) out[i] = v;
-  }
-  if (__lane_id() == 0) out[n] = (double)(r.hasg & 2);  // a look-ahead overrun would be a probe bug
-}
-
 __global__ void mxa_math_probe_kernel(int mode, const double* x, const double* y, double* out, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

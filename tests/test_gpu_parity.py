@@ -45,25 +45,6 @@ def test_device_rng_matches_numpy_kats(mx, golden):
         assert out.tolist() == [float(x) for x in ref]
 
 
-def test_device_wave_gauss_equals_serial(mx):
-    """rs_gauss_wave (the run kernel's normal draws: 16 polar candidates across the wave, first
-    accepted wins) against the serial legacy_gauss loop and the oracle, from an HBM stream and
-    through the LDS window, over enough draws to cross many MT blocks and rejections"""
-    L = mx.load()
-    n = 5000
-    for seed in (424242, 7, 123456789):
-        ref = np.zeros(n, dtype=np.float64)
-        assert L.mxa_rng_probe(0, seed, 3, 1e5, 100.0, n, ref.ctypes.data) == 0
-        r = pyoracle.RandomState(seed)
-        assert ref.tolist() == [float(r.normal(1e5, 100.0)) for _ in range(n)]
-        for mode in (6, 7):
-            out = np.zeros(n + 1, dtype=np.float64)
-            assert L.mxa_rng_probe(0, seed, mode, 1e5, 100.0, n, out.ctypes.data) == 0
-            assert out[n] == 0, "look-ahead overrun in the probe"
-            bad = np.nonzero(out[:n] != ref)[0]
-            assert len(bad) == 0, (seed, mode, int(bad[0]))
-
-
 def test_device_glibc_math(mx):
     import ctypes
     L = mx.load()
