@@ -558,6 +558,30 @@ def traffic_record(config, envs, parity_hash, tape=None):
     return p.get("bytes_per_launch"), src
 
 
+def issue_record(config, envs, parity_hash, tape=None):
+    """The dominant kernel's instruction issue rates from the SQ counter record of THIS build
+    (profiles/issue_<config>.json, tools/sq_counters.sh + tools/issue_summary.py: separate rocprofv3
+    --pmc passes of this bench command): instructions of each type per CU per elapsed cycle.  A CU
+    issues at most one instruction of a type per cycle (one scalar unit per CU), so SALU near 1.0
+    means the scalar unit bounds the kernel.  Matched like traffic_record."""
+    import mxabides
+    name = config if tape in (None, "IBM_2003-01-14") else "%s_%s" % (config, tape)
+    prof = os.path.join(ROOT, "profiles", "issue_%s.json" % name)
+    if not os.path.exists(prof):
+        return None
+    with open(prof) as f:
+        p = json.load(f)
+    bid = mxabides.build_id()
+    ok = (p.get("build_id") == bid and p.get("config") == config and p.get("envs") == envs
+          and bool(p.get("parity_hash")) == parity_hash)
+    out = {"record": os.path.relpath(prof, ROOT), "build_id": p.get("build_id"), "match": ok}
+    if ok:
+        out["per_cu_cycle"] = p["per_cu_cycle"]
+        out["per_event"] = p["per_event"]
+        out["ceiling"] = "1.0 instruction of a type per CU per cycle"
+    return out
+
+
 def host_info():
     model = None
     try:
@@ -670,6 +694,9 @@ def main():
                                "nominal_bytes_per_event": NOMINAL_BYTES_PER_EVENT}
             if traffic:
                 out["roofline"]["traffic_per_event"] = traffic / my_ev_per_launch
+            iss = issue_record(args.config, eng.n, bool(args.parity_hash), args.tape)
+            if iss:
+                out["roofline"]["issue"] = iss
             if not args.no_count:
                 strict = mc.strict_bytes_per_event(eng.last_counters)
                 a_strict = strict * my_ev_per_launch / (avg_ms * 1e-3) / 1e9

@@ -91,7 +91,10 @@ enum {
   ERR_TWAP_MARKET = 27,   // placeMarketOrder at horizon[-2] (not restated; unreachable in the script)
   // SpreadBasedMarketMakerAgent.receiveMessage: a QUERY_SPREAD with a missing side before any mid
   // was known leaves `mid` unbound (UnboundLocalError)
-  ERR_SB_MID = 28
+  ERR_SB_MID = 28,
+  // an order quantity beyond the device's 32-bit order words (POVMarketMakerAgent: pov x transacted
+  // volume with a large --mm-pov); the reference's Python int has no bound, so the env stops
+  ERR_ORDER_SIZE = 29
 };
 
 // per-env scalar header (first bytes of the env block)

@@ -52,7 +52,8 @@ ERR_NAMES = {0: "none", 1: "event queue capacity", 2: "order book capacity", 3: 
              25: "ExecutionAgent.placeOrders: schedule[Interval(t, t + 30 s)] of a 60 s TWAP schedule (KeyError)",
              26: "ExecutionAgent.placeOrders: (bid + ask) / 2 with a None side (TypeError)",
              27: "ExecutionAgent.placeOrders: placeMarketOrder at horizon[-2] (not restated)",
-             28: "SpreadBasedMarketMakerAgent: mid unbound (UnboundLocalError)"}
+             28: "SpreadBasedMarketMakerAgent: mid unbound (UnboundLocalError)",
+             29: "order quantity beyond the device's 32-bit order words (POVMarketMakerAgent pov x volume)"}
 
 
 class EnvSummary(ctypes.Structure):

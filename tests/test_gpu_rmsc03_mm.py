@@ -100,3 +100,14 @@ def test_gpu_mixed_options_bench_size_equal_oracle(mx):
         assert (er == 0).all()
         bad = np.nonzero((s["status"] != 1) | (s["events"] != ev) | (s["hash"] != hs))[0]
         assert len(bad) == 0, [(int(i), int(s["err"][i]), p[i]) for i in bad[:10]]
+
+
+def test_gpu_mm_order_size_beyond_int32_is_an_env_error(mx):
+    """pov x transacted volume beyond the 32-bit order words: the env stops with error 29
+    (ERR_ORDER_SIZE), never a wrapped order size; the reference's Python int has no
+    bound, so this is a capacity error of the device, not a reference path"""
+    seeds = [30, 31, 32, 33]
+    m = mx.VecMarket("rmsc03", seeds, mm_params=mm_params(len(seeds), pov=1e6))
+    m.run()
+    s = m.summary()
+    assert (s["status"] == 2).all() and (s["err"] == 29).all(), (s["status"], s["err"])

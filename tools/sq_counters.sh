@@ -36,3 +36,4 @@ for k, d in tot.items():
         print("  %-24s %.4g" % (c, d[c]))
 PY
 cat $OUT/summary.txt
+python3 tools/issue_summary.py $OUT $CFG $ENVS
