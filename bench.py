@@ -425,6 +425,43 @@ class GymEngine(Engine):
     def gym_steps(self):
         return self.n * self.ctx.world * self.n_steps
 
+    def latency_bound(self):
+        """SURVEY.md §8(d)'s latency bound for the step kernel: resident envs / the per-event
+        latency of one env's serial chain, measured on one env per CU (256 envs, a full episode of
+        the same action distribution, step kernels timed on the handle's stream)"""
+        torch = self.torch
+        from mxabides.gym import ACTION_SIZE, OBS_SIZE, VecABIDESEnv
+        n = 256
+        s = (VecABIDESEnv(self.tp, n, device=self.ctx.local) if self.replay else
+             VecABIDESEnv(seeds=self.seeds(0)[:n], device=self.ctx.local))
+        s.set_stream(self.stream.cuda_stream)
+        s.set_parity_hash(self.args.parity_hash)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(7)
+        act = torch.rand((self.n_steps, n, ACTION_SIZE), generator=g, dtype=torch.float64, device="cuda")
+        act[:, :, 0] *= 0.01
+        obs = torch.empty((n, OBS_SIZE), dtype=torch.float64, device="cuda")
+        flags = torch.empty((n,), dtype=torch.int32, device="cuda")
+        s.reset()
+        pairs = []
+        for i in range(self.n_steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(self.stream)
+            s.step_device(act[i].data_ptr(), obs.data_ptr(), flags.data_ptr())
+            e1.record(self.stream)
+            pairs.append((e0, e1))
+        self.stream.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in pairs)
+        ev = s.summary()["events"]
+        s.close()
+        ns = ms * 1e6 / max(1, int(ev.max()))
+        res = self.v.resident_envs
+        return {"resident_envs": res, "solo_envs": n, "solo_kernel_ms": ms, "solo_ns_per_event": ns,
+                "bound_env_steps_per_s": res / (ns * 1e-9),
+                "how": "256 envs (one per CU), one episode of %d step launches: summed step-kernel time / the "
+                       "longest env's events; resident envs = step-kernel occupancy x CUs, at most the "
+                       "workload's envs (mxa_resident_envs)" % self.n_steps}
+
     def cpu_baseline(self, threads, min_s):
         import numpy as np
         import pyoracle

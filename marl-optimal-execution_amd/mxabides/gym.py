@@ -158,6 +158,12 @@ class VecABIDESEnv:
     def last_kernel_ms(self):
         return self.L.mxa_last_kernel_ms(self._h)
 
+    @property
+    def resident_envs(self):
+        """envs resident on the device at once (step-kernel occupancy x CUs, at most n_envs;
+        include/mxa.h mxa_resident_envs)"""
+        return self._check(self.L.mxa_resident_envs(self._h), "mxa_resident_envs")
+
     def close(self):
         if self._h:
             self.L.mxa_destroy(self._h)
