@@ -18,8 +18,13 @@ N_CONFIGS = 18  # csrc/mxa_entry.h MXA_N_CONFIGS
 DEPS = ["mxa_api.hip", "mxa_inst.hip", "mxa_entry.h", "mxa_kernels.hip", "mxa_layout.h", "mxa_config.h", "glibc_math.h",
         "glibc_math_tables.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -structurizecfg-skip-uniform-regions: branches on wave-uniform conditions stay plain scalar
+# branches instead of being structurized into exec-mask regions (saveexec / restore pairs and
+# flow blocks on the event loop's paths).  The CU's one scalar unit is what bounds the run kernel
+# (instruction issue); same per-env digests, r05: rmsc03 x4096 41.0 -> 38.3 ms,
+# sparse_zi_1000 x1024 720.5 -> 607.8 ms (profiles/r05/ab_mr/ab_flags.txt)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
-         "-Wno-unused-result", "-Wno-unused-value"]
+         "-Wno-unused-result", "-Wno-unused-value", "-mllvm", "-structurizecfg-skip-uniform-regions"]
 
 
 def sources():
@@ -41,7 +46,7 @@ def up_to_date():
     if not os.path.exists(OUT):
         return False
     t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(s) <= t for s in sources())
+    return all(os.path.getmtime(s) <= t for s in sources() + [os.path.abspath(__file__)])
 
 
 def build(force=False, verbose=True, jobs=None):

@@ -321,8 +321,10 @@ static int check_mm(const mxa_mm_params* p, int n) {
   for (int i = 0; i < n; i++) {
     const mxa_mm_params& x = p[i];
     // the reference raises nowhere on these, but a negative window / tick count, a
-    // non-positive wake-up period or a size beyond int32 is no option the script can run
-    if (!(x.mm_pov == x.mm_pov) || x.mm_pov < 0 || x.mm_pov > 1e6 || x.mm_min_order_size < 0 || x.mm_window_size < 0 ||
+    // non-positive wake-up period or a NaN / negative pov is no option the script can run.  A pov
+    // whose order size outgrows the 32-bit order words stops that env with MXA_ERR_ORDER_SIZE
+    // at the order (the cap here only keeps pov x volume exact in a double)
+    if (!(x.mm_pov == x.mm_pov) || x.mm_pov < 0 || x.mm_pov > 1e12 || x.mm_min_order_size < 0 || x.mm_window_size < 0 ||
         x.mm_num_ticks < 0 || x.mm_num_ticks > 100000 || x.mm_wake_up_freq_ns <= 0)
       return MXA_EINVAL;
   }

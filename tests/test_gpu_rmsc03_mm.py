@@ -105,9 +105,11 @@ def test_gpu_mixed_options_bench_size_equal_oracle(mx):
 def test_gpu_mm_order_size_beyond_int32_is_an_env_error(mx):
     """pov x transacted volume beyond the 32-bit order words: the env stops with error 29
     (ERR_ORDER_SIZE), never a wrapped order size; the reference's Python int has no
-    bound, so this is a capacity error of the device, not a reference path"""
+    bound, so this is a capacity error of the device, not a reference path.  rmsc03's exchange
+    keeps 10 orders of history (stream_history), so the transacted volume the market maker sees
+    stays in the hundreds: pov 1e9 outgrows int32 from 3 shares"""
     seeds = [30, 31, 32, 33]
-    m = mx.VecMarket("rmsc03", seeds, mm_params=mm_params(len(seeds), pov=1e6))
+    m = mx.VecMarket("rmsc03", seeds, mm_params=mm_params(len(seeds), pov=1e9))
     m.run()
     s = m.summary()
     assert (s["status"] == 2).all() and (s["err"] == 29).all(), (s["status"], s["err"])

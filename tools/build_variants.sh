@@ -7,7 +7,7 @@ for spec in "$@"; do
   IFS=: read name root flags <<< "$spec"
   [ "$root" = "." ] && root=$R
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -fno-fast-math -fPIC -shared \
-    -Wno-unused-result -Wno-unused-value -DMXA_ONLY_RMSC03 $flags -I$root/marl-optimal-execution_amd/csrc -I$root/include \
+    -Wno-unused-result -Wno-unused-value -mllvm -structurizecfg-skip-uniform-regions -DMXA_ONLY_RMSC03 $flags -I$root/marl-optimal-execution_amd/csrc -I$root/include \
     $root/marl-optimal-execution_amd/csrc/mxa_api.hip -o $R/marl-optimal-execution_amd/lib/libmxa_$name.so &
   pids+=($!)
 done

@@ -9,7 +9,7 @@ import sys
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = os.path.join(R, "marl-optimal-execution_amd/csrc/mxa_api.hip")
 out = "/tmp/isa_lines.s"
-cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fno-fast-math",
+cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fno-fast-math", "-mllvm", "-structurizecfg-skip-uniform-regions",
        "-DMXA_ONLY_RMSC03", "--cuda-device-only", "-S", "-gline-tables-only",
        "-I" + os.path.join(R, "marl-optimal-execution_amd/csrc"), "-I" + os.path.join(R, "include"), src, "-o", out] + sys.argv[1:]
 subprocess.check_call(cmd, stderr=subprocess.DEVNULL)
