@@ -39,6 +39,24 @@ constexpr int lat_lds(int cfg);
 #ifndef MXA_W_RMSC02
 #define MXA_W_RMSC02 2
 #endif
+// rmsc02's book arrays held in LDS for a launch instead of VGPRs (bit: 0 price, 1 qty, 2 order id,
+// 3 agent/side, 4 arrival, 5 history epoch).  The 576-slot book in VGPRs left the run kernel at 256
+// VGPRs and 352 B/lane of scratch, ~900 B/event of spill writes in the PMC record (r05).  The
+// order id, arrival and epoch arrays (read only when an order is matched or cancelled) move to LDS,
+// price / side / quantity (every best-price and level scan) stay in VGPRs; 88 B/lane of scratch
+// remain.  To keep 8 waves per CU with the payloads in LDS the queue has 4 slots per lane (256;
+// the oracle's maximum over the 131,072 bench seeds is 225 pending events, a full queue is env
+// error 1).  r05 A/B, rmsc02 x4096 run kernel, same digest (profiles/r05/ab_mr/ab_book.txt): 871.5
+// -> 816.9 ms; the whole book in LDS with HBM payloads 936.5, HBM payloads alone 1052.4
+#ifndef MXA_BOOK_LDS_RMSC02
+#define MXA_BOOK_LDS_RMSC02 0x34
+#endif
+#ifndef MXA_PL_RMSC02
+#define MXA_PL_RMSC02 1
+#endif
+#ifndef MXA_SQ_RMSC02
+#define MXA_SQ_RMSC02 4
+#endif
 #ifndef MXA_SO_RMSC02
 // 576 book slots: the oracle's maximum over every seed of bench.py --gpus <= 8 is 537 (512
 // overflowed).  The book lives in VGPRs: 640 slots measured 1319 ms against 1054 ms for 576
@@ -119,8 +137,8 @@ constexpr Shape shape(int cfg) {
        : cfg == MXA_CFG_RMSC01 ? Shape{3, 2, true, MXA_RMSC01_WAVES, 8, 0}
        // rmsc02: oracle maxima over the 131,072 seeds bench.py draws at --gpus 1-8 (batches 0-3 of
        // ranks 0-7, tools/capacity_sweep.py, profiles/r04/capacity_rmsc02.json): 225 pending
-       // events, 537 resting orders, 59 open orders of one agent (576 book slots)
-       : cfg == MXA_CFG_RMSC02 ? Shape{6, MXA_SO_RMSC02, true, MXA_W_RMSC02, 8, 0}
+       // events (256 queue slots), 537 resting orders, 59 open orders of one agent (576 book slots)
+       : cfg == MXA_CFG_RMSC02 ? Shape{MXA_SQ_RMSC02, MXA_SO_RMSC02, MXA_PL_RMSC02 != 0, MXA_W_RMSC02, 8, 0}
        // obi_rmsc02: oracle maxima over the 131,072 seeds of bench.py --gpus 1-8: 211 pending
        // events, 149 resting orders (192 book slots; 128 overflowed)
        : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 3, true, MXA_W_OBI, 8, 0}
@@ -147,12 +165,14 @@ constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(c
 constexpr bool rp_hdr_lds(int cfg) {
   return cfg == MXA_CFG_MARKETREPLAY || cfg == MXA_CFG_MARKETREPLAY_RUNNER || cfg == MXA_CFG_MARKETREPLAY_TWAP;
 }
+constexpr int book_lds(int cfg) { return cfg == MXA_CFG_RMSC02 ? MXA_BOOK_LDS_RMSC02 : 0; }
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)sq_lds(cfg) * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
          + 1024                                                                               // RNG stream windows
          + (size_t)lat_lds(cfg) * 8                                                           // exchange latency row
          + (rp_hdr_lds(cfg) ? 256 : 0)                                                        // RpHdr (replay / gym)
+         + (size_t)__builtin_popcount(book_lds(cfg)) * shape(cfg).so * 256                    // LDS book arrays
          + 256  // batched-push scratch: slot table
 #ifdef MXA_PROF
          + 1024  // phase counters and inclusive function timers (128 x u64)

@@ -755,9 +755,28 @@ struct Eng {
     else return rdl64(m, L);
   }
   QM qfree;
-  // order book pool in VGPRs: slot (j, lane)
-  i32 bp[SO], bq[SO], bo[SO], bm[SO], bh[SO];
-  u32 ba[SO];
+  // order book pool in VGPRs: slot (j, lane).  An array whose bit is set in BKL lives in LDS for
+  // a launch instead (mxa_cfg::book_lds; the builder keeps VGPR arrays and writes the env block),
+  // at [j][64], read and written through BkL with the same bp[j] syntax
+  template <class T>
+  struct BkL {
+    LDSP T* p;  // this lane's element of slot row 0
+    DEV LDSP T& operator[](int j) const { return p[j * 64]; }
+  };
+  static constexpr int BKL = BUILD ? 0 : mxa_cfg::book_lds(CFG);
+  template <int BIT, class T>
+  using BkT = typename std::conditional<((BKL >> BIT) & 1) != 0, BkL<T>, T[SO]>::type;
+  BkT<0, i32> bp;
+  BkT<1, i32> bq;
+  BkT<2, i32> bo;
+  BkT<3, i32> bm;
+  BkT<4, u32> ba;
+  BkT<5, i32> bh;
+  template <int BIT, class A>
+  DEV void bk_bind(A& a, LDSP char* base) {
+    if constexpr (((BKL >> BIT) & 1) != 0)
+      a.p = (decltype(a.p))(base + (size_t)__builtin_popcount(BKL & ((1 << BIT) - 1)) * SO * 256) + lane;
+  }
   // HBL configurations: OrderBook.history restated as an order-history ring in HBM (one OhRec
   // per handled limit order); a resting order keeps its record index to flag its transactions
   static constexpr bool OH = PC.n_hbl > 0;
@@ -836,6 +855,15 @@ struct Eng {
 #endif
     latl = (LDSP double*)(hotrec + mxa_cfg::shape(CFG).hot * 64);
     rhl = (LDSP RpHdr*)(latl + mxa_cfg::lat_lds(CFG));
+    if constexpr (BKL != 0) {
+      LDSP char* bk = (LDSP char*)rhl + (mxa_cfg::rp_hdr_lds(CFG) ? 256 : 0);
+      bk_bind<0>(bp, bk);
+      bk_bind<1>(bq, bk);
+      bk_bind<2>(bo, bk);
+      bk_bind<3>(bm, bk);
+      bk_bind<4>(ba, bk);
+      bk_bind<5>(bh, bk);
+    }
   }
 
   // ---------------- env block accessors
@@ -1690,15 +1718,25 @@ struct Eng {
     }
     return -1;
   }
-  DEV i32 b_get(const i32* arr, int slot) {
-    i32 v = 0;
-    for (int j = 0; j < SO; j++)
-      if (j == (slot >> 6)) v = rdli(arr[j], slot & 63);
-    return v;
+  template <class A>
+  DEV i32 b_get(const A& arr, int slot) {
+    if constexpr (!std::is_array<A>::value) {  // LDS: one broadcast read
+      return __builtin_amdgcn_readfirstlane((i32)arr.p[slot - lane]);
+    } else {
+      i32 v = 0;
+      for (int j = 0; j < SO; j++)
+        if (j == (slot >> 6)) v = rdli(arr[j], slot & 63);
+      return v;
+    }
   }
-  DEV void b_set(i32* arr, int slot, i32 v) {
-    for (int j = 0; j < SO; j++)
-      if (j == (slot >> 6) && lane == (slot & 63)) arr[j] = v;
+  template <class A>
+  DEV void b_set(A& arr, int slot, i32 v) {
+    if constexpr (!std::is_array<A>::value) {
+      if (lane == (slot & 63)) arr.p[slot - lane] = v;
+    } else {
+      for (int j = 0; j < SO; j++)
+        if (j == (slot >> 6) && lane == (slot & 63)) arr[j] = v;
+    }
   }
   DEV int b_free_slot() {
     for (int j = 0; j < SO; j++) {
