@@ -54,6 +54,9 @@ constexpr int lat_lds(int cfg);
 #ifndef MXA_PL_RMSC02
 #define MXA_PL_RMSC02 1
 #endif
+#ifndef MXA_HOT_RMSC02
+#define MXA_HOT_RMSC02 0
+#endif
 #ifndef MXA_SQ_RMSC02
 #define MXA_SQ_RMSC02 4
 #endif
@@ -138,7 +141,7 @@ constexpr Shape shape(int cfg) {
        // rmsc02: oracle maxima over the 131,072 seeds bench.py draws at --gpus 1-8 (batches 0-3 of
        // ranks 0-7, tools/capacity_sweep.py, profiles/r04/capacity_rmsc02.json): 225 pending
        // events (256 queue slots), 537 resting orders, 59 open orders of one agent (576 book slots)
-       : cfg == MXA_CFG_RMSC02 ? Shape{MXA_SQ_RMSC02, MXA_SO_RMSC02, MXA_PL_RMSC02 != 0, MXA_W_RMSC02, 8, 0}
+       : cfg == MXA_CFG_RMSC02 ? Shape{MXA_SQ_RMSC02, MXA_SO_RMSC02, MXA_PL_RMSC02 != 0, MXA_W_RMSC02, 8, MXA_HOT_RMSC02}
        // obi_rmsc02: oracle maxima over the 131,072 seeds of bench.py --gpus 1-8: 211 pending
        // events, 149 resting orders (192 book slots; 128 overflowed)
        : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 3, true, MXA_W_OBI, 8, 0}

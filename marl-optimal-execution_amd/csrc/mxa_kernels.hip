@@ -1323,10 +1323,20 @@ struct Eng {
   DEV void pl_write(int slot, const Msg& m) {
     for (int i = 0; i < PW; i++) qpl[slot * PW + i] = m.w[i];
   }
+  // the popped message's words as SGPRs (readfirstlane) in the configurations listed: where the
+  // run kernel sits at its VGPR budget the message was spilled at every pop (rmsc02: a 12-byte
+  // scratch store per lane per event, ~800 B/event of HBM writes, r05)
+#ifndef MXA_MSG_SGPR_MASK
+#define MXA_MSG_SGPR_MASK 0
+#endif
+  static constexpr bool MSG_S = !BUILD && (((MXA_MSG_SGPR_MASK) >> CFG) & 1);
   DEV Msg pl_read(int slot) {
     Msg m;
-    // (readfirstlane'd SGPR copies of the words measured 3 % slower: r01 s3b)
-    for (int i = 0; i < PW; i++) m.w[i] = qpl[slot * PW + i];
+    // (readfirstlane'd SGPR copies of the words measured 3 % slower on rmsc03: r01 s3b)
+    for (int i = 0; i < PW; i++) {
+      const u32 v = qpl[slot * PW + i];
+      m.w[i] = MSG_S ? (u32)__builtin_amdgcn_readfirstlane((int)v) : v;
+    }
     for (int i = PW; i < 8; i++) m.w[i] = 0;
     return m;
   }
@@ -3343,7 +3353,13 @@ struct Eng {
         t23 += cat == 2 ? 1u : cat == 3 ? 0x10000u : 0u;
       }
     }
-    __threadfence();
+    // every lane's atomics performed at L2 before any lane reads a bucket back, and the reads
+    // bypass the CU's L1 (agent-scope loads below), which may hold a stale line of the buckets.  A
+    // device-scope __threadfence here also wrote back this XCD's whole L2 on every call: ~900 B of
+    // HBM writes per rmsc02 event (r05 PMC, tools/ab_traffic.sh)
+    wfence();
+    __builtin_amdgcn_s_waitcnt(0);
+    wfence();
     t01 = wsum_u32(t01);
     t23 = wsum_u32(t23);
     const i64 T0 = t01 & 0xFFFF, T1 = t01 >> 16, T2 = t23 & 0xFFFF, T3 = t23 >> 16;
@@ -3354,7 +3370,7 @@ struct Eng {
       const i64 i = b + lane;
       u64 x = 0;
       if (i < NB) {
-        x = hist[i];
+        x = __hip_atomic_load(&hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         hist[i] = 0;
       }
       const u32 c01 = (u32)(x & 0xFFFF) | ((u32)((x >> 16) & 0xFFFF) << 16);
