@@ -47,15 +47,13 @@ constexpr int lat_lds(int cfg);
 // remain.  To keep 8 waves per CU with the payloads in LDS the queue has 4 slots per lane (256;
 // the oracle's maximum over the 131,072 bench seeds is 225 pending events, a full queue is env
 // error 1).  r05 A/B, rmsc02 x4096 run kernel, same digest (profiles/r05/ab_mr/ab_book.txt): 871.5
-// -> 816.9 ms; the whole book in LDS with HBM payloads 936.5, HBM payloads alone 1052.4
+// -> 816.9 ms; the whole book in LDS with HBM payloads 936.5, HBM payloads alone 1052.4.  (The
+// exchange record in LDS as well, which fills the 160 KB exactly: 815.1 -> 817.5 ms, r05)
 #ifndef MXA_BOOK_LDS_RMSC02
 #define MXA_BOOK_LDS_RMSC02 0x34
 #endif
 #ifndef MXA_PL_RMSC02
 #define MXA_PL_RMSC02 1
-#endif
-#ifndef MXA_HOT_RMSC02
-#define MXA_HOT_RMSC02 0
 #endif
 #ifndef MXA_SQ_RMSC02
 #define MXA_SQ_RMSC02 4
@@ -141,7 +139,7 @@ constexpr Shape shape(int cfg) {
        // rmsc02: oracle maxima over the 131,072 seeds bench.py draws at --gpus 1-8 (batches 0-3 of
        // ranks 0-7, tools/capacity_sweep.py, profiles/r04/capacity_rmsc02.json): 225 pending
        // events (256 queue slots), 537 resting orders, 59 open orders of one agent (576 book slots)
-       : cfg == MXA_CFG_RMSC02 ? Shape{MXA_SQ_RMSC02, MXA_SO_RMSC02, MXA_PL_RMSC02 != 0, MXA_W_RMSC02, 8, MXA_HOT_RMSC02}
+       : cfg == MXA_CFG_RMSC02 ? Shape{MXA_SQ_RMSC02, MXA_SO_RMSC02, MXA_PL_RMSC02 != 0, MXA_W_RMSC02, 8, 0}
        // obi_rmsc02: oracle maxima over the 131,072 seeds of bench.py --gpus 1-8: 211 pending
        // events, 149 resting orders (192 book slots; 128 overflowed)
        : cfg == MXA_CFG_OBI_RMSC02 ? Shape{4, 3, true, MXA_W_OBI, 8, 0}

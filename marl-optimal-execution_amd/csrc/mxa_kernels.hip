@@ -1323,20 +1323,11 @@ struct Eng {
   DEV void pl_write(int slot, const Msg& m) {
     for (int i = 0; i < PW; i++) qpl[slot * PW + i] = m.w[i];
   }
-  // the popped message's words as SGPRs (readfirstlane) in the configurations listed: where the
-  // run kernel sits at its VGPR budget the message was spilled at every pop (rmsc02: a 12-byte
-  // scratch store per lane per event, ~800 B/event of HBM writes, r05)
-#ifndef MXA_MSG_SGPR_MASK
-#define MXA_MSG_SGPR_MASK 0
-#endif
-  static constexpr bool MSG_S = !BUILD && (((MXA_MSG_SGPR_MASK) >> CFG) & 1);
   DEV Msg pl_read(int slot) {
     Msg m;
-    // (readfirstlane'd SGPR copies of the words measured 3 % slower on rmsc03: r01 s3b)
-    for (int i = 0; i < PW; i++) {
-      const u32 v = qpl[slot * PW + i];
-      m.w[i] = MSG_S ? (u32)__builtin_amdgcn_readfirstlane((int)v) : v;
-    }
+    // (readfirstlane'd SGPR copies of the words measured 3 % slower on rmsc03, r01 s3b, and
+    // neutral on rmsc02 / random_fund_value / random_fund_diverse, r05 ab_rmsc02_writes.txt)
+    for (int i = 0; i < PW; i++) m.w[i] = qpl[slot * PW + i];
     for (int i = PW; i < 8; i++) m.w[i] = 0;
     return m;
   }
