@@ -92,8 +92,10 @@ constexpr int lat_lds(int cfg);
 // (bit = config id; measured per configuration)
 #ifndef MXA_DIRTY_WB_MASK
 // r03 s5: random_fund_value 840 -> 795 ms; rmsc03 +2 % (s38 on the final build: +5 %); rmsc01 +4 % in s5, but
-// -4.6 % on the final build (s48: 1023 -> 976 ms); rmsc02 unchanged (s48)
-#define MXA_DIRTY_WB_MASK ((1 << 9) | (1 << 10) | (1 << 11) | (1 << 12) | (1 << MXA_CFG_RMSC01))
+// -4.6 % on the final build (s48: 1023 -> 976 ms); rmsc02 unchanged (s48).  r05, after the HBL fence
+// fix: rmsc02 PMC writes 300 -> 240 B/event (reads 297) for 780 -> 790 ms (ab_dwb_rmsc02.txt), on;
+// obi_rmsc02 307 vs 305 ms, rmsc03 39.4 vs 38.2 ms (ab_dwb_levels.txt), off
+#define MXA_DIRTY_WB_MASK ((1 << 9) | (1 << 10) | (1 << 11) | (1 << 12) | (1 << MXA_CFG_RMSC01) | (1 << MXA_CFG_RMSC02))
 #endif
 #ifndef MXA_OPEN_RFD
 #define MXA_OPEN_RFD 128
