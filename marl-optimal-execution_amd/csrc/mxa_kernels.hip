@@ -69,6 +69,8 @@ DEV u64 rdl64(u64 v, int l) {
 DEV double rdl_d(double v, int l) { return __builtin_bit_cast(double, rdl64(__builtin_bit_cast(u64, v), l)); }
 DEV u64 bal(bool p) { return __ballot(p); }
 DEV int ffs64(u64 b) { return __ffsll((unsigned long long)b) - 1; }
+// the lowest set bit of a mask known to be non-zero: one s_ff1, without ffs64's zero test
+DEV int ctz64(u64 b) { return __builtin_ctzll(b); }
 DEV int ffs32(u32 b) { return __ffs(b) - 1; }
 DEV u32 sxor(u32 v, int m) { return (u32)__shfl_xor((int)v, m, 64); }
 // ---- wave reductions on DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast15/31
@@ -746,6 +748,14 @@ struct Eng {
       return ffs64(m);
     }
   }
+  static DEV int qm_ctz(QM m) {  // m != 0
+    if constexpr (SQ > 64) {
+      const u64 lo = (u64)m;
+      return lo ? ctz64(lo) : 64 + ctz64((u64)(m >> 64));
+    } else {
+      return ctz64(m);
+    }
+  }
   static DEV int qm_pop(QM m) {
     if constexpr (SQ > 64) return __popcll((u64)m) + __popcll((u64)(m >> 64));
     else return __popcll(m);
@@ -1249,19 +1259,19 @@ struct Eng {
     }
     q_lanemin();
   }
-  DEV void q_gupd(int j, u64 k, u32 s) {  // QHIER: slot j of this lane now holds (k, s)
+  DEV void q_gupd(int j, u64 k, u32 s, bool me = true) {  // QHIER: slot j of this lane (me) now holds (k, s)
     const int g = (TIER && j >= SQL) ? NG - 1 : j / QG;
     if constexpr (QTREE) {
 #pragma unroll
       for (int gg = 0; gg < NG; gg++) {  // selects: g differs between lanes
-        const bool w = (gg == g) & ((k < gk[gg]) | ((k == gk[gg]) & (s < gs[gg])));
+        const bool w = me & (gg == g) & ((k < gk[gg]) | ((k == gk[gg]) & (s < gs[gg])));
         gk[gg] = w ? k : gk[gg];
         gs[gg] = w ? s : gs[gg];
         gj[gg] = w ? j : gj[gg];
       }
     } else {
       for (int gg = 0; gg < NG; gg++) {
-        if (gg == g && (k < gk[gg] || (k == gk[gg] && s < gs[gg]))) {
+        if (me && gg == g && (k < gk[gg] || (k == gk[gg] && s < gs[gg]))) {
           gk[gg] = k;
           gs[gg] = s;
           gj[gg] = j;
@@ -1362,19 +1372,19 @@ struct Eng {
     // the lowest lane with a free slot (r05: a lane chosen round-robin by seq cost a 64-bit rotate
     // on the chain; placement is invisible to the pop: replay step 0.361 -> 0.356 ms, rmsc03 41.5
     // -> 40.8, sparse_zi_1000 725 -> 721, same per-env digests), then its first free slot
-    const int L = ffs64(b);
-    const int jl = qm_ffs(qm_rdl(use, L));
-    qset(jl, key, seq, lane == L);
-    if (lane == L) {
-      qfree &= ~qm_bit(jl);
-      if (key < mk || (key == mk && seq < ms)) {
-        mk = key;
-        ms = seq;
-        mj = jl;
-      }
-      if constexpr (QHIER) q_gupd(jl, key, seq);
-      if (PL_LDS) pl_write(jl * 64 + lane, m);
-    }
+    const int L = ctz64(b);
+    const int jl = qm_ctz(qm_rdl(use, L));  // lane L has a free slot
+    const bool me = lane == L;
+    qset(jl, key, seq, me);
+    // lane L's minimum and free mask by selects, not a branch: the short-circuit test inside a
+    // lane-divergent region compiled to ~10 exec-mask instructions on the scalar unit per push
+    const bool lt = me & ((key < mk) | ((key == mk) & (seq < ms)));
+    mk = lt ? key : mk;
+    ms = lt ? seq : ms;
+    mj = lt ? jl : mj;
+    qfree = me ? (qfree & ~qm_bit(jl)) : qfree;
+    if constexpr (QHIER) q_gupd(jl, key, seq, me);
+    if (PL_LDS && me) pl_write(jl * 64 + lane, m);
     if (!PL_LDS) {
       const int slot = jl * 64 + L;
       if (lane < PW) qpl[slot * PW + lane] = msel(m, lane);
@@ -1467,7 +1477,7 @@ struct Eng {
         b = bal(kh == m1 && kl == m2 && ms == m3);
       }
     }
-    const int L = ffs64(b);
+    const int L = ctz64(b);
     key = ((u64)m1 << 32) | rdl(kl, L);
     seq = rdl(ms, L);
     return rdli(mj, L) * 64 + L;
@@ -1700,6 +1710,35 @@ struct Eng {
       if (bm[j] >= 0 && (bm[j] & 1) == buy_side && bp[j] == price) s += bq[j];
     return wsum_i64(s);
   }
+  // the SPREAD reply's inside of both sides in two fused passes (OrderBook.getInsideBids/Asks(1)):
+  // best bid / ask (INT_MIN / INT_MAX if a side is empty) and the quantity at each.  The level
+  // sums take one packed 32-bit wave sum when every lane's partials are below 2^10 (the totals
+  // then fit 16 bits each), else two 64-bit ones.  b_best x2 + b_level_qty x2 before: four passes
+  // over the pool and six DPP reductions
+  DEV void b_inside(i32& bb, i32& aa, i64& bqs, i64& aqs) {
+    i32 vb = INT32_MIN, va = INT32_MAX;
+    for (int j = 0; j < SO; j++) {
+      const bool live = bm[j] >= 0, buy = (bm[j] & 1) != 0;
+      vb = live && buy && bp[j] > vb ? bp[j] : vb;
+      va = live && !buy && bp[j] < va ? bp[j] : va;
+    }
+    bb = wmax_i32(vb);
+    aa = wmin_i32(va);
+    i64 sb = 0, sa = 0;
+    for (int j = 0; j < SO; j++) {
+      const bool live = bm[j] >= 0, buy = (bm[j] & 1) != 0;
+      sb += live && buy && bp[j] == bb ? (i64)bq[j] : 0;
+      sa += live && !buy && bp[j] == aa ? (i64)bq[j] : 0;
+    }
+    if (!bal(sb >= 1024 || sa >= 1024)) {
+      const u32 t = wsum_u32((u32)sb | ((u32)sa << 16));
+      bqs = t & 0xFFFF;
+      aqs = t >> 16;
+    } else {
+      bqs = wsum_i64(sb);
+      aqs = wsum_i64(sa);
+    }
+  }
   // FIFO head of a price level: min arrival; returns slot j*64+L
   DEV int b_head(int buy_side, i32 price) {
     u32 a = 0xFFFFFFFFu;
@@ -1708,14 +1747,14 @@ struct Eng {
     u32 amin = wmin_u32(a);
     for (int j = 0; j < SO; j++) {
       u64 b = bal(bm[j] >= 0 && (bm[j] & 1) == buy_side && bp[j] == price && ba[j] == amin);
-      if (b) return j * 64 + ffs64(b);
+      if (b) return j * 64 + ctz64(b);
     }
     return -1;
   }
   DEV int b_find(int buy_side, i32 price, i32 oid) {
     for (int j = 0; j < SO; j++) {
       u64 b = bal(bm[j] >= 0 && (bm[j] & 1) == buy_side && bp[j] == price && bo[j] == oid);
-      if (b) return j * 64 + ffs64(b);
+      if (b) return j * 64 + ctz64(b);
     }
     return -1;
   }
@@ -1742,7 +1781,7 @@ struct Eng {
   DEV int b_free_slot() {
     for (int j = 0; j < SO; j++) {
       u64 b = bal(bm[j] < 0);
-      if (b) return j * 64 + ffs64(b);
+      if (b) return j * 64 + ctz64(b);
     }
     return -1;
   }
@@ -2145,7 +2184,7 @@ struct Eng {
       else na = c;
     }
     while (b) {
-      const int L = ffs64(b);
+      const int L = ctz64(b);
       b &= b - 1;
       const i32 ag = rdli(r.agent, L), lv = rdli(r.levels, L);
       const i32 nbs = nb < lv ? nb : lv, nas = na < lv ? na : lv;
@@ -2228,15 +2267,17 @@ struct Eng {
     case MK_SPREAD_REQ: {
       i32 depth = (i32)m.w[1];
       Msg r = msg_make(MK_SPREAD, 0);
-      i32 bb = b_best(1), aa = b_best(0);
+      i32 bb, aa;
+      i64 bqs, aqs;
+      b_inside(bb, aa, bqs, aqs);
       bool hb = bb != INT32_MIN && depth > 0, ha = aa != INT32_MAX && depth > 0;
       if (hb) {
         r.w[1] = (u32)bb;
-        r.w[2] = (u32)b_level_qty(1, bb);
+        r.w[2] = (u32)bqs;
       }
       if (ha) {
         r.w[3] = (u32)aa;
-        r.w[4] = (u32)b_level_qty(0, aa);
+        r.w[4] = (u32)aqs;
       }
       r.w[5] = (u32)h.last_trade;
       r.w[0] |= ((u32)hb << 9) | ((u32)ha << 10) | (1u << 11) | ((u32)h.last_trade_float << 8) | ((u32)closed << 7);
@@ -2387,7 +2428,7 @@ struct Eng {
     for (int j = 0; j < OC; j++) {
       u64 b = bal(my[j].oid != -1);
       while (b) {
-        int L = ffs64(b);
+        int L = ctz64(b);
         b &= b - 1;
         i32 oid = rdli(my[j].oid, L), ib = rdli(my[j].is_buy, L), q = rdli(my[j].qty, L), p = rdli(my[j].price, L);
         Msg cm = msg_order(MK_CANCEL, oid, cur_agent, ib, q, p, 0);
@@ -2407,7 +2448,7 @@ struct Eng {
     for (int j = 0; j < OC; j++) {
       u64 hit = bal(my[j].oid == oid);
       if (hit) {
-        int L = ffs64(hit);
+        int L = ctz64(hit);
         out.oid = oid;
         out.is_buy = rdli(my[j].is_buy, L);
         out.qty = rdli(my[j].qty, L);
@@ -3543,7 +3584,7 @@ struct Eng {
       i32 x = side == 0 ? b - lane : b + lane;
       bool ok = x >= 0 && x < P && c[x] > 0;
       u64 m = bal(ok);
-      if (m) return side == 0 ? b - ffs64(m) : b + ffs64(m);
+      if (m) return side == 0 ? b - ctz64(m) : b + ctz64(m);
     }
     return -1;
   }
@@ -4624,7 +4665,7 @@ struct Eng {
     __threadfence_block();
     mslot = scr[lane];
     const u64 b = bal(mslot >= 0);
-    return ~b == 0 ? 64 : ffs64(~b);
+    return ~b == 0 ? 64 : ctz64(~b);
   }
   // the run's n slots leave the queue together (each lane rebuilds its free mask and minimum)
   DEV void q_remove_run(int n, int mslot) {
@@ -4824,7 +4865,7 @@ struct Eng {
       for (int j = 0; j < OC; j++) {
         const u64 hit = bal(j * 64 + lane < u && my[j].oid == oid);
         if (hit) {
-          const bool me = lane == ffs64(hit);
+          const bool me = lane == ctz64(hit);
           my[j].oid = me ? -1 : my[j].oid;
           dead |= me ? (1u << j) : 0u;
           nord--;
@@ -4848,7 +4889,7 @@ struct Eng {
     if (n < 2) return 0;
     const Msg mm = pl_read(mslot >= 0 ? mslot : 0);
     const u64 kb = bal(lane < n && m_kind(mm) == kind);  // same-kind prefix
-    n = ~kb == 0 ? 64 : ffs64(~kb);
+    n = ~kb == 0 ? 64 : ctz64(~kb);
     if ((i64)n > budget) n = (int)budget;
     if (n < 2) return 0;
     if (rcp == 0) {
@@ -5008,7 +5049,7 @@ struct Eng {
           for (int j = 0; j < OC; j++) {
             const u64 hit = bal(j * 64 + lane < u && my[j].oid == oid);
             if (hit) {
-              del_open(j * 64 + ffs64(hit));
+              del_open(j * 64 + ctz64(hit));
               break;
             }
           }
