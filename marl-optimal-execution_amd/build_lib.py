@@ -26,6 +26,14 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
          "-Wno-unused-result", "-Wno-unused-value", "-mllvm", "-structurizecfg-skip-uniform-regions"]
 
+# per-configuration backend options (config id -> extra flags of its translation unit).  The
+# max-ILP scheduler, same digests (profiles/r05/ab_mr/ab_sched.txt): the ABIDESEnv replay step
+# kernel (config 3, one wave per SIMD on a serial chain) IBM x512 0.3229 -> 0.3177 ms and GOOG
+# 0.4656 -> 0.4575 ms per step; sparse_zi_100 (1) 105.3 -> 103.9 ms.  It cost sparse_zi_1000
+# 1.5 %, rmsc03 1.8 %, rmsc01 2.5 %, random_fund_* 0.5-1 %, rmsc02 neutral: those keep the default.
+# A/B variant builds (tools/build_variants.sh) pass it themselves.
+CFG_FLAGS = {1: ["-mllvm", "-amdgpu-sched-strategy=max-ilp"], 3: ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+
 
 def sources():
     return [os.path.join(HERE, "csrc", d) for d in DEPS] + [os.path.join(ROOT, "include", "mxa.h")]
@@ -39,6 +47,7 @@ def build_id(extra=()):
         with open(s, "rb") as f:
             h.update(f.read())
     h.update(" ".join(FLAGS + list(extra)).encode())
+    h.update(repr(sorted(CFG_FLAGS.items())).encode())
     return h.hexdigest()[:16]
 
 
@@ -58,7 +67,8 @@ def build(force=False, verbose=True, jobs=None):
     cflags = [f for f in FLAGS if f != "-shared"] + ["-c"]
     units = [([HIPCC] + cflags + ['-DMXA_BUILD_ID="%s"' % build_id()] + inc + [SRC, "-o", os.path.join(OBJ, "mxa_api.o")])]
     for c in range(N_CONFIGS):
-        units.append([HIPCC] + cflags + ["-DMXA_INST_CFG=%d" % c] + inc + [INST, "-o", os.path.join(OBJ, "mxa_inst_%d.o" % c)])
+        units.append([HIPCC] + cflags + CFG_FLAGS.get(c, []) + ["-DMXA_INST_CFG=%d" % c] + inc +
+                     [INST, "-o", os.path.join(OBJ, "mxa_inst_%d.o" % c)])
     if verbose:
         for u in units:
             print(" ".join(u), flush=True)
