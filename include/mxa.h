@@ -286,7 +286,9 @@ int mxa_set_book_log(mxa_handle* h, int32_t cap);
  * t = fill_price << 32 | (uint32)order_id (fill_price INT32_MIN: None), price = limit price,
  * qty = quantity (> 0 buy, < 0 sell).  The BEST_BID / BEST_ASK / LAST_TRADE rows follow from the
  * limit-order records (mxabides.booklog.exchange_log rebuilds the frame).  Replaces the
- * reference's in-process log list (Agent.logEvent, Agent.py:97-110). */
+ * reference's in-process log list (Agent.logEvent, Agent.py:97-110).  Set it before the first
+ * launch (or after a whole-handle mxa_reset): switching it once envs have popped events is
+ * MXA_EINVAL, since rows would name orders placed before the log started. */
 #define MXA_BL_EV_RX (-2147483647 - 1 + 256)
 #define MXA_BL_EV_NT (MXA_BL_EV_RX + 256)
 #define MXA_BL_EV_PLACE (MXA_BL_EV_RX + 512)

@@ -186,6 +186,7 @@ struct mxa_handle {
   // episode (one process running consecutive ABIDESEnv episodes)
   bool persist_ids = false;
   int32_t exlog = 0;   // mxa_set_exchange_log: the exchange's own log rides in the book-update log
+  bool started = false;  // a launch ran since the last whole-handle mxa_reset (the exchange log is fixed then)
   int64_t t_stop = 0;  // mxa_set_stop_time: Kernel.runner's stopTime override (0: the config's)
   int32_t tcap_arg() const { return (parity_hash || P.L.trace_cap > 0) ? P.L.trace_cap : -1; }
   // the run kernel of the current settings: the log variant, the instrumented one, or (hash off,
@@ -665,6 +666,7 @@ int mxa_reset(mxa_handle* h, const uint8_t* mask) {
   h->build(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->d_seeds, dm,
            h->d_ctx);
   HIPCHK(h, hipGetLastError());
+  if (!mask) h->started = false;
   if (h->exlog) {  // the build cleared the header: the switch outlives resets
     const int n = h->P.n_envs;
     hipLaunchKernelGGL(mxa_set_exlog_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env,
@@ -716,6 +718,7 @@ int mxa_set_id_persistence(mxa_handle* h, int32_t on) {
 int mxa_launch(mxa_handle* h, int64_t max_pops) {
   if (!h || h->gym) return MXA_EINVAL;  // GymKernel handles advance by mxa_step
   HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
+  h->started = true;
   h->run_kernel()(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
          h->d_ctx, h->d_blog, h->blog_cap);
   HIPCHK(h, hipGetLastError());
@@ -734,6 +737,7 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   HIPCHK(h, hipSetDevice(h->device));
   int launches = 0;
   float total = 0;
+  h->started = true;
   for (;;) {
     if (max_launches > 0 && launches >= max_launches) break;
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
@@ -786,6 +790,12 @@ int mxa_set_book_log(mxa_handle* h, int32_t cap) {
 int mxa_set_exchange_log(mxa_handle* h, int32_t on) {
   if (!h || h->gym || !h->run_log || on < 0 || on > 1) return MXA_EINVAL;
   if (on && !h->d_blog) return MXA_EINVAL;  // it rides in the book-update log: mxa_set_book_log first
+  if (h->started && on != h->exlog) {
+    // placements logged before the switch would be missing from the log (its order rows name
+    // them), and a log switched off mid-run ends without its tail: set it before the run
+    h->err = "mxa_set_exchange_log: set it before the first launch (or after a whole-handle mxa_reset)";
+    return MXA_EINVAL;
+  }
   HIPCHK(h, hipSetDevice(h->device));
   h->exlog = on;
   const int n = h->P.n_envs;

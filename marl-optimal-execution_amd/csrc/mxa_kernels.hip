@@ -3388,7 +3388,15 @@ struct Eng {
     // every lane's atomics performed at L2 before any lane reads a bucket back, and the reads
     // bypass the CU's L1 (agent-scope loads below), which may hold a stale line of the buckets.  A
     // device-scope __threadfence here also wrote back this XCD's whole L2 on every call: ~900 B of
-    // HBM writes per rmsc02 event (r05 PMC, tools/ab_traffic.sh)
+    // HBM writes per rmsc02 event (r05 PMC, tools/ab_traffic.sh).
+    // Two assumptions pin this: (1) an env's buckets are touched by ONE wave, the
+    // env's own (every engine kernel is __launch_bounds__(64), one wave per env block), so no
+    // other wave's atomics need to be ordered with these; (2) gfx950 (gfx9 family) counts
+    // non-returning global atomics in vmcnt, so s_waitcnt(0) waits for them to be performed at
+    // L2 (gfx10+ counts them in vscnt, where this sequence would not be enough)
+#if !defined(__gfx950__) && defined(__HIP_DEVICE_COMPILE__)
+#error "the HBL histogram readback relies on gfx9-family vmcnt accounting of global atomics"
+#endif
     wfence();
     __builtin_amdgcn_s_waitcnt(0);
     wfence();
@@ -3403,7 +3411,8 @@ struct Eng {
       u64 x = 0;
       if (i < NB) {
         x = __hip_atomic_load(&hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        hist[i] = 0;
+        // the reset at agent scope as well: ordered at L2 with the next call's atomics
+        __hip_atomic_store(&hist[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       const u32 c01 = (u32)(x & 0xFFFF) | ((u32)((x >> 16) & 0xFFFF) << 16);
       const u32 c23 = (u32)((x >> 32) & 0xFFFF) | ((u32)(x >> 48) << 16);

@@ -208,6 +208,11 @@ def exchange_log(rec, symbol, agent_type="ExchangeAgent"):
     placed, pending, li, i, n = {}, [], 0, 0, len(rec)
     while i < n:
         pi, ti, qi = int(p[i]), int(rec["t"][i]), int(rec["qty"][i])
+        if (BL_EV_NT <= pi < BL_EV_PLACE or pi in (BL_EV_RX + K_LIMIT, BL_EV_RX + K_CANCEL)) and i + 1 >= n:
+            # an order row's second record is missing: the stream was cut (a full log, env error
+            # ERR_BOOK_LOG_FULL, or a partial read)
+            raise ValueError("exchange log truncated after record %d (order row without its order record; "
+                             "a full book-update log ends the env with ERR_BOOK_LOG_FULL)" % i)
         if BL_EV_NT <= pi < BL_EV_PLACE:  # a notification of the order being handled
             rows.append((ti, KIND_NAMES[pi - BL_EV_NT], _order(rec[i + 1], qi, placed, symbol, None)))
             i += 2

@@ -39,10 +39,12 @@ and never under ABIDESEnv. What the composition changes, and why:
 
 Across GPUs (bench.py --gpus N, BASELINE configs[3]) the learner is synchronous data-parallel:
 with `group` (a torch.distributed process group over RCCL) the eval and target nets start from
-rank 0's initialisation (broadcast), every update all-reduces the gradient (mean over ranks) and
-the live flag (any rank), and every rank applies the same RMSprop step, so ONE policy serves the
-whole node. Each rank samples its batch from its own envs' replay; the update equals one learner's
-on the union of the ranks' batches (batch_size x world, tests/test_ddqn_multirank.py). The market
+rank 0's initialisation (broadcast), every update all-reduces the live-weighted gradient and the
+count of live ranks in one message, and every rank applies the same RMSprop step, so ONE policy
+serves the whole node. Each rank samples its batch from its own envs' replay; the update equals
+one learner's on the union of the LIVE ranks' batches (a rank whose envs are done, or whose replay
+is below the batch size, contributes nothing; tests/test_ddqn_multirank.py). Every rank runs the
+same collectives on every learn() call, whatever its replay size. The market
 results of a given action sequence are world-size invariant (envs shard by global index,
 mxabides.shard); the policy trajectory depends on the world size through that batch union.
 
@@ -321,21 +323,18 @@ class DDQNLearner:
         from the target net as it stands (:486-505), THEN the eval -> target copy when
         learn_step_counter % replace_target_iter == 0 (:508-510), then train_on_batch (:513).
         `live` (device bool, default true) masks the whole update; `masks` are the dropout keep
-        masks (default: drawn from gen_drop). With a process group the gradient is the mean over
-        ranks and the update runs when any rank is live. Returns the (local) loss."""
+        masks (default: drawn from gen_drop). With a process group the update is one learner's on
+        the union of the LIVE ranks' batches: each rank's gradient is weighted by its own live
+        flag and the sum is divided by the number of live ranks (one all-reduce carries both), so a
+        rank whose envs are all done adds nothing from its stale replay; the update runs when any
+        rank is live. Every rank issues the same collectives on every call. Returns the (local)
+        loss."""
         if live is None:
             live = torch.ones((), dtype=torch.bool, device=self.device)
-        if self.world > 1:
-            import torch.distributed as dist
-            lv = live.to(torch.int32).reshape(1).clone()
-            dist.all_reduce(lv, op=dist.ReduceOp.MAX, group=self.group)
-            live = lv[0] > 0
+        local_live = live
         if masks is None:
             masks = self.dropout_masks(s.shape[0])
         tgt = self.q_target(s, a, s2, r)
-        with torch.no_grad():
-            do_copy = live & (self._counter % self.replace_target_iter == 0)
-            self.tflat.copy_(torch.where(do_copy, self.eflat, self.tflat))
         self.eval_model.train()  # train_on_batch: training=True (dropout active)
         for p in self.eval_model.parameters():
             p.grad = None
@@ -343,10 +342,19 @@ class DDQNLearner:
         loss.backward()
         with torch.no_grad():
             g = torch.cat([p.grad.reshape(-1) for p in self.eval_model.parameters()])
-            if self.world > 1:  # one policy for the node: the mean gradient over the ranks
+            if self.world > 1:  # one policy for the node: the mean gradient over the live ranks
                 import torch.distributed as dist
-                dist.all_reduce(g, group=self.group)
-                g /= self.world
+                w = local_live.to(g.dtype).reshape(1)
+                gl = torch.cat([g * w, w])
+                dist.all_reduce(gl, group=self.group)
+                n_live = gl[-1]
+                live = n_live > 0
+                g = gl[:-1] / torch.clamp(n_live, min=1)
+            # the target copy comes after the target (:508-510), before the RMSprop step; the
+            # gradient above is the eval net's and does not read the target parameters after
+            # q_target, so the copy can follow the all-reduce
+            do_copy = live & (self._counter % self.replace_target_iter == 0)
+            self.tflat.copy_(torch.where(do_copy, self.eflat, self.tflat))
             rms = self.rho * self.rms + (1 - self.rho) * g * g
             self.rms.copy_(torch.where(live, rms, self.rms))
             step = self.learning_rate * g / (torch.sqrt(self.rms) + self.rms_eps)
@@ -365,7 +373,13 @@ class DDQNLearner:
     def learn(self, live=None):
         """sample a batch with replacement (np.random.choice(current_size, batch)) and update."""
         m = self.memory
-        if not m.more_than(self.batch_size):
+        if self.world > 1:
+            # the size test is per rank (its own envs' outcomes fill its replay), but the
+            # collectives of learn_on must pair up on every rank: a rank below the batch size
+            # still takes part, with its own update masked off (an empty replay samples row 0)
+            ok = torch.clamp(m.n_dev, max=m.cap) > self.batch_size
+            live = ok if live is None else (live & ok)
+        elif not m.more_than(self.batch_size):
             return None
         size = torch.clamp(m.n_dev, max=m.cap).to(torch.float64)  # the current size, on the device
         u = torch.rand(self.batch_size, generator=self.gen_sample, device=self.device, dtype=torch.float64)

@@ -1,9 +1,11 @@
 """World-size-2 rehearsal (gloo, CPU) of the DDQN learner's multi-GPU semantics (mxabides.ddqn,
 BASELINE configs[3] on 8 GPUs): synchronous data parallelism.  Both ranks start from rank 0's
-eval / target initialisation, every update all-reduces the gradient (mean over ranks) and the
-live flag, so the two ranks hold the same policy after every update, and that policy equals one
-learner's trained on the union of the two ranks' batches (ddqlearning_execution_agent.py:448-530
-restated by oracle/ddqn_ref.train_step, dropout masks included).  On the GPU box the same code
+eval / target initialisation, every update all-reduces the live-weighted gradient and the
+live-rank count, so the two ranks hold the same policy after every update, and that policy equals
+one learner's trained on the union of the LIVE ranks' batches (ddqlearning_execution_agent.py:
+448-530 restated by oracle/ddqn_ref.train_step, dropout masks included).  A rank that is not live
+(its envs done, or its replay below the batch size) adds nothing, and learn() issues the same
+collectives on every rank whatever its replay size.  On the GPU box the same code
 runs over RCCL."""
 import os
 import socket
@@ -34,6 +36,11 @@ def _masks(rank, it, widths, rate=0.1):
     return [rs.uniform(size=(BATCH, w)) >= rate for w in widths]
 
 
+def _live(rank, it):
+    """per-rank, per-update live flags: both, one, the other, and neither (it 3: no update)"""
+    return (it != 3) if rank == 0 else (it % 2 == 0)
+
+
 def _worker(rank, world, port, out_dir):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -46,9 +53,9 @@ def _worker(rank, world, port, out_dir):
         # distinct seeds: without the broadcast the ranks would start from different nets
         L = ddqn.DDQNLearner(device="cpu", dropout=0.1, seed=11 + rank, dtype=torch.float64, group=dist.group.WORLD)
         widths = L.eval_model.dropout_widths()
-        live = torch.tensor(rank == 0)  # one rank live is enough for the update to run everywhere
         for it in range(N_UPDATES):
             s, a, s2, r = _batch(rank, it)
+            live = torch.tensor(_live(rank, it))  # one rank live is enough for the update to run everywhere
             L.learn_on(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(s2), torch.from_numpy(r), live=live,
                        masks=[torch.from_numpy(m) for m in _masks(rank, it, widths)])
         np.save(os.path.join(out_dir, "eval_%d.npy" % rank), L.eflat.numpy())
@@ -67,9 +74,10 @@ def test_gloo_world2_learner_is_one_policy_on_the_union_of_batches(tmp_path):
     ev = [np.load(tmp_path / ("eval_%d.npy" % r)) for r in range(world)]
     tg = [np.load(tmp_path / ("target_%d.npy" % r)) for r in range(world)]
     assert np.array_equal(ev[0], ev[1]) and np.array_equal(tg[0], tg[1])  # one policy on the node
-    assert int(np.load(tmp_path / "counter_1.npy")) == N_UPDATES
+    n_live_updates = sum(any(_live(r, it) for r in range(world)) for it in range(N_UPDATES))
+    assert int(np.load(tmp_path / "counter_1.npy")) == n_live_updates == N_UPDATES - 1
     # the single-learner reference: rank 0's initialisation, every update on the union of the
-    # two ranks' batches (and masks); mean MSE over the union = the mean of the ranks' means
+    # live ranks' batches (and masks); mean MSE over the union = the mean of the ranks' means
     L = ddqn.DDQNLearner(device="cpu", dropout=0.1, seed=11, dtype=torch.float64)
     layers = lambda net: [(l.weight.detach().numpy().T.copy(), l.bias.detach().numpy().copy())
                           for l in list(net.hidden) + [net.logits]]
@@ -78,12 +86,65 @@ def test_gloo_world2_learner_is_one_policy_on_the_union_of_batches(tmp_path):
     widths = L.eval_model.dropout_widths()
     c = 0
     for it in range(N_UPDATES):
-        bs = [_batch(r, it) for r in range(world)]
+        rl = [r for r in range(world) if _live(r, it)]
+        if not rl:
+            continue
+        bs = [_batch(r, it) for r in rl]
         batch = tuple(np.concatenate([b[k] for b in bs]) for k in range(4))
-        ms = [np.concatenate([_masks(r, it, widths)[j] for r in range(world)]).astype(np.float64)
+        ms = [np.concatenate([_masks(r, it, widths)[j] for r in rl]).astype(np.float64)
               for j in range(len(widths))]
         e, t, rms, c, _ = ddqn_ref.train_step(e, t, rms, c, batch, masks=ms)
     flat = np.concatenate([np.concatenate([W.T.reshape(-1), b]) for W, b in e])
     np.testing.assert_allclose(ev[0], flat, rtol=1e-9, atol=1e-12)
     tflat = np.concatenate([np.concatenate([W.T.reshape(-1), b]) for W, b in t])
     np.testing.assert_allclose(tg[0], tflat, rtol=1e-9, atol=1e-12)
+
+
+N_ROWS = {0: 64, 1: 8}  # replay rows per rank: rank 0 above the batch size, rank 1 below it
+N_LEARN = 3
+
+
+def _rows(rank, n):
+    rs = np.random.RandomState(50 + rank)
+    return (torch.from_numpy(rs.randint(0, 200, (n, 2)).astype(np.float32)), torch.from_numpy(rs.randint(0, 24, n)),
+            torch.from_numpy(rs.randint(0, 200, (n, 2)).astype(np.float32)), torch.from_numpy(rs.normal(0, 50, n)))
+
+
+def _fill(L, rank):
+    s, a, s2, r = _rows(rank, N_ROWS[rank])
+    L.memory.add_device(s, a, s2, r, torch.ones(len(a), dtype=torch.bool))
+
+
+def _learn_worker(rank, world, port, out_dir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "marl-optimal-execution_amd"))
+    from mxabides import ddqn
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L = ddqn.DDQNLearner(device="cpu", dropout=0.1, seed=11 + rank, dtype=torch.float64, group=dist.group.WORLD)
+        _fill(L, rank)
+        for _ in range(N_LEARN):  # rank 1's replay is below the batch size: it takes part, masked off
+            L.learn()
+        np.save(os.path.join(out_dir, "eval_%d.npy" % rank), L.eflat.numpy())
+        np.save(os.path.join(out_dir, "counter_%d.npy" % rank), np.asarray(L.learn_step_counter))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_learn_with_replay_sizes_either_side_of_the_batch(tmp_path):
+    """ranks whose replay sizes straddle the batch size run the same collectives (no hang, no
+    mispaired all-reduce); the update is rank 0's alone, equal to a single learner's on its rows"""
+    from mxabides import ddqn
+    world = 2
+    mp.start_processes(_learn_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    ev = [np.load(tmp_path / ("eval_%d.npy" % r)) for r in range(world)]
+    assert np.array_equal(ev[0], ev[1])
+    assert int(np.load(tmp_path / "counter_0.npy")) == int(np.load(tmp_path / "counter_1.npy")) == N_LEARN
+    L = ddqn.DDQNLearner(device="cpu", dropout=0.1, seed=11, dtype=torch.float64)
+    _fill(L, 0)
+    for _ in range(N_LEARN):
+        L.learn()
+    np.testing.assert_allclose(ev[0], L.eflat.numpy(), rtol=1e-12, atol=1e-15)

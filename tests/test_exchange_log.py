@@ -119,3 +119,13 @@ def test_jsons_time_placed_format():
     assert bl.jsons_dump_order(d)["time_placed"] == "2019-06-28T09:30:00Z"
     d["time_placed"] += 1234567
     assert bl.jsons_dump_order(d)["time_placed"] == "2019-06-28T09:30:00.001234Z"
+
+
+@pytest.mark.parametrize("code", [bl.BL_EV_RX + bl.K_LIMIT, bl.BL_EV_RX + bl.K_CANCEL, bl.BL_EV_NT + 1])
+def test_truncated_exchange_log_raises(code):
+    """an order row whose order record was cut off (a full log, ERR_BOOK_LOG_FULL) is a clear error"""
+    rec = np.zeros(2, dtype=bl.REC_DTYPE)
+    rec[0] = (34200 * 10**9, bl.BL_EV_PLACE, 5)
+    rec[1] = (34200 * 10**9, code, 3)
+    with pytest.raises(ValueError, match="truncated"):
+        bl.exchange_log(rec, "JPM")
