@@ -12,6 +12,9 @@
  *                        (and rmsc03 with SpreadBasedMarketMakerAgent.py:17-297, MXA_RMSC03_SBMM*)
  *                        (agent/oracle/kernel construction, global-RNG draw order) and
  *                        Kernel.__init__ (Kernel.py:13-46)
+ *   mxa_create_config .. a config script's agent list given at run time: Kernel.runner(agents, ...)
+ *                        (Kernel.py:50-64) built as config/rmsc03.py:95-197, config/value_noise.py,
+ *                        config/sparse_zi_100.py:177-334 build theirs (counts, parameters, session)
  *   mxa_reset .......... Kernel.runner kernelInitializing/kernelStarting (Kernel.py:143-177),
  *                        ABIDESEnv.reset (ABIDESEnv.py:51-57)
  *   mxa_run / mxa_launch Kernel.runner event loop (Kernel.py:190-292)
@@ -123,6 +126,67 @@ mxa_mm_params mxa_mm_defaults(void);
  * window or ticks, wake-up period <= 0). */
 int mxa_create_params(int32_t config, int32_t n_envs, const uint32_t* seeds, const mxa_mm_params* per_env,
                       int32_t device, int32_t trace_cap, mxa_handle** out);
+/* A Kernel.runner composition given at run time (SURVEY.md §8(b) "mxa_config"): the agent list a
+ * config script builds (Kernel.runner(agents, startTime, stopTime, ...), Kernel.py:50-64) from the
+ * existing agent classes, with its counts, per-class parameters, session times and date.  `base`
+ * names the script whose construction (global-RNG draw order, latency model) it follows:
+ *   MXA_RMSC03        config/rmsc03.py:95-197 (config/random_fund_value.py is the same
+ *                     construction): exchange, n_noise NoiseAgent (util.get_wake_time in the noise
+ *                     window), n_value ValueAgent, n_mm POVMarketMakerAgent (0 or 1), n_momentum
+ *                     MomentumAgent; zero latency, compute delay 0
+ *   MXA_VALUE_NOISE   config/value_noise.py:45-200: exchange, n_noise, n_value; latency matrix
+ *                     G.uniform(lat_low, lat_high) with 6-way noise, compute delay
+ *   MXA_SPARSE_ZI_100 config/sparse_zi_100.py:177-334: exchange and the ZI strategy table (count,
+ *                     R_min, R_max, eta per group); cubic LatencyModel (min_latency U(lat_low, lat_high))
+ *   MXA_SPARSE_ZI_1000 config/sparse_zi_1000.py: the same agents on the symmetric matrix latency
+ * Agent ids follow the scripts' order.  mxa_config_defaults fills the base script's values; a
+ * caller edits what its script changes.  Times are ns since midnight of the simulated date. */
+#define MXA_CONFIG_ZI_GROUPS 8
+typedef struct {
+  int32_t base;               /* MXA_RMSC03, MXA_VALUE_NOISE, MXA_SPARSE_ZI_100, MXA_SPARSE_ZI_1000 */
+  int32_t log_orders;         /* ExchangeAgent(log_orders=...) (what the exchange log records) */
+  int32_t n_noise, n_value;   /* NoiseAgent / ValueAgent counts (rmsc03, value_noise) */
+  int32_t n_mm, n_momentum;   /* POVMarketMakerAgent (0 or 1) / MomentumAgent counts (rmsc03) */
+  int32_t n_zi_groups;        /* ZI strategy table rows (sparse_zi_*), at most MXA_CONFIG_ZI_GROUPS */
+  int32_t zi_q_max;           /* ZeroIntelligenceAgent q_max (1..10) */
+  int32_t zi_count[MXA_CONFIG_ZI_GROUPS], zi_r_min[MXA_CONFIG_ZI_GROUPS], zi_r_max[MXA_CONFIG_ZI_GROUPS];
+  double zi_eta[MXA_CONFIG_ZI_GROUPS];
+  double zi_sigma_n, zi_r_bar, zi_kappa, zi_sigma_s, zi_sigma_pv, zi_lambda_a;
+  int64_t mkt_open_ns, mkt_close_ns;          /* the exchange's (and the oracle's) session */
+  int64_t kernel_start_ns, kernel_stop_ns;    /* Kernel.runner(startTime, stopTime) */
+  int64_t noise_wake_open_ns, noise_wake_close_ns; /* rmsc03: get_wake_time(noise_mkt_open, noise_mkt_close) */
+  int64_t date_ns;            /* the -d historical date (its midnight, ns since the Unix epoch): output timestamps only */
+  int64_t starting_cash;      /* TradingAgent starting_cash (cents) */
+  int64_t default_computation_delay_ns;
+  /* SparseMeanRevertingOracle symbols dict: r_bar, kappa, fund_vol, megashock_lambda_a, _mean, _var */
+  double r_bar, kappa, fund_vol, megashock_lambda_a, megashock_mean, megashock_var;
+  double value_sigma_n, value_r_bar, value_kappa, value_sigma_s, value_lambda_a;
+  int64_t value_starting_cash;
+  mxa_mm_params mm;           /* POVMarketMakerAgent (config/rmsc03.py's --mm-* options) */
+  int32_t mom_min_size, mom_max_size;
+  int64_t mom_wake_up_freq_ns;
+  double lat_low, lat_high;   /* G.uniform bounds of the latency matrix / the cubic model's min_latency */
+  int32_t queue_capacity, book_capacity; /* pending events / resting orders per env; 0: derived from the counts */
+} mxa_config;
+/* the base script's own values (MXA_EINVAL for any other config id) */
+int mxa_config_defaults(int32_t base, mxa_config* out);
+/* The engine is specialised per composition: every count and parameter becomes an immediate of
+ * the kernels, as for the built-in configurations.  mxa_config_compile builds the
+ * specialisation (hipcc, gfx950; ~40 s) into `cache_dir` (NULL: the lib/custom directory beside
+ * libmxa.so) unless it is there already, and writes the library's path to path_out.  It uses no
+ * GPU.  MXA_EINVAL for a composition outside the bounds above or the device capacities (8191
+ * agents, 128 queue slots and 16 book slots per lane). */
+int mxa_config_compile(const mxa_config* cfg, const char* cache_dir, char* path_out, int32_t path_cap);
+/* the specialisation's cache key (16 hex digits + NUL: the composition and this library's build id) */
+int mxa_config_key(const mxa_config* cfg, char* out17);
+/* a plain Kernel.runner handle (mxa_run, mxa_finalize, the readers) of the composition, one env
+ * per seed.  Its specialisation must have been compiled (mxa_config_compile, same cache_dir):
+ * MXA_ERANGE otherwise, and nothing is compiled here. */
+int mxa_create_config(const mxa_config* cfg, int32_t n_envs, const uint32_t* seeds, int32_t device, int32_t trace_cap,
+                      const char* cache_dir, mxa_handle** out);
+/* per-configuration facts of a built-in configuration id: out8 = (n_agents, ExchangeAgent
+ * log_orders, queue capacity, book capacity, mkt_open, mkt_close, kernel start, kernel stop) */
+int mxa_config_info(int32_t config, int64_t* out8);
 /* replace the options the next mxa_reset builds with (handles of mxa_create_params) */
 int mxa_set_mm_params(mxa_handle* h, const mxa_mm_params* per_env);
 /* envs of the handle resident on the device at once (run / step kernel occupancy x CUs, at most
@@ -202,7 +266,7 @@ int64_t mxa_env_bytes(const mxa_handle* h);
 int mxa_set_stream(mxa_handle* h, void* stream);
 /* HIP event timing of the last mxa_run / mxa_launch sequence, milliseconds */
 double mxa_last_kernel_ms(const mxa_handle* h);
-const char* mxa_last_error(const mxa_handle* h);
+const char* mxa_last_error(const mxa_handle* h); /* NULL: the last mxa_config_* / mxa_create_config error */
 void mxa_destroy(mxa_handle* h);
 
 /* ABIDESEnv on a replay tape: n_rec time-sorted records (ns since midnight, order id > 0,

@@ -65,7 +65,10 @@ def build(force=False, verbose=True, jobs=None):
     os.makedirs(OBJ, exist_ok=True)
     inc = ["-I" + os.path.join(HERE, "csrc"), "-I" + os.path.join(ROOT, "include")]
     cflags = [f for f in FLAGS if f != "-shared"] + ["-c"]
-    units = [([HIPCC] + cflags + ['-DMXA_BUILD_ID="%s"' % build_id()] + inc + [SRC, "-o", os.path.join(OBJ, "mxa_api.o")])]
+    # the compile line of the runtime compositions' specialisations (mxa_config_compile) is this one
+    jit = ['-DMXA_JIT_FLAGS="%s"' % " ".join(FLAGS),
+           '-DMXA_JIT_CFG_FLAGS="%s"' % ";".join("%d:%s" % (c, " ".join(f)) for c, f in sorted(CFG_FLAGS.items()))]
+    units = [([HIPCC] + cflags + ['-DMXA_BUILD_ID="%s"' % build_id()] + jit + inc + [SRC, "-o", os.path.join(OBJ, "mxa_api.o")])]
     for c in range(N_CONFIGS):
         units.append([HIPCC] + cflags + CFG_FLAGS.get(c, []) + ["-DMXA_INST_CFG=%d" % c] + inc +
                      [INST, "-o", os.path.join(OBJ, "mxa_inst_%d.o" % c)])

@@ -6,12 +6,22 @@
 // rmsc03-only variant build (-DMXA_ONLY_RMSC03) compiles everything in this one.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+#include <spawn.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
+
+extern char** environ;
 
 #include "../../include/mxa.h"
 #define MXA_API_TU
@@ -409,6 +419,208 @@ int mxa_create_hist(int32_t config, int32_t n_envs, const uint32_t* seeds, int32
   h->ctx.fs_n = n_fund;
   h->ext = true;
   return create_common(h, n_envs, seeds, device, out);
+}
+
+// ---- runtime compositions (include/mxa.h mxa_config): one specialised library per composition
+#ifndef MXA_BUILD_ID
+#define MXA_BUILD_ID "unknown"
+#endif
+// the compile line of a specialisation: build_lib.py's flags (passed in when this file is
+// compiled), per base configuration its extra flags ("<cfg>:<flags>;...")
+#ifndef MXA_JIT_FLAGS
+#define MXA_JIT_FLAGS "--offload-arch=gfx950 -O3 -std=c++20"
+#endif
+#ifndef MXA_JIT_CFG_FLAGS
+#define MXA_JIT_CFG_FLAGS ""
+#endif
+static std::string g_cfg_err;  // mxa_last_error(NULL): the last composition error
+
+static int cfg_fail(const std::string& what) {
+  g_cfg_err = what;
+  return MXA_EINVAL;
+}
+
+// the directory holding this library (lib/), from which csrc/ and include/ are found
+static std::string lib_dir() {
+  Dl_info di{};
+  if (!dladdr((void*)&mxa_config_defaults, &di) || !di.dli_fname) return ".";
+  std::string p = di.dli_fname;
+  const size_t k = p.rfind('/');
+  return k == std::string::npos ? "." : p.substr(0, k);
+}
+
+static std::vector<std::string> split_ws(const std::string& s) {
+  std::vector<std::string> v;
+  size_t i = 0;
+  while (i < s.size()) {
+    while (i < s.size() && s[i] == ' ') i++;
+    size_t j = i;
+    while (j < s.size() && s[j] != ' ') j++;
+    if (j > i) v.push_back(s.substr(i, j - i));
+    i = j;
+  }
+  return v;
+}
+
+static std::string cfg_key(const mxa_config& c) {
+  mxa_config k = c;
+  k.date_ns = 0;  // output timestamps only: one specialisation serves every date
+  uint64_t h = 0xCBF29CE484222325ull;
+  const unsigned char* b = (const unsigned char*)&k;
+  for (size_t i = 0; i < sizeof k; i++) h = (h ^ b[i]) * 0x100000001B3ull;
+  for (const char* p = MXA_BUILD_ID; *p; p++) h = (h ^ (unsigned char)*p) * 0x100000001B3ull;
+  char buf[17];
+  snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);
+  return buf;
+}
+
+static std::string cfg_dir(const char* cache_dir) { return cache_dir && *cache_dir ? cache_dir : lib_dir() + "/custom"; }
+static std::string cfg_lib(const char* cache_dir, const std::string& key) {
+  return cfg_dir(cache_dir) + "/libmxa_cfg_" + key + ".so";
+}
+
+int mxa_config_defaults(int32_t base, mxa_config* out) {
+  if (!out || !mxa_cfg::custom_base_ok(base)) return cfg_fail("mxa_config_defaults: no such base script");
+  static_assert(sizeof(mxa_config) % 8 == 0, "mxa_config: no tail padding (its bytes are the cache key)");
+  mxa_cfg::config_defaults(base, *out);
+  return MXA_OK;
+}
+
+int mxa_config_key(const mxa_config* cfg, char* out17) {
+  if (!cfg || !out17) return MXA_EINVAL;
+  snprintf(out17, 17, "%s", cfg_key(*cfg).c_str());
+  return MXA_OK;
+}
+
+int mxa_config_compile(const mxa_config* cfg, const char* cache_dir, char* path_out, int32_t path_cap) {
+  if (!cfg) return cfg_fail("mxa_config_compile: null composition");
+  if (const char* why = mxa_cfg::custom_check(*cfg)) return cfg_fail(std::string("mxa_config_compile: ") + why);
+  const std::string key = cfg_key(*cfg), dir = cfg_dir(cache_dir), so = cfg_lib(cache_dir, key);
+  if (path_out && path_cap > 0) snprintf(path_out, path_cap, "%s", so.c_str());
+  struct stat st{};
+  if (stat(so.c_str(), &st) == 0) return MXA_OK;  // compiled before
+  mkdir(dir.c_str(), 0755);
+  const std::string hdr = dir + "/mxa_cfg_" + key + ".h";
+  {
+    FILE* f = fopen(hdr.c_str(), "w");
+    if (!f) return cfg_fail("mxa_config_compile: cannot write " + hdr);
+    fprintf(f, "// a runtime composition (include/mxa.h mxa_config), written by mxa_config_compile\n");
+    fprintf(f, "#define MXA_CUSTOM_BYTES {");
+    const unsigned char* b = (const unsigned char*)cfg;
+    for (size_t i = 0; i < sizeof(mxa_config); i++) fprintf(f, "%s%u", i ? "," : "", b[i]);
+    fprintf(f, "}\n");
+    fclose(f);
+  }
+  const std::string ld = lib_dir(), src = ld + "/../csrc", inc = ld + "/../../include";
+  const char* hipcc = getenv("HIPCC");
+  std::vector<std::string> argv = {hipcc && *hipcc ? hipcc : "/opt/rocm/bin/hipcc"};
+  for (auto& x : split_ws(MXA_JIT_FLAGS)) argv.push_back(x);
+  {  // the base's own backend flags
+    const std::string all = MXA_JIT_CFG_FLAGS, pre = std::to_string(cfg->base) + ":";
+    size_t i = 0;
+    while (i < all.size()) {
+      size_t j = all.find(';', i);
+      if (j == std::string::npos) j = all.size();
+      const std::string item = all.substr(i, j - i);
+      if (item.compare(0, pre.size(), pre) == 0)
+        for (auto& x : split_ws(item.substr(pre.size()))) argv.push_back(x);
+      i = j + 1;
+    }
+  }
+  const std::string tmp = so + ".tmp." + std::to_string((long)getpid());
+  for (const std::string& x : {std::string("-fvisibility=hidden"), std::string("-fvisibility-inlines-hidden"),
+                               std::string("-Wl,-Bsymbolic"), std::string("-shared"),
+                               "-DMXA_INST_CFG=" + std::to_string(cfg->base), "-DMXA_CUSTOM_HDR=\"" + hdr + "\"",
+                               std::string("-DMXA_BUILD_ID=\"") + MXA_BUILD_ID + "\"", "-I" + src, "-I" + inc,
+                               src + "/mxa_inst.hip", std::string("-o"), tmp})
+    argv.push_back(x);
+  std::vector<char*> av;
+  for (auto& x : argv) av.push_back((char*)x.c_str());
+  av.push_back(nullptr);
+  pid_t pid = 0;
+  // a child process (posix_spawn), never an exec of this one
+  if (posix_spawn(&pid, av[0], nullptr, nullptr, av.data(), environ) != 0)
+    return cfg_fail("mxa_config_compile: cannot start " + argv[0]);
+  int status = 0;
+  if (waitpid(pid, &status, 0) < 0 || !WIFEXITED(status) || WEXITSTATUS(status) != 0) {
+    unlink(tmp.c_str());
+    std::string cmd;
+    for (auto& x : argv) cmd += x + " ";
+    return cfg_fail("mxa_config_compile: the compile failed: " + cmd);
+  }
+  if (rename(tmp.c_str(), so.c_str()) != 0) return cfg_fail("mxa_config_compile: cannot place " + so);
+  return MXA_OK;
+}
+
+typedef int (*mxa_custom_entry_fn)(MxaEntry*, MxaParams*, size_t*, mxa_config*, const char**);
+
+int mxa_create_config(const mxa_config* cfg, int32_t n_envs, const uint32_t* seeds, int32_t device, int32_t trace_cap,
+                      const char* cache_dir, mxa_handle** out) {
+  if (!out || n_envs <= 0 || !seeds || trace_cap < 0 || !cfg) return cfg_fail("mxa_create_config: bad arguments");
+  if (const char* why = mxa_cfg::custom_check(*cfg)) return cfg_fail(std::string("mxa_create_config: ") + why);
+  const std::string key = cfg_key(*cfg), so = cfg_lib(cache_dir, key);
+  static std::mutex mu;
+  static std::map<std::string, void*> loaded;  // specialisations stay loaded: their kernels are registered
+  void* dl = nullptr;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = loaded.find(so);
+    if (it != loaded.end()) {
+      dl = it->second;
+    } else {
+      struct stat st{};
+      if (stat(so.c_str(), &st) != 0) {
+        g_cfg_err = "mxa_create_config: not compiled (mxa_config_compile first): " + so;
+        return MXA_ERANGE;
+      }
+      dl = dlopen(so.c_str(), RTLD_NOW | RTLD_LOCAL);
+      if (!dl) return cfg_fail(std::string("mxa_create_config: dlopen: ") + dlerror());
+      loaded[so] = dl;
+    }
+  }
+  auto fn = (mxa_custom_entry_fn)dlsym(dl, "mxa_custom_entry");
+  if (!fn) return cfg_fail("mxa_create_config: " + so + " is not a specialisation");
+  MxaEntry e{};
+  MxaParams P{};
+  size_t lds = 0;
+  mxa_config c{};
+  const char* bid = nullptr;
+  if (fn(&e, &P, &lds, &c, &bid) != (int)sizeof(MxaParams) || !bid || strcmp(bid, MXA_BUILD_ID) != 0)
+    return cfg_fail("mxa_create_config: " + so + " was built by another libmxa");
+  c.date_ns = cfg->date_ns;
+  if (memcmp(&c, cfg, sizeof c) != 0) return cfg_fail("mxa_create_config: " + so + " holds another composition");
+  mxa_handle* h = new mxa_handle();
+  h->build = e.build;
+  h->run = e.run;
+  h->run_log = e.run_log;
+  h->run_fast = e.run_fast;
+  h->stop = e.stop;
+  h->stop_log = e.stop_log;
+  h->step = e.step;
+  h->step_fast = e.step_fast;
+  h->gym = false;
+  h->occ = e.occ;
+  h->lds = lds;
+  h->P = P;
+  h->P.n_envs = n_envs;
+  h->P.L.trace_cap = trace_cap;
+  h->P.L.env_stride = mxa_cfg::align_up(P.L.off_trace + (uint64_t)trace_cap * MXA_TRACE_WORDS * 8, 256);
+  return create_common(h, n_envs, seeds, device, out);
+}
+
+int mxa_config_info(int32_t config, int64_t* out8) {
+  if (!out8 || config < 0 || config >= MXA_N_CONFIGS) return MXA_EINVAL;
+  const MxaParams P = mxa_cfg::params(config);
+  const mxa_cfg::Shape S = mxa_cfg::shape(config);
+  out8[0] = P.n_agents;
+  out8[1] = P.ex_log_orders;
+  out8[2] = (int64_t)S.sq * 64;
+  out8[3] = (int64_t)S.so * 64;
+  out8[4] = P.mkt_open;
+  out8[5] = P.mkt_close;
+  out8[6] = P.start;
+  out8[7] = P.stop;
+  return MXA_OK;
 }
 
 static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, int32_t device, mxa_handle** out) {
@@ -1050,11 +1262,8 @@ int mxa_set_stream(mxa_handle* h, void* s) {
   return MXA_OK;
 }
 double mxa_last_kernel_ms(const mxa_handle* h) { return h ? h->last_ms : 0; }
-const char* mxa_last_error(const mxa_handle* h) { return h ? h->err.c_str() : "null handle"; }
+const char* mxa_last_error(const mxa_handle* h) { return h ? h->err.c_str() : g_cfg_err.c_str(); }
 
-#ifndef MXA_BUILD_ID
-#define MXA_BUILD_ID "unknown"
-#endif
 const char* mxa_build_id(void) { return MXA_BUILD_ID; }
 
 void mxa_destroy(mxa_handle* h) {

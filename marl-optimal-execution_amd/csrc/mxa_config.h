@@ -10,6 +10,7 @@
 #pragma once
 #include <stddef.h>
 #include "mxa_layout.h"
+#include "../../include/mxa.h"
 
 namespace mxa_cfg {
 
@@ -29,6 +30,7 @@ struct Shape {
 };
 constexpr int sq_lds(int cfg);
 constexpr int lat_lds(int cfg);
+constexpr Shape shape(int cfg);
 #ifndef MXA_RMSC03_WAVES
 #define MXA_RMSC03_WAVES 4
 #endif
@@ -121,7 +123,7 @@ constexpr int lat_lds(int cfg);
 #ifndef MXA_RP_HOT
 #define MXA_RP_HOT 2  // replay configurations: the exchange's and the MarketReplayAgent's records in LDS
 #endif
-constexpr Shape shape(int cfg) {
+constexpr Shape shape_builtin(int cfg) {
   // rmsc03: 192 queue slots (the oracle's maximum over the 4096 bench seeds is 146, over 1024
   // rmsc03_rl episodes 146), so 16 waves per CU fit the queue, the header and the exchange and
   // market-maker records in LDS
@@ -635,7 +637,7 @@ constexpr void params_value_noise(MxaParams& P) {
   P.L.lat_len = P.n_agents;
 }
 
-constexpr MxaParams params(int cfg) {
+constexpr MxaParams params_builtin(int cfg) {
   MxaParams P{};
   if (cfg == MXA_CFG_RMSC03) params_rmsc03(P);
   else if (cfg == MXA_CFG_RMSC03_MM) params_rmsc03_mm(P);
@@ -653,6 +655,264 @@ constexpr MxaParams params(int cfg) {
   else if (cfg == MXA_CFG_HIST_FUND_VALUE) params_hist_fund(P, false);
   else if (cfg == MXA_CFG_HIST_FUND_DIVERSE) params_hist_fund(P, true);
   else params_sparse_zi(P, cfg == MXA_CFG_SPARSE_ZI_1000);
+  return P;
+}
+
+// ---- runtime compositions (include/mxa.h mxa_config): a base script's construction with the
+// caller's counts and parameters.  The engine is specialised per composition (mxa_config_compile:
+// the translation unit of the base configuration, compiled with MXA_CUSTOM_HDR naming the
+// composition), so these functions run both on the host and as constant expressions.
+constexpr bool custom_base_ok(int b) {
+  return b == MXA_CFG_RMSC03 || b == MXA_CFG_VALUE_NOISE || b == MXA_CFG_SPARSE_ZI_100 || b == MXA_CFG_SPARSE_ZI_1000;
+}
+constexpr bool custom_zi(int b) { return b == MXA_CFG_SPARSE_ZI_100 || b == MXA_CFG_SPARSE_ZI_1000; }
+
+// the base script's values as a composition (mxa_config_defaults)
+constexpr void config_defaults(int base, mxa_config& c) {
+  const MxaParams P = params_builtin(base);
+  c = mxa_config{};
+  c.base = base;
+  c.log_orders = P.ex_log_orders;
+  c.n_noise = P.n_noise;
+  c.n_value = P.n_value;
+  c.n_mm = P.n_mm;
+  c.n_momentum = P.n_mom;
+  c.n_zi_groups = custom_zi(base) ? P.zi_ngroups : 0;
+  c.zi_q_max = P.zi_qmax ? P.zi_qmax : 10;
+  for (int g = 0; g < MXA_CONFIG_ZI_GROUPS; g++) {
+    c.zi_count[g] = g < c.n_zi_groups ? P.zi_group_count[g] : 0;
+    c.zi_r_min[g] = g < c.n_zi_groups ? P.zi_rmin[g] : 0;
+    c.zi_r_max[g] = g < c.n_zi_groups ? P.zi_rmax[g] : 0;
+    c.zi_eta[g] = g < c.n_zi_groups ? P.zi_eta[g] : 0.0;
+  }
+  c.zi_sigma_n = P.zi_sigma_n;
+  c.zi_r_bar = P.zi_rbar;
+  c.zi_kappa = P.zi_kappa;
+  c.zi_sigma_s = P.zi_sigma_s;
+  c.zi_sigma_pv = P.zi_sigma_pv;
+  c.zi_lambda_a = P.zi_lambda;
+  c.mkt_open_ns = P.mkt_open;
+  c.mkt_close_ns = P.mkt_close;
+  c.kernel_start_ns = P.start;
+  c.kernel_stop_ns = P.stop;
+  c.noise_wake_open_ns = P.noise_open;
+  c.noise_wake_close_ns = P.noise_close;
+  c.date_ns = 1561680000LL * NS;  // 2019-06-28, the date of the scripts' runs (-d 20190628)
+  c.starting_cash = P.starting_cash;
+  c.default_computation_delay_ns = P.default_comp_delay;
+  c.r_bar = P.o_rbar;
+  c.kappa = P.o_kappa;
+  c.fund_vol = P.o_fundvol;
+  c.megashock_lambda_a = P.o_lambda;
+  c.megashock_mean = P.o_msmean;
+  c.megashock_var = P.o_msvar;
+  c.value_sigma_n = P.v_sigma_n;
+  c.value_r_bar = P.v_rbar;
+  c.value_kappa = P.v_kappa;
+  c.value_sigma_s = P.v_sigma_s;
+  c.value_lambda_a = P.v_lambda;
+  c.value_starting_cash = P.v_starting_cash;
+  c.mm.mm_pov = P.mm_pov;
+  c.mm.mm_min_order_size = P.mm_min_size;
+  c.mm.mm_window_size = P.mm_window;
+  c.mm.mm_num_ticks = P.mm_ticks;
+  c.mm.mm_wake_up_freq_ns = P.mm_wake;
+  c.mom_min_size = P.mom_min;
+  c.mom_max_size = P.mom_max;
+  c.mom_wake_up_freq_ns = P.mom_wake;
+  c.lat_low = P.lat_lo;
+  c.lat_high = P.lat_hi;
+  c.queue_capacity = 0;
+  c.book_capacity = 0;
+}
+
+constexpr int custom_n_agents(const mxa_config& c) {
+  int n = 1 + c.n_noise + c.n_value + c.n_mm + c.n_momentum;
+  for (int g = 0; g < c.n_zi_groups && g < MXA_CONFIG_ZI_GROUPS; g++) n += c.zi_count[g];
+  return n;
+}
+
+// the engine shape: the base script's, with the queue and the book sized for the counts (or the
+// caller's capacities).  A full queue or book is an env error, never a silent drop (§4)
+constexpr Shape custom_shape(const mxa_config& c) {
+  Shape S = shape_builtin(c.base);
+  const int n = custom_n_agents(c);
+  int zi = 0;
+  for (int g = 0; g < c.n_zi_groups && g < MXA_CONFIG_ZI_GROUPS; g++) zi += c.zi_count[g];
+  const int ladder = c.n_mm * 2 * (c.mm.mm_num_ticks + 1);  // the POV market maker's cancel + place cycle
+  // pending events: one wakeup per agent plus what is in flight; the base scripts' measured peaks
+  // (§4: rmsc03 146 of 192 at 64 agents, value_noise 301 of 384 at 151, sparse_zi_1000 2,007 of
+  // 2,304 at 1,001) sit under these
+  int q = c.queue_capacity > 0 ? c.queue_capacity
+        : custom_zi(c.base) || c.base == MXA_CFG_VALUE_NOISE ? 2 * n + 128
+                                                              : n + 2 * ladder + 32;
+  int sq = (q + 63) / 64;
+  if (sq < 2) sq = 2;
+  if (sq >= 9 && sq < 16) sq += sq & 1;       // grouped minima: groups of sq / 2 (Eng::QG)
+  if (sq >= 16) sq = (sq + 11) / 12 * 12;     // groups of 12
+  // resting orders: the value / ZI agents' quotes, the noise agents' unfilled orders, the ladder
+  int b = c.book_capacity > 0 ? c.book_capacity : 2 * c.n_value + c.n_noise / 2 + ladder + (3 * zi) / 4 + 64;
+  int so = (b + 63) / 64;
+  if (so < 1) so = 1;
+  S.sq = sq;
+  S.so = so;
+  S.sql = 0;
+  // queue payloads in LDS up to 12 slots per lane (sparse_zi_1000's 36 keep them in HBM)
+  S.pl = sq <= 12;
+  // the register budget: the base's waves per SIMD while the book fits its VGPRs
+  if (so > 2 && S.waves > 2) S.waves = 2;
+  if ((so > 6 || sq > 12) && S.waves > 1) S.waves = 1;
+  return S;
+}
+
+// 0, or why the composition cannot be built (mxa_config_compile / mxa_create_config: MXA_EINVAL)
+constexpr const char* custom_check(const mxa_config& c) {
+  if (!custom_base_ok(c.base)) return "base must be MXA_RMSC03, MXA_VALUE_NOISE, MXA_SPARSE_ZI_100 or MXA_SPARSE_ZI_1000";
+  if (c.n_noise < 0 || c.n_value < 0 || c.n_mm < 0 || c.n_momentum < 0 || c.n_zi_groups < 0) return "negative count";
+  if (c.n_zi_groups > MXA_CONFIG_ZI_GROUPS) return "more than MXA_CONFIG_ZI_GROUPS ZI groups";
+  for (int g = 0; g < c.n_zi_groups; g++)
+    if (c.zi_count[g] < 0 || c.zi_r_min[g] < 0 || c.zi_r_max[g] < c.zi_r_min[g] || !(c.zi_eta[g] >= 0))
+      return "ZI group: count >= 0, 0 <= R_min <= R_max, eta >= 0";
+  if (custom_zi(c.base)) {
+    if (c.n_noise || c.n_value || c.n_mm || c.n_momentum) return "sparse_zi bases hold ZI agents only";
+    if (c.n_zi_groups < 1) return "sparse_zi bases need a ZI strategy table";
+    if (c.zi_q_max < 1 || c.zi_q_max > 10) return "zi_q_max in 1..10";
+    if (!(c.zi_sigma_pv >= 0) || !(c.zi_lambda_a > 0) || !(c.zi_sigma_n >= 0)) return "ZI parameters";
+  } else {
+    if (c.n_zi_groups) return "ZI groups belong to the sparse_zi bases";
+    if (c.base == MXA_CFG_VALUE_NOISE && (c.n_mm || c.n_momentum)) return "value_noise holds noise and value agents";
+    if (c.n_mm > 1) return "at most one POVMarketMakerAgent";
+    if (c.n_mm && (c.mm.mm_window_size < 0 || c.mm.mm_num_ticks < 0 || c.mm.mm_num_ticks > 60 ||
+                   c.mm.mm_wake_up_freq_ns <= 0 || !(c.mm.mm_pov >= 0) || c.mm.mm_min_order_size < 0))
+      return "market maker options (num_ticks <= 60)";
+    if (c.n_momentum && (c.mom_min_size < 0 || c.mom_max_size <= c.mom_min_size || c.mom_wake_up_freq_ns <= 0))
+      return "momentum options: 0 <= min_size < max_size, wake_up_freq > 0";
+    if (!(c.value_lambda_a > 0) || !(c.value_sigma_n >= 0)) return "value agent parameters";
+  }
+  const int n = custom_n_agents(c);
+  if (n < 2 || n > MXA_MAX_AGENTS) return "2 to 8191 agents";
+  if (c.mkt_open_ns < 0 || c.mkt_close_ns <= c.mkt_open_ns || c.kernel_start_ns < 0 || c.kernel_stop_ns < c.kernel_start_ns ||
+      c.kernel_stop_ns >= (1LL << 47))
+    return "session: 0 <= mkt_open < mkt_close, 0 <= kernel_start <= kernel_stop < 2^47 ns";
+  if (c.base == MXA_CFG_RMSC03 && c.noise_wake_close_ns < c.noise_wake_open_ns) return "noise wake window";
+  if (!(c.megashock_lambda_a > 0) || !(c.megashock_var >= 0) || !(c.fund_vol >= 0)) return "oracle parameters";
+  if (c.default_computation_delay_ns < 0 || c.starting_cash < 0) return "delay / cash";
+  if (!custom_zi(c.base) && c.base != MXA_CFG_VALUE_NOISE && (c.lat_low != 0 || c.lat_high != 0)) {
+    // rmsc03's latency is zeros (no draw); the field is not used there
+  }
+  if ((c.base != MXA_CFG_RMSC03) && !(c.lat_high >= c.lat_low && c.lat_low >= 0)) return "latency bounds";
+  const Shape S = custom_shape(c);
+  if (S.sq > 128) return "more than 128 queue slots per lane (8,192 pending events)";
+  if (S.so > 16) return "more than 16 book slots per lane (1,024 resting orders)";
+  return nullptr;
+}
+
+// the parameter block of a composition (before the layout)
+constexpr MxaParams custom_params_raw(const mxa_config& c) {
+  MxaParams P = params_builtin(c.base);
+  P.ex_log_orders = c.log_orders ? 1 : 0;
+  P.mkt_open = c.mkt_open_ns;
+  P.mkt_close = c.mkt_close_ns;
+  P.start = c.kernel_start_ns;
+  P.stop = c.kernel_stop_ns;
+  P.starting_cash = c.starting_cash;
+  P.default_comp_delay = c.default_computation_delay_ns;
+  P.o_rbar = c.r_bar;
+  P.o_kappa = c.kappa;
+  P.o_fundvol = c.fund_vol;
+  P.o_lambda = c.megashock_lambda_a;
+  P.o_msmean = c.megashock_mean;
+  P.o_msvar = c.megashock_var;
+  P.lat_lo = c.lat_low;
+  P.lat_hi = c.lat_high;
+  P.first_noise = P.n_noise = P.first_value = P.n_value = P.first_mm = P.n_mm = P.first_mom = P.n_mom = 0;
+  P.first_zi = P.n_zi = 0;
+  int a = 1;
+  if (custom_zi(c.base)) {
+    P.zi_ngroups = c.n_zi_groups;
+    int nz = 0;
+    for (int g = 0; g < 8; g++) {
+      const bool on = g < c.n_zi_groups;
+      P.zi_group_count[g] = on ? c.zi_count[g] : 0;
+      P.zi_rmin[g] = on ? c.zi_r_min[g] : 0;
+      P.zi_rmax[g] = on ? c.zi_r_max[g] : 0;
+      P.zi_eta[g] = on ? c.zi_eta[g] : 0.0;
+      nz += P.zi_group_count[g];
+    }
+    P.first_zi = 1;
+    P.n_zi = nz;
+    a += nz;
+    P.zi_qmax = c.zi_q_max;
+    P.zi_sigma_n = c.zi_sigma_n;
+    P.zi_rbar = c.zi_r_bar;
+    P.zi_kappa = c.zi_kappa;
+    P.zi_sigma_s = c.zi_sigma_s;
+    P.zi_sigma_pv = c.zi_sigma_pv;
+    P.zi_lambda = c.zi_lambda_a;
+  } else {
+    P.n_noise = c.n_noise;
+    P.first_noise = c.n_noise ? a : 0;
+    a += c.n_noise;
+    P.n_value = c.n_value;
+    P.first_value = c.n_value ? a : 0;
+    a += c.n_value;
+    P.n_mm = c.n_mm;
+    P.first_mm = c.n_mm ? a : 0;
+    a += c.n_mm;
+    P.n_mom = c.n_momentum;
+    P.first_mom = c.n_momentum ? a : 0;
+    a += c.n_momentum;
+    P.noise_open = c.noise_wake_open_ns;
+    P.noise_close = c.noise_wake_close_ns;
+    P.v_sigma_n = c.value_sigma_n;
+    P.v_rbar = c.value_r_bar;
+    P.v_kappa = c.value_kappa;
+    P.v_sigma_s = c.value_sigma_s;
+    P.v_lambda = c.value_lambda_a;
+    P.v_starting_cash = c.value_starting_cash;
+    P.mm_pov = c.mm.mm_pov;
+    P.mm_min_size = c.mm.mm_min_order_size;
+    P.mm_window = c.mm.mm_window_size;
+    P.mm_ticks = c.mm.mm_num_ticks;
+    P.mm_wake = c.mm.mm_wake_up_freq_ns;
+    P.mom_min = c.mom_min_size;
+    P.mom_max = c.mom_max_size;
+    P.mom_wake = c.mom_wake_up_freq_ns;
+  }
+  P.n_agents = a;
+  // the latency rows the engine reads: exchange row and column (cubic model), the exchange row
+  // of the symmetric matrix, none for zero latency
+  P.L.lat_len = c.base == MXA_CFG_SPARSE_ZI_100 ? 2 * a : (c.base == MXA_CFG_RMSC03 ? 0 : a);
+  // open orders per agent: the market maker's cancelled ladder stays in TradingAgent.orders until
+  // ORDER_CANCELLED (twice its ladder), the base's otherwise
+  if (c.n_mm) {
+    const int need = 4 * (c.mm.mm_num_ticks + 1) + 16;
+    int cap = 64;
+    while (cap < need) cap *= 2;
+    if (cap > P.L.open_cap) P.L.open_cap = cap;
+  }
+  // the transaction ring: the base's, and more for a crowded book
+  if (a > 256 && P.L.tx_cap < 512) P.L.tx_cap = 512;
+  return P;
+}
+
+#ifdef MXA_CUSTOM_HDR
+// the composition of this specialisation (mxa_config_compile): its bytes, and the base it follows
+#include MXA_CUSTOM_HDR
+struct CustomBytes {
+  unsigned char b[sizeof(mxa_config)];
+};
+constexpr mxa_config custom_cfg() { return __builtin_bit_cast(mxa_config, CustomBytes{MXA_CUSTOM_BYTES}); }
+static_assert(custom_cfg().base == MXA_INST_CFG, "the specialisation is compiled in its base's translation unit");
+static_assert(custom_check(custom_cfg()) == nullptr, "a composition mxa_config_compile accepted");
+constexpr bool is_custom(int cfg) { return cfg == MXA_INST_CFG; }
+#else
+constexpr bool is_custom(int) { return false; }
+constexpr mxa_config custom_cfg() { return mxa_config{}; }
+#endif
+constexpr Shape shape(int cfg) { return is_custom(cfg) ? custom_shape(custom_cfg()) : shape_builtin(cfg); }
+constexpr MxaParams params(int cfg) {
+  MxaParams P = is_custom(cfg) ? custom_params_raw(custom_cfg()) : params_builtin(cfg);
   layout(P, cfg);
   return P;
 }

@@ -79,6 +79,24 @@ MxaEntry make_entry() {
 
 }  // namespace
 
+#ifdef MXA_CUSTOM_HDR
+// a runtime composition's specialisation (mxa_config_compile): a library of its own, loaded by
+// mxa_create_config.  Everything but this entry point is hidden (-fvisibility=hidden), so its
+// kernels and launchers never interpose on libmxa's instantiation of the same base
+#ifndef MXA_BUILD_ID
+#error "a specialisation carries the build id of the libmxa that compiled it"
+#endif
+extern "C" __attribute__((visibility("default"))) int mxa_custom_entry(MxaEntry* e, MxaParams* P, size_t* lds,
+                                                                      mxa_config* cfg, const char** build_id) {
+  *e = make_entry<MXA_INST_CFG>();
+  *P = mxa_cfg::params(MXA_INST_CFG);
+  *lds = mxa_cfg::lds_bytes(MXA_INST_CFG);
+  *cfg = mxa_cfg::custom_cfg();
+  *build_id = MXA_BUILD_ID;
+  return (int)sizeof(MxaParams);
+}
+#else
 #define MXA_ENTRY_CAT2(a, b) a##b
 #define MXA_ENTRY_CAT(a, b) MXA_ENTRY_CAT2(a, b)
 MxaEntry MXA_ENTRY_CAT(mxa_entry_, MXA_INST_CFG)() { return make_entry<MXA_INST_CFG>(); }
+#endif

@@ -81,7 +81,8 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_build_id", "mxa_set_book_log", "mxa_read_book_log", "mxa_write_records", "mxa_set_id_persistence",
            "mxa_read_counters", "mxa_create_hist", "mxa_create_replay_runner",
            "mxa_set_stop_time", "mxa_run_until", "mxa_create_replay_twap", "mxa_create_params", "mxa_set_mm_params",
-           "mxa_mm_defaults", "mxa_resident_envs", "mxa_set_exchange_log"]
+           "mxa_mm_defaults", "mxa_resident_envs", "mxa_set_exchange_log", "mxa_config_defaults",
+           "mxa_config_compile", "mxa_config_key", "mxa_create_config", "mxa_config_info"]
 COUNTER_WORDS = 34  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
@@ -132,7 +133,10 @@ def load():
                        ("mxa_create_replay_twap", [P, P, P, P, P, I32, I32, I32, I32, I32, ctypes.POINTER(P)]),
                        ("mxa_create_params", [I32, I32, P, P, I32, I32, ctypes.POINTER(P)]),
                        ("mxa_set_mm_params", [P, P]), ("mxa_resident_envs", [P]),
-                       ("mxa_set_exchange_log", [P, I32])):
+                       ("mxa_set_exchange_log", [P, I32]),
+                       ("mxa_config_defaults", [I32, P]), ("mxa_config_compile", [P, ctypes.c_char_p, P, I32]),
+                       ("mxa_config_key", [P, P]), ("mxa_config_info", [I32, P]),
+                       ("mxa_create_config", [P, I32, P, I32, I32, ctypes.c_char_p, ctypes.POINTER(P)])):
         if hasattr(L, name):  # (older single-configuration A/B builds lack them; libmxa.so has all)
             getattr(L, name).argtypes = args
     L.mxa_write_rl_state.argtypes = [P, P]

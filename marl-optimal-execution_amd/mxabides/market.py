@@ -32,8 +32,14 @@ class VecMarket:
         record or one per env; include/mxa.h mxa_create_params).
         exchange_log: the exchange's own log (ExchangeAgent.log, EXCHANGE_AGENT.bz2) rides in the
         book-update log (include/mxa.h mxa_set_exchange_log; needs book_log)."""
-        if config not in _lib.CONFIG_IDS:
-            raise ValueError("unknown config %r (supported: %s)" % (config, sorted(_lib.CONFIG_IDS)))
+        from .composition import MarketConfig
+        self.composition = None
+        if isinstance(config, MarketConfig):  # a runtime composition (mxabides.composition)
+            self.composition = MarketConfig.from_buffer_copy(bytes(config))
+            config = self.composition.base_name
+        elif config not in _lib.CONFIG_IDS:
+            raise ValueError("unknown config %r (supported: %s, or a composition.MarketConfig)" %
+                             (config, sorted(_lib.CONFIG_IDS)))
         self.L = _lib.load()
         self.config = config
         if symbol is not None:
@@ -66,6 +72,16 @@ class VecMarket:
             rc = self.L.mxa_create_hist(_lib.CONFIG_IDS[config], self.n_envs, self.seeds.ctypes.data, device, trace_cap,
                                         f.t.ctypes.data, f.v.ctypes.data, len(f), ctypes.byref(self._h))
             self._check(rc, "mxa_create_hist")
+        elif self.composition is not None:
+            if mm_params is not None or fundamental is not None or tape is not None:
+                raise ValueError("a composition carries its own parameters (MarketConfig.mm)")
+            rc = self.L.mxa_create_config(ctypes.byref(self.composition), self.n_envs, self.seeds.ctypes.data, device,
+                                          trace_cap, None, ctypes.byref(self._h))
+            if rc == -4:  # MXA_ERANGE: not compiled yet
+                raise _lib.MxaError("%s; compile it first (mxabides.composition.compile)" %
+                                    self.L.mxa_last_error(None).decode())
+            if rc < 0:
+                raise _lib.MxaError("mxa_create_config failed (%d): %s" % (rc, self.L.mxa_last_error(None).decode()))
         elif mm_params is not None:
             if config != "rmsc03":
                 raise ValueError("mm_params are config/rmsc03.py's market-maker options")
@@ -86,6 +102,18 @@ class VecMarket:
         self.exchange_log_on = False
         if exchange_log:
             self.set_exchange_log(True)
+
+    def _agent_names(self):
+        if self.composition is not None:
+            from .composition import agent_names as names
+            return names(self.composition)
+        return agent_names(self.config)
+
+    def _agent_type_names(self):
+        if self.composition is not None:
+            from .composition import agent_type_names as names
+            return names(self.composition)
+        return agent_type_names(self.config)
 
     @property
     def symbol(self):
@@ -259,7 +287,7 @@ class VecMarket:
         lines (TradingAgent.py:121-126) and Kernel's mean ending value per agent type
         (Kernel.py:337-341)."""
         FL_LAST_FLOAT = 1024
-        names, tnames, sym = agent_names(self.config), agent_type_names(self.config), self.symbol
+        names, tnames, sym = self._agent_names(), self._agent_type_names(), self.symbol
         lines, gains, counts, order = [], {}, {}, []
         for a, st in enumerate(self.agents(env)):
             if a == 0:
@@ -295,7 +323,7 @@ class VecMarket:
             self.finalize()
         fin = (_lib.AgentFinal * self.n_agents)()
         self._check(self.L.mxa_read_final(self._h, env, fin, self.n_agents), "mxa_read_final")
-        tnames = agent_type_names(self.config)
+        tnames = self._agent_type_names()
         ag = self.agents(env)
         FL_LAST_FLOAT = 1024
         rows = [dict(AgentID=a, AgentStrategy=tnames[a], EventType="STARTING_CASH", Event=int(ag[a]["starting_cash"]))
@@ -352,6 +380,9 @@ class VecMarket:
         from .booklog import SESSION_DATE
         if self.config in REPLAY_CONFIGS and getattr(self.tape, "date", None):
             return self.tape.date
+        if self.composition is not None:  # its -d historical date
+            import pandas as pd
+            return pd.Timestamp(int(self.composition.date_ns), unit="ns").strftime("%Y-%m-%d")
         return SESSION_DATE
 
     def exchange_events(self, env):
@@ -366,7 +397,7 @@ class VecMarket:
         from .booklog import exchange_log
         if not self.exchange_log_on:
             raise ValueError("created without exchange_log")
-        return exchange_log(self.book_log_records(env), self.symbol, agent_type_names(self.config)[0])
+        return exchange_log(self.book_log_records(env), self.symbol, self._agent_type_names()[0])
 
     def exchange_log_frame(self, env):
         """the DataFrame Agent.kernelTerminating writes to EXCHANGE_AGENT.bz2 (Agent.py:86-95)"""
@@ -377,7 +408,7 @@ class VecMarket:
         """log_dir/<exchange name without spaces>.bz2 as Kernel.writeLog pickles it
         (Kernel.py:520-547): EXCHANGE_AGENT.bz2, or ExchangeAgent0.bz2 for an "Exchange Agent 0"."""
         os.makedirs(log_dir, exist_ok=True)
-        path = os.path.join(log_dir, "%s.bz2" % agent_names(self.config)[0].replace(" ", ""))
+        path = os.path.join(log_dir, "%s.bz2" % self._agent_names()[0].replace(" ", ""))
         self.exchange_log_frame(env).to_pickle(path, compression="bz2")
         return path
 

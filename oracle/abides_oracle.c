@@ -282,6 +282,7 @@ typedef struct {
 #define HIST_RETIRED 48
 struct ora_env {
     char config[32];
+    int has_cfg, cfg_log_orders; /* a runtime composition (ora_create_config) and its exchange's log_orders */
     int n;
     agent_t* ag;
     /* exchange (agent 0) */
@@ -2693,16 +2694,118 @@ static int64_t get_wake_time(ora_env* e, int64_t open, int64_t close) {
     return open + (int64_t)(mult * (double)(close - open));
 }
 
-static int build_sparse_zi(ora_env* e, uint32_t seed, int big) {
-    /* config/sparse_zi_100.py:73-334 (sparse_zi_1000.py for big) */
+/* the base scripts' compositions (include/mxa.h mxa_config_defaults: mxa_config.h config_defaults
+ * restates the same values for the device; tests/test_composition.py checks they agree) */
+int ora_config_defaults(const char* base, ora_config* c) {
+    memset(c, 0, sizeof *c);
+    const int64_t open = 9 * NS_HOUR + 30 * NS_MIN;
+    c->date_ns = 1561680000LL * NS_SEC; /* 2019-06-28 */
+    c->r_bar = 1e5;
+    c->kappa = 1.67e-12;
+    c->fund_vol = 1e-4;
+    c->megashock_lambda_a = 2.77778e-13;
+    c->megashock_mean = 1e3;
+    c->megashock_var = 5e4;
+    c->starting_cash = 10000000;
+    c->mkt_open_ns = open;
+    c->zi_q_max = 10;
+    /* the fields the base leaves at params_base / MxaParams defaults (device config_defaults) */
+    c->mm.mm_pov = 0;
+    if (!strcmp(base, "rmsc03")) { /* config/rmsc03.py:55-235 */
+        c->base = 0;
+        c->log_orders = 1;
+        c->n_noise = 50;
+        c->n_value = 10;
+        c->n_mm = 1;
+        c->n_momentum = 2;
+        c->mkt_close_ns = 9 * NS_HOUR + 45 * NS_MIN;
+        c->kernel_start_ns = open;
+        c->kernel_stop_ns = c->mkt_close_ns + NS_MIN;
+        c->noise_wake_open_ns = 9 * NS_HOUR;
+        c->noise_wake_close_ns = 16 * NS_HOUR;
+        c->value_sigma_n = 1e5 / 10;
+        c->value_r_bar = 1e5;
+        c->value_kappa = 1.67e-15;
+        c->value_sigma_s = 100000;
+        c->value_lambda_a = 7e-11;
+        c->value_starting_cash = 10000000;
+        c->mm.mm_pov = 0.05;
+        c->mm.mm_min_order_size = 20;
+        c->mm.mm_window_size = 5;
+        c->mm.mm_num_ticks = 20;
+        c->mm.mm_wake_up_freq_ns = NS_SEC;
+        c->mom_min_size = 1;
+        c->mom_max_size = 10;
+        c->mom_wake_up_freq_ns = 20 * NS_SEC;
+        return 0;
+    }
+    if (!strcmp(base, "value_noise")) { /* config/value_noise.py:45-200 */
+        c->base = 5;
+        c->log_orders = 0;
+        c->n_noise = 100;
+        c->n_value = 50;
+        c->mkt_close_ns = 10 * NS_HOUR + 30 * NS_MIN;
+        c->kernel_start_ns = 0;
+        c->kernel_stop_ns = 17 * NS_HOUR;
+        c->default_computation_delay_ns = 1000000000;
+        c->value_sigma_n = 1000000.0;
+        c->value_r_bar = 1e5;
+        c->value_kappa = 1.67e-15;
+        c->value_sigma_s = 1e-4;
+        c->value_lambda_a = 1e-12;
+        c->value_starting_cash = 100000;
+        c->lat_low = 21000;
+        c->lat_high = 13000000;
+        return 0;
+    }
+    if (!strcmp(base, "sparse_zi_100") || !strcmp(base, "sparse_zi_1000")) { /* config/sparse_zi_100.py:73-334 */
+        const int big = !strcmp(base, "sparse_zi_1000");
+        static const int n100[7] = {15, 15, 14, 14, 14, 14, 14};
+        static const int n1000[7] = {143, 143, 143, 143, 143, 143, 142};
+        static const int rmin[7] = {0, 0, 0, 0, 0, 250, 250};
+        static const int rmax[7] = {250, 500, 1000, 1000, 2000, 500, 500};
+        static const double eta[7] = {1, 1, 0.8, 1, 0.8, 0.8, 1};
+        c->base = big ? 2 : 1;
+        c->log_orders = big ? 0 : 1;
+        c->n_zi_groups = 7;
+        for (int g = 0; g < 7; g++) {
+            c->zi_count[g] = big ? n1000[g] : n100[g];
+            c->zi_r_min[g] = rmin[g];
+            c->zi_r_max[g] = rmax[g];
+            c->zi_eta[g] = eta[g];
+        }
+        c->zi_sigma_n = 1000000.0;
+        c->zi_r_bar = 1e5;
+        c->zi_kappa = 1.67e-15;
+        c->zi_sigma_s = 1e-4;
+        c->zi_sigma_pv = 5e6;
+        c->zi_lambda_a = 1e-12;
+        c->mkt_close_ns = 16 * NS_HOUR;
+        c->kernel_start_ns = 0;
+        c->kernel_stop_ns = 17 * NS_HOUR;
+        c->default_computation_delay_ns = 1000000000;
+        c->lat_low = 21000;
+        c->lat_high = big ? 13000000 : 100000;
+        return 0;
+    }
+    return -1;
+}
+
+/* %g of a strategy table's eta as the script's "{}" prints it (1 for the int 1, 0.8) */
+static void eta_str(char* b, size_t n, double eta) { snprintf(b, n, "%g", eta); }
+
+static int build_sparse_zi(ora_env* e, uint32_t seed, const ora_config* c) {
+    /* config/sparse_zi_100.py:73-334 (sparse_zi_1000.py: big, the symmetric latency matrix) */
+    const int big = c->base == 2;
     rs_seed(&e->G, seed);
     rs_seed(&e->O, seed_u32(&e->G));
     rs_seed(&e->K, seed_u32(&e->G));
     if (!big) rs_seed(&e->L, seed_u32(&e->G));
-    e->start = 0;
-    e->stop = 17 * NS_HOUR;
-    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 16 * NS_HOUR;
-    oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+    e->start = c->kernel_start_ns;
+    e->stop = c->kernel_stop_ns;
+    int64_t open = c->mkt_open_ns, close = c->mkt_close_ns;
+    oracle_init(e, open, close, c->r_bar, c->kappa, c->fund_vol, c->megashock_lambda_a, c->megashock_mean,
+                c->megashock_var);
     agent_t* ex = add_agent(e, AG_EXCHANGE);
     rs_seed(&ex->rs, seed_u32(&e->G));
     snprintf(ex->name, 96, "Exchange Agent 0");
@@ -2712,48 +2815,45 @@ static int build_sparse_zi(ora_env* e, uint32_t seed, int big) {
     e->ex_pipeline = 0;
     e->ex_comp = 0;
     e->stream_history = 10;
-    static const int n100[7] = {15, 15, 14, 14, 14, 14, 14};
-    static const int n1000[7] = {143, 143, 143, 143, 143, 143, 142};
-    static const int rmin[7] = {0, 0, 0, 0, 0, 250, 250};
-    static const int rmax[7] = {250, 500, 1000, 1000, 2000, 500, 500};
-    static const double eta[7] = {1, 1, 0.8, 1, 0.8, 0.8, 1};
-    static const char* etas[7] = {"1", "1", "0.8", "1", "0.8", "0.8", "1"};
-    for (int g = 0; g < 7; g++) {
-        int cnt = big ? n1000[g] : n100[g];
-        for (int k = 0; k < cnt; k++) {
+    const int nq = 2 * c->zi_q_max;
+    for (int g = 0; g < c->n_zi_groups; g++) {
+        char etas[32];
+        eta_str(etas, sizeof etas, c->zi_eta[g]);
+        for (int k = 0; k < c->zi_count[g]; k++) {
             agent_t* a = add_agent(e, AG_ZI);
             rs_seed(&a->rs, seed_u32(&e->G));
-            snprintf(a->name, 96, "ZI Agent %d Type %d [%d <= R <= %d, eta=%s]", a->id, g + 1, rmin[g], rmax[g], etas[g]);
-            snprintf(a->tname, 96, "ZeroIntelligenceAgent Type %d [%d <= R <= %d, eta=%s]", g + 1, rmin[g], rmax[g], etas[g]);
-            trading_init(a, 10000000);
-            a->sigma_n = 1000000.0;
-            a->r_bar = 1e5;
-            a->kappa = 1.67e-15;
-            a->sigma_s = 1e-4;
-            a->q_max = 10;
-            a->R_min = rmin[g];
-            a->R_max = rmax[g];
-            a->eta = eta[g];
-            a->lambda_a = 1e-12;
-            a->r_t = 1e5;
+            snprintf(a->name, 96, "ZI Agent %d Type %d [%d <= R <= %d, eta=%s]", a->id, g + 1, c->zi_r_min[g],
+                     c->zi_r_max[g], etas);
+            snprintf(a->tname, 96, "ZeroIntelligenceAgent Type %d [%d <= R <= %d, eta=%s]", g + 1, c->zi_r_min[g],
+                     c->zi_r_max[g], etas);
+            trading_init(a, c->starting_cash);
+            a->sigma_n = c->zi_sigma_n;
+            a->r_bar = c->zi_r_bar;
+            a->kappa = c->zi_kappa;
+            a->sigma_s = c->zi_sigma_s;
+            a->q_max = c->zi_q_max;
+            a->R_min = c->zi_r_min[g];
+            a->R_max = c->zi_r_max[g];
+            a->eta = c->zi_eta[g];
+            a->lambda_a = c->zi_lambda_a;
+            a->r_t = c->zi_r_bar;
             a->sigma_t = 0;
             double th[20];
-            for (int i = 0; i < 20; i++) th[i] = rint(rs_normal(&a->rs, 0, sqrt(5e6)));
-            qsort(th, 20, sizeof(double), cmp_desc);
-            for (int i = 0; i < 20; i++) a->theta[i] = (int64_t)th[i];
+            for (int i = 0; i < nq; i++) th[i] = rint(rs_normal(&a->rs, 0, sqrt(c->zi_sigma_pv)));
+            qsort(th, nq, sizeof(double), cmp_desc);
+            for (int i = 0; i < nq; i++) a->theta[i] = (int64_t)th[i];
         }
     }
     int n = e->n;
     e->lat = (double*)malloc(sizeof(double) * (size_t)n * n);
+    for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, c->lat_low, c->lat_high);
     if (!big) {
-        for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, 21000, 100000);
         e->lat_mode = 2;
         e->jitter = 0.3;
         e->clip = 0.05;
         e->unit = 5;
         e->noise_len = 0;
     } else {
-        for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, 21000, 13000000);
         for (int i = 0; i < n; i++)
             for (int j = 0; j < n; j++) {
                 if (i > j) e->lat[(size_t)i * n + j] = e->lat[(size_t)j * n + i];
@@ -2766,7 +2866,7 @@ static int build_sparse_zi(ora_env* e, uint32_t seed, int big) {
     e->comp_delay = (int64_t*)calloc(n, sizeof(int64_t));
     for (int i = 0; i < n; i++) {
         e->agent_time[i] = e->start;
-        e->comp_delay[i] = 1000000000;
+        e->comp_delay[i] = c->default_computation_delay_ns;
     }
     return 0;
 }
@@ -2779,23 +2879,24 @@ static int build_sparse_zi(ora_env* e, uint32_t seed, int big) {
 /* rfv: 0 rmsc03, 1 random_fund_value, 2 random_fund_diverse, 3 / 4 hist_fund_value / _diverse
  * (config/hist_fund_*.py: the same agents on an ExternalFileOracle, which draws nothing at
  * construction; the value agents' r_bar is the series' first value, sigma_n = r_bar / 10) */
-static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv) {
+static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv, const ora_config* c) {
     const int hist = rfv >= 3;
     if (hist) {
         if (!g_fs_n) return -2; /* ora_set_fundamental first */
         rfv -= 2;
     }
     rs_seed(&e->G, seed);
-    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = rfv ? 16 * NS_HOUR : 9 * NS_HOUR + 45 * NS_MIN;
+    int64_t open = c->mkt_open_ns, close = c->mkt_close_ns;
     rs_seed(&e->O, seed_u32(&e->G));
     if (hist) {
         e->efo = 1;
         e->o_open = open;
         e->o_close = close;
     } else {
-        oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+        oracle_init(e, open, close, c->r_bar, c->kappa, c->fund_vol, c->megashock_lambda_a, c->megashock_mean,
+                    c->megashock_var);
     }
-    const double vr_bar = hist ? g_fs_v[0] : 1e5;
+    const double vr_bar = hist ? g_fs_v[0] : c->value_r_bar;
     agent_t* ex = add_agent(e, AG_EXCHANGE);
     rs_seed(&ex->rs, seed_u32(&e->G));
     snprintf(ex->name, 96, "EXCHANGE_AGENT");
@@ -2805,8 +2906,8 @@ static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv) {
     e->ex_pipeline = 0;
     e->ex_comp = 0;
     e->stream_history = 10;
-    int64_t nopen = rfv ? open : 9 * NS_HOUR, nclose = 16 * NS_HOUR;
-    for (int j = 0; j < (rfv ? 5000 : 50); j++) {
+    int64_t nopen = c->noise_wake_open_ns, nclose = c->noise_wake_close_ns;
+    for (int j = 0; j < c->n_noise; j++) {
         int64_t wt = get_wake_time(e, nopen, nclose);
         agent_t* a = add_agent(e, AG_NOISE);
         a->wakeup_time = wt;
@@ -2814,45 +2915,45 @@ static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv) {
         a->size = rs_randint(&e->G, 20, 50);
         snprintf(a->name, 96, "NoiseAgent %d", a->id);
         snprintf(a->tname, 96, "NoiseAgent");
-        trading_init(a, 10000000);
+        trading_init(a, c->starting_cash);
     }
-    for (int j = 0; j < (rfv ? 100 : 10); j++) {
+    for (int j = 0; j < c->n_value; j++) {
         agent_t* a = add_agent(e, AG_VALUE);
         rs_seed(&a->rs, seed_u32(&e->G));
         a->size = rs_randint(&e->G, 20, 50);
         snprintf(a->name, 96, "Value Agent %d", a->id);
         snprintf(a->tname, 96, "ValueAgent");
-        trading_init(a, 10000000);
-        a->sigma_n = vr_bar / 10;
+        trading_init(a, c->value_starting_cash);
+        a->sigma_n = hist ? vr_bar / 10 : c->value_sigma_n; /* hist_fund_*: r_bar / 10 of the series' r_bar */
         a->r_bar = vr_bar;
-        a->kappa = 1.67e-15;
-        a->sigma_s = 100000;
-        a->lambda_a = rfv ? 1e-12 : 7e-11;
+        a->kappa = c->value_kappa;
+        a->sigma_s = c->value_sigma_s;
+        a->lambda_a = c->value_lambda_a;
         a->r_t = vr_bar;
         a->sigma_t = 0;
     }
-    for (int j = 0; j < (rfv ? 0 : 1); j++) {
+    for (int j = 0; j < c->n_mm; j++) {
         agent_t* a = add_agent(e, AG_POVMM);
         rs_seed(&a->rs, seed_u32(&e->G));
         snprintf(a->name, 96, "POV_MARKET_MAKER_AGENT_%d", a->id);
         snprintf(a->tname, 96, "POVMarketMakerAgent");
-        trading_init(a, 10000000);
-        a->pov = 0.05;
-        a->min_size = 20;
-        a->window = 5;
-        a->num_ticks = 20;
-        a->wake_freq = NS_SEC;
-        a->order_size = 20;
+        trading_init(a, c->starting_cash);
+        a->pov = c->mm.mm_pov;
+        a->min_size = c->mm.mm_min_order_size;
+        a->window = c->mm.mm_window_size;
+        a->num_ticks = c->mm.mm_num_ticks;
+        a->wake_freq = c->mm.mm_wake_up_freq_ns;
+        a->order_size = c->mm.mm_min_order_size; /* order_size = min_order_size */
         a->aw_spread = a->aw_tv = 1;
     }
-    for (int j = 0; j < (rfv ? 0 : 2); j++) {
+    for (int j = 0; j < c->n_momentum; j++) {
         agent_t* a = add_agent(e, AG_MOMENTUM);
         rs_seed(&a->rs, seed_u32(&e->G));
-        a->size = rs_randint(&a->rs, 1, 10);
+        a->size = rs_randint(&a->rs, c->mom_min_size, c->mom_max_size);
         snprintf(a->name, 96, "MOMENTUM_AGENT_%d", a->id);
         snprintf(a->tname, 96, "MomentumAgent");
-        trading_init(a, 10000000);
-        a->wake_freq = 20 * NS_SEC;
+        trading_init(a, c->starting_cash);
+        a->wake_freq = c->mom_wake_up_freq_ns;
     }
     if (rfv == 2) { /* config/random_fund_diverse.py:157-198: a MarketMakerAgent (100-101 shares, 1 min,
                        polling) and 25 momentum agents (1-10 shares, the default 60 s) */
@@ -2880,14 +2981,17 @@ static int build_rmsc03_like(ora_env* e, uint32_t seed, int rfv) {
         }
     }
     rs_seed(&e->K, seed_u32(&e->G));
-    e->start = open;
-    e->stop = close + NS_MIN;
+    e->start = c->kernel_start_ns;
+    e->stop = c->kernel_stop_ns;
     e->lat_mode = 0;
     e->noise_len = 1;
     int n = e->n;
     e->agent_time = (int64_t*)calloc(n, sizeof(int64_t));
     e->comp_delay = (int64_t*)calloc(n, sizeof(int64_t));
-    for (int i = 0; i < n; i++) e->agent_time[i] = e->start;
+    for (int i = 0; i < n; i++) {
+        e->agent_time[i] = e->start;
+        e->comp_delay[i] = c->default_computation_delay_ns;
+    }
     return 0;
 }
 
@@ -2924,7 +3028,9 @@ static void zi_params(agent_t* a, int64_t rmin, int64_t rmax, double sigma_n, do
  * from the same arguments (tests/golden/gen_fixtures.py rmsc03_sbmm*): window 5, 20 ticks, wake-up
  * 1 s, order_size = --mm-min-order-size (20); the random_state draw is the POV maker's */
 static int build_rmsc03_sbmm(ora_env* e, uint32_t seed, int subscribe) {
-    int rc = build_rmsc03_like(e, seed, 0);
+    ora_config c;
+    ora_config_defaults("rmsc03", &c);
+    int rc = build_rmsc03_like(e, seed, 0, &c);
     if (rc) return rc;
     agent_t* a = &e->ag[61];
     a->type = AG_SBMM;
@@ -3031,12 +3137,13 @@ static int build_rmsc0x(ora_env* e, uint32_t seed, int v2, int obi) {
  * exponential, exchange seed; per noise agent its seed, then wakeup_time = open + rand() *
  * (close - open) (pandas float * Timedelta truncates to ns), then NoiseAgent.__init__'s
  * size; per value agent its seed, then its size; then the 151 x 151 latency draws. */
-static int build_value_noise(ora_env* e, uint32_t seed) {
+static int build_value_noise(ora_env* e, uint32_t seed, const ora_config* c) {
     rs_seed(&e->G, seed);
-    int64_t open = 9 * NS_HOUR + 30 * NS_MIN, close = 10 * NS_HOUR + 30 * NS_MIN;
+    int64_t open = c->mkt_open_ns, close = c->mkt_close_ns;
     rs_seed(&e->O, seed_u32(&e->G));
     rs_seed(&e->K, seed_u32(&e->G));
-    oracle_init(e, open, close, 1e5, 1.67e-12, 1e-4, 2.77778e-13, 1e3, 5e4);
+    oracle_init(e, open, close, c->r_bar, c->kappa, c->fund_vol, c->megashock_lambda_a, c->megashock_mean,
+                c->megashock_var);
     agent_t* ex = add_agent(e, AG_EXCHANGE);
     rs_seed(&ex->rs, seed_u32(&e->G));
     snprintf(ex->name, 96, "Exchange Agent 0");
@@ -3046,33 +3153,33 @@ static int build_value_noise(ora_env* e, uint32_t seed) {
     e->ex_pipeline = 0;
     e->ex_comp = 0;
     e->stream_history = 10;
-    for (int j = 0; j < 100; j++) {
+    for (int j = 0; j < c->n_noise; j++) {
         agent_t* a = add_agent(e, AG_NOISE);
         rs_seed(&a->rs, seed_u32(&e->G));
         a->wakeup_time = open + (int64_t)(rs_double(&e->G) * (double)(close - open));
         a->size = rs_randint(&e->G, 20, 50);
         snprintf(a->name, 96, "NoiseAgent %d", a->id);
         snprintf(a->tname, 96, "NoiseAgent");
-        trading_init(a, 10000000);
+        trading_init(a, c->starting_cash);
     }
-    for (int j = 0; j < 50; j++) {
+    for (int j = 0; j < c->n_value; j++) {
         agent_t* a = add_agent(e, AG_VALUE);
         rs_seed(&a->rs, seed_u32(&e->G));
         a->size = rs_randint(&e->G, 20, 50);
         snprintf(a->name, 96, "Value Agent %d", a->id);
         snprintf(a->tname, 96, "ValueAgent %d", a->id);
-        trading_init(a, 100000); /* ValueAgent's default starting_cash */
-        a->sigma_n = 1000000.0;
-        a->r_bar = 1e5;
-        a->kappa = 1.67e-15;
-        a->sigma_s = 1e-4;
-        a->lambda_a = 1e-12;
-        a->r_t = 1e5;
+        trading_init(a, c->value_starting_cash); /* ValueAgent's default starting_cash in the script */
+        a->sigma_n = c->value_sigma_n;
+        a->r_bar = c->value_r_bar;
+        a->kappa = c->value_kappa;
+        a->sigma_s = c->value_sigma_s;
+        a->lambda_a = c->value_lambda_a;
+        a->r_t = c->value_r_bar;
         a->sigma_t = 0;
     }
     int n = e->n;
     e->lat = (double*)malloc(sizeof(double) * (size_t)n * n);
-    for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, 21000, 13000000);
+    for (size_t i = 0; i < (size_t)n * n; i++) e->lat[i] = rs_uniform(&e->G, c->lat_low, c->lat_high);
     for (int i = 0; i < n; i++)
         for (int j = 0; j < n; j++) {
             if (i > j) e->lat[(size_t)i * n + j] = e->lat[(size_t)j * n + i];
@@ -3080,13 +3187,13 @@ static int build_value_noise(ora_env* e, uint32_t seed) {
         }
     e->lat_mode = 1;
     e->noise_len = 6;
-    e->start = 0;
-    e->stop = 17 * NS_HOUR;
+    e->start = c->kernel_start_ns;
+    e->stop = c->kernel_stop_ns;
     e->agent_time = (int64_t*)calloc(n, sizeof(int64_t));
     e->comp_delay = (int64_t*)calloc(n, sizeof(int64_t));
     for (int i = 0; i < n; i++) {
         e->agent_time[i] = e->start;
-        e->comp_delay[i] = 1000000000;
+        e->comp_delay[i] = c->default_computation_delay_ns;
     }
     return 0;
 }
@@ -3097,7 +3204,9 @@ static int build_value_noise(ora_env* e, uint32_t seed) {
  * pd.date_range(09:31, 09:44, "30S"), run by a GymKernel with rmsc03's start/stop, latency
  * zeros(65, 65), noise [0.0] and compute delay 0.  The DummyRL draws nothing. */
 static int build_rmsc03_rl(ora_env* e, uint32_t seed) {
-    int rc = build_rmsc03_like(e, seed, 0);
+    ora_config c;
+    ora_config_defaults("rmsc03", &c);
+    int rc = build_rmsc03_like(e, seed, 0, &c);
     if (rc) return rc;
     agent_t* r = add_agent(e, AG_DUMMYRL);
     trading_init(r, 0);
@@ -3246,25 +3355,74 @@ int ora_rl_state(const ora_env* e, int64_t* out4) {
     return 0;
 }
 
+/* config/random_fund_value.py:59-180 as a composition of rmsc03's construction: 5000 noise agents
+ * waking in 09:30-16:00, 100 value agents (lambda_a 1e-12), no market maker or momentum agents,
+ * market 09:30-16:00, kernel 09:30-16:01 (random_fund_diverse / hist_fund_* add their extras) */
+static void cfg_random_fund(ora_config* c) {
+    ora_config_defaults("rmsc03", c);
+    c->mkt_close_ns = 16 * NS_HOUR;
+    c->kernel_start_ns = c->mkt_open_ns;
+    c->kernel_stop_ns = c->mkt_close_ns + NS_MIN;
+    c->noise_wake_open_ns = c->mkt_open_ns;
+    c->noise_wake_close_ns = 16 * NS_HOUR;
+    c->n_noise = 5000;
+    c->n_value = 100;
+    c->n_mm = 0;
+    c->n_momentum = 0;
+    c->value_lambda_a = 1e-12;
+}
+
+/* a composition's construction by its base script */
+static int build_config(ora_env* e, uint32_t seed, const ora_config* c) {
+    switch (c->base) {
+    case 0: return build_rmsc03_like(e, seed, 0, c);
+    case 5: return build_value_noise(e, seed, c);
+    case 1:
+    case 2: return build_sparse_zi(e, seed, c);
+    default: return -1;
+    }
+}
+
+/* kernelInitializing / kernelStarting of a built env (every creation path) */
+static int create_finish(ora_env* e, int rc, ora_env** out);
+
+int ora_create_config(const ora_config* c, uint32_t seed, ora_env** out) {
+    static const char* names[6] = {"rmsc03", "sparse_zi_100", "sparse_zi_1000", NULL, NULL, "value_noise"};
+    if (!c || c->base < 0 || c->base > 5 || !names[c->base]) return -1;
+    if (c->n_zi_groups < 0 || c->n_zi_groups > ORA_CONFIG_ZI_GROUPS || c->zi_q_max < 0 || c->zi_q_max > 10) return -1;
+    ora_env* e = (ora_env*)calloc(1, sizeof(ora_env));
+    snprintf(e->config, sizeof e->config, "%s", names[c->base]);
+    e->cfg_log_orders = c->log_orders ? 1 : 0;
+    e->has_cfg = 1;
+    return create_finish(e, build_config(e, seed, c), out);
+}
+
 int ora_create(const char* config, uint32_t seed, ora_env** out) {
     ora_env* e = (ora_env*)calloc(1, sizeof(ora_env));
     snprintf(e->config, sizeof e->config, "%s", config);
     int rc;
-    if (!strcmp(config, "sparse_zi_100")) rc = build_sparse_zi(e, seed, 0);
-    else if (!strcmp(config, "sparse_zi_1000")) rc = build_sparse_zi(e, seed, 1);
-    else if (!strcmp(config, "rmsc03")) rc = build_rmsc03_like(e, seed, 0);
+    ora_config c;
+    if (!strcmp(config, "sparse_zi_100") || !strcmp(config, "sparse_zi_1000") || !strcmp(config, "value_noise") ||
+        !strcmp(config, "rmsc03")) {
+        ora_config_defaults(config, &c);
+        rc = build_config(e, seed, &c);
+    } else if (!strncmp(config, "random_fund_", 12) || !strncmp(config, "hist_fund_", 10)) {
+        cfg_random_fund(&c);
+        const int rfv = !strcmp(config, "random_fund_value") ? 1 : !strcmp(config, "random_fund_diverse") ? 2
+                        : !strcmp(config, "hist_fund_value") ? 3 : !strcmp(config, "hist_fund_diverse") ? 4 : -1;
+        rc = rfv < 0 ? -1 : build_rmsc03_like(e, seed, rfv, &c);
+    }
     else if (!strcmp(config, "rmsc03_sbmm")) rc = build_rmsc03_sbmm(e, seed, 1);
     else if (!strcmp(config, "rmsc03_sbmm_poll")) rc = build_rmsc03_sbmm(e, seed, 0);
-    else if (!strcmp(config, "random_fund_value")) rc = build_rmsc03_like(e, seed, 1);
-    else if (!strcmp(config, "random_fund_diverse")) rc = build_rmsc03_like(e, seed, 2);
-    else if (!strcmp(config, "hist_fund_value")) rc = build_rmsc03_like(e, seed, 3);
-    else if (!strcmp(config, "hist_fund_diverse")) rc = build_rmsc03_like(e, seed, 4);
     else if (!strcmp(config, "rmsc03_rl")) rc = build_rmsc03_rl(e, seed);
-    else if (!strcmp(config, "value_noise")) rc = build_value_noise(e, seed);
     else if (!strcmp(config, "rmsc01")) rc = build_rmsc0x(e, seed, 0, 0);
     else if (!strcmp(config, "rmsc02")) rc = build_rmsc0x(e, seed, 1, 0);
     else if (!strcmp(config, "obi_rmsc02")) rc = build_rmsc0x(e, seed, 1, 1);
     else rc = -1;
+    return create_finish(e, rc, out);
+}
+
+static int create_finish(ora_env* e, int rc, ora_env** out) {
     if (rc) {
         free(e);
         return rc;
@@ -3425,6 +3583,7 @@ typedef struct {
     int32_t* err; /* optional: the env's oracle error code (0 ok, negative: fail() codes) */
     int64_t* stats; /* optional: [n][4] ora_stats of each env */
     const ora_mm_params* mm; /* optional: rmsc03 with per-env market-maker options */
+    const ora_config* cfg;   /* optional: a runtime composition */
     pthread_mutex_t mu;
     int rc;
 } batch_t;
@@ -3437,7 +3596,8 @@ static void* batch_worker(void* p) {
         pthread_mutex_unlock(&b->mu);
         if (i >= b->n) break;
         ora_env* e = NULL;
-        if (b->mm ? ora_create_mm(b->seeds[i], &b->mm[i], &e) : ora_create(b->config, b->seeds[i], &e)) {
+        if (b->cfg ? ora_create_config(b->cfg, b->seeds[i], &e)
+            : b->mm ? ora_create_mm(b->seeds[i], &b->mm[i], &e) : ora_create(b->config, b->seeds[i], &e)) {
             b->rc = -1;
             continue;
         }
@@ -3453,10 +3613,11 @@ static void* batch_worker(void* p) {
 
 static int run_batch_impl(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
                           int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out,
-                          double* seconds_out, const ora_mm_params* mm) {
+                          double* seconds_out, const ora_mm_params* mm, const ora_config* cfg) {
     batch_t b;
     memset(&b, 0, sizeof b);
     b.mm = mm;
+    b.cfg = cfg;
     b.err = err_out;
     b.stats = stats_out;
     b.config = config;
@@ -3481,30 +3642,36 @@ static int run_batch_impl(const char* config, const uint32_t* seeds, int n, int 
 
 int ora_run_batch(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
                   int64_t* events_out, uint64_t* hash_out, double* seconds_out) {
-    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, NULL, NULL, seconds_out, NULL);
+    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, NULL, NULL, seconds_out, NULL, NULL);
 }
 
 /* the same, with each env's error code (ora_error) in err_out[n] */
 int ora_run_batch_err(const char* config, const uint32_t* seeds, int n, int threads, int64_t max_pops,
                       int64_t* events_out, uint64_t* hash_out, int32_t* err_out, double* seconds_out) {
-    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, err_out, NULL, seconds_out, NULL);
+    return run_batch_impl(config, seeds, n, threads, max_pops, events_out, hash_out, err_out, NULL, seconds_out, NULL, NULL);
 }
 
 /* capacity statistics (ora_stats) of n envs: stats_out[n][4] */
 int ora_run_batch_stats(const char* config, const uint32_t* seeds, int n, int threads, int64_t* stats_out) {
     int64_t* ev = (int64_t*)calloc(n, sizeof(int64_t));
     uint64_t* h = (uint64_t*)calloc(n, sizeof(uint64_t));
-    int rc = run_batch_impl(config, seeds, n, threads, -1, ev, h, NULL, stats_out, NULL, NULL);
+    int rc = run_batch_impl(config, seeds, n, threads, -1, ev, h, NULL, stats_out, NULL, NULL, NULL);
     free(ev);
     free(h);
     return rc;
 }
 
+int ora_run_batch_config(const ora_config* c, const uint32_t* seeds, int n, int threads, int64_t max_pops,
+                         int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out,
+                         double* seconds_out) {
+    return run_batch_impl("composition", seeds, n, threads, max_pops, events_out, hash_out, err_out, stats_out,
+                          seconds_out, NULL, c);
+}
 int ora_run_batch_mm(const uint32_t* seeds, const ora_mm_params* params, int n, int threads, int64_t max_pops,
                      int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out, double* seconds_out) {
     if (!params) return -1;
     return run_batch_impl("rmsc03", seeds, n, threads, max_pops, events_out, hash_out, err_out, stats_out, seconds_out,
-                          params);
+                          params, NULL);
 }
 
 void ora_set_book_log(ora_env* e, int on) {
@@ -3519,13 +3686,19 @@ void ora_set_book_log(ora_env* e, int on) {
 /* the exchange's own log in the record stream (include/mxa.h mxa_set_exchange_log); log_orders is
  * the config script's ExchangeAgent(log_orders=...) */
 void ora_set_exchange_log(ora_env* e, int on) {
-    static const char* lo[] = {"rmsc03", "sparse_zi_100", "rmsc02", "random_fund_value", "random_fund_diverse",
-                               "hist_fund_value", "hist_fund_diverse", "marketreplay", "marketreplay_runner",
-                               "marketreplay_twap", "rmsc03_sbmm", "rmsc03_sbmm_poll", NULL};
     e->exlog = on;
-    e->ex_log_orders = 0;
+    e->ex_log_orders = e->has_cfg ? e->cfg_log_orders : ora_config_log_orders(e->config);
+}
+int ora_config_log_orders(const char* config) {
+    /* each script's ExchangeAgent(log_orders=...): config/rmsc03.py:102 (its compositions: the
+     * market-maker sweep, the SpreadBasedMarketMakerAgent and DummyRL ones), sparse_zi_100.py:187,
+     * rmsc02.py:84, random_fund_*.py, hist_fund_*.py, marketreplay.py:77 / agent_config.py:54 */
+    static const char* lo[] = {"rmsc03", "rmsc03_rl", "sparse_zi_100", "rmsc02", "random_fund_value",
+                               "random_fund_diverse", "hist_fund_value", "hist_fund_diverse", "marketreplay",
+                               "marketreplay_runner", "marketreplay_twap", "rmsc03_sbmm", "rmsc03_sbmm_poll", NULL};
     for (int i = 0; lo[i]; i++)
-        if (strcmp(e->config, lo[i]) == 0) e->ex_log_orders = 1;
+        if (strcmp(config, lo[i]) == 0) return 1;
+    return 0;
 }
 int64_t ora_book_records(const ora_env* e, int64_t* buf, int64_t cap) {
     if (buf) memcpy(buf, e->blr, sizeof(int64_t) * (size_t)(cap < e->nblr ? cap : e->nblr));

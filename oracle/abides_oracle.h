@@ -121,6 +121,36 @@ int ora_create_mm(uint32_t seed, const ora_mm_params* p, ora_env** out);
 /* ora_run_batch_err / _stats of rmsc03 envs with per-env market-maker options params[n] */
 int ora_run_batch_mm(const uint32_t* seeds, const ora_mm_params* params, int n, int threads, int64_t max_pops,
                      int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out, double* seconds_out);
+/* runtime compositions (include/mxa.h mxa_config, the same layout): a base script's construction
+ * ("rmsc03", "value_noise", "sparse_zi_100", "sparse_zi_1000") with the caller's agent counts,
+ * per-class parameters and session.  rmsc03, random_fund_value, value_noise and sparse_zi_* are
+ * built through the same parameterised builders, so their fixtures pin them. */
+#define ORA_CONFIG_ZI_GROUPS 8
+typedef struct {
+    int32_t base; /* 0 rmsc03, 5 value_noise, 1 sparse_zi_100, 2 sparse_zi_1000 (include/mxa.h ids) */
+    int32_t log_orders, n_noise, n_value, n_mm, n_momentum, n_zi_groups, zi_q_max;
+    int32_t zi_count[ORA_CONFIG_ZI_GROUPS], zi_r_min[ORA_CONFIG_ZI_GROUPS], zi_r_max[ORA_CONFIG_ZI_GROUPS];
+    double zi_eta[ORA_CONFIG_ZI_GROUPS];
+    double zi_sigma_n, zi_r_bar, zi_kappa, zi_sigma_s, zi_sigma_pv, zi_lambda_a;
+    int64_t mkt_open_ns, mkt_close_ns, kernel_start_ns, kernel_stop_ns, noise_wake_open_ns, noise_wake_close_ns;
+    int64_t date_ns, starting_cash, default_computation_delay_ns;
+    double r_bar, kappa, fund_vol, megashock_lambda_a, megashock_mean, megashock_var;
+    double value_sigma_n, value_r_bar, value_kappa, value_sigma_s, value_lambda_a;
+    int64_t value_starting_cash;
+    ora_mm_params mm;
+    int32_t mom_min_size, mom_max_size;
+    int64_t mom_wake_up_freq_ns;
+    double lat_low, lat_high;
+    int32_t queue_capacity, book_capacity; /* the device's capacities (unused here) */
+} ora_config;
+int ora_config_defaults(const char* base, ora_config* out);
+int ora_create_config(const ora_config* c, uint32_t seed, ora_env** out);
+/* ora_run_batch_err / _stats of one composition over n seeds */
+int ora_run_batch_config(const ora_config* c, const uint32_t* seeds, int n, int threads, int64_t max_pops,
+                         int64_t* events_out, uint64_t* hash_out, int32_t* err_out, int64_t* stats_out,
+                         double* seconds_out);
+/* the ExchangeAgent's log_orders of a configuration (the exchange-log switch) */
+int ora_config_log_orders(const char* config);
 /* n GymKernel episodes, each stepped with actions[k][i][0..2] until done or error (config
  * "rmsc03_rl" with seeds, or NULL: the replay composition on the tape t/oid/price/size/buy).
  * Per env: pops, hash, error code, steps taken and the last valid observation [n][9]. */

@@ -112,21 +112,77 @@ MM_DTYPE = np.dtype([("mm_pov", "<f8"), ("mm_min_order_size", "<i4"), ("mm_windo
                      ("mm_num_ticks", "<i4"), ("pad", "<i4"), ("mm_wake_up_freq_ns", "<i8")])
 
 
+class _Mm(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double if t == "<f8" else ctypes.c_int64 if t == "<i8" else ctypes.c_int32)
+                for n, (t, _) in ((k, (MM_DTYPE.fields[k][0].str, 0)) for k in MM_DTYPE.names)]
+
+
+_I, _Q, _F, _G = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, 8
+
+
+class OraConfig(ctypes.Structure):
+    """ora_config (abides_oracle.h): a runtime composition, the layout of include/mxa.h mxa_config"""
+    _fields_ = ([(n, _I) for n in ("base", "log_orders", "n_noise", "n_value", "n_mm", "n_momentum", "n_zi_groups",
+                                  "zi_q_max")] +
+                [("zi_count", _I * _G), ("zi_r_min", _I * _G), ("zi_r_max", _I * _G), ("zi_eta", _F * _G)] +
+                [(n, _F) for n in ("zi_sigma_n", "zi_r_bar", "zi_kappa", "zi_sigma_s", "zi_sigma_pv", "zi_lambda_a")] +
+                [(n, _Q) for n in ("mkt_open_ns", "mkt_close_ns", "kernel_start_ns", "kernel_stop_ns",
+                                  "noise_wake_open_ns", "noise_wake_close_ns", "date_ns", "starting_cash",
+                                  "default_computation_delay_ns")] +
+                [(n, _F) for n in ("r_bar", "kappa", "fund_vol", "megashock_lambda_a", "megashock_mean",
+                                  "megashock_var", "value_sigma_n", "value_r_bar", "value_kappa", "value_sigma_s",
+                                  "value_lambda_a")] +
+                [("value_starting_cash", _Q), ("mm", _Mm), ("mom_min_size", _I), ("mom_max_size", _I),
+                 ("mom_wake_up_freq_ns", _Q), ("lat_low", _F), ("lat_high", _F), ("queue_capacity", _I),
+                 ("book_capacity", _I)])
+
+
+def config_defaults(base):
+    """ora_config_defaults: the base script's composition"""
+    L = lib()
+    L.ora_config_defaults.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    c = OraConfig()
+    if L.ora_config_defaults(base.encode(), ctypes.byref(c)):
+        raise ValueError("no such base %r" % base)
+    return c
+
+
+def as_config(cfg):
+    """an ora_config from any object holding mxa_config's bytes (mxabides.composition.MarketConfig)"""
+    b = bytes(cfg)
+    if len(b) != ctypes.sizeof(OraConfig):
+        raise ValueError("a composition is %d bytes, got %d" % (ctypes.sizeof(OraConfig), len(b)))
+    return OraConfig.from_buffer_copy(b)
+
+
+def config_log_orders(config):
+    L = lib()
+    L.ora_config_log_orders.argtypes = [ctypes.c_char_p]
+    return L.ora_config_log_orders(config.encode())
+
+
 class OracleEnv:
     """One reference-semantics simulation (config + seed); config "rmsc03" with `mm` (one
-    MM_DTYPE record) runs config/rmsc03.py with those --mm-* options."""
+    MM_DTYPE record) runs config/rmsc03.py with those --mm-* options; a composition (an
+    OraConfig, or a MarketConfig's bytes) runs ora_create_config."""
 
     def __init__(self, config, seed, trace_cap=0, mm=None):
         L = lib()
-        _ensure_fundamental(config)
         self._h = ctypes.c_void_p()
-        if mm is not None:
+        if not isinstance(config, str):
+            self._cfg = as_config(config)
+            L.ora_create_config.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
+            rc = L.ora_create_config(ctypes.byref(self._cfg), seed & 0xFFFFFFFF, ctypes.byref(self._h))
+            if rc:
+                raise ValueError("oracle: bad composition")
+        elif mm is not None:
             if config != "rmsc03":
                 raise ValueError("market-maker options are config/rmsc03.py's")
             self._mm = np.ascontiguousarray(np.asarray(mm, dtype=MM_DTYPE).reshape(1))
             L.ora_create_mm.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
             rc = L.ora_create_mm(seed & 0xFFFFFFFF, self._mm.ctypes.data, ctypes.byref(self._h))
         else:
+            _ensure_fundamental(config)
             rc = L.ora_create(config.encode(), seed & 0xFFFFFFFF, ctypes.byref(self._h))
         if rc:
             raise ValueError("oracle: bad config %r" % config)
@@ -303,6 +359,26 @@ def batch_stats(config, seeds, threads):
     if L.ora_run_batch_stats(config.encode(), seeds.ctypes.data, len(seeds), threads, out.ctypes.data):
         raise RuntimeError("oracle batch failed")
     return out
+
+
+def run_batch_config(cfg, seeds, threads, max_pops=-1, stats=False):
+    """one composition over many seeds: events, hashes, error codes, seconds (and [n][4] capacity
+    statistics with stats=True)"""
+    L = lib()
+    L.ora_run_batch_config.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64] + \
+        [ctypes.c_void_p] * 4 + [ctypes.POINTER(ctypes.c_double)]
+    c = as_config(cfg)
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+    n = len(seeds)
+    ev = np.zeros(n, dtype=np.int64)
+    hs = np.zeros(n, dtype=np.uint64)
+    er = np.zeros(n, dtype=np.int32)
+    st = np.zeros((n, 4), dtype=np.int64)
+    sec = ctypes.c_double()
+    if L.ora_run_batch_config(ctypes.byref(c), seeds.ctypes.data, n, threads, max_pops, ev.ctypes.data, hs.ctypes.data,
+                              er.ctypes.data, st.ctypes.data if stats else None, ctypes.byref(sec)):
+        raise RuntimeError("oracle batch failed")
+    return (ev, hs, er, sec.value, st) if stats else (ev, hs, er, sec.value)
 
 
 def run_batch_mm(seeds, params, threads, max_pops=-1, stats=False):

@@ -238,7 +238,9 @@ def install_stubs():
     sys.path.insert(0, REF)
 
 
-def run_config(cfg, seed, out, full):
+def run_config(cfg, seed, out, full, composition=None):
+    """composition: {"date": "YYYY-MM-DD", "script": callable} of gen_config_fixtures.py, which builds
+    its agent list from the reference's classes and calls Kernel.runner itself"""
     global MIDNIGHT
     install_stubs()
     import queue
@@ -348,7 +350,8 @@ def run_config(cfg, seed, out, full):
             "obi_rmsc02": "2019-06-28", "random_fund_value": "2019-06-28",
             "random_fund_diverse": "2019-06-28", "hist_fund_value": "2019-06-28",
             "hist_fund_diverse": "2019-06-28", "marketreplay": replay[1] if replay else None,
-            "rmsc03_sbmm": "2019-06-28", "rmsc03_sbmm_poll": "2019-06-28"}[cfg]
+            "rmsc03_sbmm": "2019-06-28", "rmsc03_sbmm_poll": "2019-06-28"}[cfg] if composition is None \
+        else composition["date"]
     MIDNIGHT = int(pd.Timestamp(date).value)
     argv = ["abides.py", "-c", cfg_script, "-s", str(seed)]
     if cfg_script in ("rmsc03", "random_fund_value", "random_fund_diverse"):
@@ -373,7 +376,10 @@ def run_config(cfg, seed, out, full):
     sys.stdout = buf
     stop_error = None
     try:
-        importlib.import_module(module)
+        if composition is None:
+            importlib.import_module(module)
+        else:
+            composition["script"]()
     except Exception as ex:  # e.g. ZeroIntelligenceAgent.kernelStopping's IndexError (rmsc01)
         if "kernel" not in CAPTURE:
             raise

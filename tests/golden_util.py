@@ -146,3 +146,18 @@ def exlog_digest(rows):
         for w in exlog_row_words(*exlog_row_tuple(row)):
             h = ((h ^ (int(w) & 0xFFFFFFFFFFFFFFFF)) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
     return h
+
+
+# runtime compositions (tests/golden/gen_config_fixtures.py): (name, seed) of cfg_<name>_<seed>.*
+COMPOSITION_FIXTURES = [("rmsc03_n100_v20", 123456789), ("rmsc03_n100_v20", 7), ("rmsc03_alt", 123456789),
+                        ("rmsc03_alt", 11), ("sparse_zi_alt", 123456789), ("sparse_zi_alt", 7),
+                        ("sparse_zi_matrix_200", 123456789), ("value_noise_alt", 123456789), ("value_noise_alt", 7)]
+
+
+def load_composition(name, seed):
+    """(fixture dict with its "composition" fields, trace, summary rows) of cfg_<name>_<seed>"""
+    return load_named("cfg_%s_%d" % (name, seed))
+
+
+def composition_names():
+    return sorted({n for n, _ in COMPOSITION_FIXTURES})
