@@ -66,6 +66,19 @@ DEFAULT_ENVS = {"marketreplay": 512, "sparse_zi_1000": 1024, "random_fund_value"
 FUND = os.path.join(ROOT, "tests", "golden", "fund_JPM_20190628.npz")  # hist_fund_*: the JPM mid-price series
 
 
+def composition_of(name):
+    """--config cfg:NAME: the runtime composition of tests/golden/cfg_NAME_*.json (the agent list of
+    gen_config_fixtures.py, e.g. cfg:rmsc03_n100_v20 = rmsc03 with 100 noise and 20 value agents)"""
+    import glob
+    from mxabides import composition
+    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "cfg_%s_*.json" % name.split(":", 1)[1])))
+    files = [f for f in files if not f.endswith("_summary.json")]
+    if not files:
+        raise SystemExit("no composition %s under tests/golden" % name)
+    with open(files[0]) as f:
+        return composition.from_dict(json.load(f)["composition"])
+
+
 # ----------------------------------------------------------------------------------------------
 # rank processes
 def _free_port():
@@ -238,13 +251,19 @@ class MarketEngine(Engine):
             from mxabides.configs import mm_params
             kw["mm_params"] = mm_params(self.n, **SWEEP_OPTIONS)
             cfg = "rmsc03"
+        self.composition = None
+        if cfg.startswith("cfg:"):  # a runtime composition of the reference-run fixtures (mxa_create_config)
+            self.composition = composition_of(cfg)
+            cfg = self.composition
         self.m = mxabides.VecMarket(cfg, self.seeds(0), device=ctx.local, **kw)
         self.stream = self.torch.cuda.Stream()  # a real stream object (the legacy default stream's handle is 0)
         self.torch.cuda.set_stream(self.stream)
         self.m.set_stream(self.stream.cuda_stream)
         self.m.set_parity_hash(args.parity_hash)
-        cid = mxabides.CONFIG_IDS[cfg] if args.config != "rmsc03_sweep" else mxabides._lib.MXA_RMSC03_MM
-        self.kernel = "mxa_run_kernel<%d> (%s)" % (cid, args.config)
+        cid = (self.composition.base if self.composition is not None else mxabides.CONFIG_IDS[cfg]
+               if args.config != "rmsc03_sweep" else mxabides._lib.MXA_RMSC03_MM)
+        self.kernel = "mxa_run_kernel<%d> (%s%s)" % (cid, args.config,
+                                                      ", specialised" if self.composition is not None else "")
 
     def step(self, k, timed):
         m = self.m
@@ -313,6 +332,8 @@ class MarketEngine(Engine):
             cseeds = ((self.shard.SEED0 + first + np.arange(k, dtype=np.int64)) & 0xFFFFFFFF).astype(np.uint32)
             if self.args.config == "rmsc03_sweep":
                 cev, _, _, csec = pyoracle.run_batch_mm(cseeds, self.m.mm_params[:1].repeat(k), threads)
+            elif self.composition is not None:
+                cev, _, _, csec = pyoracle.run_batch_config(self.composition, cseeds, threads)
             else:
                 cev, _, csec = pyoracle.run_batch(self.args.config, cseeds, threads)
             ev += int(cev.sum())
@@ -332,7 +353,8 @@ class MarketEngine(Engine):
             kw["fundamental"] = self.m.fundamental
         if self.tname:
             kw["tape"] = self.m.tape
-        s = self.mx.VecMarket(self.m.config, seeds, device=self.ctx.local, **kw)
+        s = self.mx.VecMarket(self.composition if self.composition is not None else self.m.config, seeds,
+                              device=self.ctx.local, **kw)
         s.set_stream(self.stream.cuda_stream)
         s.set_parity_hash(self.args.parity_hash)
         s.run(chunk=self.args.chunk)

@@ -1345,9 +1345,12 @@ struct Eng {
   // and saved with the header) instead of an LDS read-modify-write on every push
 #ifndef MXA_MAXQ_REG_MASK
   // same results: r03 s28 sparse_zi_1000 762 -> 736 ms, rmsc02 1096 -> 1084; s31 random_fund_value
-  // 553 -> 541; not set where it cost: rmsc03 40.7 -> 42.8 (s28), rmsc01 1013 -> 1051 (s31)
+  // 553 -> 541; not set where it cost: rmsc03 40.7 -> 42.8 (s28), rmsc01 1013 -> 1051 (s31).  r06
+  // (profiles/r06/ab/ab2_ibm.txt, same digests): the replay step kernel, IBM x512 0.3164 -> 0.3099 ms,
+  // GOOG 0.4559 -> 0.4478; its Kernel.runner twins take it too
 #define MXA_MAXQ_REG_MASK ((1 << MXA_CFG_SPARSE_ZI_1000) | (1 << MXA_CFG_RMSC02) | (1 << MXA_CFG_RANDOM_FUND_VALUE) | \
-                           (1 << MXA_CFG_RANDOM_FUND_DIVERSE) | (1 << MXA_CFG_HIST_FUND_VALUE) | (1 << MXA_CFG_HIST_FUND_DIVERSE))
+                           (1 << MXA_CFG_RANDOM_FUND_DIVERSE) | (1 << MXA_CFG_HIST_FUND_VALUE) | (1 << MXA_CFG_HIST_FUND_DIVERSE) | \
+                           (1 << MXA_CFG_MARKETREPLAY) | (1 << MXA_CFG_MARKETREPLAY_RUNNER) | (1 << MXA_CFG_MARKETREPLAY_TWAP))
 #endif
   static constexpr bool MAXQ_REG = !BUILD && (((MXA_MAXQ_REG_MASK) >> CFG) & 1);
   i32 maxq;
