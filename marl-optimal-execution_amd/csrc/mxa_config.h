@@ -88,7 +88,7 @@ constexpr Shape shape(int cfg);
 #define MXA_RFD_WAVES 1
 #endif
 #ifndef MXA_RFD_SQL
-#define MXA_RFD_SQL 48
+#define MXA_RFD_SQL 24  // r06: 48 -> 24 with the LDS book arrays, 1315.2 -> 1180.7 ms (ab6_rfd_book_lds.txt)
 #endif
 // configurations whose agent-record write-back stores only the changed 128-byte quarters
 // (bit = config id; measured per configuration)
@@ -118,7 +118,9 @@ constexpr Shape shape(int cfg);
 #define MXA_RFV_WAVES 2  // random_fund_value / _diverse waves per SIMD (rfv run kernel x2048: 1 wave 1412 ms, 2 waves 1230; x4096: 2 waves 2446, 3 4014, 4 4378)
 #endif
 #ifndef MXA_RFV_SQL
-#define MXA_RFV_SQL 24  // LDS-resident queue slots per lane (96 = no HBM tier); rfv x2048 run kernel: 12 -> 1220 ms, 24 -> 840, 36 -> 1237 (fewer waves fit)
+#define MXA_RFV_SQL 12  // LDS-resident queue slots per lane (96 = no HBM tier); rfv x2048 run kernel (r02, before the
+                        // lane-major HBM tier): 12 -> 1220 ms, 24 -> 840, 36 -> 1237 (fewer waves fit); r06: 24 -> 338.1,
+                        // 12 with the LDS book arrays 330.2 (MXA_BOOK_LDS_RFV)
 #endif
 #ifndef MXA_RP_HOT
 #define MXA_RP_HOT 2  // replay configurations: the exchange's and the MarketReplayAgent's records in LDS
@@ -152,7 +154,7 @@ constexpr Shape shape_builtin(int cfg) {
        : cfg == MXA_CFG_SPARSE_ZI_1000 ? Shape{MXA_SQ_Z1K, MXA_SO_Z1K, false, 1, 6, 0}
        // random_fund_value: 6,144 queue slots (every agent keeps a wakeup pending: the oracle's
        // maximum over the 8,192 bench seeds is 5,125 events), payload in HBM; 320 book slots (max 279)
-       // the first MXA_RFV_SQL slots per lane (24: 1,536) in LDS for events due within a second,
+       // the first MXA_RFV_SQL slots per lane (12: 768) in LDS for events due within a second,
        // the other 72 per lane an HBM tier for the far wakeups (the two-tier queue, q_push)
        : (cfg == MXA_CFG_RANDOM_FUND_VALUE || cfg == MXA_CFG_HIST_FUND_VALUE) ? Shape{96, 5, false, MXA_RFV_WAVES, 6, 0, MXA_RFV_SQL}
        // random_fund_diverse: the same queue; 576 book slots (oracle max 503 resting orders and 5,153
@@ -170,7 +172,19 @@ constexpr int sq_lds(int cfg) { return shape(cfg).sql ? shape(cfg).sql : shape(c
 constexpr bool rp_hdr_lds(int cfg) {
   return cfg == MXA_CFG_MARKETREPLAY || cfg == MXA_CFG_MARKETREPLAY_RUNNER || cfg == MXA_CFG_MARKETREPLAY_TWAP;
 }
-constexpr int book_lds(int cfg) { return cfg == MXA_CFG_RMSC02 ? MXA_BOOK_LDS_RMSC02 : 0; }
+// random_fund_* / hist_fund_*: the book's order-id, arrival and epoch arrays in LDS for a launch
+// (as rmsc02's), with a 12-slot-per-lane LDS queue tier (random_fund_value) or 24 (the _diverse
+// pair) so the arrays fit.  r06 A/B, same digests (profiles/r06/ab/ab5_rfv_book_lds.txt, ab6_rf?_book_*.txt):
+// random_fund_value x2048 360.3 -> 330.2 ms (the smaller tier alone 338.1; the arrays at 24 slots
+// overflow the LDS budget: 639.3); random_fund_diverse x2048 1315.2 -> 1180.7 ms
+#ifndef MXA_BOOK_LDS_RFV
+#define MXA_BOOK_LDS_RFV 0x34
+#endif
+constexpr int book_lds(int cfg) {
+  return cfg == MXA_CFG_RMSC02 ? MXA_BOOK_LDS_RMSC02
+         : (cfg >= MXA_CFG_RANDOM_FUND_VALUE && cfg <= MXA_CFG_HIST_FUND_DIVERSE) ? MXA_BOOK_LDS_RFV
+                                                                                 : 0;
+}
 constexpr size_t lds_bytes(int cfg) {
   return (size_t)sq_lds(cfg) * 64 * (12 + (shape(cfg).pl ? 4 * shape(cfg).pw : 0)) + 512  // queue + EnvHdr
          + (size_t)shape(cfg).hot * 512                                                       // hot agent records
