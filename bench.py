@@ -67,11 +67,11 @@ FUND = os.path.join(ROOT, "tests", "golden", "fund_JPM_20190628.npz")  # hist_fu
 
 
 def composition_of(name):
-    """--config cfg:NAME: the runtime composition of tests/golden/cfg_NAME_*.json (the agent list of
-    gen_config_fixtures.py, e.g. cfg:rmsc03_n100_v20 = rmsc03 with 100 noise and 20 value agents)"""
+    """--config cfg.NAME: the runtime composition of tests/golden/cfg_NAME_*.json (the agent list of
+    gen_config_fixtures.py, e.g. cfg.rmsc03_n100_v20 = rmsc03 with 100 noise and 20 value agents)"""
     import glob
     from mxabides import composition
-    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "cfg_%s_*.json" % name.split(":", 1)[1])))
+    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "cfg_%s_*.json" % name.split(".", 1)[1])))
     files = [f for f in files if not f.endswith("_summary.json")]
     if not files:
         raise SystemExit("no composition %s under tests/golden" % name)
@@ -252,7 +252,7 @@ class MarketEngine(Engine):
             kw["mm_params"] = mm_params(self.n, **SWEEP_OPTIONS)
             cfg = "rmsc03"
         self.composition = None
-        if cfg.startswith("cfg:"):  # a runtime composition of the reference-run fixtures (mxa_create_config)
+        if cfg.startswith("cfg."):  # a runtime composition of the reference-run fixtures (mxa_create_config)
             self.composition = composition_of(cfg)
             cfg = self.composition
         self.m = mxabides.VecMarket(cfg, self.seeds(0), device=ctx.local, **kw)

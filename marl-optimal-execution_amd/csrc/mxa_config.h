@@ -764,8 +764,13 @@ constexpr Shape custom_shape(const mxa_config& c) {
   if (sq < 2) sq = 2;
   if (sq >= 9 && sq < 16) sq += sq & 1;       // grouped minima: groups of sq / 2 (Eng::QG)
   if (sq >= 16) sq = (sq + 11) / 12 * 12;     // groups of 12
-  // resting orders: the value / ZI agents' quotes, the noise agents' unfilled orders, the ladder
-  int b = c.book_capacity > 0 ? c.book_capacity : 2 * c.n_value + c.n_noise / 2 + ladder + (3 * zi) / 4 + 64;
+  // resting orders: the market maker's ladder, the value agents' quotes, a few noise orders; ZI
+  // books hold ~0.8 orders per agent.  Oracle peaks over 2,048 seeds (r06): rmsc03 with 100 noise /
+  // 20 value agents 74 (128 here), rmsc03_alt 58 (128), 60 ZI 52 (128), 199 ZI 160 (256),
+  // value_noise_alt 37 (128); the base scripts' own peaks are in DESIGN.md §4
+  int b = c.book_capacity > 0 ? c.book_capacity
+        : custom_zi(c.base) ? (3 * zi) / 4 + 64
+                            : ladder + 2 * c.n_value + c.n_noise / 8 + 32;
   int so = (b + 63) / 64;
   if (so < 1) so = 1;
   S.sq = sq;
