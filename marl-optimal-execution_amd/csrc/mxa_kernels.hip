@@ -213,6 +213,67 @@ DEV void mt_gen_block(u32* key, int b) {
   wfence();
 }
 
+// the same block in ONE memory round trip (build kernel): lane L computes the words L + 64k of
+// each dependency phase, and a phase's recurrence term B[i - 227] is the word the same lane and
+// k computed in the phase before, so it stays in a register; every A word is loaded up front and
+// B[623] takes B[396] and B[0] by readlane.  One store pass, one fence.
+DEV u32 mt_mix(u32 a0, u32 a1) {
+  const u32 y = (a0 & 0x80000000u) | (a1 & 0x7fffffffu);
+  return (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+}
+// two streams' blocks in the same round trip (both streams' A words loaded before either is
+// stored: one in-order vmcnt covers loads and stores); `two` false: the first only
+DEV void mt_gen_pair(u32* k1, int b1, u32* k2, int b2, bool two) {
+  const int lane = laneid();
+  u32* key[2] = {k1, k2};
+  const int bb[2] = {b1, b2};
+  u32 a0[2][11], a1[2][11], a3[2][4], a623[2];
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const u32* A = key[q] + ((bb[q] - 1) & 1) * MXA_MT_N;
+    const bool on = q == 0 || two;
+#pragma unroll
+    for (int k = 0; k < 11; k++) {  // k 0-3: phase 1, 4-7: phase 2, 8-10: phase 3
+      const int ph = k < 4 ? 0 : k < 8 ? 1 : 2, kk = k - 4 * ph;
+      const int i = 227 * ph + lane + 64 * kk;
+      const bool ok = on && kk * 64 + lane < (ph < 2 ? 227 : 169);
+      a0[q][k] = ok ? A[i] : 0u;
+      a1[q][k] = ok ? A[i + 1] : 0u;
+      if (ph == 0) a3[q][k] = ok ? A[i + 397] : 0u;
+    }
+    a623[q] = on ? A[623] : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    if (q == 1 && !two) break;
+    u32* B = key[q] + (bb[q] & 1) * MXA_MT_N;
+    u32 y[11];
+#pragma unroll
+    for (int k = 0; k < 4; k++) y[k] = a3[q][k] ^ mt_mix(a0[q][k], a1[q][k]);
+#pragma unroll
+    for (int k = 4; k < 11; k++) y[k] = y[k - 4] ^ mt_mix(a0[q][k], a1[q][k]);
+    const u32 b396 = rdl(y[6], 41), b0 = rdl(y[0], 0);  // 396 = 227 + 41 + 64 * 2; 0 = lane 0, k 0
+#pragma unroll
+    for (int k = 0; k < 11; k++) {
+      const int ph = k < 4 ? 0 : k < 8 ? 1 : 2, kk = k - 4 * ph;
+      if (kk * 64 + lane < (ph < 2 ? 227 : 169)) B[227 * ph + lane + 64 * kk] = y[k];
+    }
+    if (lane == 0) B[623] = b396 ^ mt_mix(a623[q], b0);
+  }
+  wfence();
+}
+DEV void mt_gen_block_batched(u32* key, int b) { mt_gen_pair(key, b, key, b, false); }
+
+// the build kernel's block generation (the run kernel keeps mt_gen_block: a register-staged
+// form inlined into the event loop cost every configuration 1-3 %)
+#ifndef MXA_BUILD_BATCHED_GEN
+#define MXA_BUILD_BATCHED_GEN 1
+#endif
+DEV void mt_gen_build(u32* key, int b) {
+  if constexpr (MXA_BUILD_BATCHED_GEN) mt_gen_block_batched(key, b);
+  else mt_gen_block(key, b);
+}
+
 // init_genrand (numpy _legacy_seeding with an int) into block 0: every lane runs the
 // recurrence, lane (i % 64) stores word i.
 DEV void mt_seed(u32* key, u32 s) {
@@ -224,6 +285,12 @@ DEV void mt_seed(u32* key, u32 s) {
   wfence();
 }
 
+// the build kernel's draws through LDS windows too (one coalesced 64-word fill instead of a
+// dependent load per word): G/O/K/L their run-kernel windows, an agent stream the L window (the
+// build never draws from L)
+#ifndef MXA_BUILD_WINDOWS
+#define MXA_BUILD_WINDOWS 1
+#endif
 // refill a stream window from position p: lane i loads output word p + i if its block is in
 // the double buffer (materialized and not yet overwritten); the window ends at the first word
 // that is not, and an empty window is the look-ahead overrun
@@ -243,10 +310,17 @@ DEV void rs_fill(RSt<B>& r) {
 }
 template <bool B>
 DEV u32 rs_u32(RSt<B>& r) {
-  if constexpr (!B) {
+  if constexpr (!B || MXA_BUILD_WINDOWS) {
     if (r.lw) {
       u32 off = (u32)(r.p - r.lw0);
       if (off >= (u32)r.lwn) {
+        if constexpr (B) {  // the build materializes blocks as it draws
+          const int blk = r.p / MXA_MT_N;
+          while (r.m < blk) {
+            mt_gen_build(r.key, r.m + 1);
+            r.m++;
+          }
+        }
         rs_fill(r);
         off = 0;
       }
@@ -262,7 +336,7 @@ DEV u32 rs_u32(RSt<B>& r) {
   int blk = r.p / MXA_MT_N;
   if (B) {
     while (r.m < blk) {
-      mt_gen_block(r.key, r.m + 1);
+      mt_gen_build(r.key, r.m + 1);
       r.m++;
     }
   } else if (blk > r.m) {
@@ -332,17 +406,36 @@ DEV double rs_uniform(RSt<B>& r, double lo, double hi) { return lo + (hi - lo) *
 DEV void rs_skip_words(RSt<true>& r, i64 k) {
   i64 target = (i64)r.p + k;
   while ((i64)r.m < target / MXA_MT_N) {
-    mt_gen_block(r.key, r.m + 1);
+    mt_gen_build(r.key, r.m + 1);
     r.m++;
   }
   r.p = (i32)target;
 }
 // keep one block of look-ahead materialized (called at event boundaries)
+// agent streams keep MXA_AGENT_LA words of look-ahead materialized instead of a whole block:
+// an agent event draws a few dozen words at most (the MarketMakerAgent's ladder sizes), and most
+// agents of the wide configurations draw a few words per session, so their second block is never
+// built.  A draw past the look-ahead is still ERR_RNG_OVERRUN, never a silent value.
+#ifndef MXA_MAINT_LANES
+#define MXA_MAINT_LANES 1
+#endif
+#ifndef MXA_WAKE_LANES
+#define MXA_WAKE_LANES 1
+#endif
+#ifndef MXA_ZI_THETA_LANES
+#define MXA_ZI_THETA_LANES 1
+#endif
+#ifndef MXA_SEED_TILE
+#define MXA_SEED_TILE 1
+#endif
+#ifndef MXA_AGENT_LA
+#define MXA_AGENT_LA 256
+#endif
 template <bool B>
-DEV void rs_maint(RSt<B>& r) {
-  int b = r.p / MXA_MT_N;
-  while (r.m < b + 1) {
-    mt_gen_block(r.key, r.m + 1);
+DEV void rs_maint(RSt<B>& r, int la = MXA_MT_N) {
+  while (r.m < (r.p + la) / MXA_MT_N) {
+    if constexpr (B) mt_gen_build(r.key, r.m + 1);
+    else mt_gen_block(r.key, r.m + 1);
     r.m++;
   }
 }
@@ -967,7 +1060,7 @@ struct Eng {
   // agent RNG stream (Agent.random_state): key words in HBM, pos/gauss cache in the record
   DEV RS agent_rs() {
     RS r;
-    r.lw = nullptr;
+    r.lw = BUILD && MXA_BUILD_WINDOWS ? rwin + 3 * 64 : nullptr;
     r.lw0 = r.lwn = 0;
     r.key = rng_key(4 + cur_agent);
     r.p = rgi(AF_RS_POS);
@@ -981,14 +1074,14 @@ struct Eng {
     rs(AF_RS_M, (u32)r.m);
     rs(AF_RS_HASG, (u32)r.hasg);
     rsd(AF_RS_GAUSS, r.gauss);
-    dirty |= rs_needs_maint(r) ? 16u : 0u;
+    dirty |= rs_needs_maint(r, MXA_AGENT_LA) ? 16u : 0u;
   }
   // whether rng_maint has work for a stream in this state: a look-ahead overrun to report, or
   // no materialized block after the one holding position p.  Decided where the state is put
   // (registers) instead of re-read from the header and the record at the event's end
-  DEV bool rs_needs_maint(const RS& r) {
+  DEV bool rs_needs_maint(const RS& r, int la = MXA_MT_N) {
     if constexpr (BUILD) return true;
-    return (r.hasg & 2) || r.m < r.p / MXA_MT_N + 1;
+    return (r.hasg & 2) || r.m < (r.p + la) / MXA_MT_N;
   }
   // global streams: 0 = G (np.random), 1 = O (oracle symbol), 2 = K (kernel), 3 = L (latency)
   DEV RS grs(int s) {
@@ -998,8 +1091,8 @@ struct Eng {
     r.m = h.rs_m[s];
     r.hasg = h.rs_has_gauss[s];
     r.gauss = h.rs_gauss[s];
-    if constexpr (BUILD) {
-      r.lw = nullptr;
+    if constexpr (BUILD) {  // an empty window: the first draw fills it
+      r.lw = MXA_BUILD_WINDOWS ? rwin + s * 64 : nullptr;
       r.lw0 = r.lwn = 0;
     } else {
       r.lw = rwin + s * 64;
@@ -1062,9 +1155,10 @@ struct Eng {
       const i32 p = kr ? kp : k < 4 ? h.rs_pos[k] : rgi(AF_RS_POS), m = kr ? km : k < 4 ? h.rs_m[k] : rgi(AF_RS_M);
       const i32 hg = kr ? khg : k < 4 ? h.rs_has_gauss[k] : rgi(AF_RS_HASG);
       if (hg & 2) fail(ERR_RNG_OVERRUN);
-      if (m >= p / MXA_MT_N + 1) continue;  // the look-ahead block is there (almost always)
+      const int la = k < 4 ? MXA_MT_N : MXA_AGENT_LA;
+      if (m >= (p + la) / MXA_MT_N) continue;  // the look-ahead is there (almost always)
       RS r = kr ? grs_k() : k < 4 ? grs(k) : agent_rs();
-      rs_maint(r);
+      rs_maint(r, la);
       if (kr) {
         km = r.m;
       } else if (k < 4) {
@@ -1865,7 +1959,6 @@ struct Eng {
     int first = h.tx_head - n;
     i64 start = cur - lookback;
     i64 vol = 0;
-    int live_total = 0;
     // Newest records first, 64 per chunk (lane L = record lo + L, chronological).  Records are
     // appended in time order, so once a chunk's oldest record is before `start` every older
     // record is too, and the window is usually inside the newest chunk.  Whether ANY live
@@ -1875,7 +1968,6 @@ struct Eng {
     // the largest epoch of the ring.  Duplicate (t, q) pairs sit in one contiguous equal-t
     // block: lanes compare with their predecessors by shuffles, and only a block that crosses
     // into the older chunk walks back through memory.
-    (void)live_total;
     bool any = false;
     for (int hi = n; hi > 0; hi -= 64) {
       const int lo = hi > 64 ? hi - 64 : 0;
@@ -1890,14 +1982,20 @@ struct Eng {
       const bool inwin = valid && r.t >= start;
       if (hi == n) any = bal(live) != 0;
       bool dup = false;
-      for (int d = 1; d < 64; d++) {
-        const int src = lane - d < 0 ? 0 : lane - d;
-        const i64 pt = (i64)(((u64)(u32)__shfl((i32)((u64)r.t >> 32), src, 64) << 32) |
-                             (u32)__shfl((i32)(u32)(u64)r.t, src, 64));
-        const i32 pq = __shfl(r.q, src, 64), pe = __shfl(r.epoch, src, 64);
-        const bool same = lane - d >= 0 && pt == r.t;
-        dup = dup || (same && pe >= lo_ep && pq == r.q);
-        if (!bal(same && live && inwin && !dup)) break;
+      {  // equal-t blocks from one ballot of block starts, then one shuffle per distance (four shuffles and
+         // a ballot per distance before: rmsc03 x4096 37.9 -> 37.8 ms, profiles/r06/ab/ab10_tv_blocks.txt)
+        const int src1 = lane == 0 ? 0 : lane - 1;
+        const i64 pt = (i64)(((u64)(u32)__shfl((i32)((u64)r.t >> 32), src1, 64) << 32) |
+                             (u32)__shfl((i32)(u32)(u64)r.t, src1, 64));
+        const u64 S = bal(lane == 0 || pt != r.t);
+        const u64 below = lane == 63 ? S : S & ((2ull << lane) - 1);
+        const int bs = 63 - __clzll((long long)below);  // bit 0 is always set
+        const int dmax = wmax_i32(live && inwin ? lane - bs : 0);
+        const i32 qk = live ? r.q : INT32_MIN;
+        for (int d = 1; d <= dmax; d++) {
+          const i32 pq = __shfl(qk, lane - d < 0 ? 0 : lane - d, 64);
+          dup = dup || (lane - d >= bs && pq == r.q);
+        }
       }
       if (lo > 0) {  // an equal-t block that started in the older chunk
         const TxRec o = R[(first + lo - 1) % cap];
@@ -1914,32 +2012,6 @@ struct Eng {
       if (!(bal(inwin) & 1ull)) break;  // the chunk's oldest record is before the window
     }
     if (!any) *perr = 1;  // pandas raises when no transaction records exist
-    return vol;
-    for (int b = 0; b < n; b += 64) {
-      int k = b + lane;  // k-th record in chronological order
-      bool live = false, dup = false, inwin = false;
-      i64 t = 0;
-      i32 q = 0;
-      if (k < n) {
-        TxRec r = R[(first + k) % cap];
-        t = r.t;
-        q = r.q;
-        live = r.epoch >= lo_ep;
-        inwin = t >= start;
-        // records are chronological: equal (t, q) pairs sit in one contiguous t-block
-        for (int j = k - 1; live && j >= 0; j--) {
-          TxRec o = R[(first + j) % cap];
-          if (o.t != t) break;
-          if (o.epoch >= lo_ep && o.q == q) {
-            dup = true;
-            break;
-          }
-        }
-      }
-      live_total += __popcll(bal(live));
-      vol += wsum_i64((live && !dup && inwin) ? (i64)q : 0);
-    }
-    if (live_total == 0) *perr = 1;  // pandas raises when no transaction records exist
     return vol;
   }
 
@@ -4611,14 +4683,16 @@ struct Eng {
     }
     SavedOrder* so = (SavedOrder*)(env + PC.L.off_book);
     for (int j = 0; j < SO; j++) {
+      // a free slot saves zeros: its registers (or LDS words) are whatever an earlier wave left
+      const bool live = bm[j] >= 0;
       SavedOrder o;
-      o.price = bp[j];
-      o.qty = bq[j];
-      o.oid = bo[j];
+      o.price = live ? bp[j] : 0;
+      o.qty = live ? bq[j] : 0;
+      o.oid = live ? bo[j] : 0;
       o.meta = bm[j];
-      o.arrival = ba[j];
-      o.hepoch = bh[j];
-      o.pad[0] = OH ? bx[OH ? j : 0] : 0;
+      o.arrival = live ? ba[j] : 0u;
+      o.hepoch = live ? bh[j] : 0;
+      o.pad[0] = OH && live ? bx[OH ? j : 0] : 0;
       o.pad[1] = 0;
       so[j * 64 + lane] = o;
     }
@@ -5175,21 +5249,59 @@ struct Builder : Eng<CFG, true> {
     this->rs64(AF_ATIME, E::PC.start);
     this->rs64(AF_COMP, E::PC.default_comp_delay);
   }
-  DEV i64 get_wake_time(RS& G, i64 open, i64 close) {  // util/util.py:35-58
-    double u = rs_double(G);
+  DEV i64 get_wake_time(RS& G, i64 open, i64 close) { return wake_time_of(rs_double(G), open, close); }
+  // the noise agents' wakeup times from their uniforms (kept in AF_WAKEUP_TIME by the draw loop),
+  // lane = agent: the same glibc pow restatement per lane
+  DEV void wake_times_lanes() {
+    const MxaParams& P = E::PC;
+    wfence();
+    for (int a0 = P.first_noise; a0 < P.first_noise + P.n_noise; a0 += 64) {
+      const int a = a0 + this->lane;
+      if (a < P.first_noise + P.n_noise) {
+        u32* rw = (u32*)this->agent_ptr(a);
+        const double u = as_d(((u64)rw[AF_WAKEUP_TIME + 1] << 32) | rw[AF_WAKEUP_TIME]);
+        const u64 wt = (u64)wake_time_of(u, P.noise_open, P.noise_close);
+        rw[AF_WAKEUP_TIME] = (u32)wt;
+        rw[AF_WAKEUP_TIME + 1] = (u32)(wt >> 32);
+      }
+    }
+    wfence();
+  }
+  DEV i64 wake_time_of(double u, i64 open, i64 close) {  // util/util.py:35-58
     double alpha = 12.0, beta = 0.5;
     double n = (3 / alpha) * u - gm_pow(beta - 0, 3.0);
     double c = n < 0 ? -gm_pow(-n, 1.0 / 3.0) : gm_pow(n, 1.0 / 3.0);
     double mult = c + beta;
     return open + (i64)(mult * (double)(close - open));
   }
-  // expand every stream's init_genrand in parallel (lane = stream)
+  // expand every stream's init_genrand in parallel (lane = stream).  With room in the LDS queue
+  // area (empty until the kernelStarting wakeups) each lane's 16-word runs go through an LDS tile
+  // and leave as 64-byte runs of 4 streams per store instead of 64 scattered dwords.
+  static constexpr bool SEED_TILE = MXA_SEED_TILE && E::LDS_Q >= 64 * 17 * 4;
   DEV void seed_streams(int first) {
     const MxaParams& P = E::PC;
     wfence();
+    const int lane = this->lane;
     for (int b = first; b < P.n_streams; b += 64) {
-      int s = b + this->lane;
-      if (s < P.n_streams) {
+      int s = b + lane;
+      if constexpr (SEED_TILE) {
+        LDSP u32* tile = (LDSP u32*)this->qk;  // [64 streams][17] (16 words + a bank-conflict pad)
+        u32 x = s < P.n_streams ? this->rng_key(s)[0] : 0u;
+        for (int i0 = 1; i0 < MXA_MT_N; i0 += 16) {
+#pragma unroll
+          for (int j = 0; j < 16; j++) {
+            x = 1812433253u * (x ^ (x >> 30)) + (u32)(i0 + j);
+            tile[lane * 17 + j] = x;
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int t = 0; t < 16; t++) {  // 4 streams x 16 words per store
+            const int st = 4 * t + (lane >> 4), w = lane & 15;
+            if (b + st < P.n_streams && i0 + w < MXA_MT_N) this->rng_key(b + st)[i0 + w] = tile[st * 17 + w];
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      } else if (s < P.n_streams) {
         u32* key = this->rng_key(s);
         u32 x = key[0];
         for (int i = 1; i < MXA_MT_N; i++) {
@@ -5197,6 +5309,139 @@ struct Builder : Eng<CFG, true> {
           key[i] = x;
         }
       }
+    }
+    wfence();
+    if constexpr (SEED_TILE) {  // the queue area again: every slot empty
+      for (int j = 0; j < E::SQ; j++) this->qset(j, KEY_EMPTY, 0xFFFFFFFFu, true);
+      if constexpr (E::QHIER) this->q_rescan();
+    }
+  }
+
+  // rs_maint(agent stream, MXA_AGENT_LA) for every agent without a record round trip each: 64
+  // records' stream position and block per load, the blocks two streams per round trip, the
+  // block numbers written back per lane (the builder's records are all in HBM: HOT is 0)
+  DEV void maint_agents() {
+    const int n = E::PC.n_agents, lane = this->lane;
+    wfence();  // the records' stores above
+    for (int a0 = 0; a0 < n; a0 += 64) {
+      const int a = a0 + lane;
+      const bool act = a < n;
+      u32* rw = (u32*)this->agent_ptr(act ? a : a0);
+      const i32 p = act ? (i32)rw[AF_RS_POS] : 0;
+      i32 m = act ? (i32)rw[AF_RS_M] : 0;
+      const i32 need = (p + MXA_AGENT_LA) / MXA_MT_N;
+      for (;;) {
+        u64 t = bal(act && m < need);
+        if (!t) break;
+        const int l1 = ctz64(t);
+        t &= t - 1;
+        const int l2 = t ? ctz64(t) : l1;
+        const int m1 = rdl((u32)m, l1), m2 = rdl((u32)m, l2);
+        mt_gen_pair(this->rng_key(4 + a0 + l1), m1 + 1, this->rng_key(4 + a0 + l2), m2 + 1, l2 != l1);
+        m += (lane == l1 || lane == l2) ? 1 : 0;
+      }
+      if (act) rw[AF_RS_M] = (u32)m;
+    }
+    wfence();
+  }
+
+  // The ZI / HBL agents' theta (ZeroIntelligenceAgent.py:65-71: sorted(np.round(random_state.normal(
+  // 0, sqrt(sigma_pv), 2 q_max)), reverse=True)), 64 agents at once: lane L runs agent a0 + L's
+  // polar normals on its own stream (numpy legacy_gauss: pairs of doubles from 4 words, the second
+  // normal cached), sorts them and writes the agent's record fields.  Every stream is fresh here
+  // (p = 624, block 1 materialized just before); a lane whose draws would leave block 1 leaves its
+  // agent untouched and flags it for the one-agent-at-a-time path below (never in practice: 2 q_max
+  // normals take ~6 q_max words of the 624).
+  u64 zi_fb[(E::PC.n_zi + E::PC.n_hbl + 63) / 64 + 1];
+  DEV bool zi_fallback(int a) {
+    const int i = a - E::PC.first_zi;
+    return (zi_fb[i >> 6] >> (i & 63)) & 1;
+  }
+  DEV void zi_theta_lanes() {
+    const MxaParams& P = E::PC;
+    constexpr int NQ = 2 * E::PC.zi_qmax;
+    static_assert(NQ <= 20, "theta fits the agent record");
+    const int lo = P.first_zi, hi = P.first_zi + P.n_zi + P.n_hbl;
+    const double sd = __builtin_sqrt(P.zi_sigma_pv);
+    const int lane = this->lane;
+    for (int a0 = lo; a0 < hi; a0 += 64) {
+      for (int j = 0; j < 64 && a0 + j < hi; j += 2)
+        mt_gen_pair(this->rng_key(4 + a0 + j), 1, this->rng_key(4 + a0 + j + 1), 1, a0 + j + 1 < hi);
+      const int a = a0 + lane;
+      const bool act = a < hi;
+      const u32* key = this->rng_key(4 + (act ? a : a0));
+      i32 p = MXA_MT_N;
+      bool cached = false, fb = false;
+      double cache = 0.0;
+      double th[NQ];
+#pragma unroll
+      for (int i = 0; i < NQ; i++) th[i] = 0.0;
+      int k = 0;
+      while (bal(act && !fb && k < NQ)) {
+        if (act && !fb && k < NQ) {
+          double z = 0.0;
+          bool out = false;
+          if (cached) {
+            z = cache;
+            cached = false;
+            cache = 0.0;
+            out = true;
+          } else if (p + 4 > 2 * MXA_MT_N) {
+            fb = true;
+          } else {
+            u32 w[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+              u32 y = key[p + t];  // block 1 holds words 624..1247 at key[624..1247]
+              y ^= (y >> 11);
+              y ^= (y << 7) & 0x9d2c5680u;
+              y ^= (y << 15) & 0xefc60000u;
+              y ^= (y >> 18);
+              w[t] = y;
+            }
+            p += 4;
+            const double d1 = ((double)(i32)(w[0] >> 5) * 67108864.0 + (double)(i32)(w[1] >> 6)) / 9007199254740992.0;
+            const double d2 = ((double)(i32)(w[2] >> 5) * 67108864.0 + (double)(i32)(w[3] >> 6)) / 9007199254740992.0;
+            const double x1 = 2.0 * d1 - 1.0, x2 = 2.0 * d2 - 1.0;
+            const double r2 = x1 * x1 + x2 * x2;
+            if (!(r2 >= 1.0 || r2 == 0.0)) {
+              const double f = __builtin_sqrt(-2.0 * gm_log(r2) / r2);
+              cache = f * x1;
+              cached = true;
+              z = f * x2;
+              out = true;
+            }
+          }
+          if (out) {
+            const double v = __builtin_rint(0 + sd * z);
+#pragma unroll
+            for (int i = 0; i < NQ; i++) th[i] = i == k ? v : th[i];
+            k++;
+          }
+        }
+      }
+      // descending (sorted(..., reverse=True)); equal values are equal doubles, so order among
+      // them is invisible
+#pragma unroll
+      for (int i = 0; i < NQ; i++)
+#pragma unroll
+        for (int j = 0; j + 1 < NQ - i; j++) {
+          const double x = th[j], y = th[j + 1];
+          th[j] = x < y ? y : x;
+          th[j + 1] = x < y ? x : y;
+        }
+      if (act && !fb) {
+        u32* rw = (u32*)this->agent_ptr(a);
+#pragma unroll
+        for (int i = 0; i < NQ; i++) rw[AF_THETA + i] = (u32)(i32)th[i];
+        rw[AF_RS_POS] = (u32)p;
+        rw[AF_RS_M] = 1u;
+        rw[AF_RS_HASG] = cached ? 1u : 0u;
+        const u64 gb = as_u(cached ? cache : 0.0);
+        rw[AF_RS_GAUSS] = (u32)gb;
+        rw[AF_RS_GAUSS + 1] = (u32)(gb >> 32);
+      }
+      zi_fb[(a0 - lo) >> 6] = bal(act && fb);
     }
     wfence();
   }
@@ -5356,14 +5601,17 @@ struct Builder : Eng<CFG, true> {
       tmp = g_seed(G);  // exchange
       set_seed(4 + 0, tmp);
       for (int a = P.first_noise; a < P.first_noise + P.n_noise; a++) {
-        i64 wt = get_wake_time(G, P.noise_open, P.noise_close);
+        // get_wake_time's uniform now; its math for 64 agents at once below (wake_times_lanes)
+        const double u = rs_double(G);
         set_seed(4 + a, g_seed(G));
         i64 size = rs_randint(G, 20, 50);
         rec_init(a, AG_NOISE);
-        this->rs64(AF_WAKEUP_TIME, wt);
+        if constexpr (MXA_WAKE_LANES) this->rsd(AF_WAKEUP_TIME, u);
+        else this->rs64(AF_WAKEUP_TIME, wake_time_of(u, P.noise_open, P.noise_close));
         this->rs(AF_SIZE, (u32)size);
         this->rec_store();
       }
+      if constexpr (MXA_WAKE_LANES) wake_times_lanes();
       for (int a = P.first_value; a < P.first_value + P.n_value; a++) {
         set_seed(4 + a, g_seed(G));
         i64 size = rs_randint(G, 20, 50);
@@ -5575,7 +5823,10 @@ struct Builder : Eng<CFG, true> {
       this->agent_rs_put(A);
       this->rec_store();
     }
+    constexpr bool ZI_LANES = MXA_ZI_THETA_LANES && E::PC.n_zi + E::PC.n_hbl > 0;
+    if constexpr (ZI_LANES) zi_theta_lanes();
     for (int a = P.first_zi; a < P.first_zi + P.n_zi + P.n_hbl; a++) {  // HBL agents are ZI subclasses
+      if (ZI_LANES && !zi_fallback(a)) continue;  // done by zi_theta_lanes
       this->rec_load(a);
       RS A = this->agent_rs();
       double th[20];
@@ -5602,12 +5853,16 @@ struct Builder : Eng<CFG, true> {
       rs_maint(r);
       this->grs_put(k, r);
     }
-    for (int a = 0; a < n; a++) {
-      this->rec_load(a);
-      RS A = this->agent_rs();
-      rs_maint(A);
-      this->agent_rs_put(A);
-      this->rec_store();
+    if constexpr (MXA_MAINT_LANES) {
+      maint_agents();
+    } else {
+      for (int a = 0; a < n; a++) {
+        this->rec_load(a);
+        RS A = this->agent_rs();
+        rs_maint(A, MXA_AGENT_LA);
+        this->agent_rs_put(A);
+        this->rec_store();
+      }
     }
     // Kernel.runner: kernelInitializing (exchange opening price = r_bar, a python float; with the
     // ExternalFileOracle int(round(price at the open)), ExternalFileOracle.py:37-50),

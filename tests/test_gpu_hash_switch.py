@@ -45,8 +45,13 @@ def test_hash_off_leaves_every_env_block_identical(config, n):
         assert (s_on[k] == s_off[k]).all(), k
     assert (s_off["hash"] != s_on["hash"]).all()  # the hash really was not computed
     envs = np.arange(n)
+    lay = on.layout()
     for e, a, b in zip(envs, _blocks(on, envs), _blocks(off, envs)):
-        assert np.array_equal(a, b), (config, e)
+        if not np.array_equal(a, b):
+            d = np.nonzero(a != b)[0]
+            sec = max((o, k) for k, o in lay.items() if 0 < o <= d[0]) if d[0] >= 512 else (0, "header")
+            raise AssertionError("%s env %d: %d bytes differ, first at %d (%s), last at %d: %s vs %s" % (
+                config, e, len(d), d[0], sec[1], d[-1], a[d[:8]].tolist(), b[d[:8]].tolist()))
 
 
 def test_hash_off_bench_workload_summaries_identical():
