@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU-baseline threads (default: the cores this process may run on, capped by OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--per-step", action="store_true",
+                    help="GymKernel configs: one launch per ABIDESEnv.step instead of one per episode")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample: at least this much wall time")
     ap.add_argument("--no-latency", action="store_true", help="skip the solo-latency run of the latency bound")
     ap.add_argument("--parity-hash", action="store_true",
@@ -396,21 +398,30 @@ class GymEngine(Engine):
         self.gen = torch.Generator(device="cuda")
         self.gen.manual_seed(1000 + ctx.rank)
         self.act = torch.empty((self.n_steps, self.n, ACTION_SIZE), dtype=torch.float64, device="cuda")
-        self.obs = torch.empty((self.n, OBS_SIZE), dtype=torch.float64, device="cuda")
-        self.flags = torch.empty((self.n,), dtype=torch.int32, device="cuda")
+        # the episode's actions are drawn up front, so its steps go to the device in one launch
+        # (mxa_step_many: every step the same code and results as a one-step launch); --per-step
+        # launches them one by one
+        self.many = not args.per_step
+        k = self.n_steps if self.many else 1
+        self.obs = torch.empty((k, self.n, OBS_SIZE), dtype=torch.float64, device="cuda")
+        self.flags = torch.empty((k, self.n), dtype=torch.int32, device="cuda")
         self.ev_pairs = []
-        self.kernel = "mxa_step_kernel<%d> (%s)" % (3 if self.replay else 4, args.config)
+        self.kernel = "mxa_step_kernel<%d> (%s%s)" % (3 if self.replay else 4, args.config,
+                                                      ", %d steps per launch" % self.n_steps if self.many else "")
 
     def step(self, k, timed):
         torch = self.torch
         self.v.reset(seeds=None if self.replay else self.seeds(k))
         torch.rand(self.act.shape, generator=self.gen, dtype=torch.float64, device="cuda", out=self.act)
         self.act[:, :, 0] *= 0.01
-        for i in range(self.n_steps):
+        for i in range(1 if self.many else self.n_steps):
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(self.stream)
-            self.v.step_device(self.act[i].data_ptr(), self.obs.data_ptr(), self.flags.data_ptr())
+            if self.many:
+                self.v.step_many_device(self.n_steps, self.act.data_ptr(), self.obs.data_ptr(), self.flags.data_ptr())
+            else:
+                self.v.step_device(self.act[i].data_ptr(), self.obs.data_ptr(), self.flags.data_ptr())
             if timed:
                 e1.record(self.stream)
                 self.ev_pairs.append((e0, e1))
@@ -727,6 +738,8 @@ def main():
         for key in ("agents_per_env", "tape_records", "learn_steps"):
             if key in d:
                 out["config"][key] = d[key]
+        if isinstance(eng, GymEngine):
+            out["config"]["steps_per_launch"] = eng.n_steps if eng.many else 1
         if hasattr(eng, "gym_steps"):
             out["config"]["gym_steps_per_s"] = eng.gym_steps() * (args.steps if not isinstance(eng, DDQNEngine) else 1) / elapsed
         if not args.stub:

@@ -32,6 +32,7 @@
  *   mxa_step ........... ABIDESEnv.step (ABIDESEnv.py:30-49) = GymKernel.stepRunner
  *                        (GymKernel.py:158-306) with DummyRL.place_orders/get_observation
  *                        (dummy_rl_execution_agent.py:138-179, 291-312)
+ *   mxa_step_many ...... k ABIDESEnv.step calls in a row with the actions given up front, one launch
  */
 #ifndef MXA_H
 #define MXA_H
@@ -295,6 +296,13 @@ int mxa_create_replay_twap(const int64_t* t, const int64_t* oid, const int64_t* 
 int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags);
 /* the same on device arrays, asynchronous on the handle's stream */
 int mxa_step_device(mxa_handle* h, const double* d_actions, double* d_obs, int32_t* d_flags);
+/* k consecutive ABIDESEnv.step calls in ONE launch, with every action given up front (an
+ * open-loop schedule: an impact study's order sizes, or actions drawn ahead as bench.py does):
+ * device arrays actions [k][n_envs][3] -> obs [k][n_envs][9], flags [k][n_envs].  Step i of every
+ * env equals the i-th of k mxa_step_device calls, observation and flags included; each env runs
+ * its steps without waiting for the slowest env of each step.  Asynchronous on the handle's
+ * stream; GymKernel handles only (MXA_EINVAL otherwise). */
+int mxa_step_many(mxa_handle* h, int32_t k, const double* d_actions, double* d_obs, int32_t* d_flags);
 /* the per-pop parity hash (mxa_env_summary.hash: a rolling FNV-1a over every pop's trace
  * record, the test harness's checksum; the reference computes nothing like it) is on by
  * default.  Turning it off leaves every market result identical and the hash field frozen at

@@ -176,6 +176,7 @@ struct mxa_handle {
   mxa_run_fn run = nullptr, run_log = nullptr;     // run_log: with the book-update log
   mxa_run_fn run_fast = nullptr;                   // hash off, no trace ring: instrumentation compiled out
   mxa_step_fn step = nullptr, step_fast = nullptr;  // GymKernel handles (replay, rmsc03_rl)
+  mxa_step_many_fn step_many = nullptr, step_many_fast = nullptr;  // k steps per launch
   mxa_stop_fn stop = nullptr, stop_log = nullptr;  // kernelStopping pass (plain Kernel.runner configs)
   mxa_agent_final* d_final = nullptr;
   BlRec* d_blog = nullptr;  // book-update log [n_envs][blog_cap] (mxa_set_book_log)
@@ -263,6 +264,8 @@ static bool bind(mxa_handle* h, int cfg) {
   h->stop_log = e.stop_log;
   h->step = e.step;
   h->step_fast = e.step_fast;
+  h->step_many = e.step_many;
+  h->step_many_fast = e.step_many_fast;
   h->gym = e.step != nullptr;
   h->occ = e.occ;
   h->lds = mxa_cfg::lds_bytes(cfg);
@@ -838,6 +841,23 @@ int mxa_step(mxa_handle* h, const double* actions, double* obs, int32_t* flags) 
   float ms = 0;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
   h->last_ms = ms;
+  return MXA_OK;
+#endif
+}
+
+// k consecutive steps in one launch, device arrays: actions [k][n][3] -> obs [k][n][9], flags [k][n]
+int mxa_step_many(mxa_handle* h, int32_t k, const double* d_actions, double* d_obs, int32_t* d_flags) {
+  if (!h || !h->gym || k <= 0 || !d_actions || !d_obs || !d_flags) return MXA_EINVAL;
+#ifdef MXA_NO_GYM
+  return MXA_EINVAL;
+#else
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  (h->tcap_arg() < 0 && h->step_many_fast ? h->step_many_fast : h->step_many)(
+      dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(),
+      (int64_t)1 << 40, (const RpCtx*)h->d_ctx, d_actions, d_obs, d_flags, k);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   return MXA_OK;
 #endif
 }

@@ -18,6 +18,9 @@ typedef void (*mxa_stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, in
 typedef void (*mxa_step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*,
                             const double*, double*, int32_t*);
 
+typedef void (*mxa_step_many_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*,
+                                 const double*, double*, int32_t*, int);
+
 typedef int (*mxa_occ_fn)(size_t);  // resident blocks (envs) per CU of the measured kernel at that LDS size
 
 struct MxaEntry {
@@ -26,6 +29,7 @@ struct MxaEntry {
   mxa_run_fn run_fast;         // without the parity instrumentation (hash off, no trace ring)
   mxa_stop_fn stop, stop_log;
   mxa_step_fn step, step_fast; // GymKernel configurations (step_fast: without the instrumentation)
+  mxa_step_many_fn step_many, step_many_fast;  // k steps per launch, actions given up front
   mxa_occ_fn occ;              // hipOccupancyMaxActiveBlocksPerMultiprocessor of run_fast / step_fast
 };
 

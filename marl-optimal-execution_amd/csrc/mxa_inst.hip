@@ -29,7 +29,14 @@ void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t
 template <int CFG, bool INSTR>
 void launch_step(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
                  const RpCtx* ctx, const double* act, double* obs, int32_t* flags) {
-  hipLaunchKernelGGL((mxa_step_kernel<CFG, INSTR>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, act, obs, flags);
+  hipLaunchKernelGGL((mxa_step_kernel<CFG, INSTR, false>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, act, obs,
+                     flags, 1);
+}
+template <int CFG, bool INSTR>
+void launch_step_many(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap,
+                      int64_t max_pops, const RpCtx* ctx, const double* act, double* obs, int32_t* flags, int k) {
+  hipLaunchKernelGGL((mxa_step_kernel<CFG, INSTR, true>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, act, obs,
+                     flags, k);
 }
 #endif
 
@@ -38,7 +45,7 @@ int occupancy(size_t lds) {
   int n = 0;
   hipError_t e;
 #ifndef MXA_NO_GYM
-  if constexpr (GYM) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mxa_step_kernel<CFG, false>, 64, lds);
+  if constexpr (GYM) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mxa_step_kernel<CFG, false, false>, 64, lds);
   else
 #endif
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mxa_run_kernel<CFG, false, false>, 64, lds);
@@ -72,6 +79,8 @@ MxaEntry make_entry() {
   if constexpr (gym) {
     e.step = launch_step<CFG, true>;
     e.step_fast = launch_step<CFG, false>;
+    e.step_many = launch_step_many<CFG, true>;
+    e.step_many_fast = launch_step_many<CFG, false>;
   }
 #endif
   return e;

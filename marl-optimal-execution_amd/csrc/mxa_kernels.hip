@@ -5952,39 +5952,48 @@ __global__ __launch_bounds__(64) void mxa_stop_kernel(char* base, uint64_t strid
 // ABIDESEnv.step for every env: DummyRL.place_orders(action), then the GymKernel loop until
 // the RL agent's spread reply (end of step) or the end of the episode.  obs [n][9] float64;
 // flags [n]: bit0 done, bit1 observation valid, bit2 env error.  INSTR as for the run kernel.
-template <int CFG, bool INSTR>
+// MANY: k_steps consecutive steps in one launch with actions given up front ([k][n][3];
+// obs [k][n][9], flags [k][n]): each env runs its own steps without waiting for the slowest env
+// of every step, and its state stays in LDS and registers between them.  Every step is the same
+// code as a one-step launch, so results, observations and flags are the same step by step.
+template <int CFG, bool INSTR, bool MANY>
 __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel(
     char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops, const RpCtx* ctx, const double* actions,
-    double* obs, int32_t* flags) {
+    double* obs, int32_t* flags, int k_steps) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int env = blockIdx.x;
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
   mxa::Eng<CFG, false, false, INSTR> g(e, lds, trace_cap, ctx);
   g.load();
-  if (g.status == ST_RUNNING) {
-    double a[3];
-    for (int i = 0; i < 3; i++) a[i] = actions[3 * (size_t)env + i];
-    g.rl_place_orders(a);
-    g.end_step = 0;
-    g.run(max_pops);
-    if (g.status == ST_RUNNING) {  // after the loop: terminateRunner if the queue ran dry / past stop
-      u64 key;
-      u32 s;
-      if (g.q_peek(key, s) < 0 || g.cur > mxa::Eng<CFG>::PC.stop) g.status = ST_DONE;
+  const int ks = MANY ? k_steps : 1;
+  for (int i = 0; i < ks; i++) {
+    if (g.status == ST_RUNNING) {
+      double a[3];
+      for (int j = 0; j < 3; j++) a[j] = actions[3 * ((size_t)i * n_envs + env) + j];
+      g.rl_place_orders(a);
+      g.end_step = 0;
+      g.run(max_pops);
+      if (g.status == ST_RUNNING) {  // after the loop: terminateRunner if the queue ran dry / past stop
+        u64 key;
+        u32 s;
+        if (g.q_peek(key, s) < 0 || g.cur > mxa::Eng<CFG>::PC.stop) g.status = ST_DONE;
+      }
+      if (g.status == ST_DONE) g.rp_terminate();
     }
-    if (g.status == ST_DONE) g.rp_terminate();
+    if (!MANY) g.save();
+    auto R = g.rh();
+    const size_t row = (size_t)i * n_envs + env;
+    if (g.lane < 9) obs[9 * row + g.lane] = R->obs[g.lane];
+    u64 key;
+    u32 sq;
+    const bool pending = g.q_peek(key, sq) >= 0;  // all lanes: DPP reduction
+    // ABIDESEnv.step: done = not (queue non-empty and currentTime <= stopTime)
+    const int done = !(pending && g.cur <= mxa::Eng<CFG>::PC.stop) || g.status != ST_RUNNING;
+    const int hobs = mxa::U(R->has_obs);
+    if (g.lane == 0) flags[row] = done | (hobs ? 2 : 0) | (g.status == ST_ERROR ? 4 : 0);
   }
-  g.save();
-  auto R = g.rh();
-  if (g.lane < 9) obs[9 * (size_t)env + g.lane] = R->obs[g.lane];
-  u64 key;
-  u32 sq;
-  const bool pending = g.q_peek(key, sq) >= 0;  // all lanes: DPP reduction
-  // ABIDESEnv.step: done = not (queue non-empty and currentTime <= stopTime)
-  const int done = !(pending && g.cur <= mxa::Eng<CFG>::PC.stop) || g.status != ST_RUNNING;
-  const int hobs = mxa::U(R->has_obs);
-  if (g.lane == 0) flags[env] = done | (hobs ? 2 : 0) | (g.status == ST_ERROR ? 4 : 0);
+  if (MANY) g.save();
 #ifdef MXA_PROF
   atomicAdd(&mxa::g_mxa_prof[g.lane], (unsigned long long)g.prof[g.lane]);
   atomicAdd(&mxa::g_mxa_prof[64 + g.lane], (unsigned long long)g.prof[64 + g.lane]);
@@ -5998,6 +6007,8 @@ __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_step_kernel
 __global__ __launch_bounds__(64) void mxa_rng_probe_kernel(uint32_t seed, int mode, double a, double b, int n, double* out, uint32_t* scratch) {
   mxa::mt_seed(scratch, seed);
   mxa::RSt<true> r;
+  r.lw = nullptr;  // draws read the MT block in HBM
+  r.lw0 = r.lwn = 0;
   r.key = scratch;
   r.p = MXA_MT_N;
   r.m = 0;

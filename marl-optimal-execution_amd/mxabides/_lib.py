@@ -82,7 +82,8 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_read_counters", "mxa_create_hist", "mxa_create_replay_runner",
            "mxa_set_stop_time", "mxa_run_until", "mxa_create_replay_twap", "mxa_create_params", "mxa_set_mm_params",
            "mxa_mm_defaults", "mxa_resident_envs", "mxa_set_exchange_log", "mxa_config_defaults",
-           "mxa_config_compile", "mxa_config_key", "mxa_create_config", "mxa_config_info"]
+           "mxa_config_compile", "mxa_config_key", "mxa_create_config", "mxa_config_info",
+           "mxa_step_many"]
 COUNTER_WORDS = 34  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
@@ -146,6 +147,7 @@ def load():
     L.mxa_create_replay.argtypes = [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)]
     L.mxa_step.argtypes = [P, P, P, P]
     L.mxa_step_device.argtypes = [P, P, P, P]
+    L.mxa_step_many.argtypes = [P, I32, P, P, P]
     L.mxa_finalize.argtypes = [P]
     L.mxa_read_final.argtypes = [P, I32, P, I32]
     if hasattr(L, "mxa_set_book_log"):

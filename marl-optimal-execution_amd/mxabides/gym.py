@@ -85,6 +85,13 @@ class VecABIDESEnv:
         self._check(self.L.mxa_step_device(self._h, ctypes.c_void_p(d_actions), ctypes.c_void_p(d_obs),
                                            ctypes.c_void_p(d_flags)), "mxa_step_device")
 
+    def step_many_device(self, k, d_actions, d_obs, d_flags):
+        """k steps in one asynchronous launch with the actions given up front: device buffers
+        actions [k][n][3] -> obs [k][n][9], flags [k][n] (include/mxa.h mxa_step_many); step i
+        equals the i-th of k step_device calls"""
+        self._check(self.L.mxa_step_many(self._h, int(k), ctypes.c_void_p(d_actions), ctypes.c_void_p(d_obs),
+                                         ctypes.c_void_p(d_flags)), "mxa_step_many")
+
     def set_parity_hash(self, on):
         """Per-pop parity hash (summary()["hash"]) on or off; market results are identical
         either way (include/mxa.h mxa_set_parity_hash)."""
