@@ -1437,6 +1437,14 @@ struct Eng {
   }
   // the queue's high-water mark (EnvHdr::max_q, a diagnostic): a register for the launch (loaded
   // and saved with the header) instead of an LDS read-modify-write on every push
+// get_transacted_volume's duplicate test from a ballot of equal-t block starts and one shuffle per
+// distance (rmsc03 x4096 37.9 -> 37.8 ms, profiles/r06/ab/ab10_tv_blocks.txt); rmsc01 keeps four
+// shuffles and a ballot per distance: the new form's registers cost it 4 % though it never runs
+// there (773 vs 802 ms, r06/ab/ab16_rmsc01.txt), and value_noise and rmsc02 measured the other way
+// (16.4 vs 17.0 ms, 777 vs 789 ms: r06/ab/ab16_vn.txt, r06/s10/run_kernels.txt)
+#ifndef MXA_TV_BLOCKS_MASK
+#define MXA_TV_BLOCKS_MASK (~(1 << MXA_CFG_RMSC01))
+#endif
 #ifndef MXA_MAXQ_REG_MASK
   // same results: r03 s28 sparse_zi_1000 762 -> 736 ms, rmsc02 1096 -> 1084; s31 random_fund_value
   // 553 -> 541; not set where it cost: rmsc03 40.7 -> 42.8 (s28), rmsc01 1013 -> 1051 (s31).  r06
@@ -1447,6 +1455,7 @@ struct Eng {
                            (1 << MXA_CFG_MARKETREPLAY) | (1 << MXA_CFG_MARKETREPLAY_RUNNER) | (1 << MXA_CFG_MARKETREPLAY_TWAP))
 #endif
   static constexpr bool MAXQ_REG = !BUILD && (((MXA_MAXQ_REG_MASK) >> CFG) & 1);
+  static constexpr bool TVB = ((MXA_TV_BLOCKS_MASK) >> CFG) & 1;
   i32 maxq;
   DEV void note_max_q() {
     if constexpr (MAXQ_REG) maxq = qcount > maxq ? qcount : maxq;
@@ -1982,8 +1991,17 @@ struct Eng {
       const bool inwin = valid && r.t >= start;
       if (hi == n) any = bal(live) != 0;
       bool dup = false;
-      {  // equal-t blocks from one ballot of block starts, then one shuffle per distance (four shuffles and
-         // a ballot per distance before: rmsc03 x4096 37.9 -> 37.8 ms, profiles/r06/ab/ab10_tv_blocks.txt)
+      if constexpr (!TVB) {  // per distance: four shuffles and a ballot
+        for (int d = 1; d < 64; d++) {
+          const int src = lane - d < 0 ? 0 : lane - d;
+          const i64 pt = (i64)(((u64)(u32)__shfl((i32)((u64)r.t >> 32), src, 64) << 32) |
+                               (u32)__shfl((i32)(u32)(u64)r.t, src, 64));
+          const i32 pq = __shfl(r.q, src, 64), pe = __shfl(r.epoch, src, 64);
+          const bool same = lane - d >= 0 && pt == r.t;
+          dup = dup || (same && pe >= lo_ep && pq == r.q);
+          if (!bal(same && live && inwin && !dup)) break;
+        }
+      } else {  // equal-t blocks from one ballot of block starts, then one shuffle per distance
         const int src1 = lane == 0 ? 0 : lane - 1;
         const i64 pt = (i64)(((u64)(u32)__shfl((i32)((u64)r.t >> 32), src1, 64) << 32) |
                              (u32)__shfl((i32)(u32)(u64)r.t, src1, 64));
@@ -4683,16 +4701,14 @@ struct Eng {
     }
     SavedOrder* so = (SavedOrder*)(env + PC.L.off_book);
     for (int j = 0; j < SO; j++) {
-      // a free slot saves zeros: its registers (or LDS words) are whatever an earlier wave left
-      const bool live = bm[j] >= 0;
       SavedOrder o;
-      o.price = live ? bp[j] : 0;
-      o.qty = live ? bq[j] : 0;
-      o.oid = live ? bo[j] : 0;
+      o.price = bp[j];
+      o.qty = bq[j];
+      o.oid = bo[j];
       o.meta = bm[j];
-      o.arrival = live ? ba[j] : 0u;
-      o.hepoch = live ? bh[j] : 0;
-      o.pad[0] = OH && live ? bx[OH ? j : 0] : 0;
+      o.arrival = ba[j];
+      o.hepoch = bh[j];
+      o.pad[0] = OH ? bx[OH ? j : 0] : 0;
       o.pad[1] = 0;
       so[j * 64 + lane] = o;
     }
@@ -5573,7 +5589,15 @@ struct Builder : Eng<CFG, true> {
       this->qset(j, KEY_EMPTY, 0xFFFFFFFFu, true);
     }
     if constexpr (E::QHIER) this->q_rescan();  // empty group mins
-    for (int j = 0; j < E::SO; j++) this->bm[j] = -1;
+    for (int j = 0; j < E::SO; j++) {  // every field: a slot never used is saved as the build left it
+      this->bm[j] = -1;
+      this->bp[j] = 0;
+      this->bq[j] = 0;
+      this->bo[j] = 0;
+      this->ba[j] = 0;
+      this->bh[j] = 0;
+      if constexpr (E::OH) this->bx[j] = 0;
+    }
     if constexpr (E::RP) {
       build_replay((i32)ocnt0, tape_hi0);
       return;

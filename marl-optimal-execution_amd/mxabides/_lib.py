@@ -147,7 +147,8 @@ def load():
     L.mxa_create_replay.argtypes = [P, P, P, P, P, I32, I32, I32, I32, ctypes.POINTER(P)]
     L.mxa_step.argtypes = [P, P, P, P]
     L.mxa_step_device.argtypes = [P, P, P, P]
-    L.mxa_step_many.argtypes = [P, I32, P, P, P]
+    if hasattr(L, "mxa_step_many"):  # (A/B builds of earlier sources lack it; tests check the exports)
+        L.mxa_step_many.argtypes = [P, I32, P, P, P]
     L.mxa_finalize.argtypes = [P]
     L.mxa_read_final.argtypes = [P, I32, P, I32]
     if hasattr(L, "mxa_set_book_log"):
