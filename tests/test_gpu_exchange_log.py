@@ -35,11 +35,14 @@ def oracle_recs(cfg, seed):
     return o, r
 
 
+# log_orders on: rmsc03, sparse_zi_100, rmsc02, random_fund_value, rmsc03_sbmm; off: value_noise,
+# sparse_zi_1000, rmsc01, obi_rmsc02 (seed 30: its OBI agents trade) -- ADVICE r05
 @pytest.mark.parametrize("cfg,seeds", [("rmsc03", [123456789, 7, 1008]), ("sparse_zi_100", [123456789, 5]),
                                        ("value_noise", [7, 123456789]), ("sparse_zi_1000", [123456789]),
-                                       ("rmsc02", [7])])
+                                       ("rmsc02", [7]), ("rmsc01", [7]), ("obi_rmsc02", [30]),
+                                       ("random_fund_value", [7]), ("rmsc03_sbmm", [7])])
 def test_gpu_exchange_log_records_equal_oracle(mx, cfg, seeds):
-    m = mx.VecMarket(cfg, seeds, book_log=CAP, exchange_log=True)
+    m = mx.VecMarket(cfg, seeds, book_log=CAP * (8 if cfg == "rmsc01" else 1), exchange_log=True)
     m.run()
     s = m.summary()
     for i, sd in enumerate(seeds):
