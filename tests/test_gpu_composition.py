@@ -72,3 +72,35 @@ def test_gpu_composition_batch_equals_oracle(C, name):
     assert (er == 0).all() and (s["status"] == 1).all()
     assert (s["events"] == ev).all()
     assert (s["hash"] == hs).all()
+
+
+@pytest.mark.parametrize("name", ["rmsc03_alt", "sparse_zi_alt"])
+def test_gpu_composition_chunked_launches_and_exchange_log(C, name, tmp_path):
+    """a composition's handle is an ordinary Kernel.runner handle: 997-pop launches equal one
+    launch, and its book-update stream with the exchange log on is the oracle's record for record;
+    the written run directory names the agents as the base script does"""
+    import mxabides
+    cfg = _composition(C, name)
+    seeds = [123456789, 7, 99]
+    one = mxabides.VecMarket(cfg, seeds, book_log=1 << 20, exchange_log=True)
+    one.run()
+    many = mxabides.VecMarket(cfg, seeds)
+    many.run(chunk=997)
+    s1, s2 = one.summary(), many.summary()
+    for k in ("events", "hash", "current_time", "order_counter", "status"):
+        assert (s1[k] == s2[k]).all(), k
+    for i, sd in enumerate(seeds):
+        o = pyoracle.OracleEnv(cfg, sd)
+        o.set_book_log()
+        o.set_exchange_log()
+        o.run()
+        a = o.book_records()
+        d = one.book_log_records(i)
+        assert len(d) == len(a)
+        assert (d["t"] == a[:, 0]).all() and (d["price"] == a[:, 1]).all() and (d["qty"] == a[:, 2]).all()
+    one.write_logs(0, str(tmp_path))
+    names, types = C.agent_names(cfg), C.agent_type_names(cfg)
+    assert (tmp_path / ("%s.bz2" % names[0].replace(" ", ""))).exists()  # the exchange's own log
+    assert (tmp_path / "summary_log.bz2").exists()
+    rows = one.summary_log(0)
+    assert rows and all(r["AgentStrategy"] == types[r["AgentID"]] for r in rows)
