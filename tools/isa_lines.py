@@ -1,4 +1,5 @@
-"""Static per-source-line instruction / spill counts of the rmsc03 run kernel.
+"""Static per-source-line instruction / spill counts of the rmsc03 run kernel (or of the kernel
+whose mangled name starts with $MXA_ISA_KERNEL, e.g. _Z15mxa_step_kernelILi3ELb0ELb1E).
 usage: python tools/isa_lines.py [extra hipcc flags]   (device-only compile with line tables)"""
 import collections
 import os
@@ -15,11 +16,12 @@ cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++20", "-ff
 subprocess.check_call(cmd, stderr=subprocess.DEVNULL)
 s = open(out).read()
 files = {m.group(1): m.group(3) for m in re.finditer(r'\.file\s+(\d+)\s+"([^"]*)"\s+"([^"]*)"', s)}
-i = s.find(":\n", s.find("\n_Z14mxa_run_kernel"))
+i = s.find(":\n", s.find("\n" + os.environ.get("MXA_ISA_KERNEL", "_Z14mxa_run_kernel")))
 body = s[i:s.find(".Lfunc_end", i)]
 cur = None
 ins = collections.Counter()
 spl = collections.Counter()
+sal = collections.Counter()
 for l in body.splitlines():
     l = l.strip()
     m = re.match(r"\.loc\s+(\d+)\s+(\d+)", l)
@@ -29,6 +31,8 @@ for l in body.splitlines():
     if not l or l[0] in ".;_" or l.endswith(":"):
         continue
     ins[cur] += 1
+    if l.startswith("s_") and not l.startswith(("s_waitcnt", "s_cbranch", "s_branch", "s_nop", "s_load", "s_buffer")):
+        sal[cur] += 1
     if l.startswith("scratch_"):
         spl[cur] += 1
 print("total", sum(ins.values()), "scratch", sum(spl.values()))
@@ -41,6 +45,9 @@ def text(f, n):
 print("-- top lines by scratch ops")
 for k, v in spl.most_common(25):
     print("%5d %6d %s:%d  %s" % (v, ins[k], k[0], k[1], text(*k)))
-print("-- top lines by instructions")
-for k, v in ins.most_common(25):
-    print("%5d %6d %s:%d  %s" % (spl[k], v, k[0], k[1], text(*k)))
+print("-- top lines by instructions (scratch, all, SALU)")
+for k, v in ins.most_common(40):
+    print("%5d %6d %5d %s:%d  %s" % (spl[k], v, sal[k], k[0], k[1], text(*k)))
+print("-- top lines by SALU")
+for k, v in sal.most_common(40):
+    print("%5d %6d %5d %s:%d  %s" % (spl[k], ins[k], v, k[0], k[1], text(*k)))
