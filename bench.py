@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's bench size)")
     ap.add_argument("--config", default="rmsc03")
     ap.add_argument("--chunk", type=int, default=1 << 22, help="max pops per env per kernel launch")
+    ap.add_argument("--first-chunk", type=int, default=0,
+                    help="Kernel.runner configurations: a first launch of this many pops, then launches of --chunk "
+                         "over the envs still running (mxa_set_launch_schedule); 0 = launches of --chunk only. "
+                         "Measured slower for every configuration (DESIGN.md Appendix R.6)")
     ap.add_argument("--cpu-envs", type=int, default=None, help="CPU-baseline sample size (envs)")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU-baseline threads (default: the cores this process may run on, capped by OMP_NUM_THREADS)")
@@ -262,6 +266,7 @@ class MarketEngine(Engine):
         self.torch.cuda.set_stream(self.stream)
         self.m.set_stream(self.stream.cuda_stream)
         self.m.set_parity_hash(args.parity_hash)
+        self.m.set_launch_schedule(args.first_chunk)
         cid = (self.composition.base if self.composition is not None else mxabides.CONFIG_IDS[cfg]
                if args.config != "rmsc03_sweep" else mxabides._lib.MXA_RMSC03_MM)
         self.kernel = "mxa_run_kernel<%d> (%s%s)" % (cid, args.config,

@@ -205,8 +205,16 @@ int mxa_set_id_persistence(mxa_handle* h, int32_t on);
 /* one asynchronous launch: every running env performs up to max_pops kernel pops */
 int mxa_launch(mxa_handle* h, int64_t max_pops);
 int mxa_sync(mxa_handle* h);
-/* launches of `chunk` pops until every env is done/errored (or max_launches reached) */
+/* launches of `chunk` pops until every env is done/errored (or max_launches reached).  After each
+ * launch the envs still running are compacted into a list and the next launch is one wave per
+ * listed env, so the CUs share the live envs evenly (envs that end early, e.g. rmsc03's stalled
+ * market maker, no longer leave their CU's slots idle while the others run on).  Results do not
+ * depend on the launch sizes (the engine saves and reloads its state between launches). */
 int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launches_out);
+/* mxa_run's launch sizes: first_chunk > 0 makes its first launch first_chunk pops and the later
+ * ones `chunk`, so envs that finish early (e.g. rmsc03's stalled market maker) leave the grid
+ * after one short launch; 0 (the default) = every launch `chunk` pops.  Kept across resets. */
+int mxa_set_launch_schedule(mxa_handle* h, int64_t first_chunk);
 /* Kernel.runner(startTime, stopTime) with a caller's stopTime (Kernel.py:50-64, 190-196): every env
  * of a Kernel.runner handle stops at its first pop with currentTime past t_stop_ns (ns since the
  * simulated midnight; that event is handled, as the reference's loop test comes before its get)

@@ -37,9 +37,30 @@ extern char** environ;
 
 namespace {
 
-__global__ void mxa_count_running_kernel(const char* base, uint64_t stride, int n, int* out) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && ((const EnvHdr*)(base + (size_t)i * stride))->status == ST_RUNNING) atomicAdd(out, 1);
+// the envs still running, in env order, and their count: one workgroup of 16 waves walks the env
+// headers 1024 at a time (a ballot per wave, the waves' counts through LDS).  The next launch of
+// mxa_run is one wave per listed env
+__global__ __launch_bounds__(1024) void mxa_compact_kernel(const char* base, uint64_t stride, int n, int32_t* list,
+                                                           int* count) {
+  __shared__ int wn[16];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  int done = 0;
+  for (int i0 = 0; i0 < n; i0 += 1024) {
+    const int i = i0 + (int)threadIdx.x;
+    const bool run = i < n && ((const EnvHdr*)(base + (size_t)i * stride))->status == ST_RUNNING;
+    const uint64_t m = __ballot(run);
+    if (l == 0) wn[w] = __popcll(m);
+    __syncthreads();
+    int off = done, tot = 0;
+    for (int k = 0; k < 16; k++) {
+      off += k < w ? wn[k] : 0;
+      tot += wn[k];
+    }
+    if (run) list[off + __popcll(m & ((1ull << l) - 1))] = i;
+    done += tot;
+    __syncthreads();  // wn is rewritten by the next block of envs
+  }
+  if (threadIdx.x == 0) *count = done;
 }
 
 // Kernel.runner's stopTime of every env (EnvHdr::t_stop; 0 = the config's own)
@@ -171,6 +192,8 @@ struct mxa_handle {
   uint32_t* d_seeds = nullptr;
   uint8_t* d_mask = nullptr;
   int* d_count = nullptr;
+  int32_t* d_list = nullptr;  // [n_envs] the running envs after a launch (mxa_compact_kernel)
+  int64_t first_chunk = 0;    // mxa_set_launch_schedule: mxa_run's first launch (0: every launch `chunk`)
   size_t lds = 0;
   mxa_build_fn build = nullptr;
   mxa_run_fn run = nullptr, run_log = nullptr;     // run_log: with the book-update log
@@ -643,6 +666,7 @@ static int create_common(mxa_handle* h, int32_t n_envs, const uint32_t* seeds, i
   HIPCHK(h, hipMalloc(&h->d_seeds, sizeof(uint32_t) * n_envs));
   HIPCHK(h, hipMalloc(&h->d_mask, n_envs));
   HIPCHK(h, hipMalloc(&h->d_count, sizeof(int)));
+  HIPCHK(h, hipMalloc(&h->d_list, sizeof(int32_t) * (size_t)std::max(1, h->P.n_envs)));
   HIPCHK(h, hipMemsetAsync(h->d_env, 0, bytes, h->stream));
   HIPCHK(h, hipMemcpyAsync(h->d_seeds, seeds, sizeof(uint32_t) * n_envs, hipMemcpyHostToDevice, h->stream));
   if (h->replay) {
@@ -952,7 +976,7 @@ int mxa_launch(mxa_handle* h, int64_t max_pops) {
   HIPCHK(h, hipSetDevice(h->device));  // the caller's current device may differ
   h->started = true;
   h->run_kernel()(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), max_pops,
-         h->d_ctx, h->d_blog, h->blog_cap);
+         h->d_ctx, h->d_blog, h->blog_cap, nullptr);
   HIPCHK(h, hipGetLastError());
   return MXA_OK;
 }
@@ -970,28 +994,46 @@ int mxa_run(mxa_handle* h, int64_t chunk, int32_t max_launches, int32_t* launche
   int launches = 0;
   float total = 0;
   h->started = true;
-  for (;;) {
+  const int n = h->P.n_envs;
+  // the envs still running (an earlier mxa_run / mxa_launch may have finished some)
+  auto compact = [&](int& running) -> int {
+    hipLaunchKernelGGL(mxa_compact_kernel, dim3(1), dim3(1024), 0, h->stream, h->d_env, h->P.L.env_stride, n,
+                       h->d_list, h->d_count);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(&running, h->d_count, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (running < 0 || running > n) {
+      h->err = "mxa_run: running-env count out of range";
+      return MXA_EHIP;
+    }
+    return MXA_OK;
+  };
+  int running = 0, rc;
+  if ((rc = compact(running)) != MXA_OK) return rc;
+  int64_t pops = h->first_chunk > 0 ? std::min(chunk, h->first_chunk) : chunk;
+  while (running > 0) {
     if (max_launches > 0 && launches >= max_launches) break;
+    // one wave per running env: every env (no list) while none has finished
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    h->run_kernel()(dim3(h->P.n_envs), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, h->P.n_envs, h->tcap_arg(), chunk,
-           h->d_ctx, h->d_blog, h->blog_cap);
+    h->run_kernel()(dim3(running), dim3(64), h->lds, h->stream, h->d_env, h->P.L.env_stride, n, h->tcap_arg(), pops,
+                    h->d_ctx, h->d_blog, h->blog_cap, running == n ? nullptr : h->d_list);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     launches++;
-    HIPCHK(h, hipMemsetAsync(h->d_count, 0, sizeof(int), h->stream));
-    int n = h->P.n_envs;
-    hipLaunchKernelGGL(mxa_count_running_kernel, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d_env,
-                       h->P.L.env_stride, n, h->d_count);
-    int running = 0;
-    HIPCHK(h, hipMemcpyAsync(&running, h->d_count, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if ((rc = compact(running)) != MXA_OK) return rc;
     float ms = 0;
     HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
     total += ms;
-    if (running == 0) break;
+    pops = chunk;  // mxa_set_launch_schedule: the first launch only is first_chunk
   }
   h->last_ms = total;
   if (launches_out) *launches_out = launches;
+  return MXA_OK;
+}
+
+int mxa_set_launch_schedule(mxa_handle* h, int64_t first_chunk) {
+  if (!h || first_chunk < 0) return MXA_EINVAL;
+  h->first_chunk = first_chunk;
   return MXA_OK;
 }
 
@@ -1293,6 +1335,7 @@ void mxa_destroy(mxa_handle* h) {
   if (h->d_seeds) hipFree(h->d_seeds);
   if (h->d_mask) hipFree(h->d_mask);
   if (h->d_count) hipFree(h->d_count);
+  if (h->d_list) hipFree(h->d_list);
   if (h->d_tape) hipFree(h->d_tape);
   if (h->d_ctx) hipFree(h->d_ctx);
   if (h->d_mmp) hipFree(h->d_mmp);

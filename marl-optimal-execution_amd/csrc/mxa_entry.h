@@ -12,7 +12,7 @@
 typedef void (*mxa_build_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, const uint32_t*, const uint8_t*,
                              const RpCtx*);
 typedef void (*mxa_run_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*, BlRec*,
-                           int);
+                           int, const int32_t*);
 typedef void (*mxa_stop_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, mxa_agent_final*, BlRec*, int,
                             const RpCtx*);
 typedef void (*mxa_step_fn)(dim3, dim3, size_t, hipStream_t, char*, uint64_t, int, int, int64_t, const RpCtx*,

@@ -16,9 +16,9 @@ void launch_build(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_
 }
 template <int CFG, bool LOG, bool INSTR>
 void launch_run(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, int tcap, int64_t max_pops,
-                const RpCtx* ctx, BlRec* blog, int blog_cap) {
+                const RpCtx* ctx, BlRec* blog, int blog_cap, const int32_t* list) {
   hipLaunchKernelGGL((mxa_run_kernel<CFG, LOG, INSTR>), g, b, lds, s, base, stride, n, tcap, max_pops, ctx, blog,
-                     blog_cap);
+                     blog_cap, list);
 }
 template <int CFG, bool LOG>
 void launch_stop(dim3 g, dim3 b, size_t lds, hipStream_t s, char* base, uint64_t stride, int n, mxa_agent_final* out,

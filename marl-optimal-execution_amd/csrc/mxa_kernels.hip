@@ -5941,9 +5941,13 @@ __global__ __launch_bounds__(64) void mxa_build_kernel(char* base, uint64_t stri
 // it is what a run with the hash off and no trace ring launches (same results, fewer registers)
 template <int CFG, bool LOG, bool INSTR>
 __global__ __launch_bounds__(64, mxa_cfg::shape(CFG).waves) void mxa_run_kernel(char* base, uint64_t stride, int n_envs, int trace_cap, int64_t max_pops,
-                                                                              const RpCtx* ctx, BlRec* blog, int blog_cap) {
+                                                                              const RpCtx* ctx, BlRec* blog, int blog_cap,
+                                                                              const int32_t* list) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  int env = blockIdx.x;
+  // list (nullable): the envs still running after the previous launch, compacted by
+  // mxa_compact_kernel (mxa_api.hip); the grid is then one wave per listed env, so the dispatcher
+  // spreads only live envs over the CUs instead of leaving the slots of finished ones idle
+  int env = list ? list[blockIdx.x] : (int)blockIdx.x;
   if (env >= n_envs) return;
   char* e = base + (size_t)env * stride;
   if (((EnvHdr*)e)->status != ST_RUNNING) return;

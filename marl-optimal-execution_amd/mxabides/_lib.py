@@ -83,7 +83,7 @@ EXPORTS = ["mxa_create", "mxa_reset", "mxa_launch", "mxa_sync", "mxa_run", "mxa_
            "mxa_set_stop_time", "mxa_run_until", "mxa_create_replay_twap", "mxa_create_params", "mxa_set_mm_params",
            "mxa_mm_defaults", "mxa_resident_envs", "mxa_set_exchange_log", "mxa_config_defaults",
            "mxa_config_compile", "mxa_config_key", "mxa_create_config", "mxa_config_info",
-           "mxa_step_many"]
+           "mxa_step_many", "mxa_set_launch_schedule"]
 COUNTER_WORDS = 34  # include/mxa.h MXA_COUNTER_WORDS
 RECORD_WORDS = 12  # include/mxa.h MXA_RECORD_WORDS
 
@@ -134,7 +134,7 @@ def load():
                        ("mxa_create_replay_twap", [P, P, P, P, P, I32, I32, I32, I32, I32, ctypes.POINTER(P)]),
                        ("mxa_create_params", [I32, I32, P, P, I32, I32, ctypes.POINTER(P)]),
                        ("mxa_set_mm_params", [P, P]), ("mxa_resident_envs", [P]),
-                       ("mxa_set_exchange_log", [P, I32]),
+                       ("mxa_set_exchange_log", [P, I32]), ("mxa_set_launch_schedule", [P, I64]),
                        ("mxa_config_defaults", [I32, P]), ("mxa_config_compile", [P, ctypes.c_char_p, P, I32]),
                        ("mxa_config_key", [P, P]), ("mxa_config_info", [I32, P]),
                        ("mxa_create_config", [P, I32, P, I32, I32, ctypes.c_char_p, ctypes.POINTER(P)])):

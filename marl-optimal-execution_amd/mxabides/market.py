@@ -211,6 +211,12 @@ class VecMarket:
         self._check(self.L.mxa_run(self._h, chunk, max_launches, ctypes.byref(n)), "mxa_run")
         return n.value
 
+    def set_launch_schedule(self, first_chunk):
+        """run()'s launch sizes: a first launch of first_chunk pops, then launches of run()'s
+        chunk, each over the envs still running; 0 = every launch `chunk`
+        (include/mxa.h mxa_set_launch_schedule)"""
+        self._check(self.L.mxa_set_launch_schedule(self._h, int(first_chunk)), "mxa_set_launch_schedule")
+
     def set_stop_time(self, t_stop_ns):
         """Kernel.runner's stopTime (ns since the simulated midnight) instead of the config
         script's kernelStopTime, kept across resets; None or <= 0 restores the config's

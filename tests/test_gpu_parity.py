@@ -172,6 +172,25 @@ def test_gpu_chunked_launches_equal_single(mx, cfg, seeds):
     assert (sb["events"] == ev).all() and (sb["hash"] == hs).all()
 
 
+def test_gpu_launch_schedule_compacted_grid_equals_oracle(mx):
+    """mxa_set_launch_schedule: a short first launch, then launches over the compacted list of
+    running envs (one wave per listed env); envs that end early (seed 1008's stalled market
+    maker and its like) leave the grid, and every env still equals the oracle"""
+    seeds = ((np.arange(96, dtype=np.int64) * 7919 + 1008) & 0xFFFFFFFF).astype(np.uint32)
+    m = mx.VecMarket("rmsc03", seeds)
+    m.set_launch_schedule(3000)
+    nl = m.run(chunk=40000)
+    s = m.summary()
+    ev, hs, _ = pyoracle.run_batch("rmsc03", seeds, threads=8)
+    assert (s["status"] == 1).all()
+    assert (s["events"] == ev).all() and (s["hash"] == hs).all()
+    assert 2 <= nl <= 2 + -(-(int(ev.max()) - 3000) // 40000)
+    m.set_launch_schedule(0)
+    m.reset()
+    assert m.run(chunk=1 << 22) == 1
+    assert (m.summary()["hash"] == hs).all()
+
+
 def test_gpu_reset_reproduces(mx):
     m = mx.VecMarket("rmsc03", [17, 18])
     m.run()
