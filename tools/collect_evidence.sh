@@ -17,9 +17,10 @@ for d in gpurun_out/prof_${T}_*; do
 done
 [ -f gpurun_out/final_$T/pytest_gpu.log ] && cp gpurun_out/final_$T/pytest_gpu.log $F/pytest_gpu.log
 [ -f gpurun_out/final_$T/smoke.log ] && cp gpurun_out/final_$T/smoke.log $F/smoke.log
-for d in gpurun_out/sq_${T}_*; do
+for d in gpurun_out/sq_${T}_*/; do
   [ -d "$d" ] || continue
   c=${d#gpurun_out/sq_${T}_}
+  c=${c%/}
   for f in $d/issue_*.json; do [ -f "$f" ] && cp $f profiles/; done
   [ -f $d/summary.txt ] && cp $d/summary.txt $F/sq/summary_$c.txt
   echo "sq $c"
