@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's bench size)")
     ap.add_argument("--config", default="rmsc03")
     ap.add_argument("--chunk", type=int, default=1 << 22, help="max pops per env per kernel launch")
+    ap.add_argument("--ddqn-torch", action="store_true",
+                    help="rmsc03_ddqn: the learner's per-period bookkeeping as PyTorch ops instead of "
+                         "libmxa_ddqn.so's one kernel")
     ap.add_argument("--first-chunk", type=int, default=0,
                     help="Kernel.runner configurations: a first launch of this many pops, then launches of --chunk "
                          "over the envs still running (mxa_set_launch_schedule); 0 = launches of --chunk only. "
@@ -555,7 +558,7 @@ class DDQNEngine(Engine):
         if timed and not self.timing:
             self.learns0 = self.learner.learn_step_counter
         r = self.ddqn.run_episode(self.v, self.learner, self.task, seeds=self.seeds(k),
-                                  timing=self.timing if timed else None)
+                                  timing=self.timing if timed else None, fused=not self.args.ddqn_torch)
         if timed:
             self.env_steps += r["env_steps"].sum()
         self.v.write_records(self.records.data_ptr())
@@ -587,7 +590,9 @@ class DDQNEngine(Engine):
                 "dtype": "int64 (market), fp32 (Q-network)", "data": "synthetic (seeds); actions from the DDQN learner",
                 "workload": "rmsc03_rl x%d envs per GPU + DDQN learner (NNModel_1, batch %d, train every 5 periods), "
                             "full episode per bench step, seeds %d+global_env" % (n, self.args.ddqn_batch, self.shard.SEED0),
-                "agents_per_env": self.v.n_agents, "learn_steps": self.learner.learn_step_counter - self.learns0}
+                "agents_per_env": self.v.n_agents, "learn_steps": self.learner.learn_step_counter - self.learns0,
+                "learner_period": "torch ops" if self.args.ddqn_torch or self.ddqn.period_lib() is None
+                else "one kernel (libmxa_ddqn.so, include/mxa_ddqn.h)"}
 
     def gym_steps(self):
         return int(self.env_steps.item()) * self.ctx.world  # every rank steps its own envs alike
@@ -740,7 +745,7 @@ def main():
                "config": {"workload": d["workload"], "envs_per_gpu": eng.n, "global_envs": eng.n * ctx.world,
                           "events_per_step": events / args.steps, "parallelism": "envs sharded, dp%d" % ctx.world,
                           "parity_hash": bool(args.parity_hash), "env_errors": n_err, "gathered_records": chk}}
-        for key in ("agents_per_env", "tape_records", "learn_steps"):
+        for key in ("agents_per_env", "tape_records", "learn_steps", "learner_period"):
             if key in d:
                 out["config"][key] = d[key]
         if isinstance(eng, GymEngine):

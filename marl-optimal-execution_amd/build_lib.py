@@ -91,5 +91,25 @@ def build(force=False, verbose=True, jobs=None):
     return OUT
 
 
+DDQN_SRC = os.path.join(HERE, "csrc", "ddqn_period.hip")
+DDQN_OUT = os.path.join(HERE, "lib", "libmxa_ddqn.so")
+
+
+def build_ddqn(force=False, verbose=True):
+    """libmxa_ddqn.so: the DDQN learner's per-period bookkeeping kernel (mxabides.ddqn run_episode);
+    a library of its own, outside the engine's build id"""
+    if not force and os.path.exists(DDQN_OUT) and os.path.getmtime(DDQN_OUT) >= max(
+            os.path.getmtime(DDQN_SRC), os.path.getmtime(os.path.abspath(__file__))):
+        return DDQN_OUT
+    os.makedirs(os.path.dirname(DDQN_OUT), exist_ok=True)
+    cmd = [HIPCC] + FLAGS + [DDQN_SRC, "-o", DDQN_OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(DDQN_OUT + ".tmp", DDQN_OUT)
+    return DDQN_OUT
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_ddqn(force="--force" in sys.argv)

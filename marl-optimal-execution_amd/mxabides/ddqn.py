@@ -57,6 +57,7 @@ Everything runs on the device stream the env steps on; the only host read is the
 count, when the replay ring's host-side bounds cannot decide the batch-size test.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -431,7 +432,116 @@ class ExecutionTask:
         return torch.where(dq > 0, 1e4 / q0 * (2 * dq + dcash / arrival), torch.zeros_like(dq))
 
 
-def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train=1, record=None, timing=None):
+_PERIOD_LIB = None
+
+
+def period_lib():
+    """libmxa_ddqn.so (include/mxa_ddqn.h): the per-period bookkeeping kernel of run_episode;
+    None when it is not built"""
+    global _PERIOD_LIB
+    if _PERIOD_LIB is None:
+        import ctypes
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libmxa_ddqn.so")
+        if not os.path.exists(path):
+            return None
+        L = ctypes.CDLL(path)
+        P, I, I64, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+        L.mxa_ddqn_period.argtypes = [P, I, I, I, I] + [P] * 13 + [P, I, P, I, D, D, D, P, P, P, P, I64, P, P]
+        L.mxa_ddqn_state.argtypes = [P, I, I, P, P, I, P, I, D, D, P]
+        _PERIOD_LIB = L
+    return _PERIOD_LIB
+
+
+def _state_device(L, task, obs, out):
+    rc = L.mxa_ddqn_state(torch.cuda.current_stream().cuda_stream, obs.shape[0], obs.shape[1], obs.data_ptr(),
+                          task.grid[0].data_ptr(), task.grid[0].numel(), task.grid[1].data_ptr(), task.grid[1].numel(),
+                          float(task.nh), task.q0, out.data_ptr())
+    if rc:
+        raise RuntimeError("mxa_ddqn_state: hip error %d" % rc)
+    return out
+
+
+def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train=1, record=None, timing=None,
+                fused=None):
+    """fused=True (a learner on the GPU, libmxa_ddqn.so built): the bookkeeping after each step in
+    one kernel (include/mxa_ddqn.h), bitwise the same as the PyTorch ops of the default path
+    (tests/test_gpu_ddqn.py)."""
+    L = period_lib() if fused and learner.device.type == "cuda" else None
+    if fused and L is None:
+        raise RuntimeError("run_episode(fused=True): libmxa_ddqn.so is not built (build_lib.build_ddqn)")
+    if L is not None:
+        return _run_episode_fused(L, env, learner, task, seeds, train_every, updates_per_train, record, timing)
+    return _run_episode_torch(env, learner, task, seeds, train_every, updates_per_train, record, timing)
+
+
+def _run_episode_fused(L, env, learner, task, seeds, train_every, updates_per_train, record, timing):
+    """run_episode with the per-period bookkeeping in one launch; same order of RNG draws, replay
+    appends and updates as _run_episode_torch"""
+    from .gym import OBS_SIZE, RL_STATE_WORDS
+    dev = learner.device
+    n = env.n_envs
+    nh = task.nh
+    env.reset(seeds=seeds)
+    obs = torch.zeros((n, OBS_SIZE), dtype=torch.float64, device=dev)
+    flags = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.zeros((n, RL_STATE_WORDS), dtype=torch.float64, device=dev)
+    prev = torch.zeros_like(st)
+    act0 = torch.zeros((n, 3), dtype=torch.float64, device=dev)
+    env.step_device(act0.data_ptr(), obs.data_ptr(), flags.data_ptr())
+    env.write_rl_state(st.data_ptr())
+    if record is not None:
+        record.append(act0.clone())
+    alive = ((flags & 2) != 0) & ((flags & 5) == 0)
+    alive_next = torch.zeros_like(alive)
+    live = torch.zeros((), dtype=torch.bool, device=dev)
+    lob_ok = (st[:, 7] == 3)
+    arrival = torch.where(lob_ok, (st[:, 3] + st[:, 4]) / 2, torch.ones_like(st[:, 3])).contiguous()
+    rw = torch.zeros((nh, n), dtype=torch.float64, device=dev)
+    actions = []
+    stored = torch.zeros((), dtype=torch.int64, device=dev)
+    env_steps = alive.to(torch.int64)
+    s = _state_device(L, task, obs, torch.empty((n, 2), dtype=torch.float32, device=dev))
+    s2 = torch.empty_like(s)
+    m = learner.memory
+    train = learner.mode == "train"
+    g0, g1 = task.grid
+    for step_counter in range(nh):
+        a = learner.choose_action(s).contiguous()
+        act = task.actions(a, obs)
+        if record is not None:
+            record.append(act.clone())
+        st, prev = prev, st  # write_rl_state fills the other buffer: prev keeps the state before the step
+        if timing is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        env.step_device(act.data_ptr(), obs.data_ptr(), flags.data_ptr())
+        if timing is not None:
+            e1.record()
+            timing.append((e0, e1))
+        env.write_rl_state(st.data_ptr())
+        rc = L.mxa_ddqn_period(torch.cuda.current_stream().cuda_stream, n, obs.shape[1], st.shape[1], int(train),
+                               obs.data_ptr(), st.data_ptr(), prev.data_ptr(), arrival.data_ptr(), flags.data_ptr(),
+                               alive.data_ptr(), alive_next.data_ptr(), live.data_ptr(), s.data_ptr(), a.data_ptr(),
+                               s2.data_ptr(), rw[step_counter].data_ptr(), env_steps.data_ptr(), g0.data_ptr(),
+                               g0.numel(), g1.data_ptr(), g1.numel(), float(nh), task.q0, 1e4 / task.q0,
+                               m.s.data_ptr(), m.s2.data_ptr(), m.a.data_ptr(), m.r.data_ptr(), m.cap,
+                               m.n_dev.data_ptr(), stored.data_ptr())
+        if rc:
+            raise RuntimeError("mxa_ddqn_period: hip error %d" % rc)
+        if train:
+            m.n_ub += n
+            if step_counter % train_every == 0:
+                for _ in range(updates_per_train):
+                    learner.learn(live=live)
+        actions.append(a)
+        alive, alive_next = alive_next, alive
+        s, s2 = s2, s
+    return {"rewards": rw if nh else None, "actions": torch.stack(actions) if actions else None,
+            "returns": rw.sum(0), "flags": flags, "arrival": arrival, "stored": stored, "env_steps": env_steps,
+            "steps": nh + 1}
+
+
+def _run_episode_torch(env, learner, task, seeds=None, train_every=5, updates_per_train=1, record=None, timing=None):
     """One episode of every env of a VecABIDESEnv (rmsc03 + DummyRL) driven by the learner, all on
     the current torch stream (the env must step on it: env.set_stream). Mirrors the agent's
     per-period loop (place_order, :275-299): observe, choose, act, then store the completed

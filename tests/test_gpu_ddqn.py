@@ -140,3 +140,38 @@ def test_gpu_learner_masked_update_is_a_no_op():
     L.learn_on(dv(s), torch.from_numpy(a).cuda(), dv(s2), dv(r), live=torch.zeros((), dtype=torch.bool, device="cuda"))
     assert torch.equal(L.eflat, e0) and torch.equal(L.tflat, t0) and torch.equal(L.rms, r0)
     assert L.learn_step_counter == 0
+
+
+def test_gpu_ddqn_fused_period_equals_torch_ops():
+    """include/mxa_ddqn.h: run_episode's one-kernel bookkeeping (libmxa_ddqn.so) and the PyTorch
+    ops give bitwise the same episodes: actions, rewards, step counts, replay rows, and the learner
+    after its updates (weights, RMSprop state, counter, losses)"""
+    assert ddqn.period_lib() is not None, "libmxa_ddqn.so not built"
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    seeds = SEEDS * 4  # 64 envs
+    out = {}
+    for fused in (False, True):
+        v = VecABIDESEnv(seeds=seeds)
+        v.set_stream(stream.cuda_stream)
+        learner = ddqn.DDQNLearner(device="cuda", seed=5, batch_size=32)
+        task = ddqn.ExecutionTask(device="cuda")
+        eps = []
+        for ep in range(3):
+            res = ddqn.run_episode(v, learner, task, seeds=[s + 77 * ep for s in seeds], fused=fused)
+            eps.append({k: res[k].clone() for k in ("rewards", "actions", "returns", "env_steps", "stored", "flags")})
+        torch.cuda.synchronize()
+        m = learner.memory
+        k = int(m.n_dev.item())
+        out[fused] = (eps, m.s[:k].clone(), m.s2[:k].clone(), m.a[:k].clone(), m.r[:k].clone(), k,
+                      learner.eflat.clone(), learner.tflat.clone(), learner.rms.clone(), learner.learn_step_counter,
+                      learner.cost_hist)
+    a, b = out[False], out[True]
+    for ea, eb in zip(a[0], b[0]):
+        for key in ea:
+            assert torch.equal(ea[key], eb[key]), key
+    assert a[5] == b[5] and a[5] > 0 and a[9] == b[9] and a[9] > 0
+    for x, y in zip(a[1:5] + a[6:9], b[1:5] + b[6:9]):
+        assert torch.equal(x, y)
+    assert a[10] == b[10]

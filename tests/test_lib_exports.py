@@ -43,3 +43,16 @@ int main() { return 0; }
 """)
     inc = os.path.join(ROOT, "marl-optimal-execution_amd", "csrc")
     subprocess.check_call(["g++", "-std=c++20", "-fsyntax-only", "-I", inc, str(src)])
+
+
+def test_ddqn_period_library_exports():
+    """libmxa_ddqn.so (include/mxa_ddqn.h) loads and exports what its header declares"""
+    src = open(os.path.join(ROOT, "include", "mxa_ddqn.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = sorted(set(re.findall(r"\b(mxa_[a-z_0-9]+)\s*\(", src)))
+    assert names == ["mxa_ddqn_period", "mxa_ddqn_state"]
+    from mxabides import ddqn
+    L = ddqn.period_lib()
+    assert L is not None, "libmxa_ddqn.so not built (build_lib.build_ddqn)"
+    for n in names:
+        assert hasattr(L, n), n
