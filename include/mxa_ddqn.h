@@ -29,6 +29,10 @@ int mxa_ddqn_period(void* stream, int n, int obs_w, int st_w, int train, const d
 /* ExecutionTask.state of every env: s [n][2] f32 = discretize(obs) */
 int mxa_ddqn_state(void* stream, int n, int obs_w, const double* obs, const double* g0, int n0, const double* g1,
                    int n1, double nh, double q0, float* s);
+/* ExecutionTask.actions of every env: act [n][3] f64 = table[a] (table [k][3] f64), or on the last
+ * horizon step (obs[0] == 1) (obs[1] / q0, 1, 0) */
+int mxa_ddqn_actions(void* stream, int n, int obs_w, const double* obs, const int64_t* a, const double* table,
+                     double q0, double* act);
 #ifdef __cplusplus
 }
 #endif

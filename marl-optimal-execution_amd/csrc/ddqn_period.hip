@@ -124,9 +124,33 @@ __global__ __launch_bounds__(256) void ddqn_state_kernel(int n, int obs_w, const
   if (i < n) state_of(obs + (size_t)i * obs_w, g0, n0, g1, n1, nh, q0, s + 2 * i);
 }
 
+// ExecutionTask.actions: the action table's row of a, or on the horizon's last step
+// (remaining time 1) the whole remaining quantity at allocation (1, 0)
+__global__ __launch_bounds__(256) void ddqn_actions_kernel(int n, int obs_w, const double* obs, const int64_t* a,
+                                                           const double* table, double q0, double* act) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* t = table + 3 * a[i];
+  const double* o = obs + (size_t)i * obs_w;
+  const bool last = o[0] == 1.0;
+  act[3 * i] = last ? o[1] / q0 : t[0];
+  act[3 * i + 1] = last ? 1.0 : t[1];
+  act[3 * i + 2] = last ? 0.0 : t[2];
+}
+
 }  // namespace
 
 extern "C" {
+
+// ExecutionTask.actions for every env in one launch: act [n][3] f64 from a [n] and table [k][3]
+int mxa_ddqn_actions(hipStream_t stream, int n, int obs_w, const double* obs, const int64_t* a, const double* table,
+                     double q0, double* act) {
+  if (n < 0 || obs_w < 2) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ddqn_actions_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n, obs_w, obs, a, table, q0,
+                     act);
+  return (int)hipGetLastError();
+}
 
 // one period's bookkeeping (see PeriodArgs); 0 on success, else the hipError_t of the launch
 int mxa_ddqn_period(hipStream_t stream, int n, int obs_w, int st_w, int train, const double* obs, const double* st,

@@ -448,6 +448,7 @@ def period_lib():
         P, I, I64, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
         L.mxa_ddqn_period.argtypes = [P, I, I, I, I] + [P] * 13 + [P, I, P, I, D, D, D, P, P, P, P, I64, P, P]
         L.mxa_ddqn_state.argtypes = [P, I, I, P, P, I, P, I, D, D, P]
+        L.mxa_ddqn_actions.argtypes = [P, I, I, P, P, P, D, P]
         _PERIOD_LIB = L
     return _PERIOD_LIB
 
@@ -505,9 +506,14 @@ def _run_episode_fused(L, env, learner, task, seeds, train_every, updates_per_tr
     m = learner.memory
     train = learner.mode == "train"
     g0, g1 = task.grid
+    table = task.table.contiguous()
+    act = torch.empty((n, 3), dtype=torch.float64, device=dev)
     for step_counter in range(nh):
         a = learner.choose_action(s).contiguous()
-        act = task.actions(a, obs)
+        rc = L.mxa_ddqn_actions(torch.cuda.current_stream().cuda_stream, n, obs.shape[1], obs.data_ptr(), a.data_ptr(),
+                                table.data_ptr(), task.q0, act.data_ptr())
+        if rc:
+            raise RuntimeError("mxa_ddqn_actions: hip error %d" % rc)
         if record is not None:
             record.append(act.clone())
         st, prev = prev, st  # write_rl_state fills the other buffer: prev keeps the state before the step

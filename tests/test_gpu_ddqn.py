@@ -159,8 +159,10 @@ def test_gpu_ddqn_fused_period_equals_torch_ops():
         task = ddqn.ExecutionTask(device="cuda")
         eps = []
         for ep in range(3):
-            res = ddqn.run_episode(v, learner, task, seeds=[s + 77 * ep for s in seeds], fused=fused)
+            rec = []
+            res = ddqn.run_episode(v, learner, task, seeds=[s + 77 * ep for s in seeds], fused=fused, record=rec)
             eps.append({k: res[k].clone() for k in ("rewards", "actions", "returns", "env_steps", "stored", "flags")})
+            eps[-1]["action_vectors"] = torch.stack(rec)  # ExecutionTask.actions (mxa_ddqn_actions when fused)
         torch.cuda.synchronize()
         m = learner.memory
         k = int(m.n_dev.item())

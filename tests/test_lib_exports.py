@@ -50,7 +50,7 @@ def test_ddqn_period_library_exports():
     src = open(os.path.join(ROOT, "include", "mxa_ddqn.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     names = sorted(set(re.findall(r"\b(mxa_[a-z_0-9]+)\s*\(", src)))
-    assert names == ["mxa_ddqn_period", "mxa_ddqn_state"]
+    assert names == ["mxa_ddqn_actions", "mxa_ddqn_period", "mxa_ddqn_state"]
     from mxabides import ddqn
     L = ddqn.period_lib()
     assert L is not None, "libmxa_ddqn.so not built (build_lib.build_ddqn)"
