@@ -26,11 +26,15 @@ __device__ int64_t upper_bound(double x, const double* bd, int n) {
   return lo;
 }
 
+// PyTorch divides a tensor by a Python scalar as a multiplication by the scalar's reciprocal
+// (the true-division kernel's CPU-scalar case), which rounds differently from x / b
+__device__ double div_scalar(double x, double b) { return x * (1.0 / b); }
+
 // ExecutionTask.state: discretize([2 * rem_t / nh - 1, 2 * rem_q / q0 - 1])
 __device__ void state_of(const double* o, const double* g0, int n0, const double* g1, int n1, double nh, double q0,
                          float* out) {
-  const double tr = 2.0 * (o[0] / nh) - 1.0;
-  const double qr = 2.0 * (o[1] / q0) - 1.0;
+  const double tr = 2.0 * div_scalar(o[0], nh) - 1.0;
+  const double qr = 2.0 * div_scalar(o[1], q0) - 1.0;
   out[0] = (float)upper_bound(tr, g0, n0);
   out[1] = (float)upper_bound(qr, g1, n1);
 }
@@ -133,7 +137,7 @@ __global__ __launch_bounds__(256) void ddqn_actions_kernel(int n, int obs_w, con
   const double* t = table + 3 * a[i];
   const double* o = obs + (size_t)i * obs_w;
   const bool last = o[0] == 1.0;
-  act[3 * i] = last ? o[1] / q0 : t[0];
+  act[3 * i] = last ? div_scalar(o[1], q0) : t[0];
   act[3 * i + 1] = last ? 1.0 : t[1];
   act[3 * i + 2] = last ? 0.0 : t[2];
 }
