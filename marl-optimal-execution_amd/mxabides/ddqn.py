@@ -466,7 +466,7 @@ def run_episode(env, learner, task, seeds=None, train_every=5, updates_per_train
                 fused=None):
     """fused (default: a learner on the GPU with libmxa_ddqn.so built): the bookkeeping after each
     step in one kernel (include/mxa_ddqn.h), bitwise the same as the PyTorch ops that fused=False
-    runs (tests/test_gpu_ddqn.py; 60.0 -> 56.4 ms per rmsc03_ddqn x4096 episode on one box)."""
+    runs (tests/test_gpu_ddqn.py; 59.9 -> 55.8 ms per rmsc03_ddqn x4096 episode on one box)."""
     L = period_lib() if fused is not False and learner.device.type == "cuda" else None
     if fused and L is None:
         raise RuntimeError("run_episode(fused=True): libmxa_ddqn.so is not built (build_lib.build_ddqn)")
